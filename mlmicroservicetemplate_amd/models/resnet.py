@@ -1,0 +1,322 @@
+"""ResNet-50 v1.5 (stride on the 3x3 conv) for MI355X serving.
+
+Three execution paths over ONE parameter set:
+
+* ``resnet50_reference``  -- plain fp32 PyTorch functional ops (NCHW).  This is the
+  numerics oracle for the HIP kernels (SURVEY.md §4 "Models" row).
+* ``ResNet50Eager``       -- stock PyTorch-ROCm ops (MIOpen conv / hipBLASLt GEMM) in
+  bf16 channels-last.  This is the in-repo *comparison baseline (b)* of SURVEY.md §6:
+  the reference itself publishes no numbers.
+* ``ResNet50Fused``       -- our hand-written CDNA4 kernels (``ops``): implicit-GEMM
+  MFMA convs with BN folded into the epilogue (+residual +ReLU), max/avg pool, FC,
+  softmax and top-k, NHWC end-to-end, capturable into one hipGraph per batch bucket.
+
+The reference "model" is a constant-returning stub (reference ``src/model/model.py:23-31``);
+the GPU models here have no reference counterpart and come from BASELINE.json's configs.
+Weights are random-init (no network for checkpoints): kaiming-normal convs, BN with
+non-trivial random running statistics so that BN folding is actually exercised.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+# (blocks, mid channels, out channels, first stride) per stage
+STAGES: Tuple[Tuple[int, int, int, int], ...] = (
+    (3, 64, 256, 1),
+    (4, 128, 512, 2),
+    (6, 256, 1024, 2),
+    (3, 512, 2048, 2),
+)
+IMAGENET_MEAN = (0.485 * 255, 0.456 * 255, 0.406 * 255)
+IMAGENET_STD = (0.229 * 255, 0.224 * 255, 0.225 * 255)
+NUM_CLASSES = 1000
+
+
+@dataclass
+class ConvSpec:
+    name: str
+    cin: int
+    cout: int
+    k: int
+    stride: int
+    pad: int
+
+
+def conv_specs() -> List[ConvSpec]:
+    """All 53 convolutions of ResNet-50 v1.5 in execution order."""
+    specs = [ConvSpec("stem", 3, 64, 7, 2, 3)]
+    cin = 64
+    for si, (nblocks, mid, cout, stride) in enumerate(STAGES):
+        for bi in range(nblocks):
+            s = stride if bi == 0 else 1
+            p = f"layer{si + 1}.{bi}"
+            specs.append(ConvSpec(p + ".conv1", cin, mid, 1, 1, 0))
+            specs.append(ConvSpec(p + ".conv2", mid, mid, 3, s, 1))
+            specs.append(ConvSpec(p + ".conv3", mid, cout, 1, 1, 0))
+            if bi == 0:
+                specs.append(ConvSpec(p + ".down", cin, cout, 1, s, 0))
+            cin = cout
+    return specs
+
+
+def init_resnet50(seed: int = 0, num_classes: int = NUM_CLASSES) -> Dict[str, torch.Tensor]:
+    """Random-init fp32 parameters on CPU. Conv weights are OIHW (PyTorch layout)."""
+    g = torch.Generator().manual_seed(seed)
+    params: Dict[str, torch.Tensor] = {}
+    for spec in conv_specs():
+        fan_in = spec.cin * spec.k * spec.k
+        w = torch.randn(spec.cout, spec.cin, spec.k, spec.k, generator=g) * math.sqrt(2.0 / fan_in)
+        params[spec.name + ".w"] = w
+        c = spec.cout
+        # zero-ish gamma on the last BN of each block (as in "zero-init residual") would make
+        # the residual branch vanish and hide kernel bugs, so use O(1) random values instead.
+        params[spec.name + ".bn.gamma"] = 0.5 + 0.5 * torch.rand(c, generator=g)
+        params[spec.name + ".bn.beta"] = 0.1 * torch.randn(c, generator=g)
+        params[spec.name + ".bn.mean"] = 0.1 * torch.randn(c, generator=g)
+        params[spec.name + ".bn.var"] = 0.5 + torch.rand(c, generator=g)
+    params["fc.w"] = torch.randn(num_classes, 2048, generator=g) * math.sqrt(1.0 / 2048)
+    params["fc.b"] = 0.01 * torch.randn(num_classes, generator=g)
+    return params
+
+
+BN_EPS = 1e-5
+
+
+def fold_bn(params: Dict[str, torch.Tensor], name: str) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Per-output-channel (scale, bias) so that BN(conv(x)) == conv(x) * scale + bias."""
+    gamma = params[name + ".bn.gamma"]
+    beta = params[name + ".bn.beta"]
+    mean = params[name + ".bn.mean"]
+    var = params[name + ".bn.var"]
+    scale = gamma / torch.sqrt(var + BN_EPS)
+    bias = beta - mean * scale
+    return scale, bias
+
+
+def normalize_reference(images_u8_nhwc: torch.Tensor) -> torch.Tensor:
+    """uint8 NHWC -> fp32 NCHW normalised with ImageNet mean/std."""
+    x = images_u8_nhwc.float()
+    mean = torch.tensor(IMAGENET_MEAN, device=x.device)
+    std = torch.tensor(IMAGENET_STD, device=x.device)
+    x = (x - mean) / std
+    return x.permute(0, 3, 1, 2).contiguous()
+
+
+def _ref_conv_bn(params, x, spec: ConvSpec, relu: bool, residual=None):
+    y = F.conv2d(x, params[spec.name + ".w"], stride=spec.stride, padding=spec.pad)
+    y = F.batch_norm(
+        y,
+        params[spec.name + ".bn.mean"],
+        params[spec.name + ".bn.var"],
+        params[spec.name + ".bn.gamma"],
+        params[spec.name + ".bn.beta"],
+        training=False,
+        eps=BN_EPS,
+    )
+    if residual is not None:
+        y = y + residual
+    return F.relu(y) if relu else y
+
+
+def resnet50_reference(params: Dict[str, torch.Tensor], images_u8_nhwc: torch.Tensor) -> torch.Tensor:
+    """fp32 logits [B, num_classes]; the oracle for every other path."""
+    specs = {s.name: s for s in conv_specs()}
+    x = normalize_reference(images_u8_nhwc)
+    x = _ref_conv_bn(params, x, specs["stem"], relu=True)
+    x = F.max_pool2d(x, kernel_size=3, stride=2, padding=1)
+    for si, (nblocks, _mid, _cout, _stride) in enumerate(STAGES):
+        for bi in range(nblocks):
+            p = f"layer{si + 1}.{bi}"
+            identity = x
+            if bi == 0:
+                identity = _ref_conv_bn(params, x, specs[p + ".down"], relu=False)
+            y = _ref_conv_bn(params, x, specs[p + ".conv1"], relu=True)
+            y = _ref_conv_bn(params, y, specs[p + ".conv2"], relu=True)
+            x = _ref_conv_bn(params, y, specs[p + ".conv3"], relu=True, residual=identity)
+    x = x.mean(dim=(2, 3))
+    return F.linear(x, params["fc.w"], params["fc.b"])
+
+
+class ResNet50Eager(torch.nn.Module):
+    """Stock PyTorch-ROCm path (MIOpen convs), bf16 channels-last: comparison baseline (b).
+
+    BN is kept as a separate op (as a user of stock PyTorch would run a torchvision model in
+    eval mode); ``fold=True`` folds BN into the conv weights to give the eager path the same
+    algorithmic advantage the fused path has.
+    """
+
+    def __init__(self, params: Dict[str, torch.Tensor], device, dtype=torch.bfloat16, fold: bool = True):
+        super().__init__()
+        self.specs = {s.name: s for s in conv_specs()}
+        self.fold = fold
+        self.dtype = dtype
+        self.w: Dict[str, torch.Tensor] = {}
+        self.sb: Dict[str, Tuple[torch.Tensor, torch.Tensor]] = {}
+        for s in conv_specs():
+            w = params[s.name + ".w"]
+            scale, bias = fold_bn(params, s.name)
+            if fold:
+                w = w * scale.view(-1, 1, 1, 1)
+            self.w[s.name] = w.to(device=device, dtype=dtype).contiguous(memory_format=torch.channels_last)
+            self.sb[s.name] = (scale.to(device=device, dtype=dtype), bias.to(device=device, dtype=dtype))
+        self.fc_w = params["fc.w"].to(device=device, dtype=dtype)
+        self.fc_b = params["fc.b"].to(device=device, dtype=dtype)
+        self.mean = torch.tensor(IMAGENET_MEAN, device=device, dtype=torch.float32)
+        self.inv_std = 1.0 / torch.tensor(IMAGENET_STD, device=device, dtype=torch.float32)
+
+    def _cbr(self, x, name, relu=True, residual=None):
+        s = self.specs[name]
+        y = F.conv2d(x, self.w[name], stride=s.stride, padding=s.pad)
+        scale, bias = self.sb[name]
+        if self.fold:
+            y = y + bias.view(1, -1, 1, 1)
+        else:
+            y = y * scale.view(1, -1, 1, 1) + bias.view(1, -1, 1, 1)
+        if residual is not None:
+            y = y + residual
+        return F.relu(y) if relu else y
+
+    @torch.no_grad()
+    def forward(self, images_u8_nhwc: torch.Tensor) -> torch.Tensor:
+        x = ((images_u8_nhwc.float() - self.mean) * self.inv_std).to(self.dtype)
+        x = x.permute(0, 3, 1, 2)  # NCHW view of NHWC memory == channels_last
+        x = self._cbr(x, "stem")
+        x = F.max_pool2d(x, 3, 2, 1)
+        for si, (nblocks, _m, _c, _s) in enumerate(STAGES):
+            for bi in range(nblocks):
+                p = f"layer{si + 1}.{bi}"
+                identity = self._cbr(x, p + ".down", relu=False) if bi == 0 else x
+                y = self._cbr(x, p + ".conv1")
+                y = self._cbr(y, p + ".conv2")
+                x = self._cbr(y, p + ".conv3", residual=identity)
+        x = x.mean(dim=(2, 3))
+        return F.linear(x, self.fc_w, self.fc_b)
+
+
+def conv_shapes(image_size: int = 224) -> List[Tuple[ConvSpec, int, int]]:
+    """(spec, H_in, H_out) for every conv, in execution order (square images)."""
+    out: List[Tuple[ConvSpec, int, int]] = []
+    block_in = cur = image_size
+    for s in conv_specs():
+        if s.name.endswith(".conv1"):
+            block_in = cur
+        hin = block_in if s.name.endswith(".down") else cur
+        ho = (hin + 2 * s.pad - s.k) // s.stride + 1
+        out.append((s, hin, ho))
+        if s.name == "stem":
+            cur = (ho + 2 - 3) // 2 + 1  # maxpool 3x3/2 pad 1
+        elif not s.name.endswith(".down"):
+            cur = ho
+    return out
+
+
+def resnet50_flops_per_image(image_size: int = 224) -> float:
+    """2*MACs of all convs + FC (BN folded away)."""
+    total = 0.0
+    for s, _hin, ho in conv_shapes(image_size):
+        total += 2.0 * ho * ho * s.cout * s.cin * s.k * s.k
+    return total + 2.0 * 2048 * NUM_CLASSES
+
+
+class ResNet50Fused:
+    """ResNet-50 on the hand-written CDNA4 kernels (``ops``), NHWC bf16, BN folded.
+
+    Per conv: weights pre-multiplied by the BN scale (bf16, ``[Cout][KH][KW][Cin]``), the BN
+    bias applied in fp32 in the GEMM epilogue together with the residual add and ReLU.  One
+    split-K workspace is shared by all layers (they run back-to-back on one stream), sized at
+    construction for ``max_batch`` so nothing is allocated inside a hipGraph capture besides
+    the activations (which the capture's private pool then owns).
+
+    ``tuning`` maps a layer name to an explicit ``(cfg, splitk)`` (see ``ops.autotune``);
+    layers without an entry use the C++ heuristic.
+    """
+
+    def __init__(self, params: Dict[str, torch.Tensor], device, max_batch: int = 256,
+                 tuning: Optional[Dict[str, Tuple[int, int]]] = None, image_size: int = 224):
+        from .. import ops
+
+        self.ops = ops
+        self.device = torch.device(device)
+        self.image_size = image_size
+        self.tuning = dict(tuning or {})
+        self.specs = {s.name: s for s in conv_specs()}
+        self.w: Dict[str, torch.Tensor] = {}
+        self.b: Dict[str, torch.Tensor] = {}
+        for s in conv_specs():
+            scale, bias = fold_bn(params, s.name)
+            w = params[s.name + ".w"] * scale.view(-1, 1, 1, 1)
+            self.w[s.name] = ops.pack_conv_weight(w).to(self.device)
+            self.b[s.name] = bias.to(device=self.device, dtype=torch.float32).contiguous()
+        self.fc_w = params["fc.w"].to(device=self.device, dtype=torch.bfloat16).contiguous()
+        self.fc_b = params["fc.b"].to(device=self.device, dtype=torch.float32).contiguous()
+        self.num_classes = self.fc_w.shape[0]
+        self.mean = IMAGENET_MEAN
+        self.std = IMAGENET_STD
+        self.max_batch = max_batch
+        self.workspace = torch.empty(self._workspace_bytes(max_batch) // 4 + 1, device=self.device,
+                                     dtype=torch.float32)
+
+    # -- planning ---------------------------------------------------------------------------
+    def layer_gemm_shapes(self, batch: int) -> List[Tuple[str, int, int, int]]:
+        """(name, M, N, K) of every conv + the FC at ``batch``."""
+        out = []
+        for s, _hin, ho in conv_shapes(self.image_size):
+            k = s.k * 32 if s.name == "stem" else s.k * s.k * s.cin
+            out.append((s.name, batch * ho * ho, s.cout, k))
+        out.append(("fc", batch, self.num_classes, 2048))
+        return out
+
+    def _plan(self, name: str, M: int, N: int, K: int) -> Tuple[int, int]:
+        if name in self.tuning:
+            return self.tuning[name]
+        return self.ops.gemm_heuristic(M, N, K)
+
+    def _workspace_bytes(self, batch: int) -> int:
+        need = 0
+        for b in sorted({1, 2, 4, 8, 16, 32, 64, 128, 256, batch}):
+            if b > batch:
+                continue
+            for name, M, N, K in self.layer_gemm_shapes(b):
+                _cfg, sk = self._plan(name, M, N, K)
+                if sk > 1:
+                    need = max(need, sk * M * N * 4)
+        return max(need, 1 << 20)
+
+    # -- forward ----------------------------------------------------------------------------
+    def _conv(self, x, name, act, residual=None):
+        s = self.specs[name]
+        cfg, sk = self.tuning.get(name, (0, 0))
+        return self.ops.conv2d_nhwc(x, self.w[name], self.b[name], kernel=s.k, stride=s.stride, pad=s.pad,
+                                    residual=residual, act=act, workspace=self.workspace, cfg=cfg, splitk=sk)
+
+    def forward(self, images_u8_nhwc: torch.Tensor) -> torch.Tensor:
+        """uint8 ``[B,H,W,3]`` on device -> bf16 logits ``[B, num_classes]``."""
+        ops = self.ops
+        B = images_u8_nhwc.shape[0]
+        if B > self.max_batch:
+            raise ValueError(f"batch {B} > max_batch {self.max_batch}")
+        x = ops.normalize_u8(images_u8_nhwc, self.mean, self.std)
+        x = self._conv(x, "stem", ops.ACT_RELU)
+        x = ops.maxpool2d_nhwc(x, 3, 2, 1)
+        for si, (nblocks, _m, _c, _s) in enumerate(STAGES):
+            for bi in range(nblocks):
+                p = f"layer{si + 1}.{bi}"
+                identity = self._conv(x, p + ".down", ops.ACT_NONE) if bi == 0 else x
+                y = self._conv(x, p + ".conv1", ops.ACT_RELU)
+                y = self._conv(y, p + ".conv2", ops.ACT_RELU)
+                x = self._conv(y, p + ".conv3", ops.ACT_RELU, residual=identity)
+        pooled = ops.avgpool_global_nhwc(x)
+        cfg, sk = self.tuning.get("fc", (0, 0))
+        return ops.gemm(pooled, self.fc_w, self.fc_b, workspace=self.workspace, cfg=cfg, splitk=sk)
+
+    __call__ = forward
+
+    def classify(self, images_u8_nhwc: torch.Tensor, k: int = 5):
+        """Fused head: logits -> softmax -> top-k.  Returns (probs fp32 [B,k], ids int32 [B,k])."""
+        logits = self.forward(images_u8_nhwc)
+        return self.ops.softmax_topk(logits, k)

@@ -1,0 +1,286 @@
+"""Tensor-level wrappers over the hand-written CDNA4 kernels (T5).
+
+Every op here runs the native HIP kernel on torch's current stream -- there is no eager
+fallback for CUDA tensors (a missing library raises :class:`NativeError`).  The plain-PyTorch
+oracles the kernels are tested against live in ``ops.reference``.
+
+Layouts: activations NHWC / row-major ``[rows][features]`` bf16; conv weights
+``[Cout][KH][KW][Cin]`` bf16 (see :func:`pack_conv_weight`); per-channel scale / bias fp32.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Tuple
+
+import torch
+
+from . import _lib
+from ._lib import NativeError, available, check, lib, stream_ptr
+
+ACT_NONE, ACT_RELU, ACT_GELU, ACT_TANH, ACT_SILU = 0, 1, 2, 3, 4
+_ACTS = {None: 0, "none": 0, "relu": 1, "gelu": 2, "tanh": 3, "silu": 4}
+
+__all__ = [
+    "NativeError",
+    "available",
+    "lib",
+    "conv2d_nhwc",
+    "gemm",
+    "normalize_u8",
+    "maxpool2d_nhwc",
+    "avgpool_global_nhwc",
+    "bn_act",
+    "softmax_topk",
+    "softmax_rows",
+    "pack_conv_weight",
+    "conv_out_hw",
+    "gemm_heuristic",
+]
+
+
+def _act(a) -> int:
+    if isinstance(a, int):
+        return a
+    return _ACTS[a]
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _need(t: torch.Tensor, name: str, dtype: torch.dtype, device: torch.device) -> None:
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if t.device != device:
+        raise ValueError(f"{name}: expected device {device}, got {t.device}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+
+
+def conv_out_hw(h: int, w: int, k: int, stride: int, pad: int) -> Tuple[int, int]:
+    return (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
+
+
+def pack_conv_weight(w_oihw: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor:
+    """OIHW (PyTorch) -> ``[Cout][KH][KW][Cin]``.  Cin == 3 (image stem) is padded to 4 and KW to
+    8 so one 16-byte chunk of the K dimension is two 4-channel taps (the kernel's stem mode)."""
+    co, ci, kh, kw = w_oihw.shape
+    w = w_oihw.permute(0, 2, 3, 1)
+    if ci == 3 and kh > 1:
+        w = torch.nn.functional.pad(w, (0, 1, 0, 8 - kw))  # Cin 3->4, KW -> 8
+    return w.contiguous().to(dtype)
+
+
+def _workspace_args(ws: Optional[torch.Tensor]):
+    if ws is None:
+        return None, 0
+    return ws.data_ptr(), ws.numel() * ws.element_size()
+
+
+def conv2d_nhwc(
+    x: torch.Tensor,
+    w: torch.Tensor,
+    bias: Optional[torch.Tensor] = None,
+    *,
+    kernel: int,
+    stride: int = 1,
+    pad: int = 0,
+    scale: Optional[torch.Tensor] = None,
+    residual: Optional[torch.Tensor] = None,
+    act=ACT_NONE,
+    out: Optional[torch.Tensor] = None,
+    workspace: Optional[torch.Tensor] = None,
+    cfg: int = 0,
+    splitk: int = 0,
+) -> torch.Tensor:
+    """``act(conv(x, w) * scale + bias (+ residual))`` with x NHWC bf16 and w packed
+    ``[Cout][KH][KW][Cin]`` (stem: ``[Cout][KH][8][4]``)."""
+    dev = x.device
+    _need(x, "x", torch.bfloat16, dev)
+    _need(w, "w", torch.bfloat16, dev)
+    B, H, W, C = x.shape
+    cout = w.shape[0]
+    kh = kw = kernel
+    if C == 4 and kernel > 1:
+        if tuple(w.shape) != (cout, kh, 8, 4):
+            raise ValueError(f"stem weight must be [Cout,{kh},8,4], got {tuple(w.shape)}")
+    elif tuple(w.shape) != (cout, kh, kw, C):
+        raise ValueError(f"weight shape {tuple(w.shape)} != [{cout},{kh},{kw},{C}]")
+    if cout % 8:
+        raise ValueError("Cout must be a multiple of 8")
+    ho, wo = conv_out_hw(H, W, kernel, stride, pad)
+    for name, t in (("bias", bias), ("scale", scale)):
+        if t is not None:
+            _need(t, name, torch.float32, dev)
+            if t.numel() != cout:
+                raise ValueError(f"{name} must have {cout} elements")
+    if residual is not None:
+        _need(residual, "residual", torch.bfloat16, dev)
+        if tuple(residual.shape) != (B, ho, wo, cout):
+            raise ValueError(f"residual shape {tuple(residual.shape)} != {(B, ho, wo, cout)}")
+    if out is None:
+        out = torch.empty(B, ho, wo, cout, device=dev, dtype=torch.bfloat16)
+    else:
+        _need(out, "out", torch.bfloat16, dev)
+        if tuple(out.shape) != (B, ho, wo, cout):
+            raise ValueError("out has wrong shape")
+    wsp, wsb = _workspace_args(workspace)
+    rc = lib().mls_conv2d(
+        x.data_ptr(), w.data_ptr(), _ptr(scale), _ptr(bias), _ptr(residual), out.data_ptr(), wsp, wsb,
+        B, H, W, C, cout, kh, kw, stride, pad, _act(act), cfg, splitk, stream_ptr(dev),
+    )
+    check(rc, "mls_conv2d")
+    return out
+
+
+def gemm(
+    a: torch.Tensor,
+    w: torch.Tensor,
+    bias: Optional[torch.Tensor] = None,
+    *,
+    scale: Optional[torch.Tensor] = None,
+    residual: Optional[torch.Tensor] = None,
+    act=ACT_NONE,
+    out: Optional[torch.Tensor] = None,
+    workspace: Optional[torch.Tensor] = None,
+    cfg: int = 0,
+    splitk: int = 0,
+) -> torch.Tensor:
+    """``act(a @ w.T * scale + bias (+ residual))``; a ``[M,K]``, w ``[N,K]`` (nn.Linear layout)."""
+    dev = a.device
+    _need(a, "a", torch.bfloat16, dev)
+    _need(w, "w", torch.bfloat16, dev)
+    M, K = a.shape
+    N, K2 = w.shape
+    if K != K2:
+        raise ValueError(f"K mismatch {K} vs {K2}")
+    if N % 8 or K % 8:
+        raise ValueError("N and K must be multiples of 8")
+    for name, t in (("bias", bias), ("scale", scale)):
+        if t is not None:
+            _need(t, name, torch.float32, dev)
+            if t.numel() != N:
+                raise ValueError(f"{name} must have {N} elements")
+    if residual is not None:
+        _need(residual, "residual", torch.bfloat16, dev)
+        if tuple(residual.shape) != (M, N):
+            raise ValueError("residual must be [M, N]")
+    if out is None:
+        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    else:
+        _need(out, "out", torch.bfloat16, dev)
+        if tuple(out.shape) != (M, N):
+            raise ValueError("out must be [M, N]")
+    wsp, wsb = _workspace_args(workspace)
+    rc = lib().mls_gemm(
+        a.data_ptr(), w.data_ptr(), _ptr(scale), _ptr(bias), _ptr(residual), out.data_ptr(), wsp, wsb,
+        M, N, K, _act(act), cfg, splitk, stream_ptr(dev),
+    )
+    check(rc, "mls_gemm")
+    return out
+
+
+def gemm_heuristic(M: int, N: int, K: int) -> Tuple[int, int]:
+    cfg, sk = ctypes.c_int(0), ctypes.c_int(0)
+    lib().mls_gemm_heuristic(M, N, K, ctypes.byref(cfg), ctypes.byref(sk))
+    return cfg.value, sk.value
+
+
+_MEAN_STD_CACHE = {}
+
+
+def normalize_u8(images: torch.Tensor, mean, std, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """uint8 ``[B,H,W,3]`` -> bf16 ``[B,H,W,4]`` = ((x - mean) / std, 0)."""
+    dev = images.device
+    _need(images, "images", torch.uint8, dev)
+    B, H, W, C = images.shape
+    if C != 3:
+        raise ValueError("expected 3-channel images")
+    if out is None:
+        out = torch.empty(B, H, W, 4, device=dev, dtype=torch.bfloat16)
+    else:
+        _need(out, "out", torch.bfloat16, dev)
+        if tuple(out.shape) != (B, H, W, 4):
+            raise ValueError("out must be [B,H,W,4]")
+    m = (ctypes.c_float * 3)(*[float(v) for v in mean])
+    s = (ctypes.c_float * 3)(*[float(v) for v in std])
+    rc = lib().mls_normalize_u8(images.data_ptr(), out.data_ptr(), B * H * W, m, s, stream_ptr(dev))
+    check(rc, "mls_normalize_u8")
+    return out
+
+
+def maxpool2d_nhwc(x: torch.Tensor, k: int = 3, s: int = 2, p: int = 1, out: Optional[torch.Tensor] = None):
+    dev = x.device
+    _need(x, "x", torch.bfloat16, dev)
+    B, H, W, C = x.shape
+    ho, wo = conv_out_hw(H, W, k, s, p)
+    if out is None:
+        out = torch.empty(B, ho, wo, C, device=dev, dtype=torch.bfloat16)
+    rc = lib().mls_maxpool2d(x.data_ptr(), out.data_ptr(), B, H, W, C, k, s, p, stream_ptr(dev))
+    check(rc, "mls_maxpool2d")
+    return out
+
+
+def avgpool_global_nhwc(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    dev = x.device
+    _need(x, "x", torch.bfloat16, dev)
+    B, H, W, C = x.shape
+    if out is None:
+        out = torch.empty(B, C, device=dev, dtype=torch.bfloat16)
+    rc = lib().mls_avgpool_global(x.data_ptr(), out.data_ptr(), B, H * W, C, stream_ptr(dev))
+    check(rc, "mls_avgpool_global")
+    return out
+
+
+def bn_act(x: torch.Tensor, scale: torch.Tensor, bias: torch.Tensor, relu: bool = False, out=None) -> torch.Tensor:
+    """Standalone inference BatchNorm over the last (channel) dim (K3 unfused path)."""
+    dev = x.device
+    _need(x, "x", torch.bfloat16, dev)
+    _need(scale, "scale", torch.float32, dev)
+    _need(bias, "bias", torch.float32, dev)
+    C = x.shape[-1]
+    out = torch.empty_like(x) if out is None else out
+    rc = lib().mls_bn_act(x.data_ptr(), out.data_ptr(), scale.data_ptr(), bias.data_ptr(), x.numel() // C, C,
+                          int(relu), stream_ptr(dev))
+    check(rc, "mls_bn_act")
+    return out
+
+
+def softmax_topk(
+    x: torch.Tensor,
+    k: int,
+    *,
+    softmax: bool = True,
+    temperature: float = 1.0,
+    vals: Optional[torch.Tensor] = None,
+    idx: Optional[torch.Tensor] = None,
+) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Row-wise (softmax ->) top-k of a ``[rows, N]`` bf16/fp32 matrix; fp32 values, int32 ids."""
+    dev = x.device
+    if x.dtype not in (torch.bfloat16, torch.float32) or not x.is_contiguous():
+        raise TypeError("x must be contiguous bf16 or fp32")
+    rows, N = x.shape
+    if vals is None:
+        vals = torch.empty(rows, k, device=dev, dtype=torch.float32)
+    if idx is None:
+        idx = torch.empty(rows, k, device=dev, dtype=torch.int32)
+    rc = lib().mls_softmax_topk(x.data_ptr(), 0 if x.dtype == torch.bfloat16 else 1, vals.data_ptr(), idx.data_ptr(),
+                                rows, N, k, int(softmax), float(temperature), stream_ptr(dev))
+    check(rc, "mls_softmax_topk")
+    return vals, idx
+
+
+def softmax_rows(x: torch.Tensor, mask: Optional[torch.Tensor] = None, rows_per_mask: int = 1, scale: float = 1.0,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``softmax(x * scale + mask)`` over the last dim; mask fp32 ``[rows/rows_per_mask, N]``."""
+    dev = x.device
+    _need(x, "x", torch.bfloat16, dev)
+    N = x.shape[-1]
+    rows = x.numel() // N
+    if mask is not None:
+        _need(mask, "mask", torch.float32, dev)
+    out = torch.empty_like(x) if out is None else out
+    rc = lib().mls_softmax_rows(x.data_ptr(), out.data_ptr(), _ptr(mask), rows, N, rows_per_mask, float(scale),
+                                stream_ptr(dev))
+    check(rc, "mls_softmax_rows")
+    return out

@@ -1,0 +1,108 @@
+"""ctypes binding to ``_native/libmls_kernels.so`` (the C ABI of ``csrc/*.hip``).
+
+The library links ``libamdhip64.so.7``; torch-ROCm has already loaded its own copy with the
+same soname, so the loader reuses it and our launches share torch's HIP runtime, streams and
+graph capture (never load a second HIP runtime).  ``import torch`` therefore
+happens before the ``CDLL``.
+
+There is deliberately no silent fallback: if the library is missing on a machine that has a
+GPU, :func:`lib` raises.  Callers that want the stock-PyTorch path ask for it explicitly
+(``BACKEND=eager``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional
+
+import torch  # noqa: F401  (must load the HIP runtime first)
+
+from . import build as _build
+
+_c = ctypes
+_LOCK = threading.Lock()
+_LIB: Optional[ctypes.CDLL] = None
+
+P = _c.c_void_p
+I = _c.c_int
+L = _c.c_long
+F = _c.c_float
+SZ = _c.c_size_t
+FP = _c.POINTER(_c.c_float)
+
+_SIGS = {
+    "mls_conv2d": [P, P, P, P, P, P, P, SZ, I, I, I, I, I, I, I, I, I, I, I, I, P],
+    "mls_gemm": [P, P, P, P, P, P, P, SZ, I, I, I, I, I, I, P],
+    "mls_gemm_heuristic": [I, I, I, _c.POINTER(I), _c.POINTER(I)],
+    "mls_gemm_num_cfgs": [],
+    "mls_normalize_u8": [P, P, L, FP, FP, P],
+    "mls_maxpool2d": [P, P, I, I, I, I, I, I, I, P],
+    "mls_avgpool_global": [P, P, I, I, I, P],
+    "mls_bn_act": [P, P, P, P, L, I, I, P],
+    "mls_softmax_topk": [P, I, P, P, I, I, I, I, F, P],
+    "mls_softmax_rows": [P, P, P, I, I, I, F, P],
+}
+_OPTIONAL_SIGS: dict = {}
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def register_signatures(sigs: dict, optional: bool = False) -> None:
+    """Extension point for kernel modules added later (attention, norms, collectives...)."""
+    (_OPTIONAL_SIGS if optional else _SIGS).update(sigs)
+    if _LIB is not None:
+        _bind(_LIB)
+
+
+def _bind(lib: ctypes.CDLL) -> None:
+    for name, argtypes in list(_SIGS.items()) + list(_OPTIONAL_SIGS.items()):
+        fn = getattr(lib, name, None)
+        if fn is None:
+            if name in _SIGS:
+                raise NativeError(f"{name} missing from {lib._name}; rebuild the kernels")
+            continue
+        fn.argtypes = argtypes
+        fn.restype = _c.c_int
+
+
+def lib(build_if_missing: bool = True) -> ctypes.CDLL:
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    with _LOCK:
+        if _LIB is not None:
+            return _LIB
+        path = _build.lib_path()
+        if build_if_missing:
+            # incremental: a no-op when the stamp matches the sources
+            try:
+                path = _build.build()
+            except Exception as e:  # toolchain missing -> only OK if the .so already exists
+                if not os.path.exists(path):
+                    raise NativeError(f"native kernels unavailable and build failed: {e}") from e
+        if not os.path.exists(path):
+            raise NativeError(f"native kernel library not built: {path}")
+        handle = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        _bind(handle)
+        _LIB = handle
+        return _LIB
+
+
+def available() -> bool:
+    try:
+        lib()
+        return True
+    except Exception:
+        return False
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise NativeError(f"{what} failed with status {rc}")
+
+
+def stream_ptr(device: Optional[torch.device] = None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,137 @@
+"""Per-shape tile/split-K autotuner for the implicit-GEMM conv / GEMM kernel (a "find" step).
+
+For every ResNet-50 layer at a given batch, times each (tile cfg, split-K) candidate with
+HIP events on random data and keeps the fastest; results are cached as JSON keyed by
+(device arch, batch) so serving start-up does the search once per machine.  Also reports the
+stock PyTorch-ROCm (MIOpen) time of the same conv for comparison.
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+CACHE_DIR = os.environ.get("MLS_TUNE_DIR", os.path.join(os.path.dirname(os.path.abspath(__file__)), "_native", "tune"))
+CANDIDATES: List[Tuple[int, int]] = [(c, s) for c in (1, 2, 3, 4) for s in (1, 2, 4, 8)]
+
+
+def _time(fn, iters: int = 20, warmup: int = 3) -> float:
+    for _ in range(warmup):
+        fn()
+    start = torch.cuda.Event(enable_timing=True)
+    end = torch.cuda.Event(enable_timing=True)
+    start.record()
+    for _ in range(iters):
+        fn()
+    end.record()
+    end.synchronize()
+    return start.elapsed_time(end) / iters
+
+
+def tune_resnet50(batch: int, device="cuda:0", iters: int = 20, compare_torch: bool = True,
+                  candidates: Optional[List[Tuple[int, int]]] = None) -> Dict[str, dict]:
+    from . import conv2d_nhwc, gemm, pack_conv_weight
+    from ..models.resnet import conv_shapes
+
+    dev = torch.device(device)
+    ws = torch.empty(256 << 20, device=dev, dtype=torch.float32)
+    results: Dict[str, dict] = {}
+    cands = candidates or CANDIDATES
+    for s, hin, ho in conv_shapes():
+        cin = 4 if s.name == "stem" else s.cin
+        x = torch.randn(batch, hin, hin, cin, device=dev).to(torch.bfloat16)
+        w = (torch.randn(s.cout, s.cin, s.k, s.k, device=dev) * 0.05).to(torch.bfloat16)
+        wp = pack_conv_weight(w)
+        bias = torch.randn(s.cout, device=dev)
+        res = torch.randn(batch, ho, ho, s.cout, device=dev).to(torch.bfloat16) if s.name.endswith("conv3") else None
+        out = torch.empty(batch, ho, ho, s.cout, device=dev, dtype=torch.bfloat16)
+        k = s.k * 32 if s.name == "stem" else s.k * s.k * s.cin
+        flops = 2.0 * batch * ho * ho * s.cout * s.cin * s.k * s.k
+        best = (1e9, 0, 0)
+        tried = {}
+        for cfg, sk in [(0, 0)] + cands:
+            if sk > 1 and k // sk < 128:
+                continue
+
+            def run(cfg=cfg, sk=sk):
+                conv2d_nhwc(x, wp, bias, kernel=s.k, stride=s.stride, pad=s.pad, residual=res, act=1, out=out,
+                            workspace=ws, cfg=cfg, splitk=sk)
+
+            t = _time(run, iters)
+            tried[f"{cfg},{sk}"] = round(t * 1e3, 2)
+            if (cfg, sk) != (0, 0) and t < best[0]:
+                best = (t, cfg, sk)
+        entry = {"M": batch * ho * ho, "N": s.cout, "K": k, "best_cfg": best[1], "best_splitk": best[2],
+                 "best_us": round(best[0] * 1e3, 2), "heuristic_us": tried["0,0"],
+                 "tflops": round(flops / (best[0] * 1e-3) / 1e12, 1)}
+        if compare_torch:
+            xt = x[..., :3] if s.name == "stem" else x
+            xt = xt.permute(0, 3, 1, 2)
+            wt = w.contiguous(memory_format=torch.channels_last)
+            bt = bias.to(torch.bfloat16).view(1, -1, 1, 1)
+
+            def trun():
+                y = F.conv2d(xt, wt, stride=s.stride, padding=s.pad) + bt
+                return torch.relu(y)
+
+            entry["torch_us"] = round(_time(trun, iters) * 1e3, 2)
+        results[s.name] = entry
+    # FC
+    a = torch.randn(batch, 2048, device=dev).to(torch.bfloat16)
+    w = torch.randn(1000, 2048, device=dev).to(torch.bfloat16)
+    b = torch.randn(1000, device=dev)
+    best = (1e9, 0, 0)
+    for cfg, sk in cands:
+        t = _time(lambda: gemm(a, w, b, workspace=ws, cfg=cfg, splitk=sk), iters)
+        if t < best[0]:
+            best = (t, cfg, sk)
+    results["fc"] = {"M": batch, "N": 1000, "K": 2048, "best_cfg": best[1], "best_splitk": best[2],
+                     "best_us": round(best[0] * 1e3, 2)}
+    return results
+
+
+def cache_path(batch: int) -> str:
+    arch = "gfx950"
+    try:
+        arch = torch.cuda.get_device_properties(0).gcnArchName.split(":")[0]
+    except Exception:
+        pass
+    return os.path.join(CACHE_DIR, f"resnet50_{arch}_b{batch}.json")
+
+
+def load_or_tune(batch: int, device="cuda:0") -> Dict[str, Tuple[int, int]]:
+    path = cache_path(batch)
+    if os.path.exists(path):
+        with open(path) as f:
+            data = json.load(f)
+    else:
+        data = tune_resnet50(batch, device, compare_torch=False)
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(data, f, indent=1)
+    return {k: (v["best_cfg"], v["best_splitk"]) for k, v in data.items()}
+
+
+if __name__ == "__main__":
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--out", default="")
+    args = ap.parse_args()
+    t0 = time.time()
+    res = tune_resnet50(args.batch)
+    tot_best = sum(v["best_us"] for v in res.values())
+    tot_heur = sum(v.get("heuristic_us", v["best_us"]) for v in res.values())
+    tot_torch = sum(v.get("torch_us", 0) for v in res.values())
+    for name, v in res.items():
+        print(json.dumps({"layer": name, **v}))
+    print(json.dumps({"sum_best_us": round(tot_best, 1), "sum_heuristic_us": round(tot_heur, 1),
+                      "sum_torch_us": round(tot_torch, 1), "tune_s": round(time.time() - t0, 1)}))
+    if args.out:
+        with open(args.out, "w") as f:
+            json.dump(res, f, indent=1)

@@ -1,0 +1,108 @@
+// Shared device helpers for the MI355X (gfx950 / CDNA4) kernels of mlmicroservicetemplate_amd.
+// Wave64 everywhere; bf16 storage, fp32 accumulate.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#define MLS_DEV __device__ __forceinline__
+
+// error codes returned by every launcher (0 = launched)
+enum MlsStatus : int {
+  MLS_OK = 0,
+  MLS_BAD_ARG = 1001,
+  MLS_UNSUPPORTED = 1002,
+};
+
+MLS_DEV float bf2f(bf16 x) { return (float)x; }
+MLS_DEV bf16 f2bf(float x) { return (bf16)x; }
+
+// ---- buffer (SRD) loads: hardware range check returns 0 for an out-of-range offset, which is
+// how the implicit-GEMM gather zero-fills conv padding without branches or pointer selects.
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr int OOB = (int)0x80000000;  // any offset >= num_records reads as zero
+MLS_DEV rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+MLS_DEV uint4 bload16(rsrc_t r, int byte_off) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+}
+MLS_DEV uint2 bload8(rsrc_t r, int byte_off) {
+  return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(r, byte_off, 0, 0));
+}
+MLS_DEV uint32_t clamp_bytes(size_t n) { return n > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)n; }
+
+MLS_DEV uint4 ld16(const void* p) { return *reinterpret_cast<const uint4*>(p); }
+MLS_DEV void st16(void* p, uint4 v) { *reinterpret_cast<uint4*>(p) = v; }
+
+MLS_DEV void unpack8(uint4 v, float (&f)[8]) {
+  bf16x8 b = __builtin_bit_cast(bf16x8, v);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f[i] = (float)b[i];
+}
+MLS_DEV uint4 pack8(const float (&f)[8]) {
+  bf16x8 b;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) b[i] = (bf16)f[i];
+  return __builtin_bit_cast(uint4, b);
+}
+
+// ---- wave64 reductions ----
+MLS_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+MLS_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// block-wide sum for blockDim.x <= 1024 (multiple of 64); `red` needs >= 16 floats of LDS.
+MLS_DEV float block_sum(float v, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = lane < nw ? red[lane] : 0.f;
+  return wave_sum(t);
+}
+MLS_DEV float block_max(float v, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_max(v);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = lane < nw ? red[lane] : -INFINITY;
+  return wave_max(t);
+}
+
+// Bijective XCD-aware remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"):
+// blocks b, b+8, b+16 ... share an XCD; give each XCD a contiguous range of logical tiles so
+// neighbouring tiles (which share operand panels) hit the same L2.
+MLS_DEV int xcd_remap(int bid, int nwg) {
+  if (nwg <= 8) return bid;
+  const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, idx = bid >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+MLS_DEV float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+MLS_DEV float silu(float x) { return x / (1.f + __expf(-x)); }
+
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_TANH = 3, ACT_SILU = 4 };
+MLS_DEV float apply_act(float v, int act) {
+  switch (act) {
+    case ACT_RELU: return fmaxf(v, 0.f);
+    case ACT_GELU: return gelu_erf(v);
+    case ACT_TANH: return tanhf(v);
+    case ACT_SILU: return silu(v);
+    default: return v;
+  }
+}

@@ -1,0 +1,449 @@
+// K1 + K2 of SURVEY.md §2.E.1: implicit-GEMM NHWC convolution and plain GEMM on gfx950 MFMA,
+// with a fused epilogue  y = act(acc * scale[n] + bias[n] (+ residual[m][n])).
+//
+// GEMM view:  M = B*Ho*Wo (or rows),  N = Cout,  K = KH*KW*Cin,  out[M][N] row-major (= NHWC).
+//   A[m][k] = x[b][oh*s - p + kh][ow*s - p + kw][c]   with k = (kh*KW + kw)*Cin + c
+//   B[k][n] = w[n][k]                                  (weights stored [Cout][KH][KW][Cin])
+//
+// Design (MI355X-first, see /opt/skills/guides/cdna_hip_programming.md §5):
+//  * 256 threads = 4 waves in a 2x2 wave grid; each wave owns a (BM/2)x(BN/2) sub-tile built
+//    from v_mfma_f32_16x16x32_bf16 (the bf16 shape that holds the higher clock on random data).
+//  * BK = 64: one 128-byte row per tile row.  LDS images are [rows][8 x 16 B] with the 16-B
+//    chunk XOR-swizzled by (row & 7): the MFMA fragment reads (ds_read_b128, 16 rows x 1 chunk
+//    per lane group) are bank-conflict-free (checked exhaustively against the gfx950 lane groups).
+//  * register-staged double buffer with the async-STAGE split (T14): global loads of tile k+1
+//    are issued before the MFMAs of tile k and written to the other LDS buffer after them; one
+//    barrier per K-step.  Register staging (not LDS-DMA) because the implicit-GEMM gather needs
+//    per-lane zero-fill for the conv padding.
+//  * the im2col gather is never materialised: for Cin % 64 == 0 a whole BK step lies inside one
+//    filter tap, so the tap decomposition is wave-uniform scalar work per K-step.
+//  * stem mode (Cin padded 3->4, KW padded 7->8 in the weights): one 16-B chunk = 2 taps x 4 ch.
+//  * epilogue through LDS: accumulators are parked as fp32, then every thread emits whole
+//    16-B rows (8 channels) so residual reads and output writes are coalesced dwordx4.
+//  * split-K for the small-M / large-K layers (ResNet layer3/4, FC): fp32 slabs + a separate
+//    reduce-epilogue kernel (deterministic; the launch boundary is captured in the hipGraph).
+//  * XCD-aware bijective block remap so neighbouring tiles share an XCD's L2.
+#include "common.h"
+
+namespace {
+
+constexpr int BK = 64;
+constexpr int NTHREADS = 256;
+
+enum ConvMode : int { MODE_GENERIC = 0, MODE_1X1 = 1, MODE_STEM = 2 };
+
+struct ConvArgs {
+  const bf16* x;
+  const bf16* w;
+  const float* scale;  // [N] or nullptr
+  const float* bias;   // [N] or nullptr
+  const bf16* res;     // [M][ldr] or nullptr
+  bf16* out;           // [M][ldo]
+  float* ws;           // split-K slabs [splitk][M][N]
+  int B, H, W, Cin, Ho, Wo, N, KH, KW, stride, pad;
+  int M, K;            // K = reduction length == weight row stride
+  int act;
+  int splitk, kchunk;
+  int ldo, ldr;
+  uint32_t x_bytes, w_bytes;  // extents of x and w for the buffer-load range check
+};
+
+template <int BM, int BN, int MODE>
+__global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a) {
+  constexpr int WN = 2;
+  constexpr int WTM = BM / 2, WTN = BN / 2;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int AROWS = BM / 32, BROWS = BN / 32;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
+  constexpr int C_LD = BN + 4;
+  constexpr int EPI_BYTES = BM * C_LD * 4;
+  constexpr int LDS_BYTES = (2 * STAGE_BYTES > EPI_BYTES) ? 2 * STAGE_BYTES : EPI_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+
+  const int ntn = (a.N + BN - 1) / BN;
+  int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = t % a.splitk;
+  t /= a.splitk;
+  const int tn = t % ntn, tmi = t / ntn;
+  const int m0 = tmi * BM, n0 = tn * BN;
+  const int kbeg = split * a.kchunk;
+  const int kend = min(a.K, kbeg + a.kchunk);
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+
+  const int kc = tid & 7;     // 16-B chunk of the 128-B K-row this thread stages
+  const int rbase = tid >> 3; // first staged row; rows rbase + 32*i
+
+  // ---- per-row im2col bases (fixed for the whole K loop) ----
+  int a_off[AROWS], a_ih[AROWS], a_iw[AROWS];
+  const int HoWo = a.Ho * a.Wo;
+#pragma unroll
+  for (int i = 0; i < AROWS; ++i) {
+    const int m = m0 + rbase + 32 * i;
+    if (m < a.M) {
+      const int b = m / HoWo;
+      const int rem = m - b * HoWo;
+      const int oh = rem / a.Wo;
+      const int ow = rem - oh * a.Wo;
+      if (MODE == MODE_1X1) {
+        a_off[i] = ((b * a.H + oh * a.stride) * a.W + ow * a.stride) * a.Cin;
+        a_ih[i] = 0;
+        a_iw[i] = 0;
+      } else {
+        a_off[i] = b * a.H * a.W * a.Cin;
+        a_ih[i] = oh * a.stride - a.pad;
+        a_iw[i] = ow * a.stride - a.pad;
+      }
+    } else {
+      a_off[i] = -1;
+      a_ih[i] = -(1 << 28);
+      a_iw[i] = -(1 << 28);
+    }
+  }
+  int b_row[BROWS];
+#pragma unroll
+  for (int j = 0; j < BROWS; ++j) {
+    const int n = n0 + rbase + 32 * j;
+    b_row[j] = n < a.N ? n : -1;
+  }
+
+  uint4 ra[AROWS], rb[BROWS];
+  // SRDs over the activation and weight tensors: padding / tails become OOB offsets -> 0
+  const rsrc_t xr = make_rsrc(a.x, a.x_bytes);
+  const rsrc_t wr = make_rsrc(a.w, a.w_bytes);
+
+  auto gload = [&](int k0) {
+    const int k = k0 + kc * 8;
+    const bool kin = k < kend;
+    if (MODE == MODE_1X1) {
+#pragma unroll
+      for (int i = 0; i < AROWS; ++i)
+        ra[i] = bload16(xr, (kin && a_off[i] >= 0) ? (a_off[i] + k) * 2 : OOB);
+    } else if (MODE == MODE_GENERIC) {
+      // whole BK step inside one tap (Cin % 64 == 0): tap math is uniform
+      const int tap = k0 / a.Cin;
+      const int c = k0 - tap * a.Cin + kc * 8;
+      const int kh = tap / a.KW;
+      const int kw = tap - kh * a.KW;
+#pragma unroll
+      for (int i = 0; i < AROWS; ++i) {
+        const int ih = a_ih[i] + kh, iw = a_iw[i] + kw;
+        const bool ok = kin && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+        ra[i] = bload16(xr, ok ? (a_off[i] + (ih * a.W + iw) * a.Cin + c) * 2 : OOB);
+      }
+    } else {  // MODE_STEM: Cin == 4, weights [N][KH][8][4]; chunk = taps (kw, kw+1) of row kh
+      const int kh = k >> 5;
+      const int kw = (k & 31) >> 2;
+#pragma unroll
+      for (int i = 0; i < AROWS; ++i) {
+        const int ih = a_ih[i] + kh, iw = a_iw[i] + kw;
+        const bool rowok = kin && (unsigned)ih < (unsigned)a.H;
+        const bool ok0 = rowok && (unsigned)iw < (unsigned)a.W && kw < a.KW;
+        const bool ok1 = rowok && (unsigned)(iw + 1) < (unsigned)a.W && kw + 1 < a.KW;
+        const int off = (a_off[i] + (ih * a.W + iw) * 4) * 2;
+        const uint2 lo = bload8(xr, ok0 ? off : OOB);
+        const uint2 hi = bload8(xr, ok1 ? off + 8 : OOB);
+        ra[i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < BROWS; ++j)
+      rb[j] = bload16(wr, (kin && b_row[j] >= 0) ? (b_row[j] * a.K + k) * 2 : OOB);
+  };
+
+  auto sstore = [&](int s) {
+    uint4* As = reinterpret_cast<uint4*>(smem + s * STAGE_BYTES);
+    uint4* Bs = reinterpret_cast<uint4*>(smem + s * STAGE_BYTES + A_BYTES);
+#pragma unroll
+    for (int i = 0; i < AROWS; ++i) {
+      const int r = rbase + 32 * i;
+      As[r * 8 + (kc ^ (r & 7))] = ra[i];
+    }
+#pragma unroll
+    for (int j = 0; j < BROWS; ++j) {
+      const int r = rbase + 32 * j;
+      Bs[r * 8 + (kc ^ (r & 7))] = rb[j];
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) {
+    gload(kbeg);
+    sstore(0);
+  }
+  __syncthreads();
+
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload(kbeg + (kt + 1) * BK);
+    const uint4* As = reinterpret_cast<const uint4*>(smem + cur * STAGE_BYTES);
+    const uint4* Bs = reinterpret_cast<const uint4*>(smem + cur * STAGE_BYTES + A_BYTES);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ch = fq + 4 * kk;
+      bf16x8 af[TM], bfv[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int r = wm * WTM + i * 16 + fr;
+        af[i] = __builtin_bit_cast(bf16x8, As[r * 8 + (ch ^ (r & 7))]);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int r = wn * WTN + j * 16 + fr;
+        bfv[j] = __builtin_bit_cast(bf16x8, Bs[r * 8 + (ch ^ (r & 7))]);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) sstore(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: park fp32 accumulators in LDS, then emit 16-B rows ----
+  float* Cs = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * WTM + i * 16 + fq * 4 + r;
+        const int col = wn * WTN + j * 16 + fr;
+        Cs[row * C_LD + col] = acc[i][j][r];
+      }
+  __syncthreads();
+
+  constexpr int CPR = BN / 8;
+  for (int q = tid; q < BM * CPR; q += NTHREADS) {
+    const int row = q / CPR, c8 = q - (q / CPR) * CPR;
+    const int m = m0 + row, n = n0 + c8 * 8;
+    if (m >= a.M || n >= a.N) continue;
+    const float4 v0 = *reinterpret_cast<const float4*>(Cs + row * C_LD + c8 * 8);
+    const float4 v1 = *reinterpret_cast<const float4*>(Cs + row * C_LD + c8 * 8 + 4);
+    if (a.splitk > 1) {
+      float* dst = a.ws + ((size_t)split * a.M + m) * a.N + n;
+      *reinterpret_cast<float4*>(dst) = v0;
+      *reinterpret_cast<float4*>(dst + 4) = v1;
+      continue;
+    }
+    float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+    if (a.scale) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= a.scale[n + e];
+    }
+    if (a.bias) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += a.bias[n + e];
+    }
+    if (a.res) {
+      float r[8];
+      unpack8(ld16(a.res + (size_t)m * a.ldr + n), r);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += r[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], a.act);
+    st16(a.out + (size_t)m * a.ldo + n, pack8(v));
+  }
+}
+
+// sum split-K slabs + epilogue; one thread per 8 outputs
+__global__ __launch_bounds__(256) void splitk_epilogue_kernel(const ConvArgs a) {
+  const int nc = a.N / 8;
+  const long total = (long)a.M * nc;
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
+    const int m = (int)(q / nc), n = (int)(q - (q / nc) * nc) * 8;
+    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int s = 0; s < a.splitk; ++s) {
+      const float* src = a.ws + ((size_t)s * a.M + m) * a.N + n;
+      const float4 p0 = *reinterpret_cast<const float4*>(src);
+      const float4 p1 = *reinterpret_cast<const float4*>(src + 4);
+      v[0] += p0.x; v[1] += p0.y; v[2] += p0.z; v[3] += p0.w;
+      v[4] += p1.x; v[5] += p1.y; v[6] += p1.z; v[7] += p1.w;
+    }
+    if (a.scale) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= a.scale[n + e];
+    }
+    if (a.bias) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += a.bias[n + e];
+    }
+    if (a.res) {
+      float r[8];
+      unpack8(ld16(a.res + (size_t)m * a.ldr + n), r);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += r[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], a.act);
+    st16(a.out + (size_t)m * a.ldo + n, pack8(v));
+  }
+}
+
+struct TileCfg {
+  int bm, bn;
+};
+constexpr TileCfg kCfgs[] = {{0, 0}, {128, 128}, {128, 64}, {64, 128}, {64, 64}};
+constexpr int kNumCfgs = 5;
+
+template <int MODE>
+void launch_mode(int cfg, dim3 grid, hipStream_t st, const ConvArgs& a) {
+  switch (cfg) {
+    case 1: hipLaunchKernelGGL((conv_gemm_kernel<128, 128, MODE>), grid, dim3(NTHREADS), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((conv_gemm_kernel<128, 64, MODE>), grid, dim3(NTHREADS), 0, st, a); break;
+    case 3: hipLaunchKernelGGL((conv_gemm_kernel<64, 128, MODE>), grid, dim3(NTHREADS), 0, st, a); break;
+    default: hipLaunchKernelGGL((conv_gemm_kernel<64, 64, MODE>), grid, dim3(NTHREADS), 0, st, a); break;
+  }
+}
+
+// Heuristic tile choice: fill 256 CUs x 2 resident blocks, penalise padding waste and small tiles.
+void choose_cfg(int M, int N, int K, int& cfg, int& splitk) {
+  const float tile_eff[kNumCfgs] = {0.f, 1.0f, 0.86f, 0.86f, 0.68f};
+  float best = -1.f;
+  int bc = 4;
+  for (int c = 1; c < kNumCfgs; ++c) {
+    const int bm = kCfgs[c].bm, bn = kCfgs[c].bn;
+    const long tm = (M + bm - 1) / bm, tn = (N + bn - 1) / bn, tiles = tm * tn;
+    const float pad = (float)M * N / ((float)tiles * bm * bn);
+    const long waves = (tiles + 511) / 512;
+    const float fill = (float)tiles / (float)(waves * 512);
+    const float score = tile_eff[c] * pad * (tiles >= 256 ? fill : fill * 0.5f);
+    if (score > best) {
+      best = score;
+      bc = c;
+    }
+  }
+  cfg = bc;
+  const long tiles = (long)((M + kCfgs[bc].bm - 1) / kCfgs[bc].bm) * ((N + kCfgs[bc].bn - 1) / kCfgs[bc].bn);
+  splitk = 1;
+  while (tiles * splitk < 384 && K / (splitk * 2) >= 256 && splitk < 8) splitk *= 2;
+}
+
+int launch_conv(ConvArgs a, int mode, int cfg, int splitk, size_t ws_bytes, hipStream_t st) {
+  if (a.N % 8 != 0 || a.M <= 0 || a.N <= 0 || a.K <= 0 || a.K % 8 != 0) return MLS_BAD_ARG;
+  int acfg = 0, asplit = 1;
+  choose_cfg(a.M, a.N, a.K, acfg, asplit);
+  if (cfg <= 0 || cfg >= kNumCfgs) cfg = acfg;
+  if (splitk <= 0) splitk = asplit;
+  // K per split: multiple of BK (so MODE_GENERIC steps never straddle a tap)
+  int kchunk = ((a.K + splitk - 1) / splitk + BK - 1) / BK * BK;
+  splitk = (a.K + kchunk - 1) / kchunk;
+  if (splitk > 1 && (a.ws == nullptr || ws_bytes < (size_t)splitk * a.M * a.N * sizeof(float))) {
+    // not enough workspace: fall back to no split
+    splitk = 1;
+    kchunk = (a.K + BK - 1) / BK * BK;
+  }
+  a.splitk = splitk;
+  a.kchunk = kchunk;
+  const int bm = kCfgs[cfg].bm, bn = kCfgs[cfg].bn;
+  const long ntiles = (long)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn) * splitk;
+  if (ntiles > 0x7fffffffL) return MLS_BAD_ARG;
+  dim3 grid((unsigned)ntiles);
+  switch (mode) {
+    case MODE_1X1: launch_mode<MODE_1X1>(cfg, grid, st, a); break;
+    case MODE_GENERIC: launch_mode<MODE_GENERIC>(cfg, grid, st, a); break;
+    case MODE_STEM: launch_mode<MODE_STEM>(cfg, grid, st, a); break;
+    default: return MLS_UNSUPPORTED;
+  }
+  if (splitk > 1) {
+    const long total = (long)a.M * (a.N / 8);
+    int blocks = (int)((total + 255) / 256);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(splitk_epilogue_kernel, dim3(blocks), dim3(256), 0, st, a);
+  }
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" {
+
+// NHWC conv2d with fused epilogue. Weights [Cout][KH][KW][Cin] bf16; for the stem mode
+// (Cin == 4, KH > 1) the weights are [Cout][KH][8][4] (KW zero-padded to 8).
+int mls_conv2d(const void* x, const void* w, const float* scale, const float* bias, const void* res, void* out,
+               void* ws, size_t ws_bytes, int B, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+               int pad, int act, int cfg, int splitk, void* stream) {
+  ConvArgs a{};
+  a.x = (const bf16*)x;
+  a.w = (const bf16*)w;
+  a.scale = scale;
+  a.bias = bias;
+  a.res = (const bf16*)res;
+  a.out = (bf16*)out;
+  a.ws = (float*)ws;
+  a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.N = Cout; a.KH = KH; a.KW = KW; a.stride = stride; a.pad = pad;
+  a.Ho = (H + 2 * pad - KH) / stride + 1;
+  a.Wo = (W + 2 * pad - KW) / stride + 1;
+  a.M = B * a.Ho * a.Wo;
+  a.act = act;
+  a.ldo = Cout;
+  a.ldr = Cout;
+  const size_t xb = (size_t)B * H * W * Cin * 2;
+  if (xb >= 0x7FFFFFFFull) return MLS_UNSUPPORTED;  // 32-bit buffer offsets
+  a.x_bytes = (uint32_t)xb;
+  int mode;
+  if (Cin == 4 && KH > 1) {
+    if (KW > 8) return MLS_UNSUPPORTED;
+    mode = MODE_STEM;
+    a.K = KH * 32;
+  } else if (KH == 1 && KW == 1 && pad == 0) {
+    mode = MODE_1X1;
+    a.K = Cin;
+  } else if (Cin % 64 == 0) {
+    mode = MODE_GENERIC;
+    a.K = KH * KW * Cin;
+  } else {
+    return MLS_UNSUPPORTED;
+  }
+  const size_t wb = (size_t)Cout * a.K * 2;
+  if (wb >= 0x7FFFFFFFull) return MLS_UNSUPPORTED;
+  a.w_bytes = (uint32_t)wb;
+  return launch_conv(a, mode, cfg, splitk, ws_bytes, (hipStream_t)stream);
+}
+
+// out[M][N] = act(A[M][K] . W[N][K]^T * scale + bias (+ res[M][N]))
+int mls_gemm(const void* A, const void* W, const float* scale, const float* bias, const void* res, void* out, void* ws,
+             size_t ws_bytes, int M, int N, int K, int act, int cfg, int splitk, void* stream) {
+  ConvArgs a{};
+  a.x = (const bf16*)A;
+  a.w = (const bf16*)W;
+  a.scale = scale;
+  a.bias = bias;
+  a.res = (const bf16*)res;
+  a.out = (bf16*)out;
+  a.ws = (float*)ws;
+  a.B = M; a.H = 1; a.W = 1; a.Cin = K; a.Ho = 1; a.Wo = 1; a.N = N; a.KH = 1; a.KW = 1; a.stride = 1; a.pad = 0;
+  a.M = M;
+  a.K = K;
+  a.act = act;
+  a.ldo = N;
+  a.ldr = N;
+  const size_t xb = (size_t)M * K * 2, wb = (size_t)N * K * 2;
+  if (xb >= 0x7FFFFFFFull || wb >= 0x7FFFFFFFull) return MLS_UNSUPPORTED;
+  a.x_bytes = (uint32_t)xb;
+  a.w_bytes = (uint32_t)wb;
+  return launch_conv(a, MODE_1X1, cfg, splitk, ws_bytes, (hipStream_t)stream);
+}
+
+// the tile config / split-K the heuristic would pick (for the autotuner and tests)
+int mls_gemm_heuristic(int M, int N, int K, int* cfg, int* splitk) {
+  choose_cfg(M, N, K, *cfg, *splitk);
+  return 0;
+}
+
+int mls_gemm_num_cfgs() { return kNumCfgs; }
+
+}  // extern "C"

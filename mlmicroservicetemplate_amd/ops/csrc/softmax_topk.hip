@@ -1,0 +1,146 @@
+// K6 (row softmax, numerically stable, optional additive mask) and K7 (row top-k), plus the
+// fused classifier head softmax -> top-k that ResNet-50 / BERT serving emit per request.
+// One 256-thread workgroup (4 waves) per row; the row is staged once in LDS as fp32, so the k
+// selection rounds re-read LDS, never HBM (cdna_hip_programming.md App. B "Reduction").
+#include "common.h"
+
+namespace {
+
+struct KV {
+  float v;
+  int i;
+};
+
+MLS_DEV KV better(KV a, KV b) {  // larger value wins; ties -> smaller index (stable)
+  if (b.v > a.v || (b.v == a.v && b.i < a.i && b.i >= 0)) return b;
+  return a;
+}
+
+MLS_DEV KV wave_argmax(KV x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    KV y;
+    y.v = __shfl_xor(x.v, o, 64);
+    y.i = __shfl_xor(x.i, o, 64);
+    x = better(x, y);
+  }
+  return x;
+}
+
+MLS_DEV KV block_argmax(KV x, float* rv, int* ri) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  x = wave_argmax(x);
+  __syncthreads();
+  if (lane == 0) {
+    rv[wid] = x.v;
+    ri[wid] = x.i;
+  }
+  __syncthreads();
+  KV t{-INFINITY, -1};
+  if (lane < nw) t = KV{rv[lane], ri[lane]};
+  return wave_argmax(t);
+}
+
+template <typename Tin>
+MLS_DEV float load_as_f32(const Tin* p, long i);
+template <>
+MLS_DEV float load_as_f32<bf16>(const bf16* p, long i) { return (float)p[i]; }
+template <>
+MLS_DEV float load_as_f32<float>(const float* p, long i) { return p[i]; }
+
+// softmax (optional) + top-k per row.  `apply_softmax`: 1 -> values are probabilities,
+// 0 -> raw logits (plain top-k).  Dynamic LDS: N floats.
+template <typename Tin>
+__global__ __launch_bounds__(256) void softmax_topk_kernel(const Tin* __restrict__ x, float* __restrict__ vals,
+                                                           int* __restrict__ idx, int N, int k, int apply_softmax,
+                                                           float temperature) {
+  extern __shared__ __attribute__((aligned(16))) float row[];
+  __shared__ float rv[16];
+  __shared__ int ri[16];
+  const long r = blockIdx.x;
+  const Tin* src = x + r * (long)N;
+  const float invt = 1.f / temperature;
+  float mx = -INFINITY;
+  for (int i = threadIdx.x; i < N; i += blockDim.x) {
+    const float v = load_as_f32<Tin>(src, i) * invt;
+    row[i] = v;
+    mx = fmaxf(mx, v);
+  }
+  float denom = 1.f;
+  if (apply_softmax) {
+    mx = block_max(mx, rv);
+    float s = 0.f;
+    for (int i = threadIdx.x; i < N; i += blockDim.x) s += __expf(row[i] - mx);
+    denom = block_sum(s, rv);
+  }
+  __syncthreads();
+  for (int j = 0; j < k; ++j) {
+    KV best{-INFINITY, -1};
+    for (int i = threadIdx.x; i < N; i += blockDim.x) best = better(best, KV{row[i], i});
+    best = block_argmax(best, rv, ri);
+    if (threadIdx.x == 0) {
+      const float v = apply_softmax ? __expf(best.v - mx) / denom : best.v;
+      vals[r * k + j] = v;
+      idx[r * k + j] = best.i;
+      if (best.i >= 0) row[best.i] = -INFINITY;
+    }
+    __syncthreads();
+  }
+}
+
+// y = softmax(x * scale + mask) row-wise, bf16 in/out; mask (fp32, additive) is indexed
+// [row / rows_per_mask][N] (e.g. one padding mask per sequence shared by all heads/queries).
+__global__ __launch_bounds__(256) void softmax_rows_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
+                                                           const float* __restrict__ mask, int N, int rows_per_mask,
+                                                           float scale) {
+  extern __shared__ __attribute__((aligned(16))) float row[];
+  __shared__ float red[16];
+  const long r = blockIdx.x;
+  const bf16* src = x + r * (long)N;
+  const float* mk = mask ? mask + (r / rows_per_mask) * (long)N : nullptr;
+  float mx = -INFINITY;
+  for (int i = threadIdx.x; i < N; i += blockDim.x) {
+    float v = (float)src[i] * scale;
+    if (mk) v += mk[i];
+    row[i] = v;
+    mx = fmaxf(mx, v);
+  }
+  mx = block_max(mx, red);
+  float s = 0.f;
+  for (int i = threadIdx.x; i < N; i += blockDim.x) {
+    const float e = (mx == -INFINITY) ? 0.f : __expf(row[i] - mx);
+    row[i] = e;
+    s += e;
+  }
+  s = block_sum(s, red);
+  const float inv = s > 0.f ? 1.f / s : 0.f;
+  for (int i = threadIdx.x; i < N; i += blockDim.x) y[r * (long)N + i] = f2bf(row[i] * inv);
+}
+
+}  // namespace
+
+extern "C" {
+
+// x: [rows][N] (dtype 0 = bf16, 1 = fp32); vals fp32 [rows][k]; idx int32 [rows][k]
+int mls_softmax_topk(const void* x, int dtype, float* vals, int* idx, int rows, int N, int k, int apply_softmax,
+                     float temperature, void* stream) {
+  if (rows <= 0 || N <= 0 || k <= 0 || k > N || N > 32768 || temperature <= 0.f) return MLS_BAD_ARG;
+  const size_t lds = (size_t)N * sizeof(float);
+  if (dtype == 0)
+    hipLaunchKernelGGL(softmax_topk_kernel<bf16>, dim3(rows), dim3(256), lds, (hipStream_t)stream, (const bf16*)x,
+                       vals, idx, N, k, apply_softmax, temperature);
+  else
+    hipLaunchKernelGGL(softmax_topk_kernel<float>, dim3(rows), dim3(256), lds, (hipStream_t)stream, (const float*)x,
+                       vals, idx, N, k, apply_softmax, temperature);
+  return (int)hipGetLastError();
+}
+
+int mls_softmax_rows(const void* x, void* y, const float* mask, int rows, int N, int rows_per_mask, float scale,
+                     void* stream) {
+  if (rows <= 0 || N <= 0 || N > 32768 || (mask && rows_per_mask <= 0)) return MLS_BAD_ARG;
+  hipLaunchKernelGGL(softmax_rows_kernel, dim3(rows), dim3(256), (size_t)N * sizeof(float), (hipStream_t)stream,
+                     (const bf16*)x, (bf16*)y, mask, N, rows_per_mask > 0 ? rows_per_mask : 1, scale);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

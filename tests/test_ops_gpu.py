@@ -1,0 +1,186 @@
+"""Numerics of the hand-written HIP kernels vs plain-PyTorch fp32 references (SURVEY.md §4,
+"Kernels (GPU)" row): exact ResNet-50 shapes (at small batch), every tile config, split-K,
+residual/activation epilogues, padding/tails."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    from mlmicroservicetemplate_amd import ops
+
+    ops.lib()  # must load (fail loudly; no eager fallback)
+    yield
+
+
+def rel_err(a, b):
+    return ((a.float() - b.float()).abs().max() / (b.float().abs().max() + 1e-6)).item()
+
+
+def _conv_ref(x_nhwc, w_oihw, bias, stride, pad, act, res=None):
+    y = F.conv2d(x_nhwc.permute(0, 3, 1, 2).float(), w_oihw.float(), stride=stride, padding=pad)
+    y = y + bias.view(1, -1, 1, 1)
+    y = y.permute(0, 2, 3, 1)
+    if res is not None:
+        y = y + res.float()
+    if act == 1:
+        y = torch.relu(y)
+    return y
+
+
+RESNET_CONV_SHAPES = [
+    # cin, cout, k, s, p, h
+    (64, 64, 1, 1, 0, 56),
+    (64, 64, 3, 1, 1, 56),
+    (64, 256, 1, 1, 0, 56),
+    (256, 64, 1, 1, 0, 56),
+    (256, 128, 1, 1, 0, 56),
+    (128, 128, 3, 2, 1, 56),
+    (256, 512, 1, 2, 0, 56),
+    (512, 128, 1, 1, 0, 28),
+    (128, 128, 3, 1, 1, 28),
+    (256, 256, 3, 2, 1, 28),
+    (512, 1024, 1, 2, 0, 28),
+    (1024, 256, 1, 1, 0, 14),
+    (256, 256, 3, 1, 1, 14),
+    (512, 512, 3, 2, 1, 14),
+    (1024, 2048, 1, 2, 0, 14),
+    (2048, 512, 1, 1, 0, 7),
+    (512, 512, 3, 1, 1, 7),
+    (512, 2048, 1, 1, 0, 7),
+]
+
+
+@pytest.mark.parametrize("shape", RESNET_CONV_SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_conv_resnet_shapes(shape):
+    from mlmicroservicetemplate_amd import ops
+
+    cin, cout, k, s, p, h = shape
+    torch.manual_seed(0)
+    B = 2
+    x = torch.randn(B, h, h, cin, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(cout, cin, k, k, device=DEV) / (cin * k * k) ** 0.5).to(torch.bfloat16)
+    bias = torch.randn(cout, device=DEV)
+    ho = (h + 2 * p - k) // s + 1
+    res = torch.randn(B, ho, ho, cout, device=DEV).to(torch.bfloat16)
+    ref = _conv_ref(x, w, bias, s, p, 1, res)
+    ws = torch.empty(64 << 20, device=DEV, dtype=torch.float32)
+    for cfg in (0, 1, 2, 3, 4):
+        out = ops.conv2d_nhwc(x, ops.pack_conv_weight(w), bias, kernel=k, stride=s, pad=p, residual=res, act=1,
+                              workspace=ws, cfg=cfg)
+        torch.cuda.synchronize()
+        assert rel_err(out, ref) < 2e-2, f"cfg {cfg}"
+    # split-K
+    out = ops.conv2d_nhwc(x, ops.pack_conv_weight(w), bias, kernel=k, stride=s, pad=p, residual=res, act=1,
+                          workspace=ws, cfg=4, splitk=4)
+    assert rel_err(out, ref) < 2e-2, "splitk"
+
+
+def test_conv_stem():
+    from mlmicroservicetemplate_amd import ops
+
+    torch.manual_seed(1)
+    B, h = 2, 224
+    x3 = torch.randn(B, h, h, 3, device=DEV)
+    x4 = torch.cat([x3, torch.zeros(B, h, h, 1, device=DEV)], dim=-1).to(torch.bfloat16)
+    w = (torch.randn(64, 3, 7, 7, device=DEV) / 12.0).to(torch.bfloat16)
+    bias = torch.randn(64, device=DEV)
+    ref = _conv_ref(x4[..., :3], w, bias, 2, 3, 1)
+    for cfg in (0, 1, 2, 4):
+        out = ops.conv2d_nhwc(x4, ops.pack_conv_weight(w), bias, kernel=7, stride=2, pad=3, act=1, cfg=cfg)
+        assert out.shape == (B, 112, 112, 64)
+        assert rel_err(out, ref) < 2e-2, f"cfg {cfg}"
+
+
+@pytest.mark.parametrize("mnk", [(32, 1000, 2048), (1, 64, 64), (77, 136, 200), (300, 2304, 768), (513, 768, 3072)])
+@pytest.mark.parametrize("act", [0, 1, 2, 3, 4])
+def test_gemm(mnk, act):
+    from mlmicroservicetemplate_amd import ops
+
+    M, N, K = mnk
+    torch.manual_seed(2)
+    a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) / K**0.5).to(torch.bfloat16)
+    bias = torch.randn(N, device=DEV)
+    scale = torch.rand(N, device=DEV) + 0.5
+    res = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    y = (a.float() @ w.float().T) * scale + bias + res.float()
+    ref = {0: y, 1: torch.relu(y), 2: F.gelu(y), 3: torch.tanh(y), 4: F.silu(y)}[act]
+    ws = torch.empty(16 << 20, device=DEV, dtype=torch.float32)
+    for cfg, sk in ((0, 0), (1, 1), (4, 2), (2, 3)):
+        out = ops.gemm(a, w, bias, scale=scale, residual=res, act=act, workspace=ws, cfg=cfg, splitk=sk)
+        assert rel_err(out, ref) < 2e-2, f"cfg {cfg} sk {sk}"
+
+
+def test_gemm_identity_asymmetric():
+    """A = I with an asymmetric B catches a transposed C-write (guide §3)."""
+    from mlmicroservicetemplate_amd import ops
+
+    n = 128
+    eye = torch.eye(n, device=DEV).to(torch.bfloat16)
+    b = torch.arange(n * n, device=DEV, dtype=torch.float32).view(n, n).remainder(97).to(torch.bfloat16)
+    out = ops.gemm(eye, b)  # = I @ b.T
+    assert torch.equal(out.float(), b.float().T)
+
+
+def test_normalize_pool_head():
+    from mlmicroservicetemplate_amd import ops
+    from mlmicroservicetemplate_amd.models.resnet import IMAGENET_MEAN, IMAGENET_STD
+
+    torch.manual_seed(3)
+    img = torch.randint(0, 256, (3, 224, 224, 3), dtype=torch.uint8, device=DEV)
+    out = ops.normalize_u8(img, IMAGENET_MEAN, IMAGENET_STD)
+    ref = (img.float() - torch.tensor(IMAGENET_MEAN, device=DEV)) / torch.tensor(IMAGENET_STD, device=DEV)
+    assert rel_err(out[..., :3], ref) < 1e-2
+    assert out[..., 3].abs().max().item() == 0
+
+    x = torch.randn(2, 112, 112, 64, device=DEV).to(torch.bfloat16)
+    mp = ops.maxpool2d_nhwc(x, 3, 2, 1)
+    mref = F.max_pool2d(x.permute(0, 3, 1, 2).float(), 3, 2, 1).permute(0, 2, 3, 1)
+    assert torch.equal(mp.float(), mref)
+
+    x = torch.randn(4, 7, 7, 2048, device=DEV).to(torch.bfloat16)
+    ap = ops.avgpool_global_nhwc(x)
+    assert rel_err(ap, x.float().mean(dim=(1, 2))) < 1e-2
+
+    logits = torch.randn(32, 1000, device=DEV).to(torch.bfloat16)
+    vals, idx = ops.softmax_topk(logits, 5)
+    p = torch.softmax(logits.float(), -1)
+    rv, ri = torch.topk(p, 5, dim=-1)
+    assert torch.allclose(vals, rv, rtol=1e-3, atol=1e-5)
+    # bf16 logits have ties; the selected ids must carry the top-k probabilities
+    assert torch.allclose(p.gather(1, idx.long()), rv, rtol=1e-3, atol=1e-6)
+    v2, i2 = ops.softmax_topk(logits.float(), 3, softmax=False)
+    rv2, ri2 = torch.topk(logits.float(), 3, dim=-1)
+    assert torch.allclose(v2, rv2) and torch.allclose(logits.float().gather(1, i2.long()), rv2)
+
+    x = torch.randn(2 * 12 * 128, 128, device=DEV).to(torch.bfloat16)
+    mask = torch.zeros(2, 128, device=DEV)
+    mask[1, 100:] = -1e9
+    sm = ops.softmax_rows(x, mask, rows_per_mask=12 * 128, scale=0.125)
+    sref = torch.softmax(x.float() * 0.125 + mask.repeat_interleave(12 * 128, 0), -1)
+    assert rel_err(sm, sref) < 1e-2
+
+    x = torch.randn(64, 56, 56, 64, device=DEV).to(torch.bfloat16)
+    sc, bi = torch.rand(64, device=DEV), torch.randn(64, device=DEV)
+    y = ops.bn_act(x, sc, bi, relu=True)
+    assert rel_err(y, torch.relu(x.float() * sc + bi)) < 1e-2
+
+
+def test_resnet50_fused_matches_reference():
+    from mlmicroservicetemplate_amd.models.resnet import ResNet50Fused, init_resnet50, resnet50_reference
+
+    params = init_resnet50(0)
+    torch.manual_seed(4)
+    imgs = torch.randint(0, 256, (4, 224, 224, 3), dtype=torch.uint8, device=DEV)
+    model = ResNet50Fused(params, DEV, max_batch=32)
+    logits = model(imgs).float()
+    ref = resnet50_reference({k: v.to(DEV) for k, v in params.items()}, imgs)
+    assert rel_err(logits, ref) < 5e-2
+    vals, idx = model.classify(imgs, 5)
+    assert (idx[:, 0].long() == ref.argmax(-1)).float().mean().item() >= 0.75
