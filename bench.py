@@ -1,0 +1,162 @@
+"""Flagship serving benchmark: ResNet-50 bs=32 requests/sec (whole node) + p50 latency.
+
+BASELINE.json metric: "requests/sec (whole node) + p50 latency, ResNet-50 bs=32 at 1/2/4/8
+MI355X".  One process per GPU (``torch.distributed.run``); every rank is an independent
+data-parallel serving replica (config 4 of BASELINE.json): rank 0 initialises the random
+ResNet-50 weights and RCCL-broadcasts them over xGMI (X1), every rank builds its fused engine
+and captures its hipGraph, then serves synthetic requests.
+
+One timed *step* = one micro-batch of ``--batch`` requests through the full engine path:
+per-request uint8 images (224x224x3) copied into a pinned staging slot -> H2D ->
+hipGraph{normalise -> 53 fused MFMA convs -> pools -> FC -> softmax -> top-5} -> D2H of the
+top-5 -> per-request numpy results.  ``--inflight`` batches are kept in flight per GPU, which
+is how the server's batcher drives the engine.  Per-request latency = submit -> result.
+
+Prints ONE JSON line on rank 0 (value = total requests/s over all ranks, computed from the
+max elapsed time over ranks).  Weights are random-init and inputs synthetic (no network).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from mlmicroservicetemplate_amd.parallel import dist as mdist  # noqa: E402
+
+EAGER_BASELINE_IMG_S = 7754.8  # stock PyTorch-ROCm (MIOpen) bs=32 bf16, 1x MI355X: profiles/r1_eager_baseline_miopen.jsonl
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def build_model(backend: str, device, batch: int, params):
+    from mlmicroservicetemplate_amd.models import resnet
+
+    if backend == "fused":
+        from mlmicroservicetemplate_amd.ops import autotune
+
+        tuning = autotune.load_tuning("resnet50", batch)
+        model = resnet.ResNet50Fused(params, device, max_batch=batch, tuning=tuning)
+
+        def fwd(x):
+            return model.classify(x, 5)
+
+    elif backend == "eager":
+        model = resnet.ResNet50Eager(params, device, fold=True)
+
+        def fwd(x):
+            logits = model(x)
+            v, i = torch.topk(torch.softmax(logits.float(), -1), 5, dim=-1)
+            return v, i.to(torch.int32)
+
+    else:
+        raise ValueError(backend)
+    return fwd
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--inflight", type=int, default=2)
+    ap.add_argument("--backend", default="fused", choices=["fused", "eager"])
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--seed", type=int, default=0)
+    args = ap.parse_args(argv)
+
+    info = mdist.init_distributed()
+    world = info.world_size
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    device = torch.device("cuda", info.local_rank)
+    torch.cuda.set_device(device)
+
+    from mlmicroservicetemplate_amd.engine.worker import GpuEngine
+    from mlmicroservicetemplate_amd.models import resnet
+
+    # ---- X1: rank 0 initialises, everyone receives over RCCL (not timed) ----
+    t0 = time.perf_counter()
+    params = resnet.init_resnet50(args.seed) if info.rank == 0 else None
+    if world > 1:
+        spec = {k: (tuple(v.shape), v.dtype) for k, v in resnet.init_resnet50_spec().items()}
+        params = mdist.broadcast_state(params, src=0, device=device, spec=spec)
+    t_bcast = time.perf_counter() - t0
+
+    fwd = build_model(args.backend, device, args.batch, params)
+    engine = GpuEngine(fwd, device, (224, 224, 3), torch.uint8, buckets=[args.batch], inflight=args.inflight,
+                       use_graphs=not args.no_graphs, name=f"resnet50.r{info.rank}")
+    engine.warmup(capture=not args.no_graphs)
+
+    rng = np.random.default_rng(1234 + info.rank)
+    pool = [[rng.integers(0, 256, (224, 224, 3), dtype=np.uint8) for _ in range(args.batch)] for _ in range(4)]
+
+    def run_steps(n, lat):
+        pending = []
+        for i in range(n):
+            pending.append(engine.submit(pool[i % len(pool)]))
+            if len(pending) >= args.inflight:
+                t = pending.pop(0)
+                t.wait()
+                lat.append(time.perf_counter() - t.t_submit)
+        for t in pending:
+            t.wait()
+            lat.append(time.perf_counter() - t.t_submit)
+
+    run_steps(args.warmup, [])
+    lat: list = []
+    mdist.barrier()
+    torch.cuda.synchronize(device)
+    t_start = time.perf_counter()
+    run_steps(args.steps, lat)
+    torch.cuda.synchronize(device)
+    mdist.barrier()
+    elapsed = time.perf_counter() - t_start
+    elapsed_max = mdist.max_over_ranks(elapsed)
+    p50 = float(np.percentile(lat, 50)) * 1e3
+    p99 = float(np.percentile(lat, 99)) * 1e3
+    p50_max = mdist.max_over_ranks(p50)
+    p99_max = mdist.max_over_ranks(p99)
+
+    total_req = world * args.batch * args.steps
+    value = total_req / elapsed_max
+    if info.rank == 0:
+        out = {
+            "metric": "requests/sec (whole node) + p50 latency, ResNet-50 bs=32",
+            "value": round(value, 1),
+            "unit": "requests/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed_max * 1e3 / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic uint8 224x224x3 images, random-init weights",
+            "config": {"model": "resnet50-v1.5", "global_batch": args.batch * world, "per_gpu_batch": args.batch,
+                       "seq_len": None, "image_size": 224, "parallelism": f"dp{world}",
+                       "backend": args.backend, "hipgraph": not args.no_graphs, "inflight": args.inflight},
+            "p50_latency_ms": round(p50_max, 3),
+            "p99_latency_ms": round(p99_max, 3),
+            "per_gpu_requests_per_s": round(value / world, 1),
+            "vs_pytorch_eager_per_gpu": round(value / world / EAGER_BASELINE_IMG_S, 3),
+            "weight_broadcast_s": round(t_bcast, 3),
+        }
+        print(json.dumps(out), flush=True)
+    mdist.destroy()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,226 @@
+"""Per-GPU execution engine (T4 / P4 / P5 of SURVEY.md §1.2, §2.E.3).
+
+One :class:`GpuEngine` owns one model replica on one device and runs fixed-shape batches:
+
+    host request arrays --memcpy--> pinned slot --H2D stream--> device slot
+        --compute stream: hipGraph replay (bucket b)--> device outputs --D2H stream--> pinned out
+
+* **Buckets**: a batch of ``n`` requests is padded to the smallest graph bucket ``>= n``
+  (1, 2, 4, ... MAX_BATCH); each (slot, bucket) has its own captured hipGraph, replayed with
+  static input/output buffers, so the steady-state step is one graph launch.
+* **Slots**: ``inflight`` independent staging slots (pinned host in/out + device input) so
+  batch i+1's host copy and H2D overlap batch i's graph, and batch i's D2H overlaps batch
+  i+1's compute -- event-ordered across three HIP streams, no device-wide syncs.
+* The host thread only blocks on a *blocking-sync* event of its own slot, so concurrent
+  callers (the batcher's executor threads) keep the GPU fed.
+
+The engine is model-agnostic: a model adapter provides ``sample_shape``/``sample_dtype`` of
+one request and ``forward(device_batch) -> tuple[Tensor, ...]`` (fixed-shape outputs whose
+first dim is the batch).
+"""
+from __future__ import annotations
+
+import logging
+import queue
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ..utils import tracing
+
+logger = logging.getLogger("mlsamd.engine")
+
+_NP_DTYPES = {torch.uint8: np.uint8, torch.int32: np.int32, torch.int64: np.int64, torch.float32: np.float32,
+              torch.bfloat16: None, torch.float16: np.float16}
+
+
+def pick_bucket(n: int, buckets: Sequence[int]) -> int:
+    for b in buckets:
+        if b >= n:
+            return b
+    raise ValueError(f"batch of {n} exceeds the largest bucket {buckets[-1]}")
+
+
+@dataclass
+class _Slot:
+    idx: int
+    host_in: torch.Tensor  # pinned [max_b, *sample_shape]
+    dev_in: torch.Tensor  # device [max_b, *sample_shape]
+    outs: Dict[int, Tuple[torch.Tensor, ...]] = field(default_factory=dict)  # bucket -> device outputs
+    host_out: Dict[int, Tuple[torch.Tensor, ...]] = field(default_factory=dict)  # bucket -> pinned outputs
+    graphs: Dict[int, torch.cuda.CUDAGraph] = field(default_factory=dict)
+    ev_h2d: Optional[torch.cuda.Event] = None
+    ev_comp: Optional[torch.cuda.Event] = None
+    ev_done: Optional[torch.cuda.Event] = None
+
+
+class Ticket:
+    """Handle for an enqueued batch; :meth:`wait` returns numpy outputs trimmed to ``n`` rows."""
+
+    __slots__ = ("engine", "slot", "bucket", "n", "t_submit", "_result")
+
+    def __init__(self, engine: "GpuEngine", slot: _Slot, bucket: int, n: int):
+        self.engine = engine
+        self.slot = slot
+        self.bucket = bucket
+        self.n = n
+        self.t_submit = time.perf_counter()
+        self._result = None
+
+    def wait(self) -> Tuple[np.ndarray, ...]:
+        if self._result is None:
+            self._result = self.engine._finish(self)
+        return self._result
+
+
+class GpuEngine:
+    def __init__(
+        self,
+        forward: Callable[[torch.Tensor], Tuple[torch.Tensor, ...]],
+        device,
+        sample_shape: Tuple[int, ...],
+        sample_dtype: torch.dtype = torch.uint8,
+        buckets: Sequence[int] = (1, 2, 4, 8, 16, 32),
+        inflight: int = 2,
+        use_graphs: bool = True,
+        name: str = "engine",
+    ):
+        self.forward = forward
+        self.device = torch.device(device)
+        self.sample_shape = tuple(sample_shape)
+        self.sample_dtype = sample_dtype
+        self.buckets = sorted(set(int(b) for b in buckets))
+        self.max_batch = self.buckets[-1]
+        self.inflight = max(1, int(inflight))
+        self.use_graphs = use_graphs
+        self.name = name
+        self._enqueue_lock = threading.Lock()
+        self._free: "queue.Queue[_Slot]" = queue.Queue()
+        self.slots: List[_Slot] = []
+        self.batches = 0
+        self.samples = 0
+        self.busy_s = 0.0
+        self.healthy = True
+        self.last_error: Optional[str] = None
+        with torch.cuda.device(self.device):
+            self.s_h2d = torch.cuda.Stream(self.device)
+            self.s_comp = torch.cuda.Stream(self.device)
+            self.s_d2h = torch.cuda.Stream(self.device)
+            self._pool = torch.cuda.graph_pool_handle() if use_graphs else None
+            for i in range(self.inflight):
+                shape = (self.max_batch, *self.sample_shape)
+                slot = _Slot(
+                    idx=i,
+                    host_in=torch.zeros(shape, dtype=sample_dtype, pin_memory=True),
+                    dev_in=torch.zeros(shape, dtype=sample_dtype, device=self.device),
+                    ev_h2d=torch.cuda.Event(),
+                    ev_comp=torch.cuda.Event(),
+                    ev_done=torch.cuda.Event(blocking=True),
+                )
+                self.slots.append(slot)
+                self._free.put(slot)
+
+    # ------------------------------------------------------------------ capture
+    def warmup(self, capture: bool = True) -> None:
+        """Run every bucket eagerly once (kernel load / autotune caches), then capture graphs."""
+        with torch.cuda.device(self.device), torch.no_grad():
+            for slot in self.slots:
+                for b in self.buckets:
+                    with torch.cuda.stream(self.s_comp):
+                        outs = self.forward(slot.dev_in[:b])
+                    self.s_comp.synchronize()
+                    if not (self.use_graphs and capture):
+                        slot.outs[b] = tuple(outs)
+                    self._alloc_host_out(slot, b, outs)
+            if self.use_graphs and capture:
+                torch.cuda.synchronize(self.device)
+                for slot in self.slots:
+                    for b in self.buckets:
+                        g = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(g, pool=self._pool, stream=self.s_comp):
+                            outs = self.forward(slot.dev_in[:b])
+                        slot.graphs[b] = g
+                        slot.outs[b] = tuple(outs)
+                torch.cuda.synchronize(self.device)
+                logger.info("%s: captured %d hipGraphs (%d slots x buckets %s)", self.name,
+                            len(self.slots) * len(self.buckets), len(self.slots), self.buckets)
+
+    def _alloc_host_out(self, slot: _Slot, b: int, outs) -> None:
+        slot.host_out[b] = tuple(torch.empty(o.shape, dtype=o.dtype, pin_memory=True) for o in outs)
+
+    # ------------------------------------------------------------------ run
+    def submit(self, samples) -> Ticket:
+        """Enqueue a batch.  ``samples``: a numpy array ``[n, *sample_shape]`` or a sequence of
+        per-request arrays of ``sample_shape``.  Returns immediately with a :class:`Ticket`."""
+        n = len(samples)
+        if n == 0:
+            raise ValueError("empty batch")
+        bucket = pick_bucket(n, self.buckets)
+        slot = self._free.get()  # blocks while `inflight` batches are outstanding
+        try:
+            with tracing.range(f"{self.name}.stage"):
+                dst = slot.host_in.numpy() if self.sample_dtype != torch.bfloat16 else None
+                if isinstance(samples, np.ndarray):
+                    dst[:n] = samples
+                elif isinstance(samples, torch.Tensor):
+                    slot.host_in[:n].copy_(samples)
+                else:
+                    for i, s in enumerate(samples):
+                        dst[i] = s
+            with self._enqueue_lock, torch.cuda.device(self.device):
+                with tracing.range(f"{self.name}.enqueue"):
+                    with torch.cuda.stream(self.s_h2d):
+                        slot.dev_in[:bucket].copy_(slot.host_in[:bucket], non_blocking=True)
+                        slot.ev_h2d.record(self.s_h2d)
+                    self.s_comp.wait_event(slot.ev_h2d)
+                    with torch.cuda.stream(self.s_comp):
+                        if self.use_graphs and bucket in slot.graphs:
+                            slot.graphs[bucket].replay()
+                            outs = slot.outs[bucket]
+                        else:
+                            with torch.no_grad():
+                                outs = tuple(self.forward(slot.dev_in[:bucket]))
+                            slot.outs[bucket] = outs
+                            if bucket not in slot.host_out:
+                                self._alloc_host_out(slot, bucket, outs)
+                        slot.ev_comp.record(self.s_comp)
+                    self.s_d2h.wait_event(slot.ev_comp)
+                    with torch.cuda.stream(self.s_d2h):
+                        for h, d in zip(slot.host_out[bucket], outs):
+                            h.copy_(d, non_blocking=True)
+                        slot.ev_done.record(self.s_d2h)
+        except BaseException as e:
+            self._free.put(slot)
+            self.last_error = f"{type(e).__name__}: {e}"
+            raise
+        return Ticket(self, slot, bucket, n)
+
+    def _finish(self, t: Ticket) -> Tuple[np.ndarray, ...]:
+        slot = t.slot
+        try:
+            slot.ev_done.synchronize()
+            res = []
+            for h in slot.host_out[t.bucket]:
+                if h.dtype == torch.bfloat16:
+                    res.append(h[: t.n].float().numpy().copy())
+                else:
+                    res.append(h[: t.n].numpy().copy())
+            self.batches += 1
+            self.samples += t.n
+            self.busy_s += time.perf_counter() - t.t_submit
+            return tuple(res)
+        finally:
+            self._free.put(slot)
+
+    def run(self, samples) -> Tuple[np.ndarray, ...]:
+        return self.submit(samples).wait()
+
+    def stats(self) -> dict:
+        return {"name": self.name, "device": str(self.device), "batches": self.batches, "samples": self.samples,
+                "inflight": self.inflight, "buckets": self.buckets, "graphs": self.use_graphs,
+                "healthy": self.healthy, "last_error": self.last_error,
+                "free_slots": self._free.qsize()}

@@ -84,6 +84,19 @@ def init_resnet50(seed: int = 0, num_classes: int = NUM_CLASSES) -> Dict[str, to
     return params
 
 
+def init_resnet50_spec(num_classes: int = NUM_CLASSES) -> Dict[str, torch.Tensor]:
+    """Meta tensors with the shapes/dtypes of :func:`init_resnet50` (what non-source ranks need
+    to receive the X1 weight broadcast without generating weights themselves)."""
+    out: Dict[str, torch.Tensor] = {}
+    for spec in conv_specs():
+        out[spec.name + ".w"] = torch.empty(spec.cout, spec.cin, spec.k, spec.k, device="meta")
+        for n in ("gamma", "beta", "mean", "var"):
+            out[f"{spec.name}.bn.{n}"] = torch.empty(spec.cout, device="meta")
+    out["fc.w"] = torch.empty(num_classes, 2048, device="meta")
+    out["fc.b"] = torch.empty(num_classes, device="meta")
+    return out
+
+
 BN_EPS = 1e-5
 
 

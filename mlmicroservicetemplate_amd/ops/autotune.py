@@ -103,6 +103,20 @@ def cache_path(batch: int) -> str:
     return os.path.join(CACHE_DIR, f"resnet50_{arch}_b{batch}.json")
 
 
+SHIPPED_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned")
+
+
+def load_tuning(model: str, batch: int, arch: str = "gfx950") -> Dict[str, Tuple[int, int]]:
+    """Shipped (measured on MI355X, committed) or cached tuning table; {} -> C++ heuristic."""
+    for d in (SHIPPED_DIR, CACHE_DIR):
+        path = os.path.join(d, f"{model}_{arch}_b{batch}.json")
+        if os.path.exists(path):
+            with open(path) as f:
+                data = json.load(f)
+            return {k: (int(v["best_cfg"]), int(v["best_splitk"])) for k, v in data.items()}
+    return {}
+
+
 def load_or_tune(batch: int, device="cuda:0") -> Dict[str, Tuple[int, int]]:
     path = cache_path(batch)
     if os.path.exists(path):

@@ -1,0 +1,147 @@
+"""Process-group bootstrap and the X1 / X5 / X6 collectives of SURVEY.md §2.E.2.
+
+One process per GPU (torchrun or our own launcher sets RANK / LOCAL_RANK / WORLD_SIZE /
+MASTER_ADDR / MASTER_PORT).  On ROCm the ``"nccl"`` backend *is* RCCL, which runs over xGMI
+between the GPUs of a node; ``gloo`` is used for CPU tests.
+
+X1 (weight broadcast for DP replicas) flattens every tensor of one dtype into ONE contiguous
+buffer and broadcasts that: one large message instead of ~270 small ones, which is what a
+point-to-point xGMI ring wants (per-message latency dominates small broadcasts; bandwidth is
+per link).  Rank 0 builds/loads weights; the others receive them -- no rank re-initialises.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistInfo:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    backend: str = "none"
+
+    @property
+    def is_distributed(self) -> bool:
+        return self.world_size > 1
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+
+def env_info() -> DistInfo:
+    return DistInfo(
+        rank=int(os.environ.get("RANK", 0)),
+        world_size=int(os.environ.get("WORLD_SIZE", 1)),
+        local_rank=int(os.environ.get("LOCAL_RANK", 0)),
+    )
+
+
+def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0, device_id: Optional[int] = None) -> DistInfo:
+    """Initialise the default process group from the environment (no-op for world size 1)."""
+    info = env_info()
+    if info.world_size <= 1:
+        return info
+    if dist.is_initialized():
+        info.backend = dist.get_backend()
+        return info
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    # dmabuf IPC only on this pool's host driver (RCCL / tensor sharing across processes)
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    kwargs = {}
+    if backend == "nccl":
+        dev = info.local_rank if device_id is None else device_id
+        torch.cuda.set_device(dev)
+        kwargs["device_id"] = torch.device("cuda", dev)
+    dist.init_process_group(backend=backend, rank=info.rank, world_size=info.world_size,
+                            timeout=datetime.timedelta(seconds=timeout_s), **kwargs)
+    info.backend = backend
+    return info
+
+
+def destroy() -> None:
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def barrier(group=None) -> None:
+    if dist.is_initialized():
+        if dist.get_backend(group) == "nccl":
+            dist.barrier(group=group, device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier(group=group)
+
+
+def _group_by_dtype(tensors: Dict[str, torch.Tensor]) -> Dict[torch.dtype, List[str]]:
+    out: Dict[torch.dtype, List[str]] = {}
+    for k in sorted(tensors):
+        out.setdefault(tensors[k].dtype, []).append(k)
+    return out
+
+
+def broadcast_state(
+    state: Optional[Dict[str, torch.Tensor]],
+    src: int = 0,
+    device: Optional[torch.device] = None,
+    group=None,
+    spec: Optional[Dict[str, Tuple[Tuple[int, ...], torch.dtype]]] = None,
+) -> Dict[str, torch.Tensor]:
+    """X1: broadcast a name->tensor dict from ``src``.  Non-src ranks pass ``state=None`` plus the
+    ``spec`` (shapes/dtypes, known from the architecture) -- or ``spec=None`` to receive it via
+    a small object broadcast first.  Returns tensors on ``device`` on every rank."""
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        assert state is not None
+        return {k: v.to(device) if device is not None else v for k, v in state.items()}
+    backend = dist.get_backend(group)
+    comm_dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+    if spec is None:
+        obj = [{k: (tuple(v.shape), v.dtype) for k, v in state.items()} if rank == src else None]
+        dist.broadcast_object_list(obj, src=src, group=group)
+        spec = obj[0]
+    out: Dict[str, torch.Tensor] = {}
+    groups = _group_by_dtype({k: torch.empty(0, dtype=d) for k, (_s, d) in spec.items()})
+    for dtype, names in groups.items():
+        numels = [int(torch.Size(spec[n][0]).numel()) for n in names]
+        total = sum(numels)
+        if rank == src:
+            flat = torch.cat([state[n].reshape(-1).to(comm_dev, dtype) for n in names])
+        else:
+            flat = torch.empty(total, dtype=dtype, device=comm_dev)
+        dist.broadcast(flat, src=src, group=group)
+        off = 0
+        for n, ne in zip(names, numels):
+            t = flat[off: off + ne].view(spec[n][0])
+            out[n] = t.to(device) if device is not None and t.device != device else t.clone()
+            off += ne
+    return out
+
+
+def all_reduce_health(ok: bool, group=None) -> bool:
+    """X6: every rank reports readiness; True only if all are ready (gates ``/status``)."""
+    if not dist.is_initialized():
+        return ok
+    backend = dist.get_backend(group)
+    dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(t.item())
+
+
+def max_over_ranks(value: float, group=None) -> float:
+    if not dist.is_initialized():
+        return value
+    backend = dist.get_backend(group)
+    dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+    t = torch.tensor([value], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())
