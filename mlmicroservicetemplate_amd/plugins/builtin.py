@@ -1,0 +1,197 @@
+"""Built-in plugins: ``stub`` (reference parity), ``identity`` (config 1, CPU echo) and
+``resnet50`` (configs 2 and 4).  ``bert`` and ``llama`` register from their own modules."""
+from __future__ import annotations
+
+import io
+import logging
+import time
+import zlib
+from typing import Any, List
+
+import numpy as np
+
+from ..api.multipart import Part
+from .base import ModelPlugin, PluginContext, register
+
+logger = logging.getLogger("mlsamd.plugin")
+
+
+@register("stub")
+class StubPlugin(ModelPlugin):
+    """The reference stub model (reference ``src/model/model.py:6-31``): ``init`` sleeps
+    (1 s there; ``STUB_INIT_S`` here), ``predict`` opens the upload with PIL -- which only parses
+    the header, so a non-image raises (HTTP 500) -- and returns a constant result."""
+
+    name = "stub"
+    RESULT = {"classes": ["isGreen", "isRed"], "result": {"isGreen": 0, "isRed": 1}}
+
+    def __init__(self, init_seconds: float = 1.0):
+        self.init_seconds = init_seconds
+
+    def init(self, ctx: PluginContext) -> None:
+        secs = getattr(ctx.settings, "STUB_INIT_S", None)
+        time.sleep(self.init_seconds if secs is None else float(secs))
+
+    def predict(self, upload) -> dict:
+        from PIL import Image
+
+        Image.open(upload.file)  # header parse only, as the reference does
+        return {"classes": list(self.RESULT["classes"]), "result": dict(self.RESULT["result"])}
+
+
+@register("identity")
+class IdentityPlugin(ModelPlugin):
+    """Config 1: echo model on CPU through the full batched path (parser -> batcher ->
+    run_batch -> postprocess).  Returns size and crc32 of the upload, so a client can verify
+    the bytes made it through unchanged."""
+
+    name = "identity"
+    batched = True
+    task = "echo"
+
+    def init(self, ctx: PluginContext) -> None:
+        self.ctx = ctx
+
+    def preprocess(self, part: Part) -> Any:
+        return part.data
+
+    def replicas(self):
+        def run_batch(samples: List[bytes]):
+            return [{"bytes": len(s), "crc32": zlib.crc32(s) & 0xFFFFFFFF, "batch": len(samples)} for s in samples]
+
+        return [run_batch]
+
+    def postprocess(self, out: Any) -> dict:
+        return {"classes": ["bytes", "crc32"], "result": {"bytes": out["bytes"], "crc32": out["crc32"]},
+                "batch_size": out["batch"]}
+
+
+RAW_CONTENT_TYPES = ("application/octet-stream", "application/x-rgb8")
+
+
+def decode_image(data: bytes, content_type: str = "", size: int = 224, resize: int = 256) -> np.ndarray:
+    """Bytes -> uint8 HWC RGB ``[size, size, 3]``: raw RGB8 of exactly that size passes through;
+    otherwise PIL decode (JPEG DCT-domain downscale via ``draft``), shorter side -> ``resize``,
+    centre crop ``size``."""
+    n = size * size * 3
+    if len(data) == n and (not content_type or content_type.split(";")[0].strip() in RAW_CONTENT_TYPES):
+        return np.frombuffer(data, dtype=np.uint8).reshape(size, size, 3)
+    from PIL import Image
+
+    img = Image.open(io.BytesIO(data))
+    if img.format == "JPEG":
+        img.draft("RGB", (resize, resize))
+    img = img.convert("RGB")
+    w, h = img.size
+    s = resize / min(w, h)
+    nw, nh = max(size, round(w * s)), max(size, round(h * s))
+    img = img.resize((nw, nh), Image.BILINEAR)
+    left, top = (nw - size) // 2, (nh - size) // 2
+    img = img.crop((left, top, left + size, top + size))
+    return np.asarray(img, dtype=np.uint8)
+
+
+@register("resnet50")
+class ResNet50Plugin(ModelPlugin):
+    """ResNet-50 image classifier (configs 2 and 4).  One GPU engine per device this process
+    drives; each engine replays hipGraphs of the fused CDNA4 kernels (``BACKEND=fused``) or of
+    stock PyTorch ops (``BACKEND=eager``, the comparison baseline)."""
+
+    name = "resnet50"
+    batched = True
+    task = "image"
+
+    def __init__(self):
+        self.engines = []
+        self.labels: List[str] = []
+        self.topk = 5
+
+    def init(self, ctx: PluginContext) -> None:
+        import torch
+
+        from ..engine.worker import GpuEngine
+        from ..models import resnet
+        from ..parallel import dist as mdist
+
+        s = ctx.settings
+        self.topk = int(s.TOPK)
+        self.labels = [f"class_{i}" for i in range(resnet.NUM_CLASSES)]
+        devices = ctx.devices or (["cuda:0"] if torch.cuda.is_available() else [])
+        if not devices:
+            raise RuntimeError("resnet50 plugin needs a GPU (use MODEL=identity or stub on CPU)")
+        # X1: rank 0 builds (or loads) the weights, every other rank receives them over RCCL
+        params = None
+        if ctx.rank == 0:
+            params = resnet.init_resnet50(int(s.SEED))
+            if s.WEIGHTS:
+                from safetensors.torch import load_file
+
+                params.update(load_file(s.WEIGHTS))
+        if ctx.world_size > 1:
+            spec = {k: (tuple(v.shape), v.dtype) for k, v in resnet.init_resnet50_spec().items()}
+            params = mdist.broadcast_state(params, src=0, device=torch.device(devices[0]), spec=spec)
+        buckets = [b for b in s.GRAPH_BUCKETS if b <= s.MAX_BATCH]
+        for dev in devices:
+            fwd = self._build_forward(s.BACKEND, dev, max(buckets), params)
+            eng = GpuEngine(fwd, dev, (224, 224, 3), torch.uint8, buckets=buckets, inflight=int(s.INFLIGHT),
+                            use_graphs=bool(s.USE_GRAPHS), name=f"resnet50.{dev}")
+            eng.warmup(capture=bool(s.USE_GRAPHS))
+            self.engines.append(eng)
+        logger.info("resnet50 ready on %s (backend=%s buckets=%s)", devices, s.BACKEND, buckets)
+
+    def _build_forward(self, backend: str, dev: str, max_batch: int, params):
+        import torch
+
+        from ..models import resnet
+
+        k = self.topk
+        if backend == "fused":
+            from ..ops import autotune
+
+            tuning = autotune.load_tuning("resnet50", max_batch)
+            model = resnet.ResNet50Fused(params, dev, max_batch=max_batch, tuning=tuning)
+            return lambda x: model.classify(x, k)
+        if backend == "eager":
+            model = resnet.ResNet50Eager(params, dev)
+
+            def fwd(x):
+                v, i = torch.topk(torch.softmax(model(x).float(), -1), k, dim=-1)
+                return v, i.to(torch.int32)
+
+            return fwd
+        raise ValueError(f"unknown BACKEND {backend}")
+
+    def preprocess(self, part: Part) -> Any:
+        return decode_image(part.data, part.content_type or "")
+
+    def replicas(self):
+        out = []
+        for eng in self.engines:
+            def run_batch(samples, eng=eng):
+                vals, idx = eng.run(samples)
+                return [(vals[i], idx[i]) for i in range(len(samples))]
+
+            out.append(run_batch)
+        return out
+
+    def postprocess(self, out: Any) -> dict:
+        vals, idx = out
+        names = [self.labels[int(i)] for i in idx]
+        return {"classes": names, "result": {n: float(v) for n, v in zip(names, vals)}}
+
+    def describe(self) -> dict:
+        d = super().describe()
+        d["engines"] = [e.stats() for e in self.engines]
+        return d
+
+
+def _register_optional() -> None:
+    # GPU model families living in their own modules register themselves on import
+    for mod in ("text_classifier", "llm"):
+        try:
+            __import__(f"{__package__}.{mod}")
+        except ImportError as e:  # module not present yet
+            logger.debug("plugin module %s unavailable: %s", mod, e)
+
+
+_register_optional()
