@@ -1,0 +1,212 @@
+"""Service launcher: ``python -m mlmicroservicetemplate_amd serve``.
+
+Replaces the reference's ``uvicorn src.server.main:app --port ${PORT}`` compose command
+(reference ``docker-compose.yml:6``) with an MI355X-first process layout:
+
+* ``GPUS <= 1``: one uvicorn process, one engine (configs 1-3).
+* ``GPUS = N > 1``, data-parallel models (resnet50, bert): N processes, one per GPU, all
+  serving the SAME port through ``SO_REUSEPORT`` (the kernel spreads connections across
+  them), joined in one RCCL process group: rank 0 builds the weights and broadcasts them over
+  xGMI (X1), ``/status`` turns ready only after every rank reported healthy (X6), and only
+  rank 0 runs the orchestrator heartbeat (one registered service).  (config 4)
+* ``TP = N > 1`` (llama): N processes in one tensor-parallel group; rank 0 serves HTTP and
+  broadcasts each request's tokens to the other ranks (X5), which run the TP forward in
+  lockstep (config 5).
+
+The parent only supervises: it forwards SIGINT/SIGTERM, and if any rank dies the others are
+terminated (a dead rank would hang the collectives).
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+from typing import Dict, List, Optional
+
+from .config import Settings, load_dotenv
+
+logger = logging.getLogger("mlsamd.serve")
+
+DP_MODELS = {"resnet50", "bert", "identity", "stub"}
+
+
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def reuseport_socket(host: str, port: int) -> socket.socket:
+    sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+    if hasattr(socket, "SO_REUSEPORT"):
+        sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEPORT, 1)
+    sock.bind((host, port))
+    sock.listen(2048)
+    sock.set_inheritable(True)
+    return sock
+
+
+def _overrides_from_args(args) -> Dict[str, object]:
+    o = {}
+    for k in ("MODEL", "PORT", "GPUS", "TP", "MAX_BATCH", "MAX_WAIT_US", "BACKEND", "NAME", "SERVER_PORT"):
+        v = getattr(args, k.lower(), None)
+        if v is not None:
+            o[k] = v
+    if getattr(args, "no_register", False):
+        o["REGISTER"] = False
+    return o
+
+
+def run_rank(args) -> int:
+    """Body of one rank (also the single-process path)."""
+    import uvicorn
+
+    from .api.app import create_app
+    from .parallel import dist as mdist
+    from .plugins.base import PluginContext, load_plugin
+
+    load_dotenv(args.env_file)
+    settings = Settings.load(env_file=args.env_file, overrides=_overrides_from_args(args))
+    logging.basicConfig(level=getattr(logging, settings.LOG_LEVEL.upper(), logging.INFO),
+                        format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    info = mdist.env_info()
+    devices: List[str] = []
+    try:
+        import torch
+
+        ngpu = torch.cuda.device_count()
+    except Exception:
+        ngpu = 0
+    if ngpu and settings.MODEL not in ("stub", "identity") and "." not in settings.MODEL:
+        if info.world_size > 1:
+            devices = [f"cuda:{info.local_rank}"]
+        else:
+            devices = [f"cuda:{i}" for i in range(max(1, min(settings.GPUS, ngpu)))]
+    if info.world_size > 1:
+        mdist.init_distributed(device_id=info.local_rank if ngpu else None)
+    ctx = PluginContext(settings=settings, rank=info.rank, world_size=info.world_size, local_rank=info.local_rank,
+                        devices=devices)
+    plugin = load_plugin(settings.MODEL)
+    if info.world_size > 1 and settings.TP > 1 and info.rank != 0:
+        # tensor-parallel follower: no HTTP, run the lockstep worker loop
+        plugin.init(ctx)
+        return plugin.follower_loop() if hasattr(plugin, "follower_loop") else 0
+    app = create_app(settings, plugin, ctx)
+    config = uvicorn.Config(app, host=args.host, port=settings.PORT, log_level=settings.LOG_LEVEL.lower(),
+                            lifespan="on", timeout_graceful_shutdown=10)
+    server = uvicorn.Server(config)
+    fd = os.environ.get("MLS_LISTEN_FD")
+    if fd is not None:
+        sock = socket.socket(fileno=int(fd))
+        server.run(sockets=[sock])
+    else:
+        server.run()
+    return 0
+
+
+def launch(args) -> int:
+    load_dotenv(args.env_file)
+    settings = Settings.load(env_file=args.env_file, overrides=_overrides_from_args(args))
+    world = max(settings.GPUS, settings.TP) if (settings.GPUS > 1 or settings.TP > 1) else 1
+    if world <= 1:
+        return run_rank(args)
+    master_port = free_port()
+    sock = None
+    if settings.TP <= 1:
+        sock = reuseport_socket(args.host, settings.PORT)
+    procs: List[subprocess.Popen] = []
+    base_env = dict(os.environ)
+    base_env.update({"WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(master_port),
+                     "HSA_ENABLE_IPC_MODE_LEGACY": base_env.get("HSA_ENABLE_IPC_MODE_LEGACY", "0")})
+    cmd = [sys.executable, "-m", "mlmicroservicetemplate_amd", "rank", *args.passthrough]
+    for r in range(world):
+        env = dict(base_env, RANK=str(r), LOCAL_RANK=str(r))
+        pass_fds = ()
+        if sock is not None:
+            env["MLS_LISTEN_FD"] = str(sock.fileno())
+            pass_fds = (sock.fileno(),)
+        procs.append(subprocess.Popen(cmd, env=env, pass_fds=pass_fds))
+    stopping = {"flag": False}
+
+    def forward(sig, _frame):
+        stopping["flag"] = True
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(sig)
+
+    signal.signal(signal.SIGINT, forward)
+    signal.signal(signal.SIGTERM, forward)
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            if all(c is not None for c in codes):
+                rc = next((c for c in codes if c), 0)
+                break
+            if any(c not in (None, 0) for c in codes) and not stopping["flag"]:
+                logger.error("a rank exited with %s; stopping the others", codes)
+                forward(signal.SIGTERM, None)
+                stopping["flag"] = True
+            time.sleep(0.2)
+    finally:
+        deadline = time.time() + 20
+        for p in procs:
+            try:
+                p.wait(max(0.1, deadline - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+    return rc
+
+
+def build_parser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser(prog="mlmicroservicetemplate_amd")
+    sub = ap.add_subparsers(dest="cmd")
+    for name in ("serve", "rank"):
+        p = sub.add_parser(name)
+        p.add_argument("--env-file", default=".env")
+        p.add_argument("--host", default="0.0.0.0")
+        p.add_argument("--port", type=int)
+        p.add_argument("--model")
+        p.add_argument("--gpus", type=int)
+        p.add_argument("--tp", type=int)
+        p.add_argument("--max-batch", type=int)
+        p.add_argument("--max-wait-us", type=int)
+        p.add_argument("--backend")
+        p.add_argument("--name")
+        p.add_argument("--server-port", type=int)
+        p.add_argument("--no-register", action="store_true")
+    b = sub.add_parser("build", help="compile the HIP kernels for gfx950")
+    b.add_argument("--force", action="store_true")
+    sub.add_parser("plugins", help="list registered model plugins")
+    return ap
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    ap = build_parser()
+    args = ap.parse_args(argv)
+    if args.cmd == "build":
+        from .ops import build
+
+        print(build.build(force=args.force, verbose=True))
+        return 0
+    if args.cmd == "plugins":
+        from .plugins.base import available_plugins
+
+        print("\n".join(available_plugins()))
+        return 0
+    if args.cmd in ("serve", None):
+        if args.cmd is None:
+            args = ap.parse_args(["serve"])
+        args.passthrough = argv[1:] if argv and argv[0] == "serve" else []
+        return launch(args)
+    if args.cmd == "rank":
+        return run_rank(args)
+    ap.print_help()
+    return 2

@@ -1,0 +1,61 @@
+"""Launcher: 2 ranks (gloo on CPU) sharing one port via SO_REUSEPORT, identity model."""
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+
+import pytest
+import requests
+
+from mlmicroservicetemplate_amd.api.multipart import encode_multipart
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.timeout(120)
+def test_two_rank_identity_service():
+    port = _port()
+    env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    proc = subprocess.Popen([sys.executable, "-m", "mlmicroservicetemplate_amd", "serve", "--model", "identity",
+                             "--gpus", "2", "--port", str(port), "--host", "127.0.0.1", "--no-register",
+                             "--env-file", "/nonexistent"], cwd=ROOT, env=env, start_new_session=True)
+    try:
+        url = f"http://127.0.0.1:{port}"
+        deadline = time.time() + 90
+        ready = False
+        while time.time() < deadline:
+            try:
+                if requests.get(url + "/status", timeout=1).status_code == 200:
+                    ready = True
+                    break
+            except requests.RequestException:
+                pass
+            time.sleep(0.2)
+        assert ready, "service never became ready"
+        ranks = set()
+        for i in range(40):
+            info = requests.get(url + "/info", timeout=5).json()
+            ranks.add(info["rank"])
+            assert info["world_size"] == 2
+            body, ct = encode_multipart({"image_file": ("x", os.urandom(64), "application/octet-stream")})
+            r = requests.post(url + "/predict", data=body, headers={"content-type": ct}, timeout=5)
+            assert r.status_code == 200 and r.json()["result"]["result"]["bytes"] == 64
+            if len(ranks) == 2:
+                break
+        assert ranks == {0, 1}, f"SO_REUSEPORT did not spread connections: {ranks}"
+    finally:
+        os.killpg(proc.pid, signal.SIGTERM)
+        try:
+            proc.wait(30)
+        except subprocess.TimeoutExpired:
+            os.killpg(proc.pid, signal.SIGKILL)
