@@ -284,3 +284,132 @@ def softmax_rows(x: torch.Tensor, mask: Optional[torch.Tensor] = None, rows_per_
                                 stream_ptr(dev))
     check(rc, "mls_softmax_rows")
     return out
+
+
+# ------------------------------------------------------------------ transformer ops
+def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: Optional[torch.Tensor] = None, *,
+              residual: Optional[torch.Tensor] = None, residual_out: Optional[torch.Tensor] = None,
+              eps: float = 1e-5, rms: bool = False, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``LN(x [+ residual])`` (or RMSNorm with ``rms=True``) over the last dim, bf16.
+    ``residual_out`` receives the bf16 sum ``x + residual`` (the pre-norm residual stream)."""
+    dev = x.device
+    _need(x, "x", torch.bfloat16, dev)
+    _need(gamma, "gamma", torch.bfloat16, dev)
+    D = x.shape[-1]
+    rows = x.numel() // D
+    if beta is not None:
+        _need(beta, "beta", torch.bfloat16, dev)
+    if residual is not None:
+        _need(residual, "residual", torch.bfloat16, dev)
+    out = torch.empty_like(x) if out is None else out
+    rc = lib().mls_layernorm(x.data_ptr(), _ptr(residual), gamma.data_ptr(), _ptr(beta), out.data_ptr(),
+                             _ptr(residual_out), rows, D, float(eps), int(rms), stream_ptr(dev))
+    check(rc, "mls_layernorm")
+    return out
+
+
+def rmsnorm(x, gamma, *, residual=None, residual_out=None, eps: float = 1e-5, out=None):
+    return layernorm(x, gamma, None, residual=residual, residual_out=residual_out, eps=eps, rms=True, out=out)
+
+
+def embed_layernorm(ids: torch.Tensor, type_ids: Optional[torch.Tensor], word: torch.Tensor, pos: torch.Tensor,
+                    typ: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, seq_len: int, eps: float = 1e-12,
+                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """BERT embeddings: ``LN(word[ids] + pos[t % S] + type[type_ids])``; ids int32 ``[T]``."""
+    dev = ids.device
+    _need(ids, "ids", torch.int32, dev)
+    T = ids.numel()
+    D = word.shape[1]
+    out = torch.empty(T, D, device=dev, dtype=torch.bfloat16) if out is None else out
+    rc = lib().mls_embed_ln(ids.data_ptr(), _ptr(type_ids), word.data_ptr(), pos.data_ptr(), typ.data_ptr(),
+                            gamma.data_ptr(), beta.data_ptr(), out.data_ptr(), T, seq_len, D, word.shape[0],
+                            float(eps), stream_ptr(dev))
+    check(rc, "mls_embed_ln")
+    return out
+
+
+def embedding(ids: torch.Tensor, table: torch.Tensor, lo: int = 0, hi: Optional[int] = None,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Row gather; with a vocab shard ``[lo, hi)`` out-of-shard ids give zero rows (TP)."""
+    dev = ids.device
+    _need(ids, "ids", torch.int32, dev)
+    _need(table, "table", torch.bfloat16, dev)
+    hi = lo + table.shape[0] if hi is None else hi
+    T, D = ids.numel(), table.shape[1]
+    out = torch.empty(T, D, device=dev, dtype=torch.bfloat16) if out is None else out
+    rc = lib().mls_embedding(ids.data_ptr(), table.data_ptr(), out.data_ptr(), T, D, lo, hi, stream_ptr(dev))
+    check(rc, "mls_embedding")
+    return out
+
+
+def rope_(qkv: torch.Tensor, positions: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, n_rot_heads: int,
+          head_dim: int) -> torch.Tensor:
+    """In-place rotate-half RoPE on the first ``n_rot_heads`` heads of each row of ``qkv``
+    (Q heads then K heads in the fused projection output).  cos/sin fp32 ``[max_pos, D/2]``."""
+    dev = qkv.device
+    _need(qkv, "qkv", torch.bfloat16, dev)
+    _need(positions, "positions", torch.int32, dev)
+    T = positions.numel()
+    rc = lib().mls_rope(qkv.data_ptr(), positions.data_ptr(), cos.data_ptr(), sin.data_ptr(), T, qkv.shape[-1],
+                        n_rot_heads, head_dim, stream_ptr(dev))
+    check(rc, "mls_rope")
+    return qkv
+
+
+def kv_append(qkv: torch.Tensor, k_col: int, v_col: int, slots: torch.Tensor, k_cache: torch.Tensor,
+              v_cache: torch.Tensor, n_kv_heads: int, head_dim: int) -> None:
+    """Scatter the K/V heads of each token row of ``qkv`` into cache slot ``slots[t]``."""
+    dev = qkv.device
+    _need(slots, "slots", torch.int32, dev)
+    T = slots.numel()
+    rc = lib().mls_kv_append(qkv.data_ptr(), qkv.shape[-1], k_col, v_col, slots.data_ptr(), k_cache.data_ptr(),
+                             v_cache.data_ptr(), T, n_kv_heads, head_dim, stream_ptr(dev))
+    check(rc, "mls_kv_append")
+
+
+def flash_attention(qkv: torch.Tensor, batch: int, seq: int, n_q_heads: int, n_kv_heads: int, head_dim: int, *,
+                    kv_lens: Optional[torch.Tensor] = None, causal: bool = False, scale: Optional[float] = None,
+                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Fused attention reading Q/K/V in place from the fused projection ``qkv [B*S, (Hq+2Hkv)*D]``.
+    Returns ``[B*S, Hq*D]``."""
+    dev = qkv.device
+    _need(qkv, "qkv", torch.bfloat16, dev)
+    T, W = qkv.shape
+    if T != batch * seq or W != (n_q_heads + 2 * n_kv_heads) * head_dim:
+        raise ValueError("qkv shape does not match batch/seq/heads")
+    if kv_lens is not None:
+        _need(kv_lens, "kv_lens", torch.int32, dev)
+    out = torch.empty(T, n_q_heads * head_dim, device=dev, dtype=torch.bfloat16) if out is None else out
+    scale = head_dim ** -0.5 if scale is None else scale
+    base = qkv.data_ptr()
+    es = qkv.element_size()
+    rc = lib().mls_flash_attention(base, base + n_q_heads * head_dim * es, base + (n_q_heads + n_kv_heads) * head_dim * es,
+                                   out.data_ptr(), W, W, W, out.shape[1], batch, seq, n_q_heads, n_kv_heads, head_dim,
+                                   _ptr(kv_lens), int(causal), float(scale), stream_ptr(dev))
+    check(rc, "mls_flash_attention")
+    return out
+
+
+def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, lens: torch.Tensor,
+                     n_q_heads: int, n_kv_heads: int, head_dim: int, *, chunk: int = 256,
+                     scale: Optional[float] = None, workspace: Optional[torch.Tensor] = None,
+                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """One query token per sequence vs the cache ``[B, max_len, Hkv, D]``; q rows ``[B, >= Hq*D]``
+    (head h at column h*D, e.g. the fused QKV row).  Split-KV with a combine pass."""
+    dev = q.device
+    B = lens.numel()
+    max_len = k_cache.shape[1]
+    nsplit = (max_len + chunk - 1) // chunk
+    need = B * n_q_heads * nsplit * (head_dim + 2)
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty(need, device=dev, dtype=torch.float32)
+    ws = workspace[: B * n_q_heads * nsplit * head_dim]
+    ws_ml = workspace[B * n_q_heads * nsplit * head_dim: need]
+    out = torch.empty(B, n_q_heads * head_dim, device=dev, dtype=torch.bfloat16) if out is None else out
+    scale = head_dim ** -0.5 if scale is None else scale
+    rc = lib().mls_decode_attention(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), out.data_ptr(),
+                                    ws.data_ptr(), ws_ml.data_ptr(), q.stride(0), out.stride(0),
+                                    k_cache.stride(0), lens.data_ptr(), B, n_q_heads, n_kv_heads, head_dim,
+                                    max_len, chunk, float(scale), stream_ptr(dev))
+    check(rc, "mls_decode_attention")
+    return out

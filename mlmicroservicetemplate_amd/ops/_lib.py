@@ -42,6 +42,13 @@ _SIGS = {
     "mls_bn_act": [P, P, P, P, L, I, I, P],
     "mls_softmax_topk": [P, I, P, P, I, I, I, I, F, P],
     "mls_softmax_rows": [P, P, P, I, I, I, F, P],
+    "mls_layernorm": [P, P, P, P, P, P, L, I, F, I, P],
+    "mls_embed_ln": [P, P, P, P, P, P, P, P, L, I, I, I, F, P],
+    "mls_embedding": [P, P, P, L, I, I, I, P],
+    "mls_rope": [P, P, P, P, L, I, I, I, P],
+    "mls_kv_append": [P, I, I, I, P, P, P, L, I, I, P],
+    "mls_flash_attention": [P, P, P, P, I, I, I, I, I, I, I, I, I, P, I, F, P],
+    "mls_decode_attention": [P, P, P, P, P, P, I, I, L, P, I, I, I, I, I, I, F, P],
 }
 _OPTIONAL_SIGS: dict = {}
 

@@ -1,0 +1,271 @@
+// K4 LayerNorm (+fused residual add), K5 RMSNorm (+fused residual add), K10 embedding gathers
+// (BERT word+position+type fused with the embedding LayerNorm; Llama vocab-parallel rows that
+// zero out-of-shard ids before the TP all-reduce), K9 RoPE (in place on the Q/K heads of the
+// fused QKV buffer) and K13 KV-cache append.
+//
+// Row kernels: one wave64 per row, 16-B (8 x bf16) vector accesses, the row held in registers
+// (<= CPL chunks per lane), fp32 statistics via wave shuffles; 4 rows per 256-thread block.
+#include "common.h"
+
+namespace {
+
+constexpr int ROWS_PER_BLOCK = 4;
+
+template <int CPL>  // 16-B chunks per lane: D <= 64 * 8 * CPL
+__global__ __launch_bounds__(256) void layernorm_kernel(const bf16* __restrict__ x, const bf16* __restrict__ res,
+                                                        const bf16* __restrict__ gamma, const bf16* __restrict__ beta,
+                                                        bf16* __restrict__ out, bf16* __restrict__ res_out, long rows,
+                                                        int D, float eps, int rms) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nch = D >> 3;
+  float v[CPL][8];
+  float s = 0.f, ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nch) {
+      unpack8(ld16(x + row * D + ch * 8), v[c]);
+      if (res) {
+        float r[8];
+        unpack8(ld16(res + row * D + ch * 8), r);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[c][e] += r[e];
+      }
+      if (res_out) {
+        // the residual stream is carried in bf16; normalise what the next layer will see
+        uint4 p = pack8(v[c]);
+        st16(res_out + row * D + ch * 8, p);
+        unpack8(p, v[c]);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s += v[c][e];
+        ss += v[c][e] * v[c][e];
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[c][e] = 0.f;
+    }
+  }
+  s = wave_sum(s);
+  ss = wave_sum(ss);
+  const float inv_d = 1.f / (float)D;
+  float mean, rstd;
+  if (rms) {
+    mean = 0.f;
+    rstd = rsqrtf(ss * inv_d + eps);
+  } else {
+    mean = s * inv_d;
+    const float var = fmaxf(ss * inv_d - mean * mean, 0.f);
+    rstd = rsqrtf(var + eps);
+  }
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nch) {
+      float g[8], b[8], o[8];
+      unpack8(ld16(gamma + ch * 8), g);
+      if (beta) unpack8(ld16(beta + ch * 8), b);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (v[c][e] - mean) * rstd * g[e] + (beta ? b[e] : 0.f);
+      st16(out + row * D + ch * 8, pack8(o));
+    }
+  }
+}
+
+// BERT embeddings: out[t] = LN(word[id] + pos[t % S] + type[tt]) ; one wave per token
+template <int CPL>
+__global__ __launch_bounds__(256) void embed_ln_kernel(const int* __restrict__ ids, const int* __restrict__ type_ids,
+                                                       const bf16* __restrict__ word, const bf16* __restrict__ pos,
+                                                       const bf16* __restrict__ typ, const bf16* __restrict__ gamma,
+                                                       const bf16* __restrict__ beta, bf16* __restrict__ out,
+                                                       long rows, int S, int D, int vocab, float eps) {
+  const int lane = threadIdx.x & 63;
+  const long t = (long)blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
+  if (t >= rows) return;
+  int id = ids[t];
+  id = (id < 0 || id >= vocab) ? 0 : id;
+  const int tt = type_ids ? type_ids[t] : 0;
+  const int p = (int)(t % S);
+  const int nch = D >> 3;
+  float v[CPL][8];
+  float s = 0.f, ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nch) {
+      float a[8], b[8], d[8];
+      unpack8(ld16(word + (long)id * D + ch * 8), a);
+      unpack8(ld16(pos + (long)p * D + ch * 8), b);
+      unpack8(ld16(typ + (long)tt * D + ch * 8), d);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        v[c][e] = a[e] + b[e] + d[e];
+        s += v[c][e];
+        ss += v[c][e] * v[c][e];
+      }
+    }
+  }
+  s = wave_sum(s);
+  ss = wave_sum(ss);
+  const float mean = s / D;
+  const float rstd = rsqrtf(fmaxf(ss / D - mean * mean, 0.f) + eps);
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nch) {
+      float g[8], b[8], o[8];
+      unpack8(ld16(gamma + ch * 8), g);
+      unpack8(ld16(beta + ch * 8), b);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (v[c][e] - mean) * rstd * g[e] + b[e];
+      st16(out + t * D + ch * 8, pack8(o));
+    }
+  }
+}
+
+// vocab-parallel embedding: rows of ids outside [lo, hi) are zero (summed by the all-reduce)
+__global__ __launch_bounds__(256) void embedding_kernel(const int* __restrict__ ids, const bf16* __restrict__ table,
+                                                        bf16* __restrict__ out, long rows, int D, int lo, int hi) {
+  const int nch = D >> 3;
+  const long total = rows * nch;
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
+    const long t = q / nch;
+    const int ch = (int)(q - t * nch);
+    const int id = ids[t];
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (id >= lo && id < hi) v = ld16(table + (long)(id - lo) * D + ch * 8);
+    st16(out + t * D + ch * 8, v);
+  }
+}
+
+// RoPE (rotate-half convention) in place on the first n_rot_heads heads of each token row:
+// x[i] <- x[i] cos - x[i + D/2] sin ; x[i + D/2] <- x[i + D/2] cos + x[i] sin
+// cos/sin table: [max_pos][D/2] fp32.  One thread per (token, head, 4 pairs).
+__global__ __launch_bounds__(256) void rope_kernel(bf16* __restrict__ qkv, const int* __restrict__ positions,
+                                                   const float* __restrict__ cos_t, const float* __restrict__ sin_t,
+                                                   long tokens, int row_stride, int n_rot_heads, int D) {
+  const int half = D >> 1;
+  const int quads = half >> 2;
+  const long total = tokens * n_rot_heads * quads;
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
+    const int i4 = (int)(q % quads);
+    const long th = q / quads;
+    const int h = (int)(th % n_rot_heads);
+    const long t = th / n_rot_heads;
+    const int p = positions[t];
+    bf16* base = qkv + t * row_stride + (long)h * D;
+    const int i = i4 * 4;
+    const uint2 a_raw = *reinterpret_cast<const uint2*>(base + i);
+    const uint2 b_raw = *reinterpret_cast<const uint2*>(base + half + i);
+    const bf16x4 a = __builtin_bit_cast(bf16x4, a_raw);
+    const bf16x4 b = __builtin_bit_cast(bf16x4, b_raw);
+    const float4 c = *reinterpret_cast<const float4*>(cos_t + (long)p * half + i);
+    const float4 s = *reinterpret_cast<const float4*>(sin_t + (long)p * half + i);
+    const float cc[4] = {c.x, c.y, c.z, c.w}, sn[4] = {s.x, s.y, s.z, s.w};
+    bf16x4 oa, ob;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float x0 = (float)a[e], x1 = (float)b[e];
+      oa[e] = (bf16)(x0 * cc[e] - x1 * sn[e]);
+      ob[e] = (bf16)(x1 * cc[e] + x0 * sn[e]);
+    }
+    *reinterpret_cast<uint2*>(base + i) = __builtin_bit_cast(uint2, oa);
+    *reinterpret_cast<uint2*>(base + half + i) = __builtin_bit_cast(uint2, ob);
+  }
+}
+
+// KV-cache append: cache[slot[t]][h][:] = src[t][col0 + h*D : ...]; k and v in one launch.
+// cache layout [num_slots][Hkv][D] (slot = page * page_size + offset, or seq * max_len + pos).
+__global__ __launch_bounds__(256) void kv_append_kernel(const bf16* __restrict__ qkv, int row_stride, int k_col,
+                                                        int v_col, const int* __restrict__ slots,
+                                                        bf16* __restrict__ kc, bf16* __restrict__ vc, long tokens,
+                                                        int Hkv, int D) {
+  const int nch = (Hkv * D) >> 3;
+  const long total = tokens * nch * 2;
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
+    const int which = (int)(q & 1);
+    const long r = q >> 1;
+    const long t = r / nch;
+    const int ch = (int)(r - t * nch);
+    const int slot = slots[t];
+    if (slot < 0) continue;
+    const bf16* src = qkv + t * row_stride + (which ? v_col : k_col) + ch * 8;
+    bf16* dst = (which ? vc : kc) + (long)slot * Hkv * D + ch * 8;
+    st16(dst, ld16(src));
+  }
+}
+
+inline int grid_for(long work, int block) {
+  long g = (work + block - 1) / block;
+  return (int)(g > 4096 ? 4096 : (g < 1 ? 1 : g));
+}
+
+}  // namespace
+
+extern "C" {
+
+int mls_layernorm(const void* x, const void* res, const void* gamma, const void* beta, void* out, void* res_out,
+                  long rows, int D, float eps, int rms, void* stream) {
+  if (D % 8 || D > 64 * 8 * 16 || rows <= 0) return MLS_BAD_ARG;
+  const int cpl = (D / 8 + 63) / 64;
+  dim3 grid((unsigned)((rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK));
+  hipStream_t st = (hipStream_t)stream;
+#define LN_LAUNCH(C)                                                                                           \
+  hipLaunchKernelGGL(layernorm_kernel<C>, grid, dim3(256), 0, st, (const bf16*)x, (const bf16*)res,           \
+                     (const bf16*)gamma, (const bf16*)beta, (bf16*)out, (bf16*)res_out, rows, D, eps, rms)
+  if (cpl <= 1) LN_LAUNCH(1);
+  else if (cpl <= 2) LN_LAUNCH(2);
+  else if (cpl <= 4) LN_LAUNCH(4);
+  else if (cpl <= 8) LN_LAUNCH(8);
+  else LN_LAUNCH(16);
+#undef LN_LAUNCH
+  return (int)hipGetLastError();
+}
+
+int mls_embed_ln(const int* ids, const int* type_ids, const void* word, const void* pos, const void* typ,
+                 const void* gamma, const void* beta, void* out, long rows, int S, int D, int vocab, float eps,
+                 void* stream) {
+  if (D % 8 || D > 64 * 8 * 4 || rows <= 0 || S <= 0) return MLS_BAD_ARG;
+  const int cpl = (D / 8 + 63) / 64;
+  dim3 grid((unsigned)((rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK));
+  hipStream_t st = (hipStream_t)stream;
+#define EL_LAUNCH(C)                                                                                                 \
+  hipLaunchKernelGGL(embed_ln_kernel<C>, grid, dim3(256), 0, st, ids, type_ids, (const bf16*)word, (const bf16*)pos, \
+                     (const bf16*)typ, (const bf16*)gamma, (const bf16*)beta, (bf16*)out, rows, S, D, vocab, eps)
+  if (cpl <= 1) EL_LAUNCH(1);
+  else if (cpl <= 2) EL_LAUNCH(2);
+  else EL_LAUNCH(4);
+#undef EL_LAUNCH
+  return (int)hipGetLastError();
+}
+
+int mls_embedding(const int* ids, const void* table, void* out, long rows, int D, int lo, int hi, void* stream) {
+  if (D % 8 || rows <= 0) return MLS_BAD_ARG;
+  hipLaunchKernelGGL(embedding_kernel, dim3(grid_for(rows * (D / 8), 256)), dim3(256), 0, (hipStream_t)stream, ids,
+                     (const bf16*)table, (bf16*)out, rows, D, lo, hi);
+  return (int)hipGetLastError();
+}
+
+int mls_rope(void* qkv, const int* positions, const float* cos_t, const float* sin_t, long tokens, int row_stride,
+             int n_rot_heads, int D, void* stream) {
+  if (D % 8 || tokens <= 0) return MLS_BAD_ARG;
+  const long work = tokens * n_rot_heads * (D / 8);
+  hipLaunchKernelGGL(rope_kernel, dim3(grid_for(work, 256)), dim3(256), 0, (hipStream_t)stream, (bf16*)qkv,
+                     positions, cos_t, sin_t, tokens, row_stride, n_rot_heads, D);
+  return (int)hipGetLastError();
+}
+
+int mls_kv_append(const void* qkv, int row_stride, int k_col, int v_col, const int* slots, void* k_cache,
+                  void* v_cache, long tokens, int Hkv, int D, void* stream) {
+  if ((Hkv * D) % 8 || tokens <= 0 || k_col % 8 || v_col % 8 || row_stride % 8) return MLS_BAD_ARG;
+  const long work = tokens * (Hkv * D / 8) * 2;
+  hipLaunchKernelGGL(kv_append_kernel, dim3(grid_for(work, 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16*)qkv, row_stride, k_col, v_col, slots, (bf16*)k_cache, (bf16*)v_cache, tokens, Hkv,
+                     D);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

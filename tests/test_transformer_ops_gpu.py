@@ -1,0 +1,124 @@
+"""Transformer kernels (K4 LN, K5 RMSNorm, K8 attention, K9 RoPE, K10 embeddings, K13 KV append)
+vs the fp32 PyTorch oracles in ops.reference."""
+import pytest
+import torch
+
+from mlmicroservicetemplate_amd.ops import reference as R
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def rel(a, b):
+    return ((a.float() - b.float()).abs().max() / (b.float().abs().max() + 1e-6)).item()
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from mlmicroservicetemplate_amd import ops as o
+
+    o.lib()
+    return o
+
+
+@pytest.mark.parametrize("D", [64, 768, 1000, 4096])
+@pytest.mark.parametrize("rms", [False, True])
+def test_layernorm(ops, D, rms):
+    torch.manual_seed(0)
+    x = torch.randn(37, D, device=DEV).to(torch.bfloat16)
+    r = torch.randn(37, D, device=DEV).to(torch.bfloat16)
+    g = (torch.rand(D, device=DEV) + 0.5).to(torch.bfloat16)
+    b = torch.randn(D, device=DEV).to(torch.bfloat16)
+    res_out = torch.empty_like(x)
+    y = ops.layernorm(x, g, None if rms else b, residual=r, residual_out=res_out, rms=rms, eps=1e-5)
+    ref, hs = R.layernorm(x, g, None if rms else b, residual=r, eps=1e-5, rms=rms)
+    assert rel(y, ref) < 2e-2
+    assert rel(res_out, hs) < 1e-2
+    y2 = ops.layernorm(x, g, None if rms else b, rms=rms)
+    assert rel(y2, R.layernorm(x, g, None if rms else b, rms=rms)[0]) < 2e-2
+
+
+def test_embed_ln_and_vocab_parallel(ops):
+    torch.manual_seed(1)
+    V, P, D, B, S = 1000, 128, 768, 3, 50
+    word = torch.randn(V, D, device=DEV).to(torch.bfloat16)
+    pos = torch.randn(P, D, device=DEV).to(torch.bfloat16)
+    typ = torch.randn(2, D, device=DEV).to(torch.bfloat16)
+    g = torch.ones(D, device=DEV, dtype=torch.bfloat16)
+    b = torch.zeros(D, device=DEV, dtype=torch.bfloat16)
+    ids = torch.randint(0, V, (B * S,), device=DEV, dtype=torch.int32)
+    tt = torch.randint(0, 2, (B * S,), device=DEV, dtype=torch.int32)
+    y = ops.embed_layernorm(ids, tt, word, pos, typ, g, b, S, eps=1e-12)
+    e = word[ids.long()].float() + pos[torch.arange(B * S, device=DEV) % S].float() + typ[tt.long()].float()
+    ref = torch.nn.functional.layer_norm(e, (D,), eps=1e-12)
+    assert rel(y, ref) < 2e-2
+    # vocab shard [250, 500)
+    out = ops.embedding(ids, word[250:500].contiguous(), lo=250, hi=500)
+    inshard = ((ids >= 250) & (ids < 500)).unsqueeze(1)
+    exp = torch.where(inshard, word[ids.long().clamp(0, V - 1)], torch.zeros_like(word[:1]))
+    assert torch.equal(out, exp)
+
+
+def test_rope_and_kv_append(ops):
+    torch.manual_seed(2)
+    T, Hq, Hkv, D = 45, 8, 2, 128
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=DEV).to(torch.bfloat16)
+    pos = torch.randint(0, 1000, (T,), device=DEV, dtype=torch.int32)
+    cos, sin = R.rope_tables(2048, D, 500000.0, DEV)
+    ref_q = R.rope(qkv[:, : Hq * D].view(T, Hq, D), pos, cos, sin).reshape(T, -1)
+    ref_k = R.rope(qkv[:, Hq * D: (Hq + Hkv) * D].view(T, Hkv, D), pos, cos, sin).reshape(T, -1)
+    v_before = qkv[:, (Hq + Hkv) * D:].clone()
+    ops.rope_(qkv, pos, cos, sin, Hq + Hkv, D)
+    assert rel(qkv[:, : Hq * D], ref_q) < 1e-2
+    assert rel(qkv[:, Hq * D: (Hq + Hkv) * D], ref_k) < 1e-2
+    assert torch.equal(qkv[:, (Hq + Hkv) * D:], v_before)
+    kc = torch.zeros(4 * 64, Hkv, D, device=DEV, dtype=torch.bfloat16)
+    vc = torch.zeros_like(kc)
+    slots = torch.randperm(4 * 64, device=DEV)[:T].to(torch.int32)
+    ops.kv_append(qkv, Hq * D, (Hq + Hkv) * D, slots, kc, vc, Hkv, D)
+    assert torch.equal(kc[slots.long()].reshape(T, -1), qkv[:, Hq * D: (Hq + Hkv) * D])
+    assert torch.equal(vc[slots.long()].reshape(T, -1), qkv[:, (Hq + Hkv) * D:])
+
+
+@pytest.mark.parametrize("cfg", [
+    # B, S, Hq, Hkv, D, causal, lens
+    (3, 128, 12, 12, 64, False, [128, 77, 1]),
+    (2, 77, 12, 12, 64, False, None),
+    (2, 200, 8, 2, 128, True, None),
+    (1, 333, 4, 1, 128, True, None),
+    (2, 64, 4, 1, 128, False, [64, 5]),
+])
+def test_flash_attention(ops, cfg):
+    B, S, Hq, Hkv, D, causal, lens = cfg
+    torch.manual_seed(3)
+    qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device=DEV).to(torch.bfloat16)
+    kv_lens = torch.tensor(lens, device=DEV, dtype=torch.int32) if lens else None
+    out = ops.flash_attention(qkv, B, S, Hq, Hkv, D, kv_lens=kv_lens, causal=causal)
+    ref = R.attention(qkv, B, S, Hq, Hkv, D, kv_lens=kv_lens, causal=causal)
+    assert rel(out, ref) < 2e-2
+
+
+def test_flash_attention_spike_rescale(ops):
+    """Force the online-softmax rescale branch: one key row is a huge spike for every query,
+    placed in a late tile so the running max jumps (guide §5.4 rule 26)."""
+    B, S, H, D = 1, 256, 2, 64
+    torch.manual_seed(4)
+    qkv = torch.randn(B * S, 3 * H * D, device=DEV)
+    qkv[200, H * D: 2 * H * D] = qkv[:, : H * D].mean(0) * 40  # key 200 aligned with all queries
+    qkv = qkv.to(torch.bfloat16)
+    out = ops.flash_attention(qkv, B, S, H, H, D)
+    ref = R.attention(qkv, B, S, H, H, D)
+    assert rel(out, ref) < 2e-2
+
+
+@pytest.mark.parametrize("Hq,Hkv,D", [(4, 1, 128), (32, 8, 128), (12, 12, 64)])
+def test_decode_attention(ops, Hq, Hkv, D):
+    torch.manual_seed(5)
+    B, max_len = 3, 1024
+    kc = torch.randn(B, max_len, Hkv, D, device=DEV).to(torch.bfloat16)
+    vc = torch.randn(B, max_len, Hkv, D, device=DEV).to(torch.bfloat16)
+    q = torch.randn(B, (Hq + 2 * Hkv) * D, device=DEV).to(torch.bfloat16)
+    lens = torch.tensor([1, 300, 1024], device=DEV, dtype=torch.int32)
+    out = ops.decode_attention(q, kc, vc, lens, Hq, Hkv, D)
+    ref = R.decode_attention(q, kc, vc, lens, Hq, Hkv, D)
+    assert rel(out, ref) < 2e-2
