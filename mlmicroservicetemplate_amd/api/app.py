@@ -128,6 +128,19 @@ class ServingRuntime:
             return self.plugin.postprocess(out)
         return await run_in_threadpool(self.plugin.predict, part.to_upload_file())
 
+    async def generate(self, req: dict) -> dict:
+        plugin = self.plugin
+        if plugin.batched and hasattr(plugin, "prepare_generate"):
+            if self.router is None:
+                raise PredictionException()
+            sample = await run_in_threadpool(plugin.prepare_generate, req)
+            try:
+                out = await self.router.submit(sample, timeout=float(self.settings.REQUEST_TIMEOUT_S))
+            except QueueFull as e:
+                raise OverloadedException(str(e)) from e
+            return plugin.finish_generate(out)
+        return await run_in_threadpool(plugin.generate, req)
+
 
 def _validation_missing(field: str) -> RequestValidationError:
     return RequestValidationError([{"type": "missing", "loc": ("body", field), "msg": "Field required",
@@ -252,6 +265,17 @@ def create_app(settings: Optional[Settings] = None, plugin: Optional[ModelPlugin
                 part = parts[0]
             elif "filename" in fields and filename is None:
                 filename = fields["filename"][0].text()
+        elif ctype.lower().startswith("application/json"):
+            try:
+                payload = await request.json()
+            except Exception:
+                payload = None
+            if isinstance(payload, dict) and payload.get(plugin.form_field) is not None:
+                val = payload[plugin.form_field]
+                data = val.encode("utf-8") if isinstance(val, str) else str(val).encode("utf-8")
+                part = Part(name=plugin.form_field, data=data, content_type="text/plain")
+            elif isinstance(payload, dict) and filename is None:
+                filename = payload.get("filename")
         elif filename is None and ctype.lower().startswith("application/x-www-form-urlencoded"):
             form = await request.body()
             from urllib.parse import parse_qs
@@ -292,11 +316,10 @@ def create_app(settings: Optional[Settings] = None, plugin: Optional[ModelPlugin
         if getattr(plugin, "task", "") != "generate":
             return JSONResponse(status_code=400, content={"status": "failure",
                                                           "detail": f"model {plugin.name!r} does not generate"})
-        gen = getattr(plugin, "generate_async", None)
-        if gen is not None:
-            out = await gen(req)
-        else:
-            out = await run_in_threadpool(plugin.generate, req)
+        try:
+            out = await runtime.generate(req)
+        except ValueError as e:
+            return JSONResponse(status_code=400, content={"status": "failure", "detail": str(e)})
         metrics.tokens.inc(int(out.get("num_tokens", 0)))
         return {"status": "success", "result": out}
 

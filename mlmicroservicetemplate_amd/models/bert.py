@@ -1,0 +1,254 @@
+"""BERT-base text classifier (BASELINE.json config 3) -- no reference counterpart (the
+reference model is a constant stub, reference ``src/model/model.py:23-31``).
+
+Paths over one parameter set (random init, std 0.02, as BERT's initializer_range):
+  * :func:`bert_reference` -- fp32 PyTorch ops; the numerics oracle (runs on CPU too).
+  * :class:`BertEager`      -- stock PyTorch-ROCm ops in bf16 (hipBLASLt GEMMs + SDPA):
+                               the comparison baseline.
+  * :class:`BertFused`      -- our CDNA4 kernels: fused word+pos+type embedding + LN, MFMA
+                               GEMMs with bias / GELU / residual epilogues, MFMA flash attention
+                               reading Q/K/V in place from the fused QKV projection with a
+                               key-padding mask, LN kernels, tanh pooler and softmax/top-k head.
+
+Post-LN encoder (as BERT):  x = LN(x + Attn(x));  x = LN(x + FFN(x)).
+"""
+from __future__ import annotations
+
+import math
+import re
+import zlib
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn.functional as F
+
+
+@dataclass
+class BertConfig:
+    vocab: int = 30522
+    hidden: int = 768
+    layers: int = 12
+    heads: int = 12
+    intermediate: int = 3072
+    max_pos: int = 512
+    type_vocab: int = 2
+    eps: float = 1e-12
+    num_labels: int = 2
+
+    @property
+    def head_dim(self) -> int:
+        return self.hidden // self.heads
+
+
+BERT_BASE = BertConfig()
+CLS_ID, SEP_ID, PAD_ID, UNK_ID = 101, 102, 0, 100
+
+
+def init_bert(cfg: BertConfig = BERT_BASE, seed: int = 0, device="cpu", dtype=torch.float32) -> Dict[str, torch.Tensor]:
+    g = torch.Generator(device=device).manual_seed(seed)
+
+    def n(*shape):
+        return (torch.randn(*shape, generator=g, device=device) * 0.02).to(dtype)
+
+    def ones(c):
+        return (1.0 + 0.1 * torch.randn(c, generator=g, device=device)).to(dtype)
+
+    def small(c):
+        return (0.02 * torch.randn(c, generator=g, device=device)).to(dtype)
+
+    H, I = cfg.hidden, cfg.intermediate
+    p = {
+        "emb.word": n(cfg.vocab, H), "emb.pos": n(cfg.max_pos, H), "emb.type": n(cfg.type_vocab, H),
+        "emb.ln.g": ones(H), "emb.ln.b": small(H),
+        "pooler.w": n(H, H), "pooler.b": small(H),
+        "cls.w": n(cfg.num_labels, H), "cls.b": small(cfg.num_labels),
+    }
+    for i in range(cfg.layers):
+        p.update({
+            f"l{i}.qkv.w": n(3 * H, H), f"l{i}.qkv.b": small(3 * H),
+            f"l{i}.o.w": n(H, H), f"l{i}.o.b": small(H),
+            f"l{i}.ln1.g": ones(H), f"l{i}.ln1.b": small(H),
+            f"l{i}.ffn1.w": n(I, H), f"l{i}.ffn1.b": small(I),
+            f"l{i}.ffn2.w": n(H, I), f"l{i}.ffn2.b": small(H),
+            f"l{i}.ln2.g": ones(H), f"l{i}.ln2.b": small(H),
+        })
+    return p
+
+
+def bert_spec(cfg: BertConfig = BERT_BASE) -> Dict[str, Tuple[Tuple[int, ...], torch.dtype]]:
+    """Shapes/dtypes of :func:`init_bert` without materialising anything (X1 receivers)."""
+    H, I = cfg.hidden, cfg.intermediate
+    shapes = {"emb.word": (cfg.vocab, H), "emb.pos": (cfg.max_pos, H), "emb.type": (cfg.type_vocab, H),
+              "emb.ln.g": (H,), "emb.ln.b": (H,), "pooler.w": (H, H), "pooler.b": (H,),
+              "cls.w": (cfg.num_labels, H), "cls.b": (cfg.num_labels,)}
+    for i in range(cfg.layers):
+        shapes.update({f"l{i}.qkv.w": (3 * H, H), f"l{i}.qkv.b": (3 * H,), f"l{i}.o.w": (H, H), f"l{i}.o.b": (H,),
+                       f"l{i}.ln1.g": (H,), f"l{i}.ln1.b": (H,), f"l{i}.ffn1.w": (I, H), f"l{i}.ffn1.b": (I,),
+                       f"l{i}.ffn2.w": (H, I), f"l{i}.ffn2.b": (H,), f"l{i}.ln2.g": (H,), f"l{i}.ln2.b": (H,)})
+    return {k: (v, torch.float32) for k, v in shapes.items()}
+
+
+# ------------------------------------------------------------------------ tokenizer
+_WORD = re.compile(r"[A-Za-z0-9]+|[^\sA-Za-z0-9]")
+
+
+class HashTokenizer:
+    """Deterministic offline tokenizer: no vocab file is available in this environment (no
+    network), so words are hashed into the WordPiece id range.  With a ``vocab.txt`` the real
+    WordPiece tokenizer (``tokenizers`` package) is used instead."""
+
+    def __init__(self, vocab_size: int = 30522, vocab_file: Optional[str] = None, lowercase: bool = True):
+        self.vocab_size = vocab_size
+        self.lowercase = lowercase
+        self._wp = None
+        if vocab_file:
+            from tokenizers import BertWordPieceTokenizer
+
+            self._wp = BertWordPieceTokenizer(vocab_file, lowercase=lowercase)
+
+    def encode(self, text: str, max_len: int = 512) -> List[int]:
+        if self._wp is not None:
+            return self._wp.encode(text).ids[:max_len]
+        if self.lowercase:
+            text = text.lower()
+        ids = [CLS_ID]
+        span = self.vocab_size - 1000
+        for w in _WORD.findall(text):
+            ids.append(1000 + zlib.crc32(w.encode("utf-8")) % span)
+            if len(ids) >= max_len - 1:
+                break
+        ids.append(SEP_ID)
+        return ids
+
+
+# ------------------------------------------------------------------------ reference
+def bert_reference(p: Dict[str, torch.Tensor], ids: torch.Tensor, type_ids: Optional[torch.Tensor],
+                   lens: torch.Tensor, cfg: BertConfig = BERT_BASE) -> torch.Tensor:
+    """ids ``[B, S]`` -> fp32 logits ``[B, num_labels]``."""
+    B, S = ids.shape
+    H, nh, hd = cfg.hidden, cfg.heads, cfg.head_dim
+    f = {k: v.float() for k, v in p.items()}
+    tt = torch.zeros_like(ids) if type_ids is None else type_ids
+    x = f["emb.word"][ids.long()] + f["emb.pos"][:S].unsqueeze(0) + f["emb.type"][tt.long()]
+    x = F.layer_norm(x, (H,), f["emb.ln.g"], f["emb.ln.b"], cfg.eps)
+    mask = torch.arange(S, device=ids.device).view(1, S) < lens.view(B, 1).long()
+    bias = torch.zeros(B, 1, 1, S, device=ids.device).masked_fill(~mask.view(B, 1, 1, S), float("-inf"))
+    for i in range(cfg.layers):
+        qkv = F.linear(x, f[f"l{i}.qkv.w"], f[f"l{i}.qkv.b"])
+        q, k, v = qkv.split(H, dim=-1)
+        q = q.view(B, S, nh, hd).transpose(1, 2)
+        k = k.view(B, S, nh, hd).transpose(1, 2)
+        v = v.view(B, S, nh, hd).transpose(1, 2)
+        a = torch.softmax(q @ k.transpose(-1, -2) / math.sqrt(hd) + bias, dim=-1) @ v
+        a = a.transpose(1, 2).reshape(B, S, H)
+        x = F.layer_norm(x + F.linear(a, f[f"l{i}.o.w"], f[f"l{i}.o.b"]), (H,), f[f"l{i}.ln1.g"], f[f"l{i}.ln1.b"], cfg.eps)
+        h = F.gelu(F.linear(x, f[f"l{i}.ffn1.w"], f[f"l{i}.ffn1.b"]))
+        x = F.layer_norm(x + F.linear(h, f[f"l{i}.ffn2.w"], f[f"l{i}.ffn2.b"]), (H,), f[f"l{i}.ln2.g"], f[f"l{i}.ln2.b"], cfg.eps)
+    pooled = torch.tanh(F.linear(x[:, 0], f["pooler.w"], f["pooler.b"]))
+    return F.linear(pooled, f["cls.w"], f["cls.b"])
+
+
+class BertEager:
+    """Stock PyTorch-ROCm bf16 path (comparison baseline)."""
+
+    def __init__(self, p: Dict[str, torch.Tensor], device, cfg: BertConfig = BERT_BASE):
+        self.cfg = cfg
+        self.p = {k: v.to(device=device, dtype=torch.bfloat16) for k, v in p.items()}
+
+    @torch.no_grad()
+    def forward(self, ids: torch.Tensor, type_ids: Optional[torch.Tensor], lens: torch.Tensor) -> torch.Tensor:
+        cfg, p = self.cfg, self.p
+        B, S = ids.shape
+        H, nh, hd = cfg.hidden, cfg.heads, cfg.head_dim
+        tt = torch.zeros_like(ids) if type_ids is None else type_ids
+        x = p["emb.word"][ids.long()] + p["emb.pos"][:S].unsqueeze(0) + p["emb.type"][tt.long()]
+        x = F.layer_norm(x, (H,), p["emb.ln.g"], p["emb.ln.b"], cfg.eps)
+        mask = (torch.arange(S, device=ids.device).view(1, S) < lens.view(B, 1).long()).view(B, 1, 1, S)
+        for i in range(cfg.layers):
+            qkv = F.linear(x, p[f"l{i}.qkv.w"], p[f"l{i}.qkv.b"])
+            q, k, v = (t.view(B, S, nh, hd).transpose(1, 2) for t in qkv.split(H, dim=-1))
+            a = F.scaled_dot_product_attention(q, k, v, attn_mask=mask)
+            a = a.transpose(1, 2).reshape(B, S, H)
+            x = F.layer_norm(x + F.linear(a, p[f"l{i}.o.w"], p[f"l{i}.o.b"]), (H,), p[f"l{i}.ln1.g"], p[f"l{i}.ln1.b"], cfg.eps)
+            h = F.gelu(F.linear(x, p[f"l{i}.ffn1.w"], p[f"l{i}.ffn1.b"]))
+            x = F.layer_norm(x + F.linear(h, p[f"l{i}.ffn2.w"], p[f"l{i}.ffn2.b"]), (H,), p[f"l{i}.ln2.g"], p[f"l{i}.ln2.b"], cfg.eps)
+        pooled = torch.tanh(F.linear(x[:, 0], p["pooler.w"], p["pooler.b"]))
+        return F.linear(pooled, p["cls.w"], p["cls.b"])
+
+    __call__ = forward
+
+
+class BertFused:
+    """BERT on the CDNA4 kernels; capturable (all shapes static per (batch, seq) bucket)."""
+
+    def __init__(self, p: Dict[str, torch.Tensor], device, cfg: BertConfig = BERT_BASE):
+        from .. import ops
+
+        self.ops = ops
+        self.cfg = cfg
+        self.device = torch.device(device)
+        bf = lambda t: t.to(device=self.device, dtype=torch.bfloat16).contiguous()  # noqa: E731
+        f32 = lambda t: t.to(device=self.device, dtype=torch.float32).contiguous()  # noqa: E731
+        self.w = {}
+        for k, v in p.items():
+            if k.endswith(".b") and not k.startswith("emb.ln") and ".ln" not in k:
+                self.w[k] = f32(v)  # GEMM epilogue biases in fp32
+            else:
+                self.w[k] = bf(v)
+        # classifier padded to a multiple of 8 output columns; padded logits pinned to -1e30
+        C = cfg.num_labels
+        Cp = (C + 7) // 8 * 8
+        self.num_labels = C
+        cw = torch.zeros(Cp, cfg.hidden, device=self.device, dtype=torch.bfloat16)
+        cw[:C] = self.w["cls.w"]
+        cb = torch.full((Cp,), -1e30, device=self.device, dtype=torch.float32)
+        cb[:C] = self.w["cls.b"]
+        self.cls_w, self.cls_b = cw, cb
+        self.workspace = torch.empty(16 << 20, device=self.device, dtype=torch.float32)
+
+    def forward(self, ids: torch.Tensor, type_ids: Optional[torch.Tensor], lens: torch.Tensor) -> torch.Tensor:
+        """ids/type_ids int32 ``[B, S]``, lens int32 ``[B]`` -> bf16 logits ``[B, Cpad]``."""
+        ops, cfg, w = self.ops, self.cfg, self.w
+        B, S = ids.shape
+        H = cfg.hidden
+        ids_f = ids.reshape(-1)
+        tt_f = type_ids.reshape(-1) if type_ids is not None else None
+        x = ops.embed_layernorm(ids_f, tt_f, w["emb.word"], w["emb.pos"], w["emb.type"], w["emb.ln.g"], w["emb.ln.b"],
+                                S, eps=cfg.eps)
+        ws = self.workspace
+        for i in range(cfg.layers):
+            qkv = ops.gemm(x, w[f"l{i}.qkv.w"], w[f"l{i}.qkv.b"], workspace=ws)
+            a = ops.flash_attention(qkv, B, S, cfg.heads, cfg.heads, cfg.head_dim, kv_lens=lens)
+            h = ops.gemm(a, w[f"l{i}.o.w"], w[f"l{i}.o.b"], residual=x, workspace=ws)
+            x = ops.layernorm(h, w[f"l{i}.ln1.g"], w[f"l{i}.ln1.b"], eps=cfg.eps)
+            f1 = ops.gemm(x, w[f"l{i}.ffn1.w"], w[f"l{i}.ffn1.b"], act=ops.ACT_GELU, workspace=ws)
+            h = ops.gemm(f1, w[f"l{i}.ffn2.w"], w[f"l{i}.ffn2.b"], residual=x, workspace=ws)
+            x = ops.layernorm(h, w[f"l{i}.ln2.g"], w[f"l{i}.ln2.b"], eps=cfg.eps)
+        cls_rows = x.view(B, S, H)[:, 0].contiguous()
+        pooled = ops.gemm(cls_rows, w["pooler.w"], w["pooler.b"], act=ops.ACT_TANH, workspace=ws)
+        return ops.gemm(pooled, self.cls_w, self.cls_b, workspace=ws)
+
+    __call__ = forward
+
+    def classify(self, ids, type_ids, lens, k: int = 2):
+        logits = self.forward(ids, type_ids, lens)
+        return self.ops.softmax_topk(logits, min(k, self.num_labels))
+
+
+def pack_requests(token_lists: Sequence[Sequence[int]], seq_len: int) -> torch.Tensor:
+    """Engine sample layout for one seq bucket: int32 ``[n, 2*S + 1]`` = ids | type ids | length."""
+    n = len(token_lists)
+    out = torch.zeros(n, 2 * seq_len + 1, dtype=torch.int32)
+    for i, t in enumerate(token_lists):
+        t = list(t)[:seq_len]
+        out[i, : len(t)] = torch.tensor(t, dtype=torch.int32)
+        out[i, 2 * seq_len] = len(t)
+    return out
+
+
+def unpack_requests(x: torch.Tensor, seq_len: int):
+    ids = x[:, :seq_len].contiguous()
+    tt = x[:, seq_len: 2 * seq_len].contiguous()
+    lens = x[:, 2 * seq_len].contiguous()
+    return ids, tt, lens

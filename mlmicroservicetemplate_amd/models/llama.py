@@ -1,0 +1,398 @@
+"""Llama-3-8B generation with Megatron-style tensor parallelism (BASELINE.json config 5, P3/P6
+of SURVEY.md §2.E.3).  No reference counterpart (the reference model is a stub).
+
+Sharding per rank r of ``tp`` (one process per GPU, RCCL over xGMI):
+  * column-parallel: fused QKV (``hq = heads/tp`` query heads, ``hkv = kv_heads/tp`` KV heads),
+    fused gate/up (``I/tp`` rows each, interleaved for the SiLU-mul epilogue);
+  * row-parallel: o_proj and down_proj -> one all-reduce each per layer (X2, 2 x 32 / forward);
+  * vocab-parallel embedding (out-of-shard ids give zero rows, then all-reduce, X3) and lm_head
+    (each rank takes a local top-k of its 16032-row shard; ranks all-gather only k candidates
+    per sequence and merge -- X4 -- instead of gathering 128256 logits).
+The residual add is fused into the RMSNorm kernel AFTER the all-reduce (adding the replicated
+residual before it would count it ``tp`` times).
+
+Two backends with identical structure and communication:
+  * ``reference``: plain PyTorch fp32 math on bf16 weights (runs on CPU with gloo -- the TP
+    logic is tested there against TP=1);
+  * ``fused``: the CDNA4 kernels (MFMA GEMMs with fused SiLU-mul, RMSNorm+residual, RoPE,
+    KV-cache append, MFMA flash-attention prefill, split-KV decode attention, top-k).
+Weights are random-init (std 0.02) and generated per tensor from a (seed, name) generator on
+the target device, then sliced to the rank's shard -- every rank gets exactly the slice of the
+same full model, without any rank materialising the whole 8B model.
+"""
+from __future__ import annotations
+
+import hashlib
+import math
+import re
+import zlib
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+from ..ops import reference as R
+
+
+@dataclass
+class LlamaConfig:
+    vocab: int = 128256
+    hidden: int = 4096
+    layers: int = 32
+    heads: int = 32
+    kv_heads: int = 8
+    head_dim: int = 128
+    intermediate: int = 14336
+    rope_theta: float = 500000.0
+    eps: float = 1e-5
+    bos_id: int = 128000
+    eos_ids: Tuple[int, ...] = (128001, 128009)
+
+
+LLAMA3_8B = LlamaConfig()
+
+
+def tiny_config(**kw) -> LlamaConfig:
+    base = dict(vocab=2048, hidden=256, layers=2, heads=8, kv_heads=4, head_dim=32, intermediate=512, bos_id=1,
+                eos_ids=(2,))
+    base.update(kw)
+    return LlamaConfig(**base)
+
+
+@dataclass
+class ShardDims:
+    tp: int
+    rank: int
+    hq: int
+    hkv: int
+    inter: int
+    vocab_shard: int
+    vocab_lo: int
+
+    @property
+    def qkv_rows(self) -> int:
+        return 0
+
+
+def shard_dims(cfg: LlamaConfig, tp: int, rank: int) -> ShardDims:
+    if cfg.heads % tp or cfg.intermediate % tp:
+        raise ValueError(f"tp={tp} must divide heads and intermediate")
+    hkv = cfg.kv_heads // tp if cfg.kv_heads >= tp else 1
+    if cfg.kv_heads >= tp and cfg.kv_heads % tp:
+        raise ValueError("tp must divide kv_heads (or exceed it)")
+    vs = -(-cfg.vocab // tp)
+    vs = (vs + 7) // 8 * 8
+    return ShardDims(tp, rank, cfg.heads // tp, hkv, cfg.intermediate // tp, vs, rank * vs)
+
+
+def _gen(seed: int, name: str, device) -> torch.Generator:
+    h = int.from_bytes(hashlib.sha256(f"{seed}:{name}".encode()).digest()[:8], "little") & ((1 << 63) - 1)
+    g = torch.Generator(device=device)
+    g.manual_seed(h)
+    return g
+
+
+def _full(seed, name, shape, device, kind="normal"):
+    g = _gen(seed, name, device)
+    if kind == "norm":
+        return 1.0 + 0.1 * torch.randn(*shape, generator=g, device=device)
+    return torch.randn(*shape, generator=g, device=device) * 0.02
+
+
+def init_llama_shard(cfg: LlamaConfig, tp: int = 1, rank: int = 0, seed: int = 0, device="cpu",
+                     dtype=torch.bfloat16) -> Dict[str, torch.Tensor]:
+    """This rank's shard of a random-init Llama (the same full model for every tp)."""
+    sd = shard_dims(cfg, tp, rank)
+    H, D = cfg.hidden, cfg.head_dim
+    kv_rep = cfg.kv_heads < tp  # more ranks than KV heads: replicate a head over tp/kv_heads ranks
+    p: Dict[str, torch.Tensor] = {}
+
+    def vocab_rows(name):
+        full = _full(seed, name, (cfg.vocab, H), device)
+        lo, hi = sd.vocab_lo, min(cfg.vocab, sd.vocab_lo + sd.vocab_shard)
+        out = torch.zeros(sd.vocab_shard, H, device=device)
+        if hi > lo:
+            out[: hi - lo] = full[lo:hi]
+        return out.to(dtype)
+
+    p["embed"] = vocab_rows("embed")
+    p["lm_head"] = vocab_rows("lm_head")
+    p["final_norm"] = _full(seed, "final_norm", (H,), device, "norm").to(dtype)
+    for i in range(cfg.layers):
+        wq = _full(seed, f"l{i}.q", (cfg.heads * D, H), device)
+        wk = _full(seed, f"l{i}.k", (cfg.kv_heads * D, H), device)
+        wv = _full(seed, f"l{i}.v", (cfg.kv_heads * D, H), device)
+        q = wq[rank * sd.hq * D: (rank + 1) * sd.hq * D]
+        kvh = (rank * cfg.kv_heads) // tp if kv_rep else rank * sd.hkv
+        k = wk[kvh * D: (kvh + sd.hkv) * D]
+        v = wv[kvh * D: (kvh + sd.hkv) * D]
+        p[f"l{i}.qkv"] = torch.cat([q, k, v]).to(dtype).contiguous()
+        wo = _full(seed, f"l{i}.o", (H, cfg.heads * D), device)
+        p[f"l{i}.o"] = wo[:, rank * sd.hq * D: (rank + 1) * sd.hq * D].to(dtype).contiguous()
+        wg = _full(seed, f"l{i}.gate", (cfg.intermediate, H), device)
+        wu = _full(seed, f"l{i}.up", (cfg.intermediate, H), device)
+        sl = slice(rank * sd.inter, (rank + 1) * sd.inter)
+        p[f"l{i}.gate"] = wg[sl].to(dtype).contiguous()
+        p[f"l{i}.up"] = wu[sl].to(dtype).contiguous()
+        wd = _full(seed, f"l{i}.down", (H, cfg.intermediate), device)
+        p[f"l{i}.down"] = wd[:, sl].to(dtype).contiguous()
+        p[f"l{i}.attn_norm"] = _full(seed, f"l{i}.attn_norm", (H,), device, "norm").to(dtype)
+        p[f"l{i}.mlp_norm"] = _full(seed, f"l{i}.mlp_norm", (H,), device, "norm").to(dtype)
+        del wq, wk, wv, wo, wg, wu, wd
+    return p
+
+
+# --------------------------------------------------------------------------- tokenizer
+class LlamaTokenizer:
+    """Offline tokenizer: with a ``tokenizer.json`` the real BPE (``tokenizers``) is used;
+    otherwise words are hashed into the vocab (synthetic ids) and decoded as ``<id>``."""
+
+    _WORD = re.compile(r"\w+|[^\w\s]")
+
+    def __init__(self, cfg: LlamaConfig, tokenizer_file: Optional[str] = None):
+        self.cfg = cfg
+        self._tok = None
+        if tokenizer_file:
+            from tokenizers import Tokenizer
+
+            self._tok = Tokenizer.from_file(tokenizer_file)
+
+    def encode(self, text: str) -> List[int]:
+        if self._tok is not None:
+            return [self.cfg.bos_id] + self._tok.encode(text).ids
+        span = self.cfg.vocab - 1024
+        return [self.cfg.bos_id] + [256 + zlib.crc32(w.encode()) % span for w in self._WORD.findall(text)]
+
+    def decode(self, ids: Sequence[int]) -> str:
+        if self._tok is not None:
+            return self._tok.decode(list(ids))
+        return " ".join(f"<{i}>" for i in ids)
+
+
+# --------------------------------------------------------------------------- comm
+class TPComm:
+    """Tensor-parallel collectives over a torch.distributed group (RCCL on GPU, gloo on CPU)."""
+
+    def __init__(self, group=None, tp: int = 1):
+        self.group = group
+        self.tp = tp
+
+    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+        if self.tp > 1:
+            dist.all_reduce(t, group=self.group)
+        return t
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        if self.tp == 1:
+            return t.unsqueeze(0)
+        out = [torch.empty_like(t) for _ in range(self.tp)]
+        dist.all_gather(out, t.contiguous(), group=self.group)
+        return torch.stack(out)
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        if self.tp > 1:
+            dist.broadcast(t, src=src, group=self.group)
+        return t
+
+
+@dataclass
+class GenParams:
+    max_new_tokens: int = 16
+    top_k: int = 1  # 1 = greedy
+    temperature: float = 1.0
+    seed: int = 0
+
+
+class LlamaTP:
+    """One rank of a tensor-parallel Llama with a KV cache ``[layers][max_batch, max_seq, hkv, D]``."""
+
+    def __init__(self, params: Dict[str, torch.Tensor], cfg: LlamaConfig, tp: int = 1, rank: int = 0,
+                 comm: Optional[TPComm] = None, backend: str = "reference", device="cpu", max_batch: int = 8,
+                 max_seq: int = 1024, top_k_max: int = 50):
+        self.cfg = cfg
+        self.sd = shard_dims(cfg, tp, rank)
+        self.tp, self.rank = tp, rank
+        self.comm = comm or TPComm(None, tp)
+        self.backend = backend
+        self.device = torch.device(device)
+        self.max_batch, self.max_seq = max_batch, max_seq
+        self.top_k_max = top_k_max
+        D = cfg.head_dim
+        self.p = {k: v.to(self.device) for k, v in params.items()}
+        if backend == "fused":
+            from .. import ops
+
+            self.ops = ops
+            for i in range(cfg.layers):
+                self.p[f"l{i}.gate_up"] = ops.interleave_gate_up(self.p.pop(f"l{i}.gate"), self.p.pop(f"l{i}.up"))
+            self.workspace = torch.empty(32 << 20, device=self.device, dtype=torch.float32)
+            self.dec_ws = torch.empty(max_batch * self.sd.hq * (-(-max_seq // 256)) * (D + 2) + 16,
+                                      device=self.device, dtype=torch.float32)
+        cdt = torch.bfloat16 if backend == "fused" else torch.float32
+        self.k_cache = [torch.zeros(max_batch, max_seq, self.sd.hkv, D, device=self.device, dtype=cdt)
+                        for _ in range(cfg.layers)]
+        self.v_cache = [torch.zeros_like(self.k_cache[0]) for _ in range(cfg.layers)]
+        self.cos, self.sin = R.rope_tables(max_seq, D, cfg.rope_theta, self.device)
+
+    # ---------------------------------------------------------------- shared pieces
+    @property
+    def qkv_width(self) -> int:
+        return (self.sd.hq + 2 * self.sd.hkv) * self.cfg.head_dim
+
+    def _embed(self, ids: torch.Tensor) -> torch.Tensor:
+        sd = self.sd
+        if self.backend == "fused":
+            x = self.ops.embedding(ids, self.p["embed"], lo=sd.vocab_lo, hi=sd.vocab_lo + sd.vocab_shard)
+        else:
+            local = ids.long() - sd.vocab_lo
+            ok = (local >= 0) & (local < sd.vocab_shard)
+            x = self.p["embed"][local.clamp(0, sd.vocab_shard - 1)].float() * ok.unsqueeze(-1)
+        return self.comm.all_reduce_(x)
+
+    def _local_topk(self, logits: torch.Tensor, k: int):
+        if self.backend == "fused":
+            vals, idx = self.ops.topk_large(logits, k)
+        else:
+            vals, idx = torch.topk(logits.float(), k, dim=-1)
+            idx = idx.to(torch.int32)
+        # mask rows of the padded vocab tail
+        idx = idx + self.sd.vocab_lo
+        vals = torch.where(idx < self.cfg.vocab, vals, torch.full_like(vals, float("-inf")))
+        return vals, idx
+
+    def _merge_sample(self, vals: torch.Tensor, idx: torch.Tensor, gp: GenParams, step: int) -> torch.Tensor:
+        """X4: all-gather the ranks' top-k candidates, merge, pick the next token (identical on
+        every rank: same inputs, same seeded generator -> no broadcast needed)."""
+        allv = self.comm.all_gather(vals)  # [tp, B, k]
+        alli = self.comm.all_gather(idx)
+        B = vals.shape[0]
+        cv = allv.permute(1, 0, 2).reshape(B, -1)
+        ci = alli.permute(1, 0, 2).reshape(B, -1)
+        if gp.top_k <= 1:
+            best = cv.argmax(-1, keepdim=True)
+            return ci.gather(1, best).squeeze(1)
+        k = min(gp.top_k, cv.shape[1])
+        tv, tpos = torch.topk(cv, k, dim=-1)
+        probs = torch.softmax(tv / max(gp.temperature, 1e-5), dim=-1).cpu()
+        g = torch.Generator().manual_seed(gp.seed * 1000003 + step)
+        pick = torch.multinomial(probs, 1, generator=g).to(tpos.device)
+        return ci.gather(1, tpos.gather(1, pick)).squeeze(1)
+
+    # ---------------------------------------------------------------- reference backend
+    def _ref_layer(self, i: int, x: torch.Tensor, B: int, S: int, positions: torch.Tensor, lens: torch.Tensor,
+                   slots_b: torch.Tensor, decode: bool) -> torch.Tensor:
+        cfg, sd, p = self.cfg, self.sd, self.p
+        D = cfg.head_dim
+        xn = R.layernorm(x, p[f"l{i}.attn_norm"], None, eps=cfg.eps, rms=True)[0]
+        qkv = xn @ p[f"l{i}.qkv"].float().T
+        T = qkv.shape[0]
+        q = R.rope(qkv[:, : sd.hq * D].view(T, sd.hq, D), positions, self.cos, self.sin)
+        k = R.rope(qkv[:, sd.hq * D: (sd.hq + sd.hkv) * D].view(T, sd.hkv, D), positions, self.cos, self.sin)
+        v = qkv[:, (sd.hq + sd.hkv) * D:].view(T, sd.hkv, D)
+        b_of = torch.arange(B, device=x.device).repeat_interleave(T // B)
+        valid = positions < self.max_seq
+        if not decode:
+            valid = valid & (positions < lens.long()[b_of])
+        bi, pi = b_of[valid], positions[valid].long()
+        self.k_cache[i][bi, pi] = k[valid].to(self.k_cache[i].dtype)
+        self.v_cache[i][bi, pi] = v[valid].to(self.v_cache[i].dtype)
+        if decode:
+            qrow = q.reshape(B, sd.hq * D)
+            a = R.decode_attention(qrow, self.k_cache[i][:B], self.v_cache[i][:B], lens, sd.hq, sd.hkv, D)
+        else:
+            qkv_r = torch.cat([q.reshape(T, -1), k.reshape(T, -1), v.reshape(T, -1)], dim=1)
+            a = R.attention(qkv_r, B, S, sd.hq, sd.hkv, D, kv_lens=lens, causal=True)
+        o = self.comm.all_reduce_(a @ p[f"l{i}.o"].float().T)
+        x = x + o
+        xn = R.layernorm(x, p[f"l{i}.mlp_norm"], None, eps=cfg.eps, rms=True)[0]
+        h = F.silu(xn @ p[f"l{i}.gate"].float().T) * (xn @ p[f"l{i}.up"].float().T)
+        d = self.comm.all_reduce_(h @ p[f"l{i}.down"].float().T)
+        return x + d
+
+    def _ref_forward(self, ids: torch.Tensor, positions: torch.Tensor, lens: torch.Tensor, B: int, S: int,
+                     decode: bool, k: int):
+        x = self._embed(ids.reshape(-1))
+        for i in range(self.cfg.layers):
+            x = self._ref_layer(i, x, B, S, positions.reshape(-1), lens, None, decode)
+        xn = R.layernorm(x, self.p["final_norm"], None, eps=self.cfg.eps, rms=True)[0]
+        if not decode:
+            last = (torch.arange(B, device=x.device) * S + lens.long() - 1)
+            xn = xn[last]
+        logits = xn @ self.p["lm_head"].float().T
+        return self._local_topk(logits, k)
+
+    # ---------------------------------------------------------------- fused backend
+    def _fused_forward(self, ids: torch.Tensor, positions: torch.Tensor, lens: torch.Tensor, B: int, S: int,
+                       decode: bool, k: int, slots: torch.Tensor):
+        ops, cfg, sd, p = self.ops, self.cfg, self.sd, self.p
+        D = cfg.head_dim
+        ws = self.workspace
+        r = self._embed(ids.reshape(-1))  # residual stream (bf16)
+        delta = None
+        for i in range(cfg.layers):
+            if delta is None:
+                xn = ops.rmsnorm(r, p[f"l{i}.attn_norm"], eps=cfg.eps)
+            else:
+                xn = ops.rmsnorm(delta, p[f"l{i}.attn_norm"], residual=r, residual_out=r, eps=cfg.eps)
+            qkv = ops.gemm(xn, p[f"l{i}.qkv"], workspace=ws)
+            ops.rope_(qkv, positions.reshape(-1), self.cos, self.sin, sd.hq + sd.hkv, D)
+            ops.kv_append(qkv, sd.hq * D, (sd.hq + sd.hkv) * D, slots, self.k_cache[i], self.v_cache[i], sd.hkv, D)
+            if decode:
+                a = ops.decode_attention(qkv, self.k_cache[i][:B], self.v_cache[i][:B], lens, sd.hq, sd.hkv, D,
+                                         workspace=self.dec_ws)
+            else:
+                a = ops.flash_attention(qkv, B, S, sd.hq, sd.hkv, D, kv_lens=lens, causal=True)
+            o = self.comm.all_reduce_(ops.gemm(a, p[f"l{i}.o"], workspace=ws))
+            xn = ops.rmsnorm(o, p[f"l{i}.mlp_norm"], residual=r, residual_out=r, eps=cfg.eps)
+            gu = ops.gemm(xn, p[f"l{i}.gate_up"], act=ops.ACT_SILU_MUL, workspace=ws)
+            delta = self.comm.all_reduce_(ops.gemm(gu, p[f"l{i}.down"], workspace=ws))
+        xn = ops.rmsnorm(delta, p["final_norm"], residual=r, eps=cfg.eps)
+        if not decode:
+            last = (torch.arange(B, device=xn.device, dtype=torch.int64) * S + lens.long() - 1)
+            xn = xn.index_select(0, last)
+        logits = ops.gemm(xn.contiguous(), p["lm_head"], workspace=ws)
+        return self._local_topk(logits, k)
+
+    # ---------------------------------------------------------------- public
+    def _slots(self, B: int, S: int, positions: torch.Tensor, lens: torch.Tensor, decode: bool) -> torch.Tensor:
+        b = torch.arange(B, device=self.device, dtype=torch.int64).repeat_interleave(S)
+        pos = positions.reshape(-1).long()
+        slots = b * self.max_seq + pos
+        if not decode:
+            slots = torch.where(pos < lens.long()[b], slots, torch.full_like(slots, -1))
+        return slots.to(torch.int32)
+
+    @torch.no_grad()
+    def step(self, ids: torch.Tensor, positions: torch.Tensor, lens: torch.Tensor, decode: bool, k: int):
+        B, S = ids.shape
+        if self.backend == "fused":
+            slots = self._slots(B, S, positions, lens, decode)
+            return self._fused_forward(ids.to(torch.int32), positions.to(torch.int32), lens.to(torch.int32), B, S,
+                                       decode, k, slots)
+        return self._ref_forward(ids, positions, lens, B, S, decode, k)
+
+    @torch.no_grad()
+    def generate(self, ids: torch.Tensor, lens: torch.Tensor, gp: GenParams) -> torch.Tensor:
+        """ids int ``[B, S]`` (right-padded), lens ``[B]`` -> generated ``[B, max_new_tokens]``."""
+        B, S = ids.shape
+        if B > self.max_batch or S + gp.max_new_tokens > self.max_seq:
+            raise ValueError("batch / sequence exceed the KV cache")
+        dev = self.device
+        ids = ids.to(dev)
+        lens = lens.to(dev).to(torch.int32)
+        k = max(1, min(gp.top_k, self.top_k_max))
+        pos = torch.arange(S, device=dev, dtype=torch.int32).unsqueeze(0).expand(B, S).contiguous()
+        vals, idx = self.step(ids, pos, lens, decode=False, k=k)
+        out = []
+        tok = self._merge_sample(vals, idx, gp, 0)
+        out.append(tok)
+        cur = lens.clone()
+        for t in range(1, gp.max_new_tokens):
+            # the new token sits at position cur; attention covers cur + 1 keys
+            vals, idx = self.step(tok.view(B, 1).to(torch.int32), cur.view(B, 1), cur + 1, decode=True, k=k)
+            tok = self._merge_sample(vals, idx, gp, t)
+            out.append(tok)
+            cur = cur + 1
+        return torch.stack(out, dim=1)

@@ -17,8 +17,8 @@ import torch
 from . import _lib
 from ._lib import NativeError, available, check, lib, stream_ptr
 
-ACT_NONE, ACT_RELU, ACT_GELU, ACT_TANH, ACT_SILU = 0, 1, 2, 3, 4
-_ACTS = {None: 0, "none": 0, "relu": 1, "gelu": 2, "tanh": 3, "silu": 4}
+ACT_NONE, ACT_RELU, ACT_GELU, ACT_TANH, ACT_SILU, ACT_SILU_MUL = 0, 1, 2, 3, 4, 5
+_ACTS = {None: 0, "none": 0, "relu": 1, "gelu": 2, "tanh": 3, "silu": 4, "silu_mul": 5}
 
 __all__ = [
     "NativeError",
@@ -146,7 +146,9 @@ def gemm(
     cfg: int = 0,
     splitk: int = 0,
 ) -> torch.Tensor:
-    """``act(a @ w.T * scale + bias (+ residual))``; a ``[M,K]``, w ``[N,K]`` (nn.Linear layout)."""
+    """``act(a @ w.T * scale + bias (+ residual))``; a ``[M,K]``, w ``[N,K]`` (nn.Linear layout).
+    ``act="silu_mul"``: w rows are gate/up interleaved in groups of 8 (:func:`interleave_gate_up`)
+    and the output is ``silu(gate) * up`` of width N/2."""
     dev = a.device
     _need(a, "a", torch.bfloat16, dev)
     _need(w, "w", torch.bfloat16, dev)
@@ -165,12 +167,15 @@ def gemm(
         _need(residual, "residual", torch.bfloat16, dev)
         if tuple(residual.shape) != (M, N):
             raise ValueError("residual must be [M, N]")
+    n_out = N // 2 if _act(act) == ACT_SILU_MUL else N
+    if _act(act) == ACT_SILU_MUL and (N % 16 or scale is not None or residual is not None):
+        raise ValueError("silu_mul needs N % 16 == 0 and no scale/residual")
     if out is None:
-        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        out = torch.empty(M, n_out, device=dev, dtype=torch.bfloat16)
     else:
         _need(out, "out", torch.bfloat16, dev)
-        if tuple(out.shape) != (M, N):
-            raise ValueError("out must be [M, N]")
+        if tuple(out.shape) != (M, n_out):
+            raise ValueError(f"out must be [M, {n_out}]")
     wsp, wsb = _workspace_args(workspace)
     rc = lib().mls_gemm(
         a.data_ptr(), w.data_ptr(), _ptr(scale), _ptr(bias), _ptr(residual), out.data_ptr(), wsp, wsb,
@@ -178,6 +183,15 @@ def gemm(
     )
     check(rc, "mls_gemm")
     return out
+
+
+def interleave_gate_up(gate: torch.Tensor, up: torch.Tensor) -> torch.Tensor:
+    """``[I, K]`` gate and up projections -> ``[2I, K]`` rows interleaved in groups of 8
+    (gate 0-7, up 0-7, gate 8-15, ...), the layout of the fused SiLU-mul GEMM epilogue."""
+    I, K = gate.shape
+    if I % 8:
+        raise ValueError("intermediate size must be a multiple of 8")
+    return torch.stack([gate.view(I // 8, 8, K), up.view(I // 8, 8, K)], dim=1).reshape(2 * I, K).contiguous()
 
 
 def gemm_heuristic(M: int, N: int, K: int) -> Tuple[int, int]:
@@ -413,3 +427,21 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
                                     max_len, chunk, float(scale), stream_ptr(dev))
     check(rc, "mls_decode_attention")
     return out
+
+
+def topk_large(x: torch.Tensor, k: int, max_chunk: int = 16384) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Raw-logit top-k of rows longer than one LDS-resident row: split each row into equal
+    chunks (per-chunk top-k in the kernel), then merge the ``chunks * k`` candidates."""
+    rows, N = x.shape
+    if N <= max_chunk:
+        return softmax_topk(x, k, softmax=False)
+    c = -(-N // max_chunk)
+    while N % c:
+        c += 1
+    L = N // c
+    vals, idx = softmax_topk(x.reshape(rows * c, L), k, softmax=False)
+    vals = vals.view(rows, c * k)
+    off = (torch.arange(c, device=x.device, dtype=torch.int32) * L).repeat_interleave(k)
+    idx = idx.view(rows, c * k) + off
+    tv, tp = torch.topk(vals, k, dim=-1)
+    return tv, idx.gather(1, tp)

@@ -96,7 +96,7 @@ MLS_DEV int xcd_remap(int bid, int nwg) {
 MLS_DEV float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 MLS_DEV float silu(float x) { return x / (1.f + __expf(-x)); }
 
-enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_TANH = 3, ACT_SILU = 4 };
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_TANH = 3, ACT_SILU = 4, ACT_SILU_MUL = 5 };
 MLS_DEV float apply_act(float v, int act) {
   switch (act) {
     case ACT_RELU: return fmaxf(v, 0.f);

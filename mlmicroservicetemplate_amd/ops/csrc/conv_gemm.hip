@@ -226,6 +226,27 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
   __syncthreads();
 
   constexpr int CPR = BN / 8;
+  if (a.act == ACT_SILU_MUL && a.splitk == 1) {
+    // gate/up interleaved in 8-column groups: chunk 2p = gate, 2p+1 = up -> 8 outputs at n/2
+    for (int q = tid; q < BM * (CPR / 2); q += NTHREADS) {
+      const int row = q / (CPR / 2), p = q - (q / (CPR / 2)) * (CPR / 2);
+      const int m = m0 + row, n = n0 + p * 16;
+      if (m >= a.M || n >= a.N) continue;
+      const float* src = Cs + row * C_LD + p * 16;
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float gt = src[e], up = src[8 + e];
+        if (a.bias) {
+          gt += a.bias[n + e];
+          up += a.bias[n + 8 + e];
+        }
+        o[e] = silu(gt) * up;
+      }
+      st16(a.out + (size_t)m * a.ldo + (n >> 1), pack8(o));
+    }
+    return;
+  }
   for (int q = tid; q < BM * CPR; q += NTHREADS) {
     const int row = q / CPR, c8 = q - (q / CPR) * CPR;
     const int m = m0 + row, n = n0 + c8 * 8;
@@ -261,17 +282,32 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
 
 // sum split-K slabs + epilogue; one thread per 8 outputs
 __global__ __launch_bounds__(256) void splitk_epilogue_kernel(const ConvArgs a) {
-  const int nc = a.N / 8;
+  const bool glu = a.act == ACT_SILU_MUL;
+  const int nc = glu ? a.N / 16 : a.N / 8;  // output chunks of 8 per row
   const long total = (long)a.M * nc;
   for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
-    const int m = (int)(q / nc), n = (int)(q - (q / nc) * nc) * 8;
-    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int m = (int)(q / nc), c = (int)(q - (q / nc) * nc);
+    const int n = glu ? c * 16 : c * 8;
+    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0}, u[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int s = 0; s < a.splitk; ++s) {
       const float* src = a.ws + ((size_t)s * a.M + m) * a.N + n;
-      const float4 p0 = *reinterpret_cast<const float4*>(src);
-      const float4 p1 = *reinterpret_cast<const float4*>(src + 4);
-      v[0] += p0.x; v[1] += p0.y; v[2] += p0.z; v[3] += p0.w;
-      v[4] += p1.x; v[5] += p1.y; v[6] += p1.z; v[7] += p1.w;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += src[e];
+      if (glu) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) u[e] += src[8 + e];
+      }
+    }
+    if (glu) {
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float gt = v[e] + (a.bias ? a.bias[n + e] : 0.f);
+        const float up = u[e] + (a.bias ? a.bias[n + 8 + e] : 0.f);
+        o[e] = silu(gt) * up;
+      }
+      st16(a.out + (size_t)m * a.ldo + (n >> 1), pack8(o));
+      continue;
     }
     if (a.scale) {
 #pragma unroll
@@ -333,6 +369,7 @@ void choose_cfg(int M, int N, int K, int& cfg, int& splitk) {
 }
 
 int launch_conv(ConvArgs a, int mode, int cfg, int splitk, size_t ws_bytes, hipStream_t st) {
+  if (a.act == ACT_SILU_MUL && a.N % 16 != 0) return MLS_BAD_ARG;
   if (a.N % 8 != 0 || a.M <= 0 || a.N <= 0 || a.K <= 0 || a.K % 8 != 0) return MLS_BAD_ARG;
   int acfg = 0, asplit = 1;
   choose_cfg(a.M, a.N, a.K, acfg, asplit);
@@ -429,7 +466,7 @@ int mls_gemm(const void* A, const void* W, const float* scale, const float* bias
   a.M = M;
   a.K = K;
   a.act = act;
-  a.ldo = N;
+  a.ldo = act == ACT_SILU_MUL ? N / 2 : N;
   a.ldr = N;
   const size_t xb = (size_t)M * K * 2, wb = (size_t)N * K * 2;
   if (xb >= 0x7FFFFFFFull || wb >= 0x7FFFFFFFull) return MLS_UNSUPPORTED;

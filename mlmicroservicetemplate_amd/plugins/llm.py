@@ -1,0 +1,164 @@
+"""``llama`` plugin: ``POST /generate`` on Llama-3-8B, tensor-parallel over the node (config 5).
+
+Request: ``{"prompt": str | "input_ids": [int], "max_new_tokens": int, "top_k": int,
+"temperature": float, "seed": int}``.  Concurrent requests are micro-batched (same batcher as
+``/predict``); a batch is right-padded and generated together (batched prefill with per-sequence
+lengths, then lockstep decode steps over the KV cache).
+
+Multi-GPU: rank 0 owns HTTP.  For each batch it broadcasts a small command header and the
+token ids to the other ranks (X5); every rank then runs the same TP forward, and the
+top-k candidate merge makes the sampled token identical on all ranks, so no per-token
+broadcast is needed.  Followers sit in :meth:`follower_loop` until rank 0 sends STOP.
+"""
+from __future__ import annotations
+
+import logging
+import threading
+from typing import Any, Dict, List, Tuple
+
+import torch
+
+from .base import ModelPlugin, PluginContext, register
+
+logger = logging.getLogger("mlsamd.plugin")
+
+OP_STOP, OP_GENERATE = 0, 1
+
+
+@register("llama")
+class LlamaPlugin(ModelPlugin):
+    name = "llama"
+    batched = True
+    task = "generate"
+
+    def __init__(self):
+        self.model = None
+        self.tok = None
+        self.ctx = None
+        self.comm_dev = None
+        self._lock = threading.Lock()
+
+    def init(self, ctx: PluginContext) -> None:
+        from ..models import llama
+
+        self.ctx = ctx
+        s = ctx.settings
+        extra = s.model_yaml() if hasattr(s, "model_yaml") else {}
+        size = extra.get("config", "8b")
+        cfg = llama.LLAMA3_8B if size == "8b" else llama.tiny_config(**extra.get("overrides", {}))
+        tp = ctx.world_size if int(s.TP) > 1 else 1
+        if tp > 1 and ctx.world_size != tp:
+            raise RuntimeError(f"TP={s.TP} needs WORLD_SIZE={tp}")
+        on_gpu = torch.cuda.is_available() and bool(ctx.devices)
+        dev = ctx.devices[0] if on_gpu else "cpu"
+        backend = s.BACKEND if (on_gpu and s.BACKEND == "fused") else "reference"
+        self.comm_dev = torch.device(dev)
+        params = llama.init_llama_shard(cfg, tp, ctx.rank, int(s.SEED), device=dev)
+        self.model = llama.LlamaTP(params, cfg, tp=tp, rank=ctx.rank, comm=llama.TPComm(None, tp), backend=backend,
+                                   device=dev, max_batch=int(s.MAX_BATCH), max_seq=int(extra.get("max_seq", 2048)))
+        self.tok = llama.LlamaTokenizer(cfg, extra.get("tokenizer_file"))
+        self.cfg = cfg
+        logger.info("llama ready: tp=%d rank=%d backend=%s device=%s", tp, ctx.rank, backend, dev)
+
+    # ------------------------------------------------------------------ request path
+    def prepare_generate(self, req: dict) -> Tuple[List[int], Any]:
+        from ..models.llama import GenParams
+
+        if "input_ids" in req:
+            ids = [int(i) for i in req["input_ids"]]
+        else:
+            ids = self.tok.encode(str(req["prompt"]))
+        gp = GenParams(max_new_tokens=int(req.get("max_new_tokens", self.ctx.settings.MAX_NEW_TOKENS)),
+                       top_k=int(req.get("top_k", 1)), temperature=float(req.get("temperature", 1.0)),
+                       seed=int(req.get("seed", 0)))
+        if not ids:
+            raise ValueError("empty prompt")
+        if gp.max_new_tokens < 1:
+            raise ValueError("max_new_tokens must be >= 1")
+        return ids, gp
+
+    def finish_generate(self, out: Any) -> dict:
+        prompt_len, toks = out
+        eos = set(self.cfg.eos_ids)
+        cut = next((i + 1 for i, t in enumerate(toks) if t in eos), len(toks))
+        toks = toks[:cut]
+        return {"token_ids": toks, "text": self.tok.decode(toks), "num_tokens": len(toks), "prompt_tokens": prompt_len}
+
+    def replicas(self):
+        def run_batch(samples):
+            groups: Dict[tuple, List[int]] = {}
+            for i, (_ids, gp) in enumerate(samples):
+                groups.setdefault((gp.top_k, gp.temperature, gp.seed), []).append(i)
+            results: List[Any] = [None] * len(samples)
+            for _key, members in groups.items():
+                ids_l = [samples[i][0] for i in members]
+                gp = samples[members[0]][1]
+                from ..models.llama import GenParams
+
+                gpg = GenParams(max(samples[i][1].max_new_tokens for i in members), gp.top_k, gp.temperature, gp.seed)
+                toks = self._generate_batch(ids_l, gpg)
+                for j, i in enumerate(members):
+                    results[i] = (len(ids_l[j]), toks[j][: samples[i][1].max_new_tokens])
+            return results
+
+        return [run_batch]
+
+    # ------------------------------------------------------------------ lockstep execution
+    def _broadcast_cmd(self, op: int, ids: torch.Tensor = None, lens: torch.Tensor = None, gp=None) -> None:
+        import torch.distributed as dist
+
+        if self.model.tp == 1:
+            return
+        hdr = torch.zeros(7, dtype=torch.int64, device=self.comm_dev)
+        if op == OP_GENERATE:
+            hdr[:] = torch.tensor([op, ids.shape[0], ids.shape[1], gp.max_new_tokens, gp.top_k,
+                                   int(gp.temperature * 1000), gp.seed])
+        dist.broadcast(hdr, src=0)
+        if op == OP_GENERATE:
+            dist.broadcast(ids.to(self.comm_dev), src=0)
+            dist.broadcast(lens.to(self.comm_dev), src=0)
+
+    def _generate_batch(self, ids_l: List[List[int]], gp) -> List[List[int]]:
+        S = max(len(t) for t in ids_l)
+        B = len(ids_l)
+        ids = torch.zeros(B, S, dtype=torch.int32)
+        for i, t in enumerate(ids_l):
+            ids[i, : len(t)] = torch.tensor(t, dtype=torch.int32)
+        lens = torch.tensor([len(t) for t in ids_l], dtype=torch.int32)
+        with self._lock:
+            self._broadcast_cmd(OP_GENERATE, ids, lens, gp)
+            out = self.model.generate(ids, lens, gp)
+        return out.cpu().tolist()
+
+    def follower_loop(self) -> int:
+        """Ranks > 0: execute rank 0's generate commands until STOP."""
+        import torch.distributed as dist
+
+        from ..models.llama import GenParams
+
+        while True:
+            hdr = torch.zeros(7, dtype=torch.int64, device=self.comm_dev)
+            dist.broadcast(hdr, src=0)
+            op, B, S, mnt, topk, temp, seed = hdr.tolist()
+            if op == OP_STOP:
+                logger.info("rank %d: stop", self.ctx.rank)
+                return 0
+            ids = torch.zeros(B, S, dtype=torch.int32, device=self.comm_dev)
+            lens = torch.zeros(B, dtype=torch.int32, device=self.comm_dev)
+            dist.broadcast(ids, src=0)
+            dist.broadcast(lens, src=0)
+            self.model.generate(ids, lens, GenParams(mnt, topk, temp / 1000.0, seed))
+
+    def close(self) -> None:
+        if self.model is not None and self.model.tp > 1 and self.ctx.rank == 0:
+            try:
+                self._broadcast_cmd(OP_STOP)
+            except Exception as e:  # followers may already be gone
+                logger.warning("stop broadcast failed: %s", e)
+
+    def describe(self) -> dict:
+        d = super().describe()
+        if self.model is not None:
+            d.update({"tp": self.model.tp, "backend": self.model.backend, "max_batch": self.model.max_batch,
+                      "max_seq": self.model.max_seq})
+        return d

@@ -1,0 +1,109 @@
+"""``bert`` plugin: BERT-base text classifier with dynamic request batching (config 3).
+
+``POST /predict`` takes the text as multipart field ``text`` (or a JSON body
+``{"text": ...}``).  Requests are tokenised on the CPU pool, micro-batched, padded to the
+smallest sequence bucket (32/64/128/256/512) that holds the longest request of the batch and
+run through one engine per sequence bucket (each with its own batch-bucket hipGraphs).
+"""
+from __future__ import annotations
+
+import logging
+from typing import Any, List
+
+import numpy as np
+
+from ..api.multipart import Part
+from .base import ModelPlugin, PluginContext, register
+
+logger = logging.getLogger("mlsamd.plugin")
+
+SEQ_BUCKETS = (32, 64, 128, 256, 512)
+
+
+@register("bert")
+class BertPlugin(ModelPlugin):
+    name = "bert"
+    batched = True
+    task = "text"
+    form_field = "text"
+
+    def __init__(self):
+        self.engines = {}  # device -> {seq bucket: GpuEngine}
+        self.labels: List[str] = []
+        self.tokenizer = None
+        self.max_seq = 128
+
+    def init(self, ctx: PluginContext) -> None:
+        import torch
+
+        from ..engine.worker import GpuEngine
+        from ..models import bert
+        from ..parallel import dist as mdist
+
+        s = ctx.settings
+        extra = s.model_yaml() if hasattr(s, "model_yaml") else {}
+        cfg = bert.BertConfig(num_labels=int(extra.get("num_labels", 2)))
+        self.labels = list(extra.get("labels", [f"label_{i}" for i in range(cfg.num_labels)]))
+        self.max_seq = int(extra.get("max_seq", 128))
+        self.tokenizer = bert.HashTokenizer(cfg.vocab, extra.get("vocab_file"))
+        devices = ctx.devices or (["cuda:0"] if torch.cuda.is_available() else [])
+        if not devices:
+            raise RuntimeError("bert plugin needs a GPU")
+        params = bert.init_bert(cfg, int(s.SEED)) if ctx.rank == 0 else None
+        if ctx.world_size > 1:
+            spec = bert.bert_spec(cfg)
+            params = mdist.broadcast_state(params, src=0, device=torch.device(devices[0]), spec=spec)
+        buckets = [b for b in s.GRAPH_BUCKETS if b <= s.MAX_BATCH]
+        seqs = [q for q in SEQ_BUCKETS if q <= self.max_seq] or [self.max_seq]
+        for dev in devices:
+            if s.BACKEND == "fused":
+                model = bert.BertFused(params, dev, cfg)
+            else:
+                model = bert.BertEager(params, dev, cfg)
+            per = {}
+            for S in seqs:
+                def fwd(x, S=S, model=model):
+                    ids, tt, lens = bert.unpack_requests(x, S)
+                    logits = model(ids, tt, lens)
+                    if s.BACKEND == "fused":
+                        return model.ops.softmax_topk(logits, min(int(s.TOPK), cfg.num_labels))
+                    v, i = torch.topk(torch.softmax(logits.float(), -1), min(int(s.TOPK), cfg.num_labels), dim=-1)
+                    return v, i.to(torch.int32)
+
+                eng = GpuEngine(fwd, dev, (2 * S + 1,), torch.int32, buckets=buckets, inflight=int(s.INFLIGHT),
+                                use_graphs=bool(s.USE_GRAPHS), name=f"bert.s{S}.{dev}")
+                eng.warmup(capture=bool(s.USE_GRAPHS))
+                per[S] = eng
+            self.engines[dev] = per
+        logger.info("bert ready on %s (seq buckets %s, batch buckets %s)", devices, seqs, buckets)
+
+    def preprocess(self, part: Part) -> Any:
+        text = part.data.decode("utf-8", errors="replace")
+        return self.tokenizer.encode(text, self.max_seq)
+
+    def replicas(self):
+        from ..models import bert
+
+        out = []
+        for dev, per in self.engines.items():
+            seqs = sorted(per)
+
+            def run_batch(samples, per=per, seqs=seqs):
+                longest = max(len(t) for t in samples)
+                S = next((q for q in seqs if q >= longest), seqs[-1])
+                packed = bert.pack_requests(samples, S).numpy()
+                vals, idx = per[S].run(packed)
+                return [(vals[i], idx[i]) for i in range(len(samples))]
+
+            out.append(run_batch)
+        return out
+
+    def postprocess(self, out: Any) -> dict:
+        vals, idx = out
+        names = [self.labels[int(i)] for i in idx]
+        return {"classes": list(self.labels), "result": {n: float(v) for n, v in zip(names, vals)}}
+
+    def describe(self) -> dict:
+        d = super().describe()
+        d["engines"] = {dev: {S: e.stats() for S, e in per.items()} for dev, per in self.engines.items()}
+        return d

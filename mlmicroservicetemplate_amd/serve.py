@@ -96,6 +96,7 @@ def run_rank(args) -> int:
     if info.world_size > 1 and settings.TP > 1 and info.rank != 0:
         # tensor-parallel follower: no HTTP, run the lockstep worker loop
         plugin.init(ctx)
+        mdist.all_reduce_health(True)  # matches rank 0's readiness all-reduce (X6)
         return plugin.follower_loop() if hasattr(plugin, "follower_loop") else 0
     app = create_app(settings, plugin, ctx)
     config = uvicorn.Config(app, host=args.host, port=settings.PORT, log_level=settings.LOG_LEVEL.lower(),
