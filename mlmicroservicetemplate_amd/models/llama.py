@@ -367,6 +367,7 @@ class LlamaTP:
     @torch.no_grad()
     def step(self, ids: torch.Tensor, positions: torch.Tensor, lens: torch.Tensor, decode: bool, k: int):
         B, S = ids.shape
+        ids, positions, lens = ids.contiguous(), positions.contiguous(), lens.contiguous()
         if self.backend == "fused":
             slots = self._slots(B, S, positions, lens, decode)
             return self._fused_forward(ids.to(torch.int32), positions.to(torch.int32), lens.to(torch.int32), B, S,

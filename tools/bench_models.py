@@ -1,0 +1,111 @@
+"""Throughput of the BERT (config 3) and Llama-3-8B (config 5) paths on one MI355X.
+
+bert : sequences/s at (batch, seq) through the GpuEngine (hipGraph per bucket), fused kernels
+       vs stock PyTorch-ROCm (hipBLASLt + SDPA) on the same random weights.
+llama: TP=1 (all of Llama-3-8B on one GPU): prefill tokens/s and decode ms/step at several
+       batch sizes with the fused kernels.
+One JSON line per measurement.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def bench_bert(args):
+    from mlmicroservicetemplate_amd.engine.worker import GpuEngine
+    from mlmicroservicetemplate_amd.models import bert
+
+    dev = torch.device("cuda:0")
+    cfg = bert.BertConfig()
+    p = bert.init_bert(cfg, 0)
+    models = {"fused": bert.BertFused(p, dev, cfg), "eager": bert.BertEager(p, dev, cfg)}
+    for S in args.seqs:
+        for B in args.batches:
+            rng = np.random.default_rng(0)
+            toks = [list(rng.integers(1000, 30000, S)) for _ in range(B)]
+            packed = bert.pack_requests(toks, S).numpy()
+            for name, model in models.items():
+                def fwd(x, model=model, S=S):
+                    ids, tt, lens = bert.unpack_requests(x, S)
+                    logits = model(ids, tt, lens)
+                    v, i = torch.topk(logits.float(), 2, dim=-1)
+                    return v, i.to(torch.int32)
+
+                eng = GpuEngine(fwd, dev, (2 * S + 1,), torch.int32, buckets=[B], inflight=2)
+                eng.warmup(capture=True)
+                for _ in range(5):
+                    eng.run(packed)
+                n = args.steps
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                pend = []
+                for _ in range(n):
+                    pend.append(eng.submit(packed))
+                    if len(pend) >= 2:
+                        pend.pop(0).wait()
+                for t in pend:
+                    t.wait()
+                dt = (time.perf_counter() - t0) / n
+                print(json.dumps({"bench": "bert-base", "backend": name, "batch": B, "seq": S,
+                                  "ms_per_batch": round(dt * 1e3, 3), "seq_per_s": round(B / dt, 1),
+                                  "tokens_per_s": round(B * S / dt, 1)}), flush=True)
+                del eng
+
+
+def bench_llama(args):
+    from mlmicroservicetemplate_amd.models.llama import LLAMA3_8B, LlamaTP, init_llama_shard
+
+    dev = torch.device("cuda:0")
+    t0 = time.time()
+    p = init_llama_shard(LLAMA3_8B, 1, 0, seed=0, device=dev)
+    m = LlamaTP(p, LLAMA3_8B, backend="fused", device=dev, max_batch=max(args.batches), max_seq=2048)
+    print(json.dumps({"bench": "llama3-8b", "init_s": round(time.time() - t0, 1)}), flush=True)
+    for B in args.batches:
+        S = args.prompt
+        ids = torch.randint(1000, 100000, (B, S), device=dev, dtype=torch.int32)
+        lens = torch.full((B,), S, device=dev, dtype=torch.int32)
+        pos = torch.arange(S, device=dev, dtype=torch.int32).unsqueeze(0).expand(B, S).contiguous()
+        for _ in range(2):
+            m.step(ids, pos, lens, decode=False, k=1)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(3):
+            m.step(ids, pos, lens, decode=False, k=1)
+        torch.cuda.synchronize()
+        pre = (time.perf_counter() - t1) / 3
+        tok = torch.randint(1000, 100000, (B, 1), device=dev, dtype=torch.int32)
+        cur = lens.view(B, 1).clone()
+        for _ in range(3):
+            m.step(tok, cur, cur.view(-1) + 1, decode=True, k=1)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        n = args.steps
+        for _ in range(n):
+            m.step(tok, cur, cur.view(-1) + 1, decode=True, k=1)
+        torch.cuda.synchronize()
+        dec = (time.perf_counter() - t2) / n
+        print(json.dumps({"bench": "llama3-8b", "tp": 1, "batch": B, "prompt": S,
+                          "prefill_ms": round(pre * 1e3, 2), "prefill_tok_s": round(B * S / pre, 1),
+                          "decode_ms_per_step": round(dec * 1e3, 3), "decode_tok_s": round(B / dec, 1)}), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("which", choices=["bert", "llama"])
+    ap.add_argument("--batches", type=int, nargs="+", default=[1, 8, 32])
+    ap.add_argument("--seqs", type=int, nargs="+", default=[128])
+    ap.add_argument("--prompt", type=int, default=512)
+    ap.add_argument("--steps", type=int, default=30)
+    args = ap.parse_args()
+    {"bert": bench_bert, "llama": bench_llama}[args.which](args)
+
+
+if __name__ == "__main__":
+    main()
