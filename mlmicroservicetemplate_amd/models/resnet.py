@@ -301,10 +301,11 @@ class ResNet50Fused:
         return max(need, 1 << 20)
 
     # -- forward ----------------------------------------------------------------------------
-    def _conv(self, x, name, act, residual=None):
+    def _conv(self, x, name, act, residual=None, pad=None):
         s = self.specs[name]
         cfg, sk = self.tuning.get(name, (0, 0))
-        return self.ops.conv2d_nhwc(x, self.w[name], self.b[name], kernel=s.k, stride=s.stride, pad=s.pad,
+        return self.ops.conv2d_nhwc(x, self.w[name], self.b[name], kernel=s.k, stride=s.stride,
+                                    pad=s.pad if pad is None else pad,
                                     residual=residual, act=act, workspace=self.workspace, cfg=cfg, splitk=sk)
 
     def forward(self, images_u8_nhwc: torch.Tensor) -> torch.Tensor:
@@ -313,8 +314,8 @@ class ResNet50Fused:
         B = images_u8_nhwc.shape[0]
         if B > self.max_batch:
             raise ValueError(f"batch {B} > max_batch {self.max_batch}")
-        x = ops.normalize_u8(images_u8_nhwc, self.mean, self.std)
-        x = self._conv(x, "stem", ops.ACT_RELU)
+        x = ops.normalize_u8(images_u8_nhwc, self.mean, self.std, pad=3)  # zero border = stem padding
+        x = self._conv(x, "stem", ops.ACT_RELU, pad=0)
         x = ops.maxpool2d_nhwc(x, 3, 2, 1)
         for si, (nblocks, _m, _c, _s) in enumerate(STAGES):
             for bi in range(nblocks):

@@ -94,7 +94,7 @@ def conv2d_nhwc(
     splitk: int = 0,
 ) -> torch.Tensor:
     """``act(conv(x, w) * scale + bias (+ residual))`` with x NHWC bf16 and w packed
-    ``[Cout][KH][KW][Cin]`` (stem: ``[Cout][KH][8][4]``)."""
+    ``[Cout][KH][KW][Cin]`` (stem: ``[Cout][KH][8][4]`` on a pre-padded 4-channel image, pad 0)."""
     dev = x.device
     _need(x, "x", torch.bfloat16, dev)
     _need(w, "w", torch.bfloat16, dev)
@@ -203,22 +203,24 @@ def gemm_heuristic(M: int, N: int, K: int) -> Tuple[int, int]:
 _MEAN_STD_CACHE = {}
 
 
-def normalize_u8(images: torch.Tensor, mean, std, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """uint8 ``[B,H,W,3]`` -> bf16 ``[B,H,W,4]`` = ((x - mean) / std, 0)."""
+def normalize_u8(images: torch.Tensor, mean, std, pad: int = 0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """uint8 ``[B,H,W,3]`` -> bf16 ``[B,H+2p,W+2p,4]`` = ((x - mean) / std, 0) with a zero border
+    of ``pad`` pixels (the stem conv is then launched with pad 0 on the pre-padded image)."""
     dev = images.device
     _need(images, "images", torch.uint8, dev)
     B, H, W, C = images.shape
     if C != 3:
         raise ValueError("expected 3-channel images")
+    shape = (B, H + 2 * pad, W + 2 * pad, 4)
     if out is None:
-        out = torch.empty(B, H, W, 4, device=dev, dtype=torch.bfloat16)
+        out = torch.empty(shape, device=dev, dtype=torch.bfloat16)
     else:
         _need(out, "out", torch.bfloat16, dev)
-        if tuple(out.shape) != (B, H, W, 4):
-            raise ValueError("out must be [B,H,W,4]")
+        if tuple(out.shape) != shape:
+            raise ValueError(f"out must be {shape}")
     m = (ctypes.c_float * 3)(*[float(v) for v in mean])
     s = (ctypes.c_float * 3)(*[float(v) for v in std])
-    rc = lib().mls_normalize_u8(images.data_ptr(), out.data_ptr(), B * H * W, m, s, stream_ptr(dev))
+    rc = lib().mls_normalize_u8(images.data_ptr(), out.data_ptr(), B, H, W, pad, m, s, stream_ptr(dev))
     check(rc, "mls_normalize_u8")
     return out
 

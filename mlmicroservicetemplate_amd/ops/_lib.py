@@ -36,7 +36,7 @@ _SIGS = {
     "mls_gemm": [P, P, P, P, P, P, P, SZ, I, I, I, I, I, I, P],
     "mls_gemm_heuristic": [I, I, I, _c.POINTER(I), _c.POINTER(I)],
     "mls_gemm_num_cfgs": [],
-    "mls_normalize_u8": [P, P, L, FP, FP, P],
+    "mls_normalize_u8": [P, P, I, I, I, I, FP, FP, P],
     "mls_maxpool2d": [P, P, I, I, I, I, I, I, I, P],
     "mls_avgpool_global": [P, P, I, I, I, P],
     "mls_bn_act": [P, P, P, P, L, I, I, P],
@@ -50,7 +50,7 @@ _SIGS = {
     "mls_flash_attention": [P, P, P, P, I, I, I, I, I, I, I, I, I, P, I, F, P],
     "mls_decode_attention": [P, P, P, P, P, P, I, I, L, P, I, I, I, I, I, I, F, P],
 }
-_OPTIONAL_SIGS: dict = {}
+_OPTIONAL_SIGS: dict = {"mls_set_debug_flags": [I]}
 
 
 class NativeError(RuntimeError):

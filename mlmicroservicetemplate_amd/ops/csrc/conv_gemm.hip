@@ -45,23 +45,37 @@ struct ConvArgs {
   int act;
   int splitk, kchunk;
   int ldo, ldr;
-  uint32_t x_bytes, w_bytes;  // extents of x and w for the buffer-load range check
+  uint32_t x_bytes, w_bytes, r_bytes;  // extents of x, w, res for the buffer-load range check
+  int dbg;  // diagnostics only (ablation): 1 = skip MFMAs, 2 = skip output stores, 4 = skip operand DMA
 };
 
-template <int BM, int BN, int MODE>
-__global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a) {
-  constexpr int WN = 2;
-  constexpr int WTM = BM / 2, WTN = BN / 2;
+int g_dbg_flags = 0;  // set via mls_set_debug_flags (tools/conv_ablate.py); 0 in production
+
+#define LDS3 __attribute__((address_space(3)))
+
+MLS_DEV void glds16(rsrc_t r, char* lds, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS3 void*)lds, 16, voff, soff, 0, 0);
+}
+
+// v2: LDS-DMA (buffer_load ... lds) into a STAGES-deep ring, counted vmcnt + raw s_barrier.
+template <int BM, int BN, int WM, int WN, int STAGES, int MODE>
+__global__ __launch_bounds__(WM * WN * 64) void conv_gemm_kernel(const ConvArgs a) {
+  constexpr int NW = WM * WN, NT = NW * 64;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
-  constexpr int AROWS = BM / 32, BROWS = BN / 32;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
+  constexpr int AI = BM / 8 / NW, BI = BN / 8 / NW;  // 1-KiB DMA pieces per wave per stage
+  static_assert(AI * 8 * NW == BM && BI * 8 * NW == BN, "tile / wave mismatch");
+  static_assert(TM >= 1 && TN >= 1, "wave tile too small");
+  constexpr int LPS = AI + BI;  // vmcnt units per stage
   constexpr int C_LD = BN + 4;
   constexpr int EPI_BYTES = BM * C_LD * 4;
-  constexpr int LDS_BYTES = (2 * STAGE_BYTES > EPI_BYTES) ? 2 * STAGE_BYTES : EPI_BYTES;
+  constexpr int LDS_BYTES = (STAGES * STAGE_BYTES > EPI_BYTES) ? STAGES * STAGE_BYTES : EPI_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
 
   const int ntn = (a.N + BN - 1) / BN;
@@ -74,99 +88,78 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
   const int kend = min(a.K, kbeg + a.kchunk);
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
 
-  const int kc = tid & 7;     // 16-B chunk of the 128-B K-row this thread stages
-  const int rbase = tid >> 3; // first staged row; rows rbase + 32*i
+  // lane -> (row within an 8-row DMA piece, logical 16-B chunk).  The DMA writes LDS lane-
+  // linearly (base + 16*lane), so the XOR swizzle is applied to the SOURCE chunk instead:
+  // physical chunk (lane & 7) of row r holds logical chunk (lane & 7) ^ (r & 7).
+  const int r8 = lane >> 3;
+  const int lc = (lane & 7) ^ r8;
 
-  // ---- per-row im2col bases (fixed for the whole K loop) ----
-  int a_off[AROWS], a_ih[AROWS], a_iw[AROWS];
+  int a_v[AI];
+  uint32_t a_msk[AI];
   const int HoWo = a.Ho * a.Wo;
 #pragma unroll
-  for (int i = 0; i < AROWS; ++i) {
-    const int m = m0 + rbase + 32 * i;
+  for (int j = 0; j < AI; ++j) {
+    const int m = m0 + (wid * AI + j) * 8 + r8;
+    a_msk[j] = 0u;
+    a_v[j] = OOB;
     if (m < a.M) {
       const int b = m / HoWo;
       const int rem = m - b * HoWo;
       const int oh = rem / a.Wo;
       const int ow = rem - oh * a.Wo;
       if (MODE == MODE_1X1) {
-        a_off[i] = ((b * a.H + oh * a.stride) * a.W + ow * a.stride) * a.Cin;
-        a_ih[i] = 0;
-        a_iw[i] = 0;
-      } else {
-        a_off[i] = b * a.H * a.W * a.Cin;
-        a_ih[i] = oh * a.stride - a.pad;
-        a_iw[i] = ow * a.stride - a.pad;
+        a_v[j] = (((b * a.H + oh * a.stride) * a.W + ow * a.stride) * a.Cin + lc * 8) * 2;
+      } else if (MODE == MODE_STEM) {  // pre-padded image, Cin 4, chunk = 2 taps: kh = lc>>2, kw = 2*(lc&3)
+        a_v[j] = (((b * a.H + oh * a.stride + (lc >> 2)) * a.W + ow * a.stride + 2 * (lc & 3)) * 4) * 2;
+      } else {  // generic: per-row validity bitmask over the KH*KW taps
+        const int ih0 = oh * a.stride - a.pad, iw0 = ow * a.stride - a.pad;
+        uint32_t msk = 0u;
+        for (int kh = 0; kh < a.KH; ++kh)
+          for (int kw = 0; kw < a.KW; ++kw)
+            if ((unsigned)(ih0 + kh) < (unsigned)a.H && (unsigned)(iw0 + kw) < (unsigned)a.W)
+              msk |= 1u << (kh * a.KW + kw);
+        a_msk[j] = msk;
+        a_v[j] = ((b * a.H * a.W + ih0 * a.W + iw0) * a.Cin + lc * 8) * 2;
       }
-    } else {
-      a_off[i] = -1;
-      a_ih[i] = -(1 << 28);
-      a_iw[i] = -(1 << 28);
     }
   }
-  int b_row[BROWS];
+  int b_v[BI];
 #pragma unroll
-  for (int j = 0; j < BROWS; ++j) {
-    const int n = n0 + rbase + 32 * j;
-    b_row[j] = n < a.N ? n : -1;
+  for (int j = 0; j < BI; ++j) {
+    const int n = n0 + (wid * BI + j) * 8 + r8;
+    b_v[j] = n < a.N ? (n * a.K + lc * 8) * 2 : OOB;
   }
 
-  uint4 ra[AROWS], rb[BROWS];
-  // SRDs over the activation and weight tensors: padding / tails become OOB offsets -> 0
   const rsrc_t xr = make_rsrc(a.x, a.x_bytes);
   const rsrc_t wr = make_rsrc(a.w, a.w_bytes);
 
-  auto gload = [&](int k0) {
-    const int k = k0 + kc * 8;
-    const bool kin = k < kend;
+  auto issue = [&](int kt, int buf) {
+    const int k0 = kbeg + kt * BK;
+    char* sA = smem + buf * STAGE_BYTES;
+    char* sB = sA + A_BYTES;
+    const int left = kend - k0;  // < 64 only on a K tail
+    const bool lane_kin = lc * 8 < left;
     if (MODE == MODE_1X1) {
 #pragma unroll
-      for (int i = 0; i < AROWS; ++i)
-        ra[i] = bload16(xr, (kin && a_off[i] >= 0) ? (a_off[i] + k) * 2 : OOB);
-    } else if (MODE == MODE_GENERIC) {
-      // whole BK step inside one tap (Cin % 64 == 0): tap math is uniform
-      const int tap = k0 / a.Cin;
-      const int c = k0 - tap * a.Cin + kc * 8;
+      for (int j = 0; j < AI; ++j) glds16(xr, sA + (wid * AI + j) * 1024, lane_kin ? a_v[j] : OOB, k0 * 2);
+    } else if (MODE == MODE_STEM) {
+      const int soff = (k0 >> 5) * a.W * 8;  // kh base rows (K rows of 32 = one kh)
+#pragma unroll
+      for (int j = 0; j < AI; ++j) glds16(xr, sA + (wid * AI + j) * 1024, a_v[j], soff);
+    } else {
+      const int tap = k0 / a.Cin;  // the whole 64-wide step is inside one tap
+      const int c0 = k0 - tap * a.Cin;
       const int kh = tap / a.KW;
       const int kw = tap - kh * a.KW;
+      const int uni = ((kh * a.W + kw) * a.Cin + c0) * 2;
 #pragma unroll
-      for (int i = 0; i < AROWS; ++i) {
-        const int ih = a_ih[i] + kh, iw = a_iw[i] + kw;
-        const bool ok = kin && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-        ra[i] = bload16(xr, ok ? (a_off[i] + (ih * a.W + iw) * a.Cin + c) * 2 : OOB);
-      }
-    } else {  // MODE_STEM: Cin == 4, weights [N][KH][8][4]; chunk = taps (kw, kw+1) of row kh
-      const int kh = k >> 5;
-      const int kw = (k & 31) >> 2;
-#pragma unroll
-      for (int i = 0; i < AROWS; ++i) {
-        const int ih = a_ih[i] + kh, iw = a_iw[i] + kw;
-        const bool rowok = kin && (unsigned)ih < (unsigned)a.H;
-        const bool ok0 = rowok && (unsigned)iw < (unsigned)a.W && kw < a.KW;
-        const bool ok1 = rowok && (unsigned)(iw + 1) < (unsigned)a.W && kw + 1 < a.KW;
-        const int off = (a_off[i] + (ih * a.W + iw) * 4) * 2;
-        const uint2 lo = bload8(xr, ok0 ? off : OOB);
-        const uint2 hi = bload8(xr, ok1 ? off + 8 : OOB);
-        ra[i] = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      for (int j = 0; j < AI; ++j) {
+        const bool ok = (a_msk[j] >> tap) & 1u;
+        glds16(xr, sA + (wid * AI + j) * 1024, ok ? a_v[j] + uni : OOB, 0);
       }
     }
 #pragma unroll
-    for (int j = 0; j < BROWS; ++j)
-      rb[j] = bload16(wr, (kin && b_row[j] >= 0) ? (b_row[j] * a.K + k) * 2 : OOB);
-  };
-
-  auto sstore = [&](int s) {
-    uint4* As = reinterpret_cast<uint4*>(smem + s * STAGE_BYTES);
-    uint4* Bs = reinterpret_cast<uint4*>(smem + s * STAGE_BYTES + A_BYTES);
-#pragma unroll
-    for (int i = 0; i < AROWS; ++i) {
-      const int r = rbase + 32 * i;
-      As[r * 8 + (kc ^ (r & 7))] = ra[i];
-    }
-#pragma unroll
-    for (int j = 0; j < BROWS; ++j) {
-      const int r = rbase + 32 * j;
-      Bs[r * 8 + (kc ^ (r & 7))] = rb[j];
-    }
+    for (int j = 0; j < BI; ++j) glds16(wr, sB + (wid * BI + j) * 1024, lane_kin ? b_v[j] : OOB, k0 * 2);
   };
 
   f32x4 acc[TM][TN];
@@ -175,16 +168,70 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (nk > 0) {
-    gload(kbeg);
-    sstore(0);
+  // residual prefetch: issued before the operand DMA so its latency overlaps the K loop instead
+  // of serialising after it (the small-K layers are latency-bound).  Same thread->chunk map as
+  // the epilogue below.
+  constexpr int CPR = BN / 8;
+  constexpr int EPI_IT = (BM * CPR + NT - 1) / NT;
+  uint4 resv[EPI_IT];
+  const bool pre_res = a.res != nullptr && a.splitk == 1 && a.act != ACT_SILU_MUL;
+  if (pre_res) {
+    const rsrc_t rr = make_rsrc(a.res, a.r_bytes);
+#pragma unroll
+    for (int it = 0; it < EPI_IT; ++it) {
+      const int q = tid + it * NT;
+      const int row = q / CPR, c8 = q - (q / CPR) * CPR;
+      const int m = m0 + row, n = n0 + c8 * 8;
+      const bool ok = q < BM * CPR && m < a.M && n < a.N;
+      resv[it] = bload16(rr, ok ? (m * a.ldr + n) * 2 : OOB);
+    }
   }
-  __syncthreads();
+
+  // bias / scale prefetch: NT % CPR == 0, so every epilogue iteration of this thread touches
+  // the same 8 output columns -> one 32-B chunk of each, loaded up front.
+  static_assert(NT % CPR == 0, "epilogue column mapping");
+  const int my_n = n0 + (tid % CPR) * 8;
+  float bias8[8], scale8[8];
+  {
+    const bool nok = my_n < a.N;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      bias8[e] = 0.f;
+      scale8[e] = 1.f;
+    }
+    if (nok && a.bias) {
+      const float4 b0 = *reinterpret_cast<const float4*>(a.bias + my_n);
+      const float4 b1 = *reinterpret_cast<const float4*>(a.bias + my_n + 4);
+      bias8[0] = b0.x; bias8[1] = b0.y; bias8[2] = b0.z; bias8[3] = b0.w;
+      bias8[4] = b1.x; bias8[5] = b1.y; bias8[6] = b1.z; bias8[7] = b1.w;
+    }
+    if (nok && a.scale) {
+      const float4 s0 = *reinterpret_cast<const float4*>(a.scale + my_n);
+      const float4 s1 = *reinterpret_cast<const float4*>(a.scale + my_n + 4);
+      scale8[0] = s0.x; scale8[1] = s0.y; scale8[2] = s0.z; scale8[3] = s0.w;
+      scale8[4] = s1.x; scale8[5] = s1.y; scale8[6] = s1.z; scale8[7] = s1.w;
+    }
+  }
+
+  const int npro = nk < STAGES - 1 ? nk : STAGES - 1;
+  if (!(a.dbg & 4))
+    for (int s = 0; s < npro; ++s) issue(s, s);
 
   const int fr = lane & 15, fq = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) gload(kbeg + (kt + 1) * BK);
+    const int issued = (kt + STAGES - 1 < nk) ? kt + STAGES - 1 : nk;
+    const int ahead = issued - (kt + 1);  // stages still allowed in flight
+    if (STAGES >= 4 && ahead >= 2)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LPS) : "memory");
+    else if (ahead >= 1)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPS) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + STAGES - 1 < nk && !(a.dbg & 4)) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+    if (a.dbg & 1) continue;
+    const int cur = kt % STAGES;
     const uint4* As = reinterpret_cast<const uint4*>(smem + cur * STAGE_BYTES);
     const uint4* Bs = reinterpret_cast<const uint4*>(smem + cur * STAGE_BYTES + A_BYTES);
 #pragma unroll
@@ -207,9 +254,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) sstore(cur ^ 1);
-    __syncthreads();
   }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
 
   // ---- epilogue: park fp32 accumulators in LDS, then emit 16-B rows ----
   float* Cs = reinterpret_cast<float*>(smem);
@@ -225,10 +272,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
       }
   __syncthreads();
 
-  constexpr int CPR = BN / 8;
   if (a.act == ACT_SILU_MUL && a.splitk == 1) {
     // gate/up interleaved in 8-column groups: chunk 2p = gate, 2p+1 = up -> 8 outputs at n/2
-    for (int q = tid; q < BM * (CPR / 2); q += NTHREADS) {
+    for (int q = tid; q < BM * (CPR / 2); q += NT) {
       const int row = q / (CPR / 2), p = q - (q / (CPR / 2)) * (CPR / 2);
       const int m = m0 + row, n = n0 + p * 16;
       if (m >= a.M || n >= a.N) continue;
@@ -247,10 +293,12 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
     }
     return;
   }
-  for (int q = tid; q < BM * CPR; q += NTHREADS) {
+#pragma unroll
+  for (int it = 0; it < EPI_IT; ++it) {
+    const int q = tid + it * NT;
     const int row = q / CPR, c8 = q - (q / CPR) * CPR;
     const int m = m0 + row, n = n0 + c8 * 8;
-    if (m >= a.M || n >= a.N) continue;
+    if (q >= BM * CPR || m >= a.M || n >= a.N) continue;
     const float4 v0 = *reinterpret_cast<const float4*>(Cs + row * C_LD + c8 * 8);
     const float4 v1 = *reinterpret_cast<const float4*>(Cs + row * C_LD + c8 * 8 + 4);
     if (a.splitk > 1) {
@@ -260,22 +308,20 @@ __global__ __launch_bounds__(NTHREADS, 2) void conv_gemm_kernel(const ConvArgs a
       continue;
     }
     float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-    if (a.scale) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] *= a.scale[n + e];
-    }
-    if (a.bias) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += a.bias[n + e];
-    }
-    if (a.res) {
+    for (int e = 0; e < 8; ++e) v[e] = v[e] * scale8[e] + bias8[e];
+    if (pre_res) {
       float r[8];
-      unpack8(ld16(a.res + (size_t)m * a.ldr + n), r);
+      unpack8(resv[it], r);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] += r[e];
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], a.act);
+    if (a.dbg & 2) {
+      if (v[0] == 12345.678f) st16(a.out, pack8(v));  // keep the value live, never true
+      continue;
+    }
     st16(a.out + (size_t)m * a.ldo + n, pack8(v));
   }
 }
@@ -330,27 +376,40 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(const ConvArgs a) 
 }
 
 struct TileCfg {
-  int bm, bn;
+  int bm, bn, threads;
 };
-constexpr TileCfg kCfgs[] = {{0, 0}, {128, 128}, {128, 64}, {64, 128}, {64, 64}};
-constexpr int kNumCfgs = 5;
+// id: 0 = heuristic; 1..8 = explicit (BM x BN, waves, LDS stages)
+constexpr TileCfg kCfgs[] = {{0, 0, 0},       {128, 128, 256}, {128, 64, 256}, {64, 128, 256},
+                             {64, 64, 256},   {128, 128, 512}, {64, 64, 256},  {128, 64, 512},
+                             {64, 128, 512},  {64, 128, 512},  {128, 64, 512}, {64, 64, 256},
+                             {128, 128, 512}};
+constexpr int kNumCfgs = 13;
 
 template <int MODE>
 void launch_mode(int cfg, dim3 grid, hipStream_t st, const ConvArgs& a) {
   switch (cfg) {
-    case 1: hipLaunchKernelGGL((conv_gemm_kernel<128, 128, MODE>), grid, dim3(NTHREADS), 0, st, a); break;
-    case 2: hipLaunchKernelGGL((conv_gemm_kernel<128, 64, MODE>), grid, dim3(NTHREADS), 0, st, a); break;
-    case 3: hipLaunchKernelGGL((conv_gemm_kernel<64, 128, MODE>), grid, dim3(NTHREADS), 0, st, a); break;
-    default: hipLaunchKernelGGL((conv_gemm_kernel<64, 64, MODE>), grid, dim3(NTHREADS), 0, st, a); break;
+    case 1: hipLaunchKernelGGL((conv_gemm_kernel<128, 128, 2, 2, 2, MODE>), grid, dim3(256), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((conv_gemm_kernel<128, 64, 2, 2, 3, MODE>), grid, dim3(256), 0, st, a); break;
+    case 3: hipLaunchKernelGGL((conv_gemm_kernel<64, 128, 2, 2, 3, MODE>), grid, dim3(256), 0, st, a); break;
+    case 5: hipLaunchKernelGGL((conv_gemm_kernel<128, 128, 4, 2, 3, MODE>), grid, dim3(512), 0, st, a); break;
+    case 6: hipLaunchKernelGGL((conv_gemm_kernel<64, 64, 2, 2, 4, MODE>), grid, dim3(256), 0, st, a); break;
+    case 7: hipLaunchKernelGGL((conv_gemm_kernel<128, 64, 4, 2, 3, MODE>), grid, dim3(512), 0, st, a); break;
+    case 8: hipLaunchKernelGGL((conv_gemm_kernel<64, 128, 2, 4, 3, MODE>), grid, dim3(512), 0, st, a); break;
+    // 2-stage variants: half the LDS ring -> more resident blocks for the latency-bound small-K layers
+    case 9: hipLaunchKernelGGL((conv_gemm_kernel<64, 128, 2, 4, 2, MODE>), grid, dim3(512), 0, st, a); break;
+    case 10: hipLaunchKernelGGL((conv_gemm_kernel<128, 64, 4, 2, 2, MODE>), grid, dim3(512), 0, st, a); break;
+    case 11: hipLaunchKernelGGL((conv_gemm_kernel<64, 64, 2, 2, 2, MODE>), grid, dim3(256), 0, st, a); break;
+    case 12: hipLaunchKernelGGL((conv_gemm_kernel<128, 128, 4, 2, 2, MODE>), grid, dim3(512), 0, st, a); break;
+    default: hipLaunchKernelGGL((conv_gemm_kernel<64, 64, 2, 2, 3, MODE>), grid, dim3(256), 0, st, a); break;
   }
 }
 
 // Heuristic tile choice: fill 256 CUs x 2 resident blocks, penalise padding waste and small tiles.
 void choose_cfg(int M, int N, int K, int& cfg, int& splitk) {
-  const float tile_eff[kNumCfgs] = {0.f, 1.0f, 0.86f, 0.86f, 0.68f};
+  const float tile_eff[kNumCfgs] = {0.f, 1.0f, 0.86f, 0.86f, 0.68f, 1.0f, 0.68f, 0.86f, 0.86f, 0.86f, 0.86f, 0.68f, 1.0f};
   float best = -1.f;
   int bc = 4;
-  for (int c = 1; c < kNumCfgs; ++c) {
+  for (int c = 1; c <= 4; ++c) {
     const int bm = kCfgs[c].bm, bn = kCfgs[c].bn;
     const long tm = (M + bm - 1) / bm, tn = (N + bn - 1) / bn, tiles = tm * tn;
     const float pad = (float)M * N / ((float)tiles * bm * bn);
@@ -385,6 +444,12 @@ int launch_conv(ConvArgs a, int mode, int cfg, int splitk, size_t ws_bytes, hipS
   }
   a.splitk = splitk;
   a.kchunk = kchunk;
+  a.dbg = g_dbg_flags;
+  {
+    const size_t rb = a.res ? ((size_t)(a.M - 1) * a.ldr + a.N) * 2 : 0;
+    if (rb >= 0x7FFFFFFFull) return MLS_UNSUPPORTED;
+    a.r_bytes = (uint32_t)rb;
+  }
   const int bm = kCfgs[cfg].bm, bn = kCfgs[cfg].bn;
   const long ntiles = (long)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn) * splitk;
   if (ntiles > 0x7fffffffL) return MLS_BAD_ARG;
@@ -433,13 +498,15 @@ int mls_conv2d(const void* x, const void* w, const float* scale, const float* bi
   a.x_bytes = (uint32_t)xb;
   int mode;
   if (Cin == 4 && KH > 1) {
-    if (KW > 8) return MLS_UNSUPPORTED;
+    // pre-padded image (the normalise kernel writes the zero border): no bounds checks;
+    // taps up to KW padded to 8 must stay inside the row
+    if (KW > 8 || pad != 0 || (a.Wo - 1) * stride + 8 > W || (a.Ho - 1) * stride + 8 > H) return MLS_UNSUPPORTED;
     mode = MODE_STEM;
     a.K = KH * 32;
   } else if (KH == 1 && KW == 1 && pad == 0) {
     mode = MODE_1X1;
     a.K = Cin;
-  } else if (Cin % 64 == 0) {
+  } else if (Cin % 64 == 0 && KH * KW <= 32) {
     mode = MODE_GENERIC;
     a.K = KH * KW * Cin;
   } else {
@@ -482,5 +549,7 @@ int mls_gemm_heuristic(int M, int N, int K, int* cfg, int* splitk) {
 }
 
 int mls_gemm_num_cfgs() { return kNumCfgs; }
+
+void mls_set_debug_flags(int flags) { g_dbg_flags = flags; }
 
 }  // extern "C"

@@ -13,56 +13,39 @@ inline int grid_for(long work, int block) {
   return (int)g;
 }
 
-// 4 pixels per thread: 12 input bytes (3 dwords) -> 4 x (4 x bf16) = 32 output bytes.
-// out channel 3 is zero (Cin padded 3 -> 4 so the stem conv reads 8-byte taps).
+// uint8 [B,H,W,3] -> bf16 [B,H+2p,W+2p,4]: ((x - mean) / std, 0) with a zero border of p pixels
+// (the stem conv then needs no bounds checks) and channel 3 zero (Cin padded 3 -> 4 so the stem
+// reads two 4-channel taps per 16-B chunk).  One thread per output pixel, 8-B stores.
 __global__ __launch_bounds__(256) void normalize_u8_kernel(const uint8_t* __restrict__ in, bf16* __restrict__ out,
-                                                           long npix, float m0, float m1, float m2, float s0,
-                                                           float s1, float s2) {
-  const long nq = npix / 4;
-  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < nq; q += (long)gridDim.x * blockDim.x) {
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(in + q * 12);
-    const uint32_t w0 = src[0], w1 = src[1], w2 = src[2];
-    uint8_t b[12];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      b[i] = (w0 >> (8 * i)) & 0xff;
-      b[4 + i] = (w1 >> (8 * i)) & 0xff;
-      b[8 + i] = (w2 >> (8 * i)) & 0xff;
+                                                           int B, int H, int W, int pad, float m0, float m1,
+                                                           float m2, float s0, float s1, float s2) {
+  const int Hp = H + 2 * pad, Wp = W + 2 * pad;
+  const long total = (long)B * Hp * Wp;
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
+    const int x = (int)(q % Wp);
+    const long r = q / Wp;
+    const int y = (int)(r % Hp);
+    const int b = (int)(r / Hp);
+    const int iy = y - pad, ix = x - pad;
+    bf16x4 v;
+    if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) {
+      const uint8_t* p = in + (((long)b * H + iy) * W + ix) * 3;
+      v[0] = (bf16)(((float)p[0] - m0) * s0);
+      v[1] = (bf16)(((float)p[1] - m1) * s1);
+      v[2] = (bf16)(((float)p[2] - m2) * s2);
+      v[3] = (bf16)0.f;
+    } else {
+      v[0] = v[1] = v[2] = v[3] = (bf16)0.f;
     }
-    float f[16];
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      f[4 * p + 0] = ((float)b[3 * p + 0] - m0) * s0;
-      f[4 * p + 1] = ((float)b[3 * p + 1] - m1) * s1;
-      f[4 * p + 2] = ((float)b[3 * p + 2] - m2) * s2;
-      f[4 * p + 3] = 0.f;
-    }
-    float lo[8], hi[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      lo[i] = f[i];
-      hi[i] = f[8 + i];
-    }
-    st16(out + q * 16, pack8(lo));
-    st16(out + q * 16 + 8, pack8(hi));
-  }
-  // tail pixels (npix % 4)
-  const long tail0 = nq * 4;
-  const long t = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  if (t < npix - tail0) {
-    const long p = tail0 + t;
-    const uint8_t* s = in + p * 3;
-    bf16* d = out + p * 4;
-    d[0] = f2bf(((float)s[0] - m0) * s0);
-    d[1] = f2bf(((float)s[1] - m1) * s1);
-    d[2] = f2bf(((float)s[2] - m2) * s2);
-    d[3] = f2bf(0.f);
+    *reinterpret_cast<uint2*>(out + q * 4) = __builtin_bit_cast(uint2, v);
   }
 }
 
-// NHWC max pool; thread = (b, oh, ow, 8 channels)
+// NHWC max pool; thread = (b, oh, ow, 8 channels).  All k*k taps are loaded with clamped
+// (always valid) addresses and masked afterwards, so the loads issue back to back.
+template <int KS>
 __global__ __launch_bounds__(256) void maxpool_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int B, int H,
-                                                      int W, int C, int Ho, int Wo, int k, int s, int p) {
+                                                      int W, int C, int Ho, int Wo, int s, int p) {
   const int c8n = C / 8;
   const long total = (long)B * Ho * Wo * c8n;
   for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
@@ -72,43 +55,70 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const bf16* __restrict__ x
     r /= Wo;
     const int oh = (int)(r % Ho);
     const int b = (int)(r / Ho);
+    uint4 raw[KS * KS];
+    bool ok[KS * KS];
+#pragma unroll
+    for (int kh = 0; kh < KS; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < KS; ++kw) {
+        const int ih = oh * s - p + kh, iw = ow * s - p + kw;
+        const bool v = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+        const int cih = v ? ih : 0, ciw = v ? iw : 0;
+        ok[kh * KS + kw] = v;
+        raw[kh * KS + kw] = ld16(x + (((long)b * H + cih) * W + ciw) * C + c8 * 8);
+      }
     float m[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
-    for (int kh = 0; kh < k; ++kh) {
-      const int ih = oh * s - p + kh;
-      if ((unsigned)ih >= (unsigned)H) continue;
-      for (int kw = 0; kw < k; ++kw) {
-        const int iw = ow * s - p + kw;
-        if ((unsigned)iw >= (unsigned)W) continue;
-        float v[8];
-        unpack8(ld16(x + (((long)b * H + ih) * W + iw) * C + c8 * 8), v);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], v[e]);
-      }
+    for (int t = 0; t < KS * KS; ++t) {
+      float v[8];
+      unpack8(raw[t], v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) m[e] = ok[t] ? fmaxf(m[e], v[e]) : m[e];
     }
     st16(y + (((long)b * Ho + oh) * Wo + ow) * C + c8 * 8, pack8(m));
   }
 }
 
-// global average pool [B][HW][C] -> [B][C]; thread = (b, 8 channels)
+// global average pool [B][HW][C] -> [B][C].  Block = (batch, 64 x 8 channels); its 4 waves
+// split the HW positions (independent 16-B loads, unrolled) and combine through LDS.
 __global__ __launch_bounds__(256) void avgpool_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int B, int HW,
                                                       int C, float inv) {
+  __shared__ float part[3][64][8];
   const int c8n = C / 8;
-  const long total = (long)B * c8n;
-  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
-    const int c8 = (int)(q % c8n);
-    const int b = (int)(q / c8n);
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int groups = (c8n + 63) / 64;
+  const int b = blockIdx.x / groups;
+  const int c8 = (blockIdx.x % groups) * 64 + lane;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (c8 < c8n) {
     const bf16* src = x + (long)b * HW * C + c8 * 8;
-    for (int i = 0; i < HW; ++i) {
+    int i = wid;
+    for (; i + 12 < HW; i += 16) {
+      float v0[8], v1[8], v2[8], v3[8];
+      unpack8(ld16(src + (long)i * C), v0);
+      unpack8(ld16(src + (long)(i + 4) * C), v1);
+      unpack8(ld16(src + (long)(i + 8) * C), v2);
+      unpack8(ld16(src + (long)(i + 12) * C), v3);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += (v0[e] + v1[e]) + (v2[e] + v3[e]);
+    }
+    for (; i < HW; i += 4) {
       float v[8];
       unpack8(ld16(src + (long)i * C), v);
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc[e] += v[e];
     }
+  }
+  if (wid > 0) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] *= inv;
+    for (int e = 0; e < 8; ++e) part[wid - 1][lane][e] = acc[e];
+  }
+  __syncthreads();
+  if (wid == 0 && c8 < c8n) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = (acc[e] + part[0][lane][e] + part[1][lane][e] + part[2][lane][e]) * inv;
     st16(y + (long)b * C + c8 * 8, pack8(acc));
   }
 }
@@ -136,12 +146,13 @@ __global__ __launch_bounds__(256) void bn_act_kernel(const bf16* __restrict__ x,
 
 extern "C" {
 
-int mls_normalize_u8(const void* in, void* out, long npix, const float* mean3, const float* std3, void* stream) {
-  if (npix <= 0) return MLS_BAD_ARG;
-  const long nq = npix / 4;
-  int g = grid_for(nq > 0 ? nq : 1, 256);
-  hipLaunchKernelGGL(normalize_u8_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)in, (bf16*)out,
-                     npix, mean3[0], mean3[1], mean3[2], 1.f / std3[0], 1.f / std3[1], 1.f / std3[2]);
+int mls_normalize_u8(const void* in, void* out, int B, int H, int W, int pad, const float* mean3, const float* std3,
+                     void* stream) {
+  if (B <= 0 || H <= 0 || W <= 0 || pad < 0) return MLS_BAD_ARG;
+  const long total = (long)B * (H + 2 * pad) * (W + 2 * pad);
+  hipLaunchKernelGGL(normalize_u8_kernel, dim3(grid_for(total, 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const uint8_t*)in, (bf16*)out, B, H, W, pad, mean3[0], mean3[1], mean3[2], 1.f / std3[0],
+                     1.f / std3[1], 1.f / std3[2]);
   return (int)hipGetLastError();
 }
 
@@ -149,16 +160,22 @@ int mls_maxpool2d(const void* x, void* y, int B, int H, int W, int C, int k, int
   if (C % 8) return MLS_BAD_ARG;
   const int Ho = (H + 2 * p - k) / s + 1, Wo = (W + 2 * p - k) / s + 1;
   const long total = (long)B * Ho * Wo * (C / 8);
-  hipLaunchKernelGGL(maxpool_kernel, dim3(grid_for(total, 256)), dim3(256), 0, (hipStream_t)stream, (const bf16*)x,
-                     (bf16*)y, B, H, W, C, Ho, Wo, k, s, p);
+  if (k == 3)
+    hipLaunchKernelGGL(maxpool_kernel<3>, dim3(grid_for(total, 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16*)x, (bf16*)y, B, H, W, C, Ho, Wo, s, p);
+  else if (k == 2)
+    hipLaunchKernelGGL(maxpool_kernel<2>, dim3(grid_for(total, 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16*)x, (bf16*)y, B, H, W, C, Ho, Wo, s, p);
+  else
+    return MLS_UNSUPPORTED;
   return (int)hipGetLastError();
 }
 
 int mls_avgpool_global(const void* x, void* y, int B, int HW, int C, void* stream) {
   if (C % 8) return MLS_BAD_ARG;
-  const long total = (long)B * (C / 8);
-  hipLaunchKernelGGL(avgpool_kernel, dim3(grid_for(total, 256)), dim3(256), 0, (hipStream_t)stream, (const bf16*)x,
-                     (bf16*)y, B, HW, C, 1.f / (float)HW);
+  const int groups = (C / 8 + 63) / 64;
+  hipLaunchKernelGGL(avgpool_kernel, dim3(B * groups), dim3(256), 0, (hipStream_t)stream, (const bf16*)x, (bf16*)y, B,
+                     HW, C, 1.f / (float)HW);
   return (int)hipGetLastError();
 }
 

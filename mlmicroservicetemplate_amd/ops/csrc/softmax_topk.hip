@@ -88,6 +88,44 @@ __global__ __launch_bounds__(256) void softmax_topk_kernel(const Tin* __restrict
   }
 }
 
+// Wave-per-row variant for rows up to 4096 (the classifier heads): no block barriers, the k
+// selection rounds are pure wave shuffles.  4 rows per 256-thread block, LDS N floats per wave.
+template <typename Tin>
+__global__ __launch_bounds__(256) void softmax_topk_wave_kernel(const Tin* __restrict__ x, float* __restrict__ vals,
+                                                                int* __restrict__ idx, int rows, int N, int k,
+                                                                int apply_softmax, float temperature) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const long r = (long)blockIdx.x * 4 + wid;
+  if (r >= rows) return;
+  float* row = lds + wid * N;
+  const Tin* src = x + r * (long)N;
+  const float invt = 1.f / temperature;
+  float mx = -INFINITY;
+  for (int i = lane; i < N; i += 64) {
+    const float v = load_as_f32<Tin>(src, i) * invt;
+    row[i] = v;
+    mx = fmaxf(mx, v);
+  }
+  float denom = 1.f;
+  if (apply_softmax) {
+    mx = wave_max(mx);
+    float s = 0.f;
+    for (int i = lane; i < N; i += 64) s += __expf(row[i] - mx);
+    denom = wave_sum(s);
+  }
+  for (int j = 0; j < k; ++j) {
+    KV best{-INFINITY, -1};
+    for (int i = lane; i < N; i += 64) best = better(best, KV{row[i], i});
+    best = wave_argmax(best);
+    if (lane == 0) {
+      vals[r * k + j] = apply_softmax ? __expf(best.v - mx) / denom : best.v;
+      idx[r * k + j] = best.i;
+    }
+    if (best.i >= 0 && (best.i & 63) == lane) row[best.i] = -INFINITY;
+  }
+}
+
 // y = softmax(x * scale + mask) row-wise, bf16 in/out; mask (fp32, additive) is indexed
 // [row / rows_per_mask][N] (e.g. one padding mask per sequence shared by all heads/queries).
 __global__ __launch_bounds__(256) void softmax_rows_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
@@ -125,6 +163,17 @@ extern "C" {
 int mls_softmax_topk(const void* x, int dtype, float* vals, int* idx, int rows, int N, int k, int apply_softmax,
                      float temperature, void* stream) {
   if (rows <= 0 || N <= 0 || k <= 0 || k > N || N > 32768 || temperature <= 0.f) return MLS_BAD_ARG;
+  if (N <= 4096) {
+    const size_t lds4 = (size_t)4 * N * sizeof(float);
+    dim3 g((rows + 3) / 4);
+    if (dtype == 0)
+      hipLaunchKernelGGL(softmax_topk_wave_kernel<bf16>, g, dim3(256), lds4, (hipStream_t)stream, (const bf16*)x, vals,
+                         idx, rows, N, k, apply_softmax, temperature);
+    else
+      hipLaunchKernelGGL(softmax_topk_wave_kernel<float>, g, dim3(256), lds4, (hipStream_t)stream, (const float*)x,
+                         vals, idx, rows, N, k, apply_softmax, temperature);
+    return (int)hipGetLastError();
+  }
   const size_t lds = (size_t)N * sizeof(float);
   if (dtype == 0)
     hipLaunchKernelGGL(softmax_topk_kernel<bf16>, dim3(rows), dim3(256), lds, (hipStream_t)stream, (const bf16*)x,

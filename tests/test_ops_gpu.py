@@ -70,7 +70,7 @@ def test_conv_resnet_shapes(shape):
     res = torch.randn(B, ho, ho, cout, device=DEV).to(torch.bfloat16)
     ref = _conv_ref(x, w, bias, s, p, 1, res)
     ws = torch.empty(64 << 20, device=DEV, dtype=torch.float32)
-    for cfg in (0, 1, 2, 3, 4):
+    for cfg in range(0, 9):
         out = ops.conv2d_nhwc(x, ops.pack_conv_weight(w), bias, kernel=k, stride=s, pad=p, residual=res, act=1,
                               workspace=ws, cfg=cfg)
         torch.cuda.synchronize()
@@ -87,12 +87,13 @@ def test_conv_stem():
     torch.manual_seed(1)
     B, h = 2, 224
     x3 = torch.randn(B, h, h, 3, device=DEV)
-    x4 = torch.cat([x3, torch.zeros(B, h, h, 1, device=DEV)], dim=-1).to(torch.bfloat16)
+    x4 = torch.cat([x3, torch.zeros(B, h, h, 1, device=DEV)], dim=-1)
+    x4p = torch.nn.functional.pad(x4, (0, 0, 3, 3, 3, 3)).to(torch.bfloat16)  # pre-padded image
     w = (torch.randn(64, 3, 7, 7, device=DEV) / 12.0).to(torch.bfloat16)
     bias = torch.randn(64, device=DEV)
-    ref = _conv_ref(x4[..., :3], w, bias, 2, 3, 1)
-    for cfg in (0, 1, 2, 4):
-        out = ops.conv2d_nhwc(x4, ops.pack_conv_weight(w), bias, kernel=7, stride=2, pad=3, act=1, cfg=cfg)
+    ref = _conv_ref(x4.to(torch.bfloat16)[..., :3], w, bias, 2, 3, 1)
+    for cfg in range(0, 9):
+        out = ops.conv2d_nhwc(x4p, ops.pack_conv_weight(w), bias, kernel=7, stride=2, pad=0, act=1, cfg=cfg)
         assert out.shape == (B, 112, 112, 64)
         assert rel_err(out, ref) < 2e-2, f"cfg {cfg}"
 
@@ -112,7 +113,7 @@ def test_gemm(mnk, act):
     y = (a.float() @ w.float().T) * scale + bias + res.float()
     ref = {0: y, 1: torch.relu(y), 2: F.gelu(y), 3: torch.tanh(y), 4: F.silu(y)}[act]
     ws = torch.empty(16 << 20, device=DEV, dtype=torch.float32)
-    for cfg, sk in ((0, 0), (1, 1), (4, 2), (2, 3)):
+    for cfg, sk in ((0, 0), (1, 1), (4, 2), (2, 3), (5, 1), (6, 2), (7, 1), (8, 3)):
         out = ops.gemm(a, w, bias, scale=scale, residual=res, act=act, workspace=ws, cfg=cfg, splitk=sk)
         assert rel_err(out, ref) < 2e-2, f"cfg {cfg} sk {sk}"
 
@@ -134,10 +135,12 @@ def test_normalize_pool_head():
 
     torch.manual_seed(3)
     img = torch.randint(0, 256, (3, 224, 224, 3), dtype=torch.uint8, device=DEV)
-    out = ops.normalize_u8(img, IMAGENET_MEAN, IMAGENET_STD)
+    out = ops.normalize_u8(img, IMAGENET_MEAN, IMAGENET_STD, pad=3)
     ref = (img.float() - torch.tensor(IMAGENET_MEAN, device=DEV)) / torch.tensor(IMAGENET_STD, device=DEV)
-    assert rel_err(out[..., :3], ref) < 1e-2
+    assert out.shape == (3, 230, 230, 4)
+    assert rel_err(out[:, 3:-3, 3:-3, :3], ref) < 1e-2
     assert out[..., 3].abs().max().item() == 0
+    assert out[:, :3].abs().max().item() == 0 and out[:, :, -3:].abs().max().item() == 0
 
     x = torch.randn(2, 112, 112, 64, device=DEV).to(torch.bfloat16)
     mp = ops.maxpool2d_nhwc(x, 3, 2, 1)
