@@ -45,6 +45,7 @@ struct ConvArgs {
   int act;
   int splitk, kchunk;
   int ldo, ldr;
+  uint32_t o_bytes;
   uint32_t x_bytes, w_bytes, r_bytes;  // extents of x, w, res for the buffer-load range check
   int dbg;  // diagnostics only (ablation): 1 = skip MFMAs, 2 = skip output stores, 4 = skip operand DMA
 };
@@ -326,6 +327,242 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_kernel(const ConvArgs 
   }
 }
 
+// v3: persistent + software-pipelined across tiles.  Each block walks tiles lb, lb+G, ...; the
+// LDS-DMA ring (3 stages) runs continuously over the flattened (tile, k-step) sequence, so the
+// next tile's operands -- and, with its last k-step, its residual tile -- are in flight while the
+// current tile's epilogue runs.  Epilogue in place: acc*scale + bias + residual -> act -> bf16
+// written over the residual tile in LDS, then 16-B buffer stores (always issued, OOB-dropped, so
+// the hand-counted vmcnt stays exact).  Bias comes from a per-block LDS copy.  No split-K.
+template <int BM, int BN, int WM, int WN, int MODE>
+__global__ __launch_bounds__(WM * WN * 64) void conv_gemm_persistent(const ConvArgs a) {
+  constexpr int STAGES = 3;
+  constexpr int NW = WM * WN, NT = NW * 64;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, R_BYTES = BM * BN * 2;
+  constexpr int STAGE_BYTES = A_BYTES + B_BYTES + R_BYTES;
+  constexpr int AI = BM / 8 / NW, BI = BN / 8 / NW;
+  constexpr int RCPR = BN / 8;     // 16-B chunks per output / residual row
+  constexpr int RPP = 64 / RCPR;   // rows per 1-KiB DMA piece
+  constexpr int RI = BM / RPP / NW;
+  constexpr int EPI2 = BM * RCPR / NT;  // 16-B output stores per thread per tile
+  static_assert(AI * 8 * NW == BM && BI * 8 * NW == BN && RI * RPP * NW == BM && EPI2 * NT == BM * RCPR, "tile");
+  constexpr int LPS = AI + BI;
+  constexpr int BIAS_MAX = 2048;
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE_BYTES + BIAS_MAX * 4];
+  float* sbias = reinterpret_cast<float*>(smem + STAGES * STAGE_BYTES);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int ntm = (a.M + BM - 1) / BM, ntn = (a.N + BN - 1) / BN, T = ntm * ntn;
+  const int G = gridDim.x;
+  const int lb = xcd_remap(blockIdx.x, G);
+  if (lb >= T) return;
+  const int my_tiles = (T - lb + G - 1) / G;
+  const int nk = (a.K + BK - 1) / BK;
+  const int S_tot = my_tiles * nk;
+  const bool has_res = a.res != nullptr;
+  const bool bias_lds = a.bias != nullptr && a.N <= BIAS_MAX;
+  if (bias_lds)
+    for (int i = tid; i < a.N; i += NT) sbias[i] = a.bias[i];
+
+  const int r8 = lane >> 3, lc = (lane & 7) ^ r8;
+  const int rrow = lane / RCPR, rpc = lane % RCPR;
+  const rsrc_t xr = make_rsrc(a.x, a.x_bytes);
+  const rsrc_t wr = make_rsrc(a.w, a.w_bytes);
+  const rsrc_t rr = make_rsrc(a.res, a.r_bytes);
+  const rsrc_t orr = make_rsrc(a.out, a.o_bytes);
+  const int HoWo = a.Ho * a.Wo;
+
+  int a_v[AI], b_v[BI], r_v[RI];
+  uint32_t a_msk[AI];
+  auto setup_tile = [&](int k) {  // issue-side per-tile precompute (once per tile)
+    const int t = lb + k * G;
+    const int m0 = (t / ntn) * BM, n0 = (t % ntn) * BN;
+#pragma unroll
+    for (int j = 0; j < AI; ++j) {
+      const int m = m0 + (wid * AI + j) * 8 + r8;
+      a_msk[j] = 0u;
+      a_v[j] = OOB;
+      if (m < a.M) {
+        const int b = m / HoWo;
+        const int rem = m - b * HoWo;
+        const int oh = rem / a.Wo;
+        const int ow = rem - oh * a.Wo;
+        if (MODE == MODE_1X1) {
+          a_v[j] = (((b * a.H + oh * a.stride) * a.W + ow * a.stride) * a.Cin + lc * 8) * 2;
+        } else if (MODE == MODE_STEM) {
+          a_v[j] = (((b * a.H + oh * a.stride + (lc >> 2)) * a.W + ow * a.stride + 2 * (lc & 3)) * 4) * 2;
+        } else {
+          const int ih0 = oh * a.stride - a.pad, iw0 = ow * a.stride - a.pad;
+          uint32_t msk = 0u;
+          for (int kh = 0; kh < a.KH; ++kh)
+            for (int kw = 0; kw < a.KW; ++kw)
+              if ((unsigned)(ih0 + kh) < (unsigned)a.H && (unsigned)(iw0 + kw) < (unsigned)a.W)
+                msk |= 1u << (kh * a.KW + kw);
+          a_msk[j] = msk;
+          a_v[j] = ((b * a.H * a.W + ih0 * a.W + iw0) * a.Cin + lc * 8) * 2;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < BI; ++j) {
+      const int n = n0 + (wid * BI + j) * 8 + r8;
+      b_v[j] = n < a.N ? (n * a.K + lc * 8) * 2 : OOB;
+    }
+#pragma unroll
+    for (int j = 0; j < RI; ++j) {
+      const int row = (wid * RI + j) * RPP + rrow;
+      const int lch = rpc ^ (row & (RCPR - 1));
+      const int m = m0 + row, n = n0 + lch * 8;
+      r_v[j] = (m < a.M && n < a.N) ? (m * a.ldr + n) * 2 : OOB;
+    }
+  };
+
+  auto issue = [&](int sidx, int buf) {
+    const int k = sidx / nk, ks = sidx - k * nk;
+    if (ks == 0) setup_tile(k);
+    const int k0 = ks * BK;
+    char* sA = smem + buf * STAGE_BYTES;
+    char* sB = sA + A_BYTES;
+    char* sR = sB + B_BYTES;
+    const int left = a.K - k0;
+    const bool lane_kin = lc * 8 < left;
+    if (MODE == MODE_1X1) {
+#pragma unroll
+      for (int j = 0; j < AI; ++j) glds16(xr, sA + (wid * AI + j) * 1024, lane_kin ? a_v[j] : OOB, k0 * 2);
+    } else if (MODE == MODE_STEM) {
+      const int soff = (k0 >> 5) * a.W * 8;
+#pragma unroll
+      for (int j = 0; j < AI; ++j) glds16(xr, sA + (wid * AI + j) * 1024, a_v[j], soff);
+    } else {
+      const int tap = k0 / a.Cin;
+      const int c0 = k0 - tap * a.Cin;
+      const int kh = tap / a.KW;
+      const int kw = tap - kh * a.KW;
+      const int uni = ((kh * a.W + kw) * a.Cin + c0) * 2;
+#pragma unroll
+      for (int j = 0; j < AI; ++j) {
+        const bool ok = (a_msk[j] >> tap) & 1u;
+        glds16(xr, sA + (wid * AI + j) * 1024, ok ? a_v[j] + uni : OOB, 0);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < BI; ++j) glds16(wr, sB + (wid * BI + j) * 1024, lane_kin ? b_v[j] : OOB, k0 * 2);
+    if (has_res && ks == nk - 1) {
+#pragma unroll
+      for (int j = 0; j < RI; ++j) glds16(rr, sR + (wid * RI + j) * 1024, r_v[j], 0);
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  int issued = 0;
+  for (; issued < S_tot && issued < STAGES - 1; ++issued) issue(issued, issued);
+
+  const int fr = lane & 15, fq = lane >> 4;
+  bool prev_epi = false;
+  for (int s = 0; s < S_tot; ++s) {
+    // exact count of the VMEM ops younger than stage s: stage s+1's DMA (+ its residual pieces)
+    // and the previous epilogue's stores
+    if (issued > s + 1) {
+      const bool nr = has_res && ((s + 1) % nk == nk - 1);
+      if (nr && prev_epi)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPS + RI + EPI2) : "memory");
+      else if (nr)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPS + RI) : "memory");
+      else if (prev_epi)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPS + EPI2) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPS) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (issued < S_tot) {
+      issue(issued, issued % STAGES);
+      ++issued;
+    }
+    const int buf = s % STAGES;
+    const uint4* As = reinterpret_cast<const uint4*>(smem + buf * STAGE_BYTES);
+    const uint4* Bs = reinterpret_cast<const uint4*>(smem + buf * STAGE_BYTES + A_BYTES);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ch = fq + 4 * kk;
+      bf16x8 af[TM], bfv[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int r = wm * WTM + i * 16 + fr;
+        af[i] = __builtin_bit_cast(bf16x8, As[r * 8 + (ch ^ (r & 7))]);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int r = wn * WTN + j * 16 + fr;
+        bfv[j] = __builtin_bit_cast(bf16x8, Bs[r * 8 + (ch ^ (r & 7))]);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
+    }
+    prev_epi = false;
+    if (s % nk == nk - 1) {
+      const int t = lb + (s / nk) * G;
+      const int m0 = (t / ntn) * BM, n0 = (t % ntn) * BN;
+      char* sR = smem + buf * STAGE_BYTES + A_BYTES + B_BYTES;
+      // pass 1: in place over the residual tile (each element owned by exactly one lane)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = wn * WTN + j * 16 + fr;
+        const int n = n0 + col;
+        float bb = 0.f, sc = 1.f;
+        if (n < a.N) {
+          if (bias_lds) bb = sbias[n];
+          else if (a.bias) bb = a.bias[n];
+          if (a.scale) sc = a.scale[n];
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = wm * WTM + i * 16 + fq * 4 + r;
+            const int off = row * (BN * 2) + ((((col >> 3) ^ (row & (RCPR - 1)))) << 4) + (col & 7) * 2;
+            bf16* p = reinterpret_cast<bf16*>(sR + off);
+            float v = acc[i][j][r] * sc + bb;
+            if (has_res) v += (float)*p;
+            *p = (bf16)apply_act(v, a.act);
+          }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      // pass 2: whole 16-B rows out
+#pragma unroll
+      for (int it = 0; it < EPI2; ++it) {
+        const int q = tid + it * NT;
+        const int row = q / RCPR, c8 = q % RCPR;
+        const int m = m0 + row, n = n0 + c8 * 8;
+        const uint4 v = *reinterpret_cast<const uint4*>(sR + row * (BN * 2) + ((c8 ^ (row & (RCPR - 1))) << 4));
+        const int off = (m < a.M && n < a.N) ? (m * a.ldo + n) * 2 : OOB;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v),
+                                               orr, off, 0, 0);
+      }
+      prev_epi = true;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // sum split-K slabs + epilogue; one thread per 8 outputs
 __global__ __launch_bounds__(256) void splitk_epilogue_kernel(const ConvArgs a) {
   const bool glu = a.act == ACT_SILU_MUL;
@@ -427,9 +664,56 @@ void choose_cfg(int M, int N, int K, int& cfg, int& splitk) {
   while (tiles * splitk < 384 && K / (splitk * 2) >= 256 && splitk < 8) splitk *= 2;
 }
 
+int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
+}
+
+template <int MODE>
+void launch_persistent(int cfg, hipStream_t st, const ConvArgs& a) {
+  auto grid = [&](int bm, int bn, int per_cu) {
+    const long T = (long)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
+    const long g = (long)num_cus() * per_cu;
+    return dim3((unsigned)(T < g ? T : g));
+  };
+  switch (cfg) {
+    case 21: hipLaunchKernelGGL((conv_gemm_persistent<128, 64, 4, 2, MODE>), grid(128, 64, 1), dim3(512), 0, st, a); break;
+    case 22: hipLaunchKernelGGL((conv_gemm_persistent<64, 128, 2, 4, MODE>), grid(64, 128, 1), dim3(512), 0, st, a); break;
+    default: hipLaunchKernelGGL((conv_gemm_persistent<64, 64, 2, 2, MODE>), grid(64, 64, 2), dim3(256), 0, st, a); break;
+  }
+}
+
 int launch_conv(ConvArgs a, int mode, int cfg, int splitk, size_t ws_bytes, hipStream_t st) {
   if (a.act == ACT_SILU_MUL && a.N % 16 != 0) return MLS_BAD_ARG;
   if (a.N % 8 != 0 || a.M <= 0 || a.N <= 0 || a.K <= 0 || a.K % 8 != 0) return MLS_BAD_ARG;
+  {
+    const size_t ob = ((size_t)(a.M - 1) * a.ldo + (a.act == ACT_SILU_MUL ? a.N / 2 : a.N)) * 2;
+    if (ob >= 0x7FFFFFFFull) return MLS_UNSUPPORTED;
+    a.o_bytes = (uint32_t)ob;
+  }
+  if (cfg >= 20 && cfg <= 22) {
+    if (a.act != ACT_SILU_MUL && (splitk <= 1)) {
+      a.splitk = 1;
+      a.kchunk = a.K;
+      a.dbg = g_dbg_flags;
+      const size_t rb = a.res ? ((size_t)(a.M - 1) * a.ldr + a.N) * 2 : 0;
+      if (rb >= 0x7FFFFFFFull) return MLS_UNSUPPORTED;
+      a.r_bytes = (uint32_t)rb;
+      switch (mode) {
+        case MODE_1X1: launch_persistent<MODE_1X1>(cfg, st, a); break;
+        case MODE_GENERIC: launch_persistent<MODE_GENERIC>(cfg, st, a); break;
+        case MODE_STEM: launch_persistent<MODE_STEM>(cfg, st, a); break;
+        default: return MLS_UNSUPPORTED;
+      }
+      return (int)hipGetLastError();
+    }
+    cfg = 4;  // persistent kernel has no split-K / SiLU-mul: fall back
+  }
   int acfg = 0, asplit = 1;
   choose_cfg(a.M, a.N, a.K, acfg, asplit);
   if (cfg <= 0 || cfg >= kNumCfgs) cfg = acfg;
