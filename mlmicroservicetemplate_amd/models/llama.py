@@ -235,6 +235,13 @@ class LlamaTP:
                         for _ in range(cfg.layers)]
         self.v_cache = [torch.zeros_like(self.k_cache[0]) for _ in range(cfg.layers)]
         self.cos, self.sin = R.rope_tables(max_seq, D, cfg.rope_theta, self.device)
+        # hipGraph capture of the decode step (P4): removes ~300 host launches per token.  With
+        # tp > 1 the RCCL all-reduces are captured too (opt-in: MLS_TP_GRAPHS=1).
+        import os
+
+        self.use_graphs = backend == "fused" and self.device.type == "cuda" and (
+            tp == 1 or os.environ.get("MLS_TP_GRAPHS", "0") == "1")
+        self._graphs: Dict[Tuple[int, int], tuple] = {}
 
     # ---------------------------------------------------------------- shared pieces
     @property
@@ -337,8 +344,8 @@ class LlamaTP:
             else:
                 xn = ops.rmsnorm(delta, p[f"l{i}.attn_norm"], residual=r, residual_out=r, eps=cfg.eps)
             qkv = ops.gemm(xn, p[f"l{i}.qkv"], workspace=ws)
-            ops.rope_(qkv, positions.reshape(-1), self.cos, self.sin, sd.hq + sd.hkv, D)
-            ops.kv_append(qkv, sd.hq * D, (sd.hq + sd.hkv) * D, slots, self.k_cache[i], self.v_cache[i], sd.hkv, D)
+            ops.rope_kv_(qkv, positions.reshape(-1), self.cos, self.sin, sd.hq, sd.hkv, D, slots, self.k_cache[i],
+                         self.v_cache[i])
             if decode:
                 a = ops.decode_attention(qkv, self.k_cache[i][:B], self.v_cache[i][:B], lens, sd.hq, sd.hkv, D,
                                          workspace=self.dec_ws)
@@ -374,6 +381,40 @@ class LlamaTP:
                                        decode, k, slots)
         return self._ref_forward(ids, positions, lens, B, S, decode, k)
 
+    def _decode_graph(self, B: int, k: int):
+        """Captured decode step for batch B (static token / position / length buffers).  Must be
+        built before a prefill: its warm-up writes (garbage) into cache position 0."""
+        key = (B, k)
+        if key in self._graphs:
+            return self._graphs[key]
+        dev = self.device
+        tok = torch.zeros(B, 1, dtype=torch.int32, device=dev)
+        pos = torch.zeros(B, 1, dtype=torch.int32, device=dev)
+        lens = torch.ones(B, dtype=torch.int32, device=dev)
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                self.step(tok, pos, lens, decode=True, k=k)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            vals, idx = self.step(tok, pos, lens, decode=True, k=k)
+        self._graphs[key] = (g, tok, pos, lens, vals, idx)
+        return self._graphs[key]
+
+    def decode_step(self, tok: torch.Tensor, cur: torch.Tensor, k: int):
+        """One decode step: token at position ``cur`` (attending to cur + 1 keys)."""
+        B = tok.shape[0]
+        if self.use_graphs:
+            g, t_s, p_s, l_s, v_s, i_s = self._decode_graph(B, k)
+            t_s.copy_(tok.view(B, 1))
+            p_s.copy_(cur.view(B, 1))
+            l_s.copy_(cur.view(B) + 1)
+            g.replay()
+            return v_s, i_s
+        return self.step(tok.view(B, 1).to(torch.int32), cur.view(B, 1), cur.view(B) + 1, decode=True, k=k)
+
     @torch.no_grad()
     def generate(self, ids: torch.Tensor, lens: torch.Tensor, gp: GenParams) -> torch.Tensor:
         """ids int ``[B, S]`` (right-padded), lens ``[B]`` -> generated ``[B, max_new_tokens]``."""
@@ -384,6 +425,8 @@ class LlamaTP:
         ids = ids.to(dev)
         lens = lens.to(dev).to(torch.int32)
         k = max(1, min(gp.top_k, self.top_k_max))
+        if self.use_graphs and gp.max_new_tokens > 1:
+            self._decode_graph(B, k)  # before prefill (its warm-up touches cache position 0)
         pos = torch.arange(S, device=dev, dtype=torch.int32).unsqueeze(0).expand(B, S).contiguous()
         vals, idx = self.step(ids, pos, lens, decode=False, k=k)
         out = []
@@ -392,7 +435,7 @@ class LlamaTP:
         cur = lens.clone()
         for t in range(1, gp.max_new_tokens):
             # the new token sits at position cur; attention covers cur + 1 keys
-            vals, idx = self.step(tok.view(B, 1).to(torch.int32), cur.view(B, 1), cur + 1, decode=True, k=k)
+            vals, idx = self.decode_step(tok.to(torch.int32), cur, k)
             tok = self._merge_sample(vals, idx, gp, t)
             out.append(tok)
             cur = cur + 1

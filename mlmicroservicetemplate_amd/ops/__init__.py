@@ -177,6 +177,12 @@ def gemm(
         if tuple(out.shape) != (M, n_out):
             raise ValueError(f"out must be [M, {n_out}]")
     wsp, wsb = _workspace_args(workspace)
+    if M <= 16 and N % 16 == 0 and cfg == 0 and scale is None:
+        # decode-shaped: weight-streaming skinny MFMA kernel (splitk <= 0 -> auto K split)
+        rc = lib().mls_skinny_gemm(a.data_ptr(), w.data_ptr(), _ptr(bias), _ptr(residual), out.data_ptr(), wsp, wsb,
+                                   M, N, K, _act(act), splitk, stream_ptr(dev))
+        check(rc, "mls_skinny_gemm")
+        return out
     rc = lib().mls_gemm(
         a.data_ptr(), w.data_ptr(), _ptr(scale), _ptr(bias), _ptr(residual), out.data_ptr(), wsp, wsb,
         M, N, K, _act(act), cfg, splitk, stream_ptr(dev),
@@ -369,6 +375,19 @@ def rope_(qkv: torch.Tensor, positions: torch.Tensor, cos: torch.Tensor, sin: to
     rc = lib().mls_rope(qkv.data_ptr(), positions.data_ptr(), cos.data_ptr(), sin.data_ptr(), T, qkv.shape[-1],
                         n_rot_heads, head_dim, stream_ptr(dev))
     check(rc, "mls_rope")
+    return qkv
+
+
+def rope_kv_(qkv: torch.Tensor, positions: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, n_q_heads: int,
+             n_kv_heads: int, head_dim: int, slots: Optional[torch.Tensor] = None, k_cache=None, v_cache=None):
+    """Fused RoPE (Q and K heads, in place) + KV-cache append (slot -1 = skip) in one launch."""
+    dev = qkv.device
+    _need(qkv, "qkv", torch.bfloat16, dev)
+    _need(positions, "positions", torch.int32, dev)
+    T = positions.numel()
+    rc = lib().mls_rope_kv(qkv.data_ptr(), positions.data_ptr(), cos.data_ptr(), sin.data_ptr(), T, qkv.shape[-1],
+                           n_q_heads, n_kv_heads, head_dim, _ptr(slots), _ptr(k_cache), _ptr(v_cache), stream_ptr(dev))
+    check(rc, "mls_rope_kv")
     return qkv
 
 

@@ -21,6 +21,15 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const bf16* __restrict__
   if (row >= rows) return;
   const int nch = D >> 3;
   float v[CPL][8];
+  uint4 graw[CPL], braw[CPL];  // gamma / beta issued with x: one memory round trip, not two
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nch) {
+      graw[c] = ld16(gamma + ch * 8);
+      braw[c] = beta ? ld16(beta + ch * 8) : make_uint4(0, 0, 0, 0);
+    }
+  }
   float s = 0.f, ss = 0.f;
 #pragma unroll
   for (int c = 0; c < CPL; ++c) {
@@ -66,10 +75,10 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const bf16* __restrict__
     const int ch = lane + 64 * c;
     if (ch < nch) {
       float g[8], b[8], o[8];
-      unpack8(ld16(gamma + ch * 8), g);
-      if (beta) unpack8(ld16(beta + ch * 8), b);
+      unpack8(graw[c], g);
+      unpack8(braw[c], b);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = (v[c][e] - mean) * rstd * g[e] + (beta ? b[e] : 0.f);
+      for (int e = 0; e < 8; ++e) o[e] = (v[c][e] - mean) * rstd * g[e] + b[e];
       st16(out + row * D + ch * 8, pack8(o));
     }
   }
@@ -138,6 +147,50 @@ __global__ __launch_bounds__(256) void embedding_kernel(const int* __restrict__ 
     uint4 v = make_uint4(0, 0, 0, 0);
     if (id >= lo && id < hi) v = ld16(table + (long)(id - lo) * D + ch * 8);
     st16(out + t * D + ch * 8, v);
+  }
+}
+
+// RoPE + KV-cache append in one pass (decode / prefill): Q and K heads rotated in place, then
+// the (rotated) K heads and the V heads of each token copied to cache slot slots[t]; one launch
+// instead of two.  Block = one token; threads: (head, pair-quad) for the rotation, then 16-B copies.
+__global__ __launch_bounds__(256) void rope_kv_kernel(bf16* __restrict__ qkv, const int* __restrict__ positions,
+                                                      const float* __restrict__ cos_t, const float* __restrict__ sin_t,
+                                                      int row_stride, int Hq, int Hkv, int D,
+                                                      const int* __restrict__ slots, bf16* __restrict__ kc,
+                                                      bf16* __restrict__ vc) {
+  const long t = blockIdx.x;
+  const int half = D >> 1, quads = half >> 2;
+  const int p = positions[t];
+  bf16* row = qkv + t * row_stride;
+  const int nrot = Hq + Hkv;
+  for (int q = threadIdx.x; q < nrot * quads; q += blockDim.x) {
+    const int h = q / quads, i = (q % quads) * 4;
+    bf16* base = row + (long)h * D;
+    const bf16x4 a = __builtin_bit_cast(bf16x4, *reinterpret_cast<const uint2*>(base + i));
+    const bf16x4 b = __builtin_bit_cast(bf16x4, *reinterpret_cast<const uint2*>(base + half + i));
+    const float4 c = *reinterpret_cast<const float4*>(cos_t + (long)p * half + i);
+    const float4 sn = *reinterpret_cast<const float4*>(sin_t + (long)p * half + i);
+    const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {sn.x, sn.y, sn.z, sn.w};
+    bf16x4 oa, ob;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float x0 = (float)a[e], x1 = (float)b[e];
+      oa[e] = (bf16)(x0 * cc[e] - x1 * ss[e]);
+      ob[e] = (bf16)(x1 * cc[e] + x0 * ss[e]);
+    }
+    *reinterpret_cast<uint2*>(base + i) = __builtin_bit_cast(uint2, oa);
+    *reinterpret_cast<uint2*>(base + half + i) = __builtin_bit_cast(uint2, ob);
+  }
+  const int slot = slots ? slots[t] : -1;
+  if (slot < 0) return;
+  __syncthreads();  // rotated K visible to the copy below (LDS-free: same block, global memory)
+  __threadfence_block();
+  const int nch = (Hkv * D) >> 3;
+  for (int q = threadIdx.x; q < 2 * nch; q += blockDim.x) {
+    const int which = q / nch, ch = q % nch;
+    const bf16* src = row + (long)(Hq + which * Hkv) * D + ch * 8;
+    bf16* dst = (which ? vc : kc) + (long)slot * Hkv * D + ch * 8;
+    st16(dst, ld16(src));
   }
 }
 
@@ -255,6 +308,14 @@ int mls_rope(void* qkv, const int* positions, const float* cos_t, const float* s
   const long work = tokens * n_rot_heads * (D / 8);
   hipLaunchKernelGGL(rope_kernel, dim3(grid_for(work, 256)), dim3(256), 0, (hipStream_t)stream, (bf16*)qkv,
                      positions, cos_t, sin_t, tokens, row_stride, n_rot_heads, D);
+  return (int)hipGetLastError();
+}
+
+int mls_rope_kv(void* qkv, const int* positions, const float* cos_t, const float* sin_t, long tokens, int row_stride,
+                int Hq, int Hkv, int D, const int* slots, void* k_cache, void* v_cache, void* stream) {
+  if (D % 8 || tokens <= 0 || row_stride % 8) return MLS_BAD_ARG;
+  hipLaunchKernelGGL(rope_kv_kernel, dim3((unsigned)tokens), dim3(256), 0, (hipStream_t)stream, (bf16*)qkv, positions,
+                     cos_t, sin_t, row_stride, Hq, Hkv, D, slots, (bf16*)k_cache, (bf16*)v_cache);
   return (int)hipGetLastError();
 }
 

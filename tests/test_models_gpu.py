@@ -27,6 +27,30 @@ def test_gemm_silu_mul():
         assert rel(out, ref) < 2e-2, (cfg, sk)
 
 
+@pytest.mark.parametrize("M", [1, 5, 16, 17, 32])
+@pytest.mark.parametrize("nsplit", [0, 1, 3])
+def test_skinny_gemm(M, nsplit):
+    from mlmicroservicetemplate_amd import ops
+
+    torch.manual_seed(M)
+    N, K = 1024, 1000
+    a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) / K**0.5).to(torch.bfloat16)
+    b = torch.randn(N, device=DEV)
+    r = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    ws = torch.empty(4 << 20, device=DEV, dtype=torch.float32)
+    y = a.float() @ w.float().T + b
+    for act, ref in ((0, y + r.float()), (2, torch.nn.functional.gelu(y + r.float()))):
+        out = ops.gemm(a, w, b, residual=r, act=act, workspace=ws, splitk=nsplit)
+        assert rel(out, ref) < 2e-2
+    g = w[:512].contiguous()
+    u = w[512:].contiguous()
+    wi = ops.interleave_gate_up(g, u)
+    out = ops.gemm(a, wi, act="silu_mul", workspace=ws, splitk=nsplit)
+    ref = torch.nn.functional.silu(a.float() @ g.float().T) * (a.float() @ u.float().T)
+    assert out.shape == (M, 512) and rel(out, ref) < 2e-2
+
+
 def test_topk_large():
     from mlmicroservicetemplate_amd import ops
 

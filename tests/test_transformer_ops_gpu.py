@@ -63,6 +63,7 @@ def test_rope_and_kv_append(ops):
     torch.manual_seed(2)
     T, Hq, Hkv, D = 45, 8, 2, 128
     qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=DEV).to(torch.bfloat16)
+    qkv0 = qkv.clone()
     pos = torch.randint(0, 1000, (T,), device=DEV, dtype=torch.int32)
     cos, sin = R.rope_tables(2048, D, 500000.0, DEV)
     ref_q = R.rope(qkv[:, : Hq * D].view(T, Hq, D), pos, cos, sin).reshape(T, -1)
@@ -78,6 +79,11 @@ def test_rope_and_kv_append(ops):
     ops.kv_append(qkv, Hq * D, (Hq + Hkv) * D, slots, kc, vc, Hkv, D)
     assert torch.equal(kc[slots.long()].reshape(T, -1), qkv[:, Hq * D: (Hq + Hkv) * D])
     assert torch.equal(vc[slots.long()].reshape(T, -1), qkv[:, (Hq + Hkv) * D:])
+    # fused rope + append on a fresh copy matches the two-kernel path
+    qkv2 = qkv0.clone()
+    kc2, vc2 = torch.zeros_like(kc), torch.zeros_like(vc)
+    ops.rope_kv_(qkv2, pos, cos, sin, Hq, Hkv, D, slots, kc2, vc2)
+    assert torch.equal(qkv2, qkv) and torch.equal(kc2, kc) and torch.equal(vc2, vc)
 
 
 @pytest.mark.parametrize("cfg", [
