@@ -218,13 +218,24 @@ class BertFused:
                                 S, eps=cfg.eps)
         ws = self.workspace
         for i in range(cfg.layers):
-            qkv = ops.gemm(x, w[f"l{i}.qkv.w"], w[f"l{i}.qkv.b"], workspace=ws)
+            # large token counts: library GEMMs with the residual folded into the LayerNorm;
+            # small ones: native GEMMs with the residual in the epilogue
+            blas = B * S >= ops.BLAS_MIN_M
+            qkv = ops.linear(x, w[f"l{i}.qkv.w"], w[f"l{i}.qkv.b"], workspace=ws)
             a = ops.flash_attention(qkv, B, S, cfg.heads, cfg.heads, cfg.head_dim, kv_lens=lens)
-            h = ops.gemm(a, w[f"l{i}.o.w"], w[f"l{i}.o.b"], residual=x, workspace=ws)
-            x = ops.layernorm(h, w[f"l{i}.ln1.g"], w[f"l{i}.ln1.b"], eps=cfg.eps)
-            f1 = ops.gemm(x, w[f"l{i}.ffn1.w"], w[f"l{i}.ffn1.b"], act=ops.ACT_GELU, workspace=ws)
-            h = ops.gemm(f1, w[f"l{i}.ffn2.w"], w[f"l{i}.ffn2.b"], residual=x, workspace=ws)
-            x = ops.layernorm(h, w[f"l{i}.ln2.g"], w[f"l{i}.ln2.b"], eps=cfg.eps)
+            if blas:
+                h = ops.linear(a, w[f"l{i}.o.w"], w[f"l{i}.o.b"])
+                x = ops.layernorm(h, w[f"l{i}.ln1.g"], w[f"l{i}.ln1.b"], residual=x, eps=cfg.eps)
+            else:
+                h = ops.gemm(a, w[f"l{i}.o.w"], w[f"l{i}.o.b"], residual=x, workspace=ws)
+                x = ops.layernorm(h, w[f"l{i}.ln1.g"], w[f"l{i}.ln1.b"], eps=cfg.eps)
+            f1 = ops.linear(x, w[f"l{i}.ffn1.w"], w[f"l{i}.ffn1.b"], act=ops.ACT_GELU, workspace=ws)
+            if blas:
+                h = ops.linear(f1, w[f"l{i}.ffn2.w"], w[f"l{i}.ffn2.b"])
+                x = ops.layernorm(h, w[f"l{i}.ln2.g"], w[f"l{i}.ln2.b"], residual=x, eps=cfg.eps)
+            else:
+                h = ops.gemm(f1, w[f"l{i}.ffn2.w"], w[f"l{i}.ffn2.b"], residual=x, workspace=ws)
+                x = ops.layernorm(h, w[f"l{i}.ln2.g"], w[f"l{i}.ln2.b"], eps=cfg.eps)
         cls_rows = x.view(B, S, H)[:, 0].contiguous()
         pooled = ops.gemm(cls_rows, w["pooler.w"], w["pooler.b"], act=ops.ACT_TANH, workspace=ws)
         return ops.gemm(pooled, self.cls_w, self.cls_b, workspace=ws)

@@ -343,7 +343,7 @@ class LlamaTP:
                 xn = ops.rmsnorm(r, p[f"l{i}.attn_norm"], eps=cfg.eps)
             else:
                 xn = ops.rmsnorm(delta, p[f"l{i}.attn_norm"], residual=r, residual_out=r, eps=cfg.eps)
-            qkv = ops.gemm(xn, p[f"l{i}.qkv"], workspace=ws)
+            qkv = ops.linear(xn, p[f"l{i}.qkv"], workspace=ws)
             ops.rope_kv_(qkv, positions.reshape(-1), self.cos, self.sin, sd.hq, sd.hkv, D, slots, self.k_cache[i],
                          self.v_cache[i])
             if decode:
@@ -351,10 +351,10 @@ class LlamaTP:
                                          workspace=self.dec_ws)
             else:
                 a = ops.flash_attention(qkv, B, S, sd.hq, sd.hkv, D, kv_lens=lens, causal=True)
-            o = self.comm.all_reduce_(ops.gemm(a, p[f"l{i}.o"], workspace=ws))
+            o = self.comm.all_reduce_(ops.linear(a, p[f"l{i}.o"], workspace=ws))
             xn = ops.rmsnorm(o, p[f"l{i}.mlp_norm"], residual=r, residual_out=r, eps=cfg.eps)
-            gu = ops.gemm(xn, p[f"l{i}.gate_up"], act=ops.ACT_SILU_MUL, workspace=ws)
-            delta = self.comm.all_reduce_(ops.gemm(gu, p[f"l{i}.down"], workspace=ws))
+            gu = ops.linear(xn, p[f"l{i}.gate_up"], act=ops.ACT_SILU_MUL, workspace=ws)
+            delta = self.comm.all_reduce_(ops.linear(gu, p[f"l{i}.down"], workspace=ws))
         xn = ops.rmsnorm(delta, p["final_norm"], residual=r, eps=cfg.eps)
         if not decode:
             last = (torch.arange(B, device=xn.device, dtype=torch.int64) * S + lens.long() - 1)

@@ -10,6 +10,7 @@ Layouts: activations NHWC / row-major ``[rows][features]`` bf16; conv weights
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -189,6 +190,63 @@ def gemm(
     )
     check(rc, "mls_gemm")
     return out
+
+
+# Plain library GEMMs go to hipBLASLt (through torch.addmm): on the transformer prefill shapes it
+# runs 1.4-1.5 PFLOP/s against 0.9-1.0 for the native 128x128-tile kernel (profiles/r1_gemm_probe.jsonl).
+# The native kernels keep the decode-shaped (skinny) products and every fused epilogue hipBLASLt
+# cannot express (residual+bias, SiLU-mul is done by a native elementwise pass after it).
+BLAS_MIN_M = int(os.environ.get("MLS_BLAS_MIN_M", "512"))
+_BF16_BIAS: dict = {}
+
+
+def _bias_bf16(bias: torch.Tensor) -> torch.Tensor:
+    key = (bias.data_ptr(), bias.numel(), bias.device)
+    hit = _BF16_BIAS.get(key)
+    if hit is None or hit[0] is not bias:
+        hit = (bias, bias.to(torch.bfloat16))
+        _BF16_BIAS[key] = hit
+    return hit[1]
+
+
+def silu_mul_interleaved(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``[M, 2I]`` gate/up interleaved in groups of 8 -> ``silu(gate) * up`` ``[M, I]``."""
+    _need(x, "x", torch.bfloat16, x.device)
+    M, N2 = x.shape
+    if out is None:
+        out = torch.empty(M, N2 // 2, device=x.device, dtype=torch.bfloat16)
+    check(lib().mls_silu_mul_interleaved(x.data_ptr(), out.data_ptr(), M, N2 // 2, stream_ptr(x.device)),
+          "mls_silu_mul_interleaved")
+    return out
+
+
+def linear(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, act=ACT_NONE,
+           residual: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
+           impl: str = "auto") -> torch.Tensor:
+    """Transformer projection ``act(a @ w.T + bias (+ residual))`` with the implementation chosen by
+    shape: hipBLASLt for large-M plain GEMMs (bias and GELU as its epilogues, SiLU-mul as a native
+    pass), the native kernels otherwise (``impl`` = "auto" | "native" | "blas")."""
+    code = _act(act)
+    M = a.shape[0]
+    blas = impl == "blas" or (impl == "auto" and M >= BLAS_MIN_M)
+    if not blas or code not in (ACT_NONE, ACT_GELU, ACT_SILU_MUL) or a.device.type != "cuda":
+        return gemm(a, w, bias, act=code, residual=residual, workspace=workspace)
+    b16 = _bias_bf16(bias) if bias is not None else None
+    if code == ACT_GELU:
+        y = torch._addmm_activation(b16 if b16 is not None else torch.zeros(w.shape[0], device=a.device,
+                                    dtype=torch.bfloat16), a, w.t(), use_gelu=True)
+    elif residual is not None and b16 is None:
+        y = torch.addmm(residual, a, w.t())
+        residual = None
+    elif b16 is not None:
+        y = torch.addmm(b16, a, w.t())
+    else:
+        y = torch.mm(a, w.t())
+    if residual is not None:
+        y += residual
+    if code == ACT_SILU_MUL:
+        y = silu_mul_interleaved(y)
+    return y
 
 
 def interleave_gate_up(gate: torch.Tensor, up: torch.Tensor) -> torch.Tensor:

@@ -40,6 +40,7 @@ _SIGS = {
     "mls_maxpool2d": [P, P, I, I, I, I, I, I, I, P],
     "mls_avgpool_global": [P, P, I, I, I, P],
     "mls_bn_act": [P, P, P, P, L, I, I, P],
+    "mls_silu_mul_interleaved": [P, P, L, I, P],
     "mls_softmax_topk": [P, I, P, P, I, I, I, I, F, P],
     "mls_softmax_rows": [P, P, P, I, I, I, F, P],
     "mls_layernorm": [P, P, P, P, P, P, L, I, F, I, P],

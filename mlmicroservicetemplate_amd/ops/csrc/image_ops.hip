@@ -142,6 +142,17 @@ __global__ __launch_bounds__(256) void bn_act_kernel(const bf16* __restrict__ x,
   }
 }
 
+__global__ __launch_bounds__(256) void silu_mul_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, long groups) {
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < groups; q += (long)gridDim.x * blockDim.x) {
+    float g[8], u[8], o[8];
+    unpack8(ld16(x + q * 16), g);
+    unpack8(ld16(x + q * 16 + 8), u);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = silu(g[e]) * u[e];
+    st16(y + q * 8, pack8(o));
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -176,6 +187,16 @@ int mls_avgpool_global(const void* x, void* y, int B, int HW, int C, void* strea
   const int groups = (C / 8 + 63) / 64;
   hipLaunchKernelGGL(avgpool_kernel, dim3(B * groups), dim3(256), 0, (hipStream_t)stream, (const bf16*)x, (bf16*)y, B,
                      HW, C, 1.f / (float)HW);
+  return (int)hipGetLastError();
+}
+
+// SiLU-mul over a gate/up-interleaved GEMM output (groups of 8: gate 0-7, up 0-7, ...):
+// y[m][8j+e] = silu(x[m][16j+e]) * x[m][16j+8+e]; the epilogue of a library (hipBLASLt) gate/up GEMM.
+int mls_silu_mul_interleaved(const void* x, void* y, long rows, int n_out, void* stream) {
+  if (n_out % 8) return MLS_BAD_ARG;
+  const long total = rows * (n_out / 8);
+  hipLaunchKernelGGL(silu_mul_kernel, dim3(grid_for(total, 256)), dim3(256), 0, (hipStream_t)stream, (const bf16*)x,
+                     (bf16*)y, total);
   return (int)hipGetLastError();
 }
 
