@@ -225,8 +225,14 @@ class LlamaTP:
             from .. import ops
 
             self.ops = ops
+            # RMSNorm gains folded into the projections that consume the normalised activations
             for i in range(cfg.layers):
-                self.p[f"l{i}.gate_up"] = ops.interleave_gate_up(self.p.pop(f"l{i}.gate"), self.p.pop(f"l{i}.up"))
+                gu = ops.interleave_gate_up(self.p.pop(f"l{i}.gate"), self.p.pop(f"l{i}.up"))
+                mlp_g = self.p.pop(f"l{i}.mlp_norm")
+                self.p[f"l{i}.gate_up"] = ops.fold_norm(gu, mlp_g)
+                self.p[f"l{i}.qkv"] = ops.fold_norm(self.p[f"l{i}.qkv"], self.p.pop(f"l{i}.attn_norm"))
+            self.p["lm_head"] = ops.fold_norm(self.p["lm_head"], self.p.pop("final_norm"))
+            self.ones = torch.ones(cfg.hidden, device=self.device, dtype=torch.bfloat16)
             self.workspace = torch.empty(32 << 20, device=self.device, dtype=torch.float32)
             self.dec_ws = torch.empty(max_batch * self.sd.hq * (-(-max_seq // 256)) * (D + 2) + 16,
                                       device=self.device, dtype=torch.float32)
@@ -332,53 +338,58 @@ class LlamaTP:
 
     # ---------------------------------------------------------------- fused backend
     def _fused_forward(self, ids: torch.Tensor, positions: torch.Tensor, lens: torch.Tensor, B: int, S: int,
-                       decode: bool, k: int, slots: torch.Tensor):
+                       decode: bool, k: int):
+        """Native-kernel forward.  The RMSNorm gains are folded into the following projections, so
+        for decode-shaped token counts (<= 16) each pre-norm + residual add rides inside the skinny
+        GEMM (``ops.gemm_rmsnorm``: 7 launches per layer); larger counts run a gain-free RMSNorm and
+        the library / native GEMM (``ops.linear``)."""
         ops, cfg, sd, p = self.ops, self.cfg, self.sd, self.p
-        D = cfg.head_dim
+        D, eps = cfg.head_dim, cfg.eps
         ws = self.workspace
+        fuse = B * S <= 16
+        pos = positions.reshape(-1)
         r = self._embed(ids.reshape(-1))  # residual stream (bf16)
         delta = None
+
+        def pre_norm(x, w, d, act=ops.ACT_NONE):
+            if fuse:
+                r_new = None if d is None else torch.empty_like(x)
+                y = ops.gemm_rmsnorm(x, w, d, r_new, act=act, eps=eps, workspace=ws)
+                return y, (x if d is None else r_new)
+            xn = ops.rmsnorm(x if d is None else d, self.ones, residual=None if d is None else x,
+                             residual_out=None if d is None else x, eps=eps)
+            return ops.linear(xn, w, act=act, workspace=ws), x
+
         for i in range(cfg.layers):
-            if delta is None:
-                xn = ops.rmsnorm(r, p[f"l{i}.attn_norm"], eps=cfg.eps)
-            else:
-                xn = ops.rmsnorm(delta, p[f"l{i}.attn_norm"], residual=r, residual_out=r, eps=cfg.eps)
-            qkv = ops.linear(xn, p[f"l{i}.qkv"], workspace=ws)
-            ops.rope_kv_(qkv, positions.reshape(-1), self.cos, self.sin, sd.hq, sd.hkv, D, slots, self.k_cache[i],
-                         self.v_cache[i])
+            qkv, r = pre_norm(r, p[f"l{i}.qkv"], delta)
+            ops.rope_kv_(qkv, pos, self.cos, self.sin, sd.hq, sd.hkv, D, None, self.k_cache[i], self.v_cache[i],
+                         lens=lens, seq=S, max_seq=self.max_seq)
             if decode:
                 a = ops.decode_attention(qkv, self.k_cache[i][:B], self.v_cache[i][:B], lens, sd.hq, sd.hkv, D,
                                          workspace=self.dec_ws)
             else:
                 a = ops.flash_attention(qkv, B, S, sd.hq, sd.hkv, D, kv_lens=lens, causal=True)
             o = self.comm.all_reduce_(ops.linear(a, p[f"l{i}.o"], workspace=ws))
-            xn = ops.rmsnorm(o, p[f"l{i}.mlp_norm"], residual=r, residual_out=r, eps=cfg.eps)
-            gu = ops.linear(xn, p[f"l{i}.gate_up"], act=ops.ACT_SILU_MUL, workspace=ws)
+            gu, r = pre_norm(r, p[f"l{i}.gate_up"], o, act=ops.ACT_SILU_MUL)
             delta = self.comm.all_reduce_(ops.linear(gu, p[f"l{i}.down"], workspace=ws))
-        xn = ops.rmsnorm(delta, p["final_norm"], residual=r, eps=cfg.eps)
         if not decode:
-            last = (torch.arange(B, device=xn.device, dtype=torch.int64) * S + lens.long() - 1)
-            xn = xn.index_select(0, last)
-        logits = ops.gemm(xn.contiguous(), p["lm_head"], workspace=ws)
+            last = (torch.arange(B, device=r.device, dtype=torch.int64) * S + lens.long() - 1)
+            r, delta = r.index_select(0, last), delta.index_select(0, last)
+        if B <= 16:
+            logits = ops.gemm_rmsnorm(r, p["lm_head"], delta, eps=eps, workspace=ws)
+        else:
+            xn = ops.rmsnorm(delta, self.ones, residual=r, eps=eps)
+            logits = ops.gemm(xn, p["lm_head"], workspace=ws)
         return self._local_topk(logits, k)
 
     # ---------------------------------------------------------------- public
-    def _slots(self, B: int, S: int, positions: torch.Tensor, lens: torch.Tensor, decode: bool) -> torch.Tensor:
-        b = torch.arange(B, device=self.device, dtype=torch.int64).repeat_interleave(S)
-        pos = positions.reshape(-1).long()
-        slots = b * self.max_seq + pos
-        if not decode:
-            slots = torch.where(pos < lens.long()[b], slots, torch.full_like(slots, -1))
-        return slots.to(torch.int32)
-
     @torch.no_grad()
     def step(self, ids: torch.Tensor, positions: torch.Tensor, lens: torch.Tensor, decode: bool, k: int):
         B, S = ids.shape
         ids, positions, lens = ids.contiguous(), positions.contiguous(), lens.contiguous()
         if self.backend == "fused":
-            slots = self._slots(B, S, positions, lens, decode)
             return self._fused_forward(ids.to(torch.int32), positions.to(torch.int32), lens.to(torch.int32), B, S,
-                                       decode, k, slots)
+                                       decode, k)
         return self._ref_forward(ids, positions, lens, B, S, decode, k)
 
     def _decode_graph(self, B: int, k: int):

@@ -192,6 +192,40 @@ def gemm(
     return out
 
 
+def gemm_rmsnorm(x: torch.Tensor, w_folded: torch.Tensor, delta: Optional[torch.Tensor] = None,
+                 resid_out: Optional[torch.Tensor] = None, *, act=ACT_NONE, eps: float = 1e-5,
+                 workspace: Optional[torch.Tensor] = None, splitk: int = 0) -> torch.Tensor:
+    """Decode-shaped (M <= 32) ``act(RMSNorm(x + delta) @ W^T)`` in ONE launch, with the RMSNorm gain
+    pre-folded into ``w_folded`` (:func:`fold_norm`); ``x + delta`` is also written to ``resid_out``
+    (a buffer distinct from ``x``/``delta``) when given."""
+    dev = x.device
+    _need(x, "x", torch.bfloat16, dev)
+    _need(w_folded, "w", torch.bfloat16, dev)
+    M, K = x.shape
+    N = w_folded.shape[0]
+    if M > 32 or N % 16 or w_folded.shape[1] != K:
+        raise ValueError("gemm_rmsnorm: M <= 32, N % 16 == 0, matching K")
+    for name, t in (("delta", delta), ("resid_out", resid_out)):
+        if t is not None:
+            _need(t, name, torch.bfloat16, dev)
+            if tuple(t.shape) != (M, K):
+                raise ValueError(f"{name} must be [M, K]")
+    if resid_out is not None and delta is None:
+        raise ValueError("resid_out needs delta")
+    code = _act(act)
+    out = torch.empty(M, N // 2 if code == ACT_SILU_MUL else N, device=dev, dtype=torch.bfloat16)
+    wsp, wsb = _workspace_args(workspace)
+    rc = lib().mls_skinny_gemm_norm(x.data_ptr(), _ptr(delta), _ptr(resid_out), w_folded.data_ptr(), None, None,
+                                    out.data_ptr(), wsp, wsb, M, N, K, code, splitk, 1, float(eps), stream_ptr(dev))
+    check(rc, "mls_skinny_gemm_norm")
+    return out
+
+
+def fold_norm(w: torch.Tensor, gain: torch.Tensor) -> torch.Tensor:
+    """``W[:, k] * gain[k]`` in fp32, rounded once to bf16: RMSNorm(x) @ W^T == rstd * (x @ fold^T)."""
+    return (w.float() * gain.float().view(1, -1)).to(w.dtype)
+
+
 # Plain library GEMMs go to hipBLASLt (through torch.addmm): on the transformer prefill shapes it
 # runs 1.4-1.5 PFLOP/s against 0.9-1.0 for the native 128x128-tile kernel (profiles/r1_gemm_probe.jsonl).
 # The native kernels keep the decode-shaped (skinny) products and every fused epilogue hipBLASLt
@@ -437,14 +471,18 @@ def rope_(qkv: torch.Tensor, positions: torch.Tensor, cos: torch.Tensor, sin: to
 
 
 def rope_kv_(qkv: torch.Tensor, positions: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, n_q_heads: int,
-             n_kv_heads: int, head_dim: int, slots: Optional[torch.Tensor] = None, k_cache=None, v_cache=None):
-    """Fused RoPE (Q and K heads, in place) + KV-cache append (slot -1 = skip) in one launch."""
+             n_kv_heads: int, head_dim: int, slots: Optional[torch.Tensor] = None, k_cache=None, v_cache=None,
+             lens: Optional[torch.Tensor] = None, seq: int = 1, max_seq: int = 0):
+    """Fused RoPE (Q and K heads, in place) + KV-cache append in one launch.  Cache slots come from
+    ``slots`` (-1 = skip) or, with ``slots=None`` and ``max_seq > 0``, from the token index: token t
+    is (batch t // seq, position p) -> slot ``b * max_seq + p``, skipped unless ``p < lens[b]``."""
     dev = qkv.device
     _need(qkv, "qkv", torch.bfloat16, dev)
     _need(positions, "positions", torch.int32, dev)
     T = positions.numel()
     rc = lib().mls_rope_kv(qkv.data_ptr(), positions.data_ptr(), cos.data_ptr(), sin.data_ptr(), T, qkv.shape[-1],
-                           n_q_heads, n_kv_heads, head_dim, _ptr(slots), _ptr(k_cache), _ptr(v_cache), stream_ptr(dev))
+                           n_q_heads, n_kv_heads, head_dim, _ptr(slots), _ptr(k_cache), _ptr(v_cache), _ptr(lens),
+                           seq, max_seq, stream_ptr(dev))
     check(rc, "mls_rope_kv")
     return qkv
 

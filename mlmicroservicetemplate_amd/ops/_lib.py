@@ -47,10 +47,11 @@ _SIGS = {
     "mls_embed_ln": [P, P, P, P, P, P, P, P, L, I, I, I, F, P],
     "mls_embedding": [P, P, P, L, I, I, I, P],
     "mls_rope": [P, P, P, P, L, I, I, I, P],
-    "mls_rope_kv": [P, P, P, P, L, I, I, I, I, P, P, P, P],
+    "mls_rope_kv": [P, P, P, P, L, I, I, I, I, P, P, P, P, I, I, P],
     "mls_kv_append": [P, I, I, I, P, P, P, L, I, I, P],
     "mls_flash_attention": [P, P, P, P, I, I, I, I, I, I, I, I, I, P, I, F, P],
     "mls_skinny_gemm": [P, P, P, P, P, P, SZ, I, I, I, I, I, P],
+    "mls_skinny_gemm_norm": [P, P, P, P, P, P, P, P, SZ, I, I, I, I, I, I, F, P],
     "mls_decode_attention": [P, P, P, P, P, P, I, I, L, P, I, I, I, I, I, I, F, P],
 }
 _OPTIONAL_SIGS: dict = {"mls_set_debug_flags": [I]}

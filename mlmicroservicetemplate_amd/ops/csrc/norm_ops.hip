@@ -157,7 +157,8 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(bf16* __restrict__ qkv, co
                                                       const float* __restrict__ cos_t, const float* __restrict__ sin_t,
                                                       int row_stride, int Hq, int Hkv, int D,
                                                       const int* __restrict__ slots, bf16* __restrict__ kc,
-                                                      bf16* __restrict__ vc) {
+                                                      bf16* __restrict__ vc, const int* __restrict__ lens, int S,
+                                                      int max_seq) {
   const long t = blockIdx.x;
   const int half = D >> 1, quads = half >> 2;
   const int p = positions[t];
@@ -181,8 +182,16 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(bf16* __restrict__ qkv, co
     *reinterpret_cast<uint2*>(base + i) = __builtin_bit_cast(uint2, oa);
     *reinterpret_cast<uint2*>(base + half + i) = __builtin_bit_cast(uint2, ob);
   }
-  const int slot = slots ? slots[t] : -1;
-  if (slot < 0) return;
+  // cache slot: explicit, or derived -- token t is (batch t / S, position p) in a [B][max_seq] cache,
+  // written only while p < lens[b] (prefill padding skipped; decode: lens = position + 1)
+  int slot = -1;
+  if (slots) {
+    slot = slots[t];
+  } else if (max_seq > 0) {
+    const int b = (int)(t / S);
+    if (p < max_seq && (!lens || p < lens[b])) slot = b * max_seq + p;
+  }
+  if (slot < 0 || !kc) return;
   __syncthreads();  // rotated K visible to the copy below (LDS-free: same block, global memory)
   __threadfence_block();
   const int nch = (Hkv * D) >> 3;
@@ -312,10 +321,11 @@ int mls_rope(void* qkv, const int* positions, const float* cos_t, const float* s
 }
 
 int mls_rope_kv(void* qkv, const int* positions, const float* cos_t, const float* sin_t, long tokens, int row_stride,
-                int Hq, int Hkv, int D, const int* slots, void* k_cache, void* v_cache, void* stream) {
-  if (D % 8 || tokens <= 0 || row_stride % 8) return MLS_BAD_ARG;
+                int Hq, int Hkv, int D, const int* slots, void* k_cache, void* v_cache, const int* lens, int S,
+                int max_seq, void* stream) {
+  if (D % 8 || tokens <= 0 || row_stride % 8 || (!slots && max_seq > 0 && S <= 0)) return MLS_BAD_ARG;
   hipLaunchKernelGGL(rope_kv_kernel, dim3((unsigned)tokens), dim3(256), 0, (hipStream_t)stream, (bf16*)qkv, positions,
-                     cos_t, sin_t, row_stride, Hq, Hkv, D, slots, (bf16*)k_cache, (bf16*)v_cache);
+                     cos_t, sin_t, row_stride, Hq, Hkv, D, slots, (bf16*)k_cache, (bf16*)v_cache, lens, S, max_seq);
   return (int)hipGetLastError();
 }
 

@@ -8,100 +8,188 @@
 // splits K across blocks (fp32 slabs + a finishing epilogue kernel).  The epilogue fuses bias,
 // activation, residual and the SiLU-mul of the interleaved gate/up projection (a 16-column
 // tile = 8 gate + 8 up columns).
+//
+// Fused pre-norm (decode): with `norm` set the kernel computes RMSNorm(a + a2) on the fly -- the
+// RMSNorm gain is folded into W's columns at load time, so x_norm @ W^T = rstd[m] * ((a+a2) @ W'^T)
+// and rstd only scales the epilogue.  Each block already streams every element of its rows of
+// (a + a2) through registers for the MFMA, so the sum of squares costs nothing extra; blocks of
+// column tile 0 also write the updated residual stream a + a2 to a_out (a separate buffer: other
+// blocks still read a).  This removes the standalone RMSNorm launch (2 per layer) from decode.
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
 
 struct SkArgs {
-  const bf16* a;  // [M][lda]
-  const bf16* w;  // [N][K]
+  const bf16* a;   // [M][lda]
+  const bf16* a2;  // optional [M][lda] added to a (residual-stream update)
+  bf16* a_out;     // optional [M][lda] <- a + a2 (written by column-tile-0 blocks)
+  const bf16* w;   // [N][K]
   const float* bias;
   const bf16* res;  // [M][N]
   bf16* out;        // [M][ldo]
   float* ws;        // [nsplit][M][N]
-  int M, N, K, lda, ldo, act, nsplit, ksteps_per_split;
+  int M, N, K, lda, ldo, act, nsplit, ksteps_per_split, norm;
+  float eps;
   uint32_t a_bytes, w_bytes;
 };
 
+// fusion modes of the A prologue (template parameter, so the unrolled k loop has no runtime
+// branches -- a branch there makes hipcc drain vmcnt(0) per k-step, cdna_hip_programming.md item 4c)
+enum { FUSE_NONE = 0, FUSE_NORM = 1, FUSE_ADD_NORM = 2 };
+
+MLS_DEV uint4 add_round(uint4 a, uint4 b) {  // bf16 + bf16 -> bf16 (the residual stream's precision)
+  float x[8], y[8];
+  unpack8(a, x);
+  unpack8(b, y);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) x[e] += y[e];
+  return pack8(x);
+}
+
+MLS_DEV float sumsq8(uint4 v) {
+  float x[8];
+  unpack8(v, x);
+  float r = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) r += x[e] * x[e];
+  return r;
+}
+
 MLS_DEV float epi(float v, int n, const SkArgs& s) { return v + (s.bias ? s.bias[n] : 0.f); }
 
-template <int TMS, int UNROLL, int NWV>
+// NT 16-column tiles per block: every A fragment a wave loads feeds NT MFMAs, so the activation
+// traffic from L2 (M rows x K per block) is amortised over NT weight tiles -- at M = 16 it equals
+// the weight traffic when NT = 1.
+template <int TMS, int UNROLL, int NWV, int FUSE, int NT>
 __global__ __launch_bounds__(NWV * 64) void skinny_gemm_kernel(const SkArgs s) {
-  __shared__ float red[NWV][TMS * 16][17];
+  __shared__ float red[NWV][TMS * 16][NT * 16 + 1];
+  __shared__ float ssq_red[NWV][TMS * 16];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int nr = lane & 15, g = lane >> 4;
-  const int n0 = blockIdx.x * 16;
+  const int n0 = blockIdx.x * 16 * NT;
   const int split = blockIdx.y;
   const int ks_beg = split * s.ksteps_per_split;
   const int ksteps = (s.K + 31) / 32;
   const int ks_end = min(ksteps, ks_beg + s.ksteps_per_split);
   const rsrc_t ar = make_rsrc(s.a, s.a_bytes);
   const rsrc_t wr = make_rsrc(s.w, s.w_bytes);
-  const int wbase = ((n0 + nr) * s.K + 8 * g) * 2;
+  const rsrc_t a2r = make_rsrc(s.a2, FUSE == FUSE_ADD_NORM ? s.a_bytes : 0);
+  const bool wr_res = FUSE == FUSE_ADD_NORM && s.a_out && blockIdx.x == 0;
+  int wbase[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) wbase[j] = ((n0 + 16 * j + nr) * s.K + 8 * g) * 2;
   int abase[TMS];
 #pragma unroll
   for (int t = 0; t < TMS; ++t) {
     const int m = 16 * t + nr;
     abase[t] = m < s.M ? (m * s.lda + 8 * g) * 2 : OOB;
   }
-  f32x4 acc[TMS];
+  f32x4 acc[TMS][NT];
+  float ssq[TMS];
 #pragma unroll
-  for (int t = 0; t < TMS; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < TMS; ++t) {
+    ssq[t] = 0.f;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 
-  int ks = ks_beg + wid;
-  for (; ks + NWV * (UNROLL - 1) < ks_end; ks += NWV * UNROLL) {
-    uint4 wv[UNROLL], av[UNROLL][TMS];
+  // U k-steps per trip: issue every load first, then the math, then (tile-0 blocks) the
+  // residual-stream stores
+  auto body = [&](int ks0, auto U_) {
+    constexpr int U = decltype(U_)::value;
+    uint4 wv[U][NT], av[U][TMS], a2v[U][TMS];
+    int aoff[U][TMS];
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
-      const int k = (ks + NWV * u) * 32;
+    for (int u = 0; u < U; ++u) {
+      const int k = (ks0 + NWV * u) * 32;
       const bool kin = k + 8 * g < s.K;
-      wv[u] = bload16(wr, kin ? wbase + k * 2 : OOB);
 #pragma unroll
-      for (int t = 0; t < TMS; ++t) av[u][t] = bload16(ar, (kin && abase[t] != OOB) ? abase[t] + k * 2 : OOB);
+      for (int j = 0; j < NT; ++j) wv[u][j] = bload16(wr, kin ? wbase[j] + k * 2 : OOB);
+#pragma unroll
+      for (int t = 0; t < TMS; ++t) {
+        aoff[u][t] = (kin && abase[t] != OOB) ? abase[t] + k * 2 : OOB;
+        av[u][t] = bload16(ar, aoff[u][t]);
+        if constexpr (FUSE == FUSE_ADD_NORM) a2v[u][t] = bload16(a2r, aoff[u][t]);
+      }
     }
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u)
+    for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int t = 0; t < TMS; ++t)
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, av[u][t]),
-                                                         __builtin_bit_cast(bf16x8, wv[u]), acc[t], 0, 0, 0);
-  }
-  for (; ks < ks_end; ks += NWV) {
-    const int k = ks * 32;
-    const bool kin = k + 8 * g < s.K;
-    const uint4 wv = bload16(wr, kin ? wbase + k * 2 : OOB);
+      for (int t = 0; t < TMS; ++t) {
+        if constexpr (FUSE == FUSE_ADD_NORM) av[u][t] = add_round(av[u][t], a2v[u][t]);
+        if constexpr (FUSE != FUSE_NONE) ssq[t] += sumsq8(av[u][t]);
 #pragma unroll
-    for (int t = 0; t < TMS; ++t) {
-      const uint4 av = bload16(ar, (kin && abase[t] != OOB) ? abase[t] + k * 2 : OOB);
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, av), __builtin_bit_cast(bf16x8, wv),
-                                                       acc[t], 0, 0, 0);
+        for (int j = 0; j < NT; ++j)
+          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, av[u][t]),
+                                                              __builtin_bit_cast(bf16x8, wv[u][j]), acc[t][j], 0, 0, 0);
+      }
+    if constexpr (FUSE == FUSE_ADD_NORM) {
+      if (wr_res) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int t = 0; t < TMS; ++t)
+            if (aoff[u][t] != OOB) st16(s.a_out + aoff[u][t] / 2, av[u][t]);
+      }
     }
-  }
-  // C layout: acc[t][j] = out[m = 16t + 4g + j][n = n0 + nr]
+  };
+  int ks = ks_beg + wid;
+  for (; ks + NWV * (UNROLL - 1) < ks_end; ks += NWV * UNROLL) body(ks, std::integral_constant<int, UNROLL>{});
+  for (; ks < ks_end; ks += NWV) body(ks, std::integral_constant<int, 1>{});
+
+  // C layout: acc[t][j][i] = out[m = 16t + 4g + i][n = n0 + 16j + nr]
 #pragma unroll
   for (int t = 0; t < TMS; ++t)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) red[wid][16 * t + 4 * g + j][nr] = acc[t][j];
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[wid][16 * t + 4 * g + i][16 * j + nr] = acc[t][j][i];
+  if constexpr (FUSE != FUSE_NONE) {
+    // lanes nr, nr+16, nr+32, nr+48 hold row nr's four 8-element k slices
+#pragma unroll
+    for (int t = 0; t < TMS; ++t) {
+      float v = ssq[t];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      if (g == 0) ssq_red[wid][16 * t + nr] = v;
+    }
+  }
   __syncthreads();
   const bool glu = s.act == ACT_SILU_MUL;
-  for (int q = tid; q < TMS * 16 * 16; q += NWV * 64) {
-    const int m = q >> 4, c = q & 15;
+  constexpr int COLS = NT * 16;
+  for (int q = tid; q < TMS * 16 * COLS; q += NWV * 64) {
+    const int m = q / COLS, c = q % COLS;
     if (m >= s.M) continue;
     float v = 0.f;
 #pragma unroll
     for (int w = 0; w < NWV; ++w) v += red[w][m][c];
     const int n = n0 + c;
+    float rs = 1.f;
+    if constexpr (FUSE != FUSE_NONE) {
+      float t2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < NWV; ++w) t2 += ssq_red[w][m];
+      if (s.nsplit > 1) {  // partial square sums ride after the slabs; the finisher combines them
+        if (blockIdx.x == 0 && c == 0) s.ws[(size_t)s.nsplit * s.M * s.N + split * s.M + m] = t2;
+      } else {
+        rs = rsqrtf(t2 / (float)s.K + s.eps);
+      }
+    }
     if (s.nsplit > 1) {
       s.ws[((size_t)split * s.M + m) * s.N + n] = v;
       continue;
     }
+    v *= rs;
     if (glu) {
-      if (c < 8) {
+      if ((c & 15) < 8) {
         float up = 0.f;
 #pragma unroll
         for (int w = 0; w < NWV; ++w) up += red[w][m][c + 8];
+        up *= rs;
         const float gt = epi(v, n, s);
-        s.out[(size_t)m * s.ldo + (n0 >> 1) + c] = (bf16)(silu(gt) * epi(up, n + 8, s));
+        s.out[(size_t)m * s.ldo + (n >> 4) * 8 + (n & 7)] = (bf16)(silu(gt) * epi(up, n + 8, s));
       }
       continue;
     }
@@ -124,6 +212,13 @@ __global__ __launch_bounds__(256) void skinny_finish_kernel(const SkArgs s) {
       v += row[n];
       if (glu) u += row[n + 8];
     }
+    if (s.norm) {
+      float t2 = 0.f;
+      for (int sp = 0; sp < s.nsplit; ++sp) t2 += s.ws[(size_t)s.nsplit * s.M * s.N + sp * s.M + m];
+      const float rs = rsqrtf(t2 / (float)s.K + s.eps);
+      v *= rs;
+      u *= rs;
+    }
     if (glu) {
       s.out[(size_t)m * s.ldo + c] = (bf16)(silu(epi(v, n, s)) * epi(u, n + 8, s));
     } else {
@@ -138,12 +233,19 @@ __global__ __launch_bounds__(256) void skinny_finish_kernel(const SkArgs s) {
 
 extern "C" {
 
-// M <= 32, N % 16 == 0, K % 8 == 0.  nsplit <= 0: auto (fill the chip).  ws: >= nsplit*M*N floats.
-int mls_skinny_gemm(const void* A, const void* W, const float* bias, const void* res, void* out, void* ws,
-                    size_t ws_bytes, int M, int N, int K, int act, int nsplit, void* stream) {
+// M <= 32, N % 16 == 0, K % 8 == 0.  nsplit <= 0: auto (fill the chip).  ws: >= nsplit*M*(N+1) floats.
+// A2 / A_out / norm: the fused residual-add + RMSNorm prologue (header comment); A_out must not alias A/A2.
+int mls_skinny_gemm_norm(const void* A, const void* A2, void* A_out, const void* W, const float* bias, const void* res,
+                         void* out, void* ws, size_t ws_bytes, int M, int N, int K, int act, int nsplit, int norm,
+                         float eps, void* stream) {
   if (M <= 0 || M > 32 || N % 16 || K % 8 || K <= 0) return MLS_BAD_ARG;
+  if (A_out && (A_out == A || A_out == A2)) return MLS_BAD_ARG;
   SkArgs s{};
   s.a = (const bf16*)A;
+  s.a2 = (const bf16*)A2;
+  s.a_out = (bf16*)A_out;
+  s.norm = norm;
+  s.eps = eps;
   s.w = (const bf16*)W;
   s.bias = bias;
   s.res = (const bf16*)res;
@@ -156,21 +258,49 @@ int mls_skinny_gemm(const void* A, const void* W, const float* bias, const void*
   if (ab >= 0x7FFFFFFFull || wb >= 0x7FFFFFFFull) return MLS_UNSUPPORTED;
   s.a_bytes = (uint32_t)ab;
   s.w_bytes = (uint32_t)wb;
-  const int tiles = N / 16;
+  // M > 2: NT tiles per block while that still leaves >= 384 blocks (1.5 per CU) -- measured: NT = 4
+  // halves gate_up at M = 16 but costs ~10 % at M = 1, where the activation traffic is negligible
+  // and the deeper single-tile unroll wins (profiles/r1_decode_probe.jsonl).  K is split across
+  // blocks only when even single-tile blocks cannot cover 256 CUs.
+  int nt = 1;
+  while (M > 2 && nt < 4 && N % (32 * nt) == 0 && N / (32 * nt) >= 384) nt *= 2;
+  const int tiles = N / (16 * nt);
   const int ksteps = (K + 31) / 32;
-  if (nsplit <= 0) {  // 8 waves split K inside a block; split across blocks only below 256 tiles
+  if (nsplit <= 0) {  // 8 waves split K inside a block; split across blocks only below 256 blocks
     nsplit = 1;
     while (tiles * nsplit < 256 && ksteps / (nsplit * 2) >= 32) nsplit *= 2;
   }
-  if (nsplit > 1 && (ws == nullptr || ws_bytes < (size_t)nsplit * M * N * 4)) nsplit = 1;
+  if (nsplit > 1 && (ws == nullptr || ws_bytes < (size_t)nsplit * M * (N + 1) * 4)) nsplit = 1;
   s.nsplit = nsplit;
   s.ksteps_per_split = (ksteps + nsplit - 1) / nsplit;
   dim3 grid(tiles, nsplit);
   hipStream_t st = (hipStream_t)stream;
-  if (M <= 16)
-    hipLaunchKernelGGL((skinny_gemm_kernel<1, 8, 8>), grid, dim3(512), 0, st, s);
-  else
-    hipLaunchKernelGGL((skinny_gemm_kernel<2, 4, 8>), grid, dim3(512), 0, st, s);
+  if ((A2 || A_out) && !norm) return MLS_UNSUPPORTED;  // the residual add exists only as the norm prologue
+  const int mode = A2 ? FUSE_ADD_NORM : norm ? FUSE_NORM : FUSE_NONE;
+#define MLS_SKINNY_F(TMS, UN, NT_)                                                                             \
+  switch (mode) {                                                                                              \
+    case FUSE_NONE:                                                                                            \
+      hipLaunchKernelGGL((skinny_gemm_kernel<TMS, UN, 8, FUSE_NONE, NT_>), grid, dim3(512), 0, st, s); break;   \
+    case FUSE_NORM:                                                                                            \
+      hipLaunchKernelGGL((skinny_gemm_kernel<TMS, UN, 8, FUSE_NORM, NT_>), grid, dim3(512), 0, st, s); break;   \
+    default:                                                                                                   \
+      hipLaunchKernelGGL((skinny_gemm_kernel<TMS, UN, 8, FUSE_ADD_NORM, NT_>), grid, dim3(512), 0, st, s); break; \
+  }
+#define MLS_SKINNY(TMS, UN)                      \
+  if (nt == 4) {                                 \
+    MLS_SKINNY_F(TMS, (UN > 4 ? 4 : UN), 4)      \
+  } else if (nt == 2) {                          \
+    MLS_SKINNY_F(TMS, UN, 2)                     \
+  } else {                                       \
+    MLS_SKINNY_F(TMS, UN, 1)                     \
+  }
+  if (M <= 16) {
+    MLS_SKINNY(1, 8)
+  } else {
+    MLS_SKINNY(2, 4)
+  }
+#undef MLS_SKINNY
+#undef MLS_SKINNY_F
   if (nsplit > 1) {
     const long total = (long)M * (act == ACT_SILU_MUL ? N / 2 : N);
     int blocks = (int)((total + 255) / 256);
@@ -178,6 +308,12 @@ int mls_skinny_gemm(const void* A, const void* W, const float* bias, const void*
     hipLaunchKernelGGL(skinny_finish_kernel, dim3(blocks), dim3(256), 0, st, s);
   }
   return (int)hipGetLastError();
+}
+
+int mls_skinny_gemm(const void* A, const void* W, const float* bias, const void* res, void* out, void* ws,
+                    size_t ws_bytes, int M, int N, int K, int act, int nsplit, void* stream) {
+  return mls_skinny_gemm_norm(A, nullptr, nullptr, W, bias, res, out, ws, ws_bytes, M, N, K, act, nsplit, 0, 0.f,
+                              stream);
 }
 
 }  // extern "C"

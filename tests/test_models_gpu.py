@@ -51,6 +51,36 @@ def test_skinny_gemm(M, nsplit):
     assert out.shape == (M, 512) and rel(out, ref) < 2e-2
 
 
+@pytest.mark.parametrize("M", [1, 7, 16, 32])
+@pytest.mark.parametrize("nsplit", [0, 1, 4])
+def test_gemm_rmsnorm_fused(M, nsplit):
+    """Skinny GEMM with the residual add + RMSNorm prologue vs fp32 (gain folded into W)."""
+    from mlmicroservicetemplate_amd import ops
+    from mlmicroservicetemplate_amd.ops import reference as R
+
+    torch.manual_seed(10 + M)
+    N, K = 768, 1024
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    d = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    gain = (torch.rand(K, device=DEV) + 0.5).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) / K**0.5).to(torch.bfloat16)
+    ws = torch.empty(4 << 20, device=DEV, dtype=torch.float32)
+    wf = ops.fold_norm(w, gain)
+    xn, hs = R.layernorm(x, gain, None, residual=d, eps=1e-5, rms=True)
+    r_out = torch.empty_like(x)
+    y = ops.gemm_rmsnorm(x, wf, d, r_out, eps=1e-5, workspace=ws, splitk=nsplit)
+    assert rel(y, xn.float() @ w.float().T) < 2e-2
+    assert rel(r_out, hs) < 1e-2
+    y0 = ops.gemm_rmsnorm(x, wf, eps=1e-5, workspace=ws, splitk=nsplit)  # no residual update
+    xn0 = R.layernorm(x, gain, None, eps=1e-5, rms=True)[0]
+    assert rel(y0, xn0.float() @ w.float().T) < 2e-2
+    g, u = w[:384].contiguous(), w[384:].contiguous()
+    wi = ops.fold_norm(ops.interleave_gate_up(g, u), gain)
+    out = ops.gemm_rmsnorm(x, wi, d, None, act="silu_mul", eps=1e-5, workspace=ws, splitk=nsplit)
+    ref = torch.nn.functional.silu(xn.float() @ g.float().T) * (xn.float() @ u.float().T)
+    assert out.shape == (M, 384) and rel(out, ref) < 2e-2
+
+
 @pytest.mark.parametrize("impl", ["blas", "native"])
 def test_linear_dispatch(impl):
     """ops.linear: hipBLASLt (+ native SiLU-mul pass) and native paths agree with fp32."""

@@ -84,6 +84,22 @@ def test_rope_and_kv_append(ops):
     kc2, vc2 = torch.zeros_like(kc), torch.zeros_like(vc)
     ops.rope_kv_(qkv2, pos, cos, sin, Hq, Hkv, D, slots, kc2, vc2)
     assert torch.equal(qkv2, qkv) and torch.equal(kc2, kc) and torch.equal(vc2, vc)
+    # slots derived in-kernel: 3 sequences x 15 positions into a [4][64] cache, padding skipped
+    B, S, MS = 3, 15, 64
+    pos3 = torch.arange(S, device=DEV, dtype=torch.int32).repeat(B)
+    lens3 = torch.tensor([15, 7, 1], device=DEV, dtype=torch.int32)
+    qkv3 = qkv0.clone()
+    kc3, vc3 = torch.zeros_like(kc), torch.zeros_like(vc)
+    ops.rope_kv_(qkv3, pos3, cos, sin, Hq, Hkv, D, None, kc3, vc3, lens=lens3, seq=S, max_seq=MS)
+    kref = R.rope(qkv0[:, Hq * D: (Hq + Hkv) * D].view(T, Hkv, D), pos3, cos, sin).reshape(T, -1)
+    for b in range(B):
+        for p_ in range(S):
+            row = kc3[b * MS + p_].reshape(-1)
+            if p_ < int(lens3[b]):
+                assert rel(row, kref[b * S + p_]) < 1e-2
+                assert torch.equal(vc3[b * MS + p_].reshape(-1), qkv0[b * S + p_, (Hq + Hkv) * D:])
+            else:
+                assert not row.any()
 
 
 @pytest.mark.parametrize("cfg", [

@@ -1,0 +1,61 @@
+"""Aggregate a rocprofv3 ``--kernel-trace`` CSV by kernel name: total/avg µs and call count,
+optionally restricted to the last ``--window`` kernels and normalised per ``--per`` steps.
+Usage: python tools/kernel_summary.py <dir-or-csv> [--window N] [--per K] [--top 30]"""
+import argparse
+import collections
+import csv
+import glob
+import os
+
+
+def load(path):
+    if os.path.isdir(path):
+        cands = glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True)
+        if not cands:
+            raise SystemExit(f"no kernel_trace.csv under {path}")
+        path = cands[0]
+    rows = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    rows.sort()
+    return rows
+
+
+def short(name):
+    name = name.replace("(anonymous namespace)::", "").replace("void ", "", 1)
+    depth, out = 0, []
+    for ch in name:  # cut at the argument list, keeping template arguments
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == "(" and depth == 0:
+            break
+        out.append(ch)
+    return "".join(out)[:90]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("path")
+    ap.add_argument("--window", type=int, default=0, help="only the last N kernels")
+    ap.add_argument("--per", type=float, default=1.0, help="divide totals by this many steps")
+    ap.add_argument("--top", type=int, default=30)
+    a = ap.parse_args()
+    rows = load(a.path)
+    if a.window:
+        rows = rows[-a.window:]
+    agg = collections.defaultdict(lambda: [0.0, 0])
+    for s, e, n in rows:
+        agg[short(n)][0] += (e - s) / 1e3
+        agg[short(n)][1] += 1
+    tot = sum(v[0] for v in agg.values())
+    span = (rows[-1][1] - rows[0][0]) / 1e3 if rows else 0.0
+    print(f"kernels {len(rows)}  kernel-sum {tot / a.per:.1f} us  span {span / a.per:.1f} us  (per {a.per:g})")
+    for n, (t, c) in sorted(agg.items(), key=lambda kv: -kv[1][0])[: a.top]:
+        print(f"{t / a.per:10.1f} us  n={c / a.per:7.1f}  avg={t / c:8.2f} us  {n}")
+
+
+if __name__ == "__main__":
+    main()
