@@ -234,8 +234,9 @@ class LlamaTP:
             self.p["lm_head"] = ops.fold_norm(self.p["lm_head"], self.p.pop("final_norm"))
             self.ones = torch.ones(cfg.hidden, device=self.device, dtype=torch.bfloat16)
             self.workspace = torch.empty(32 << 20, device=self.device, dtype=torch.float32)
-            self.dec_ws = torch.empty(max_batch * self.sd.hq * (-(-max_seq // 256)) * (D + 2) + 16,
+            self.dec_ws = torch.empty(max_batch * self.sd.hq * (-(-max_seq // 64)) * (D + 2) + 16,
                                       device=self.device, dtype=torch.float32)
+            self.dec_cnt = torch.zeros(max_batch * self.sd.hkv, device=self.device, dtype=torch.int32)
         cdt = torch.bfloat16 if backend == "fused" else torch.float32
         self.k_cache = [torch.zeros(max_batch, max_seq, self.sd.hkv, D, device=self.device, dtype=cdt)
                         for _ in range(cfg.layers)]
@@ -247,7 +248,8 @@ class LlamaTP:
 
         self.use_graphs = backend == "fused" and self.device.type == "cuda" and (
             tp == 1 or os.environ.get("MLS_TP_GRAPHS", "0") == "1")
-        self._graphs: Dict[Tuple[int, int], tuple] = {}
+        self._graphs: Dict[Tuple[int, int, int], tuple] = {}
+        self._dec_ctx: Optional[int] = None  # host bound on decode context (sizes the split grid)
 
     # ---------------------------------------------------------------- shared pieces
     @property
@@ -362,12 +364,13 @@ class LlamaTP:
 
         for i in range(cfg.layers):
             qkv, r = pre_norm(r, p[f"l{i}.qkv"], delta)
-            ops.rope_kv_(qkv, pos, self.cos, self.sin, sd.hq, sd.hkv, D, None, self.k_cache[i], self.v_cache[i],
-                         lens=lens, seq=S, max_seq=self.max_seq)
-            if decode:
+            if decode:  # RoPE + KV append ride inside the decode-attention launch
                 a = ops.decode_attention(qkv, self.k_cache[i][:B], self.v_cache[i][:B], lens, sd.hq, sd.hkv, D,
-                                         workspace=self.dec_ws)
+                                         workspace=self.dec_ws, counters=self.dec_cnt, positions=pos, cos=self.cos,
+                                         sin=self.sin, max_len=self._dec_ctx)
             else:
+                ops.rope_kv_(qkv, pos, self.cos, self.sin, sd.hq, sd.hkv, D, None, self.k_cache[i],
+                             self.v_cache[i], lens=lens, seq=S, max_seq=self.max_seq)
                 a = ops.flash_attention(qkv, B, S, sd.hq, sd.hkv, D, kv_lens=lens, causal=True)
             o = self.comm.all_reduce_(ops.linear(a, p[f"l{i}.o"], workspace=ws))
             gu, r = pre_norm(r, p[f"l{i}.gate_up"], o, act=ops.ACT_SILU_MUL)
@@ -392,39 +395,57 @@ class LlamaTP:
                                        decode, k)
         return self._ref_forward(ids, positions, lens, B, S, decode, k)
 
-    def _decode_graph(self, B: int, k: int):
-        """Captured decode step for batch B (static token / position / length buffers).  Must be
-        built before a prefill: its warm-up writes (garbage) into cache position 0."""
-        key = (B, k)
+    def ctx_bucket(self, max_ctx: Optional[int]) -> int:
+        """Power-of-two context bound (>= 256, <= max_seq) a decode graph is captured for."""
+        if max_ctx is None:
+            return self.max_seq
+        return min(self.max_seq, max(256, 1 << (max(1, int(max_ctx)) - 1).bit_length()))
+
+    def _decode_graph(self, B: int, k: int, ctx: int):
+        """Captured decode step for batch B and context bound ctx (static token / position / length
+        buffers).  The warm-up runs at position max_seq - 1, which no generation ever reads (and
+        which the split grid of ctx < max_seq does not even reach), so graphs can be captured while
+        sequences are in flight."""
+        key = (B, k, ctx)
         if key in self._graphs:
             return self._graphs[key]
         dev = self.device
         tok = torch.zeros(B, 1, dtype=torch.int32, device=dev)
-        pos = torch.zeros(B, 1, dtype=torch.int32, device=dev)
-        lens = torch.ones(B, dtype=torch.int32, device=dev)
-        side = torch.cuda.Stream(dev)
-        side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(side):
-            for _ in range(2):
-                self.step(tok, pos, lens, decode=True, k=k)
-        torch.cuda.current_stream(dev).wait_stream(side)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            vals, idx = self.step(tok, pos, lens, decode=True, k=k)
+        pos = torch.full((B, 1), self.max_seq - 1, dtype=torch.int32, device=dev)
+        lens = torch.full((B,), self.max_seq, dtype=torch.int32, device=dev)
+        self._dec_ctx = ctx
+        try:
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                for _ in range(2):
+                    self.step(tok, pos, lens, decode=True, k=k)
+            torch.cuda.current_stream(dev).wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                vals, idx = self.step(tok, pos, lens, decode=True, k=k)
+        finally:
+            self._dec_ctx = None
         self._graphs[key] = (g, tok, pos, lens, vals, idx)
         return self._graphs[key]
 
-    def decode_step(self, tok: torch.Tensor, cur: torch.Tensor, k: int):
-        """One decode step: token at position ``cur`` (attending to cur + 1 keys)."""
+    def decode_step(self, tok: torch.Tensor, cur: torch.Tensor, k: int, max_ctx: Optional[int] = None):
+        """One decode step: token at position ``cur`` (attending to cur + 1 keys).  ``max_ctx``: a
+        host-side bound on cur + 1 (e.g. prompt length + step), used to pick a tight split grid."""
         B = tok.shape[0]
+        ctx = self.ctx_bucket(max_ctx)
         if self.use_graphs:
-            g, t_s, p_s, l_s, v_s, i_s = self._decode_graph(B, k)
+            g, t_s, p_s, l_s, v_s, i_s = self._decode_graph(B, k, ctx)
             t_s.copy_(tok.view(B, 1))
             p_s.copy_(cur.view(B, 1))
             l_s.copy_(cur.view(B) + 1)
             g.replay()
             return v_s, i_s
-        return self.step(tok.view(B, 1).to(torch.int32), cur.view(B, 1), cur.view(B) + 1, decode=True, k=k)
+        self._dec_ctx = ctx
+        try:
+            return self.step(tok.view(B, 1).to(torch.int32), cur.view(B, 1), cur.view(B) + 1, decode=True, k=k)
+        finally:
+            self._dec_ctx = None
 
     @torch.no_grad()
     def generate(self, ids: torch.Tensor, lens: torch.Tensor, gp: GenParams) -> torch.Tensor:
@@ -436,8 +457,6 @@ class LlamaTP:
         ids = ids.to(dev)
         lens = lens.to(dev).to(torch.int32)
         k = max(1, min(gp.top_k, self.top_k_max))
-        if self.use_graphs and gp.max_new_tokens > 1:
-            self._decode_graph(B, k)  # before prefill (its warm-up touches cache position 0)
         pos = torch.arange(S, device=dev, dtype=torch.int32).unsqueeze(0).expand(B, S).contiguous()
         vals, idx = self.step(ids, pos, lens, decode=False, k=k)
         out = []
@@ -446,7 +465,7 @@ class LlamaTP:
         cur = lens.clone()
         for t in range(1, gp.max_new_tokens):
             # the new token sits at position cur; attention covers cur + 1 keys
-            vals, idx = self.decode_step(tok.to(torch.int32), cur, k)
+            vals, idx = self.decode_step(tok.to(torch.int32), cur, k, max_ctx=S + t)
             tok = self._merge_sample(vals, idx, gp, t)
             out.append(tok)
             cur = cur + 1

@@ -522,26 +522,37 @@ def flash_attention(qkv: torch.Tensor, batch: int, seq: int, n_q_heads: int, n_k
 
 
 def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, lens: torch.Tensor,
-                     n_q_heads: int, n_kv_heads: int, head_dim: int, *, chunk: int = 256,
+                     n_q_heads: int, n_kv_heads: int, head_dim: int, *, chunk: int = 64,
                      scale: Optional[float] = None, workspace: Optional[torch.Tensor] = None,
-                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                     counters: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+                     positions: Optional[torch.Tensor] = None, cos: Optional[torch.Tensor] = None,
+                     sin: Optional[torch.Tensor] = None, max_len: Optional[int] = None) -> torch.Tensor:
     """One query token per sequence vs the cache ``[B, max_len, Hkv, D]``; q rows ``[B, >= Hq*D]``
-    (head h at column h*D, e.g. the fused QKV row).  Split-KV with a combine pass."""
+    (head h at column h*D, e.g. the fused QKV row).  Split-KV, combined in the same launch.
+    With ``positions``/``cos``/``sin`` (rope mode) q is the raw fused QKV row: RoPE is applied to q
+    and to the new K (row ``lens - 1 == positions``), and the new K/V are appended to the cache.
+    ``max_len``: a host-side bound on ``lens`` (default: the cache length) -- it sizes the split grid,
+    so a tight bound keeps idle split blocks out of short-context launches; keys beyond it are not
+    visited, so it must be >= every ``lens[b]``."""
     dev = q.device
     B = lens.numel()
-    max_len = k_cache.shape[1]
+    max_len = k_cache.shape[1] if max_len is None else min(int(max_len), k_cache.shape[1])
     nsplit = (max_len + chunk - 1) // chunk
     need = B * n_q_heads * nsplit * (head_dim + 2)
     if workspace is None or workspace.numel() < need:
         workspace = torch.empty(need, device=dev, dtype=torch.float32)
+    if counters is None or counters.numel() < B * n_kv_heads:
+        counters = torch.zeros(B * n_kv_heads, device=dev, dtype=torch.int32)
     ws = workspace[: B * n_q_heads * nsplit * head_dim]
     ws_ml = workspace[B * n_q_heads * nsplit * head_dim: need]
     out = torch.empty(B, n_q_heads * head_dim, device=dev, dtype=torch.bfloat16) if out is None else out
     scale = head_dim ** -0.5 if scale is None else scale
+    if positions is not None:
+        _need(positions, "positions", torch.int32, dev)
     rc = lib().mls_decode_attention(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), out.data_ptr(),
-                                    ws.data_ptr(), ws_ml.data_ptr(), q.stride(0), out.stride(0),
-                                    k_cache.stride(0), lens.data_ptr(), B, n_q_heads, n_kv_heads, head_dim,
-                                    max_len, chunk, float(scale), stream_ptr(dev))
+                                    ws.data_ptr(), ws_ml.data_ptr(), counters.data_ptr(), q.stride(0), out.stride(0),
+                                    k_cache.stride(0), lens.data_ptr(), _ptr(positions), _ptr(cos), _ptr(sin), B,
+                                    n_q_heads, n_kv_heads, head_dim, max_len, chunk, float(scale), stream_ptr(dev))
     check(rc, "mls_decode_attention")
     return out
 

@@ -52,7 +52,7 @@ _SIGS = {
     "mls_flash_attention": [P, P, P, P, I, I, I, I, I, I, I, I, I, P, I, F, P],
     "mls_skinny_gemm": [P, P, P, P, P, P, SZ, I, I, I, I, I, P],
     "mls_skinny_gemm_norm": [P, P, P, P, P, P, P, P, SZ, I, I, I, I, I, I, F, P],
-    "mls_decode_attention": [P, P, P, P, P, P, I, I, L, P, I, I, I, I, I, I, F, P],
+    "mls_decode_attention": [P, P, P, P, P, P, P, I, I, L, P, P, P, P, I, I, I, I, I, I, F, P],
 }
 _OPTIONAL_SIGS: dict = {"mls_set_debug_flags": [I]}
 

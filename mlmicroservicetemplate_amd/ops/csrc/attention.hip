@@ -197,35 +197,114 @@ __global__ __launch_bounds__(256) void flash_fwd_kernel(const AttnArgs a) {
 
 // ------------------------------------------------------------------------------- decode
 struct DecodeArgs {
-  const bf16* q;   // [B][q_stride], head h at h*D
-  const bf16* kc;  // [B][max_len][Hkv][D]
-  const bf16* vc;
+  const bf16* q;   // [B][q_stride], head h at h*D (rope mode: the fused QKV row, K at Hq*D, V at (Hq+Hkv)*D)
+  bf16* kc;        // [B][max_len][Hkv][D]
+  bf16* vc;
   bf16* o;         // [B][o_stride]
   float* ws;       // [B][Hq][nsplit][D]
   float* ws_ml;    // [B][Hq][nsplit][2]
+  int* counters;   // [B][Hkv], zero between launches (the last arriver resets its entry)
   int q_stride, o_stride;
   long seq_stride;  // elements per sequence in the cache (max_len * Hkv * D)
   const int* lens;
-  int Hq, Hkv, chunk, nsplit;
+  const int* positions;  // rope mode: query position per sequence (== lens[b] - 1)
+  const float* cos_t;    // [max_pos][D/2]
+  const float* sin_t;
+  int Hq, Hkv, nsplit;
   float scale_log2;
 };
 
-template <int D, int G>
-__global__ __launch_bounds__(256) void decode_split_kernel(const DecodeArgs a) {
+// rotate-half RoPE of this lane's 8 dims (d = gl*8 + e) given the partner lane's 8 (d +- D/2)
+template <int D>
+MLS_DEV void rope8(float (&x)[8], const float (&xp)[8], const float* cos_t, const float* sin_t, int pos, int gl) {
+  constexpr int HALF = D / 2, HL = D / 16;  // HL = lanes per half row
+  const int i0 = (gl % HL) * 8;
+  const float4 c0 = *reinterpret_cast<const float4*>(cos_t + (long)pos * HALF + i0);
+  const float4 c1 = *reinterpret_cast<const float4*>(cos_t + (long)pos * HALF + i0 + 4);
+  const float4 s0 = *reinterpret_cast<const float4*>(sin_t + (long)pos * HALF + i0);
+  const float4 s1 = *reinterpret_cast<const float4*>(sin_t + (long)pos * HALF + i0 + 4);
+  const float c[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+  const float sn[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+  const float sgn = gl < HL ? -1.f : 1.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) x[e] = x[e] * c[e] + sgn * xp[e] * sn[e];
+}
+
+// Decode attention: grid (splits, Hkv, B), 4 waves; the G query heads of a KV head share every
+// K/V row load.  A lane owns 8 of a row's D dims (LPR lanes per row, RPW rows per wave, ROWS =
+// 4*RPW rows per block pass); all NIT passes' K/V loads are issued before any math (one memory
+// round trip per block).  Rope mode also applies RoPE to q and to the new token's K (row lens-1,
+// taken from the QKV row, not the cache) and appends that K/V to the cache -- the standalone
+// rope/KV-append kernel is gone from decode.  The RPW row groups of a wave merge by shuffles, the
+// 4 waves through LDS; a sequence that fits one split writes its output directly, otherwise each
+// split writes an fp32 partial (m, l, o) for decode_combine_kernel.  (An in-launch last-arriver
+// merge was measured slower: its per-block release fences serialise per XCD, and write-through
+// partials read back serially cost more than the extra launch.)
+template <int D, int G, int NIT>
+__global__ __launch_bounds__(256) void decode_attn_kernel(const DecodeArgs a) {
   constexpr int LPR = D / 8;      // lanes per key row
   constexpr int RPW = 64 / LPR;   // rows per wave step
-  constexpr int NPART = 4 * RPW;  // partial states per block
-  __shared__ float sm_m[NPART][G], sm_l[NPART][G];
-  __shared__ __attribute__((aligned(16))) float sm_o[NPART][G][D];
+  constexpr int ROWS = 4 * RPW;   // rows per block pass
+  constexpr int CHUNK = ROWS * NIT;
+  __shared__ float sm_m[4][G], sm_l[4][G];
+  __shared__ __attribute__((aligned(16))) float sm_o[4][G][D];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int grp = lane / LPR, gl = lane % LPR;
+  const int grp = lane / LPR, gl = lane % LPR, glp = gl ^ (LPR / 2);
   const int b = blockIdx.z, hk = blockIdx.y, sp = blockIdx.x;
   const int L = a.lens[b];
-  const int start = sp * a.chunk, end = min(L, start + a.chunk);
+  const int start = sp * CHUNK;
+  if (start >= L) {
+    if (L <= 0 && sp == 0)
+      for (int idx = tid; idx < G * D; idx += 256) a.o[(long)b * a.o_stride + (long)hk * G * D + idx] = (bf16)0.f;
+    return;
+  }
+  const int end = min(L, start + CHUNK);
+  const bool rope = a.positions != nullptr;
+  const int pos = rope ? a.positions[b] : 0;
+  const bf16* qrow = a.q + (long)b * a.q_stride;
+  const long rstride = (long)a.Hkv * D;
+  const long cbase = (long)b * a.seq_stride + (long)hk * D + gl * 8;
 
+  // issue every K/V row load of this block first
+  uint4 kraw[NIT], vraw[NIT];
+#pragma unroll
+  for (int i = 0; i < NIT; ++i) {
+    const int r = start + i * ROWS + wid * RPW + grp;
+    const bool ld = r < end && !(rope && r == L - 1);
+    kraw[i] = ld ? ld16(a.kc + cbase + r * rstride) : make_uint4(0, 0, 0, 0);
+    vraw[i] = ld ? ld16(a.vc + cbase + r * rstride) : make_uint4(0, 0, 0, 0);
+  }
   float qv[G][8];
 #pragma unroll
-  for (int hh = 0; hh < G; ++hh) unpack8(ld16(a.q + (long)b * a.q_stride + (long)(hk * G + hh) * D + gl * 8), qv[hh]);
+  for (int hh = 0; hh < G; ++hh) {
+    const bf16* qh = qrow + (long)(hk * G + hh) * D;
+    unpack8(ld16(qh + gl * 8), qv[hh]);
+    if (rope) {
+      float xp[8];
+      unpack8(ld16(qh + glp * 8), xp);
+      rope8<D>(qv[hh], xp, a.cos_t, a.sin_t, pos, gl);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) qv[hh][e] = (float)(bf16)qv[hh][e] * a.scale_log2;  // bf16 q, as the cache path
+  }
+  if (rope && L - 1 >= start && L - 1 < end) {  // the new token's row, appended to the cache
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      const int r = start + i * ROWS + wid * RPW + grp;
+      if (r == L - 1) {
+        const bf16* kh = qrow + (long)(a.Hq + hk) * D;
+        float kx[8], kp[8];
+        unpack8(ld16(kh + gl * 8), kx);
+        unpack8(ld16(kh + glp * 8), kp);
+        rope8<D>(kx, kp, a.cos_t, a.sin_t, pos, gl);
+        kraw[i] = pack8(kx);
+        vraw[i] = ld16(qrow + (long)(a.Hq + a.Hkv + hk) * D + gl * 8);
+        st16(a.kc + cbase + r * rstride, kraw[i]);
+        st16(a.vc + cbase + r * rstride, vraw[i]);
+      }
+    }
+  }
+
   float m[G], l[G], acc[G][8];
 #pragma unroll
   for (int hh = 0; hh < G; ++hh) {
@@ -234,13 +313,14 @@ __global__ __launch_bounds__(256) void decode_split_kernel(const DecodeArgs a) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[hh][e] = 0.f;
   }
-  const bf16* kbase = a.kc + (long)b * a.seq_stride + (long)hk * D + gl * 8;
-  const bf16* vbase = a.vc + (long)b * a.seq_stride + (long)hk * D + gl * 8;
-  const long rstride = (long)a.Hkv * D;
-  for (int r = start + wid * RPW + grp; r < end; r += 4 * RPW) {
+#pragma unroll
+  for (int i = 0; i < NIT; ++i) {
+    if (start + i * ROWS >= end) break;  // block-uniform
+    const int r = start + i * ROWS + wid * RPW + grp;
     float kf[8], vf[8];
-    unpack8(ld16(kbase + r * rstride), kf);
-    unpack8(ld16(vbase + r * rstride), vf);
+    unpack8(kraw[i], kf);
+    unpack8(vraw[i], vf);
+    const bool valid = r < end;
 #pragma unroll
     for (int hh = 0; hh < G; ++hh) {
       float d = 0.f;
@@ -248,8 +328,9 @@ __global__ __launch_bounds__(256) void decode_split_kernel(const DecodeArgs a) {
       for (int e = 0; e < 8; ++e) d += qv[hh][e] * kf[e];
 #pragma unroll
       for (int o = LPR / 2; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
-      const float sc = d * a.scale_log2;
+      const float sc = valid ? d : -INFINITY;
       const float mn = fmaxf(m[hh], sc);
+      if (mn == -INFINITY) continue;
       const float al = __builtin_amdgcn_exp2f(m[hh] - mn);
       const float p = __builtin_amdgcn_exp2f(sc - mn);
       l[hh] = l[hh] * al + p;
@@ -258,56 +339,108 @@ __global__ __launch_bounds__(256) void decode_split_kernel(const DecodeArgs a) {
       m[hh] = mn;
     }
   }
-  const int part = wid * RPW + grp;
+  // merge the wave's RPW row groups (lanes gl + LPR*grp) by shuffles
 #pragma unroll
   for (int hh = 0; hh < G; ++hh) {
-    if (gl == 0) {
-      sm_m[part][hh] = m[hh];
-      sm_l[part][hh] = l[hh];
-    }
 #pragma unroll
-    for (int e = 0; e < 8; ++e) sm_o[part][hh][gl * 8 + e] = acc[hh][e];
+    for (int o = LPR; o < 64; o <<= 1) {
+      const float m2 = __shfl_xor(m[hh], o, 64), l2 = __shfl_xor(l[hh], o, 64);
+      const float mn = fmaxf(m[hh], m2);
+      const float w1 = mn == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m[hh] - mn);
+      const float w2 = mn == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m2 - mn);
+      l[hh] = l[hh] * w1 + l2 * w2;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[hh][e] = acc[hh][e] * w1 + __shfl_xor(acc[hh][e], o, 64) * w2;
+      m[hh] = mn;
+    }
+    if (grp == 0) {
+      if (gl == 0) {
+        sm_m[wid][hh] = m[hh];
+        sm_l[wid][hh] = l[hh];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sm_o[wid][hh][gl * 8 + e] = acc[hh][e];
+    }
   }
   __syncthreads();
+  const bool direct = L <= CHUNK;
   for (int idx = tid; idx < G * D; idx += 256) {
     const int hh = idx / D, d = idx % D;
     float M = -INFINITY;
-    for (int p = 0; p < NPART; ++p) M = fmaxf(M, sm_m[p][hh]);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) M = fmaxf(M, sm_m[p][hh]);
     float Ls = 0.f, O = 0.f;
     if (M != -INFINITY) {
-      for (int p = 0; p < NPART; ++p) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
         const float w = __builtin_amdgcn_exp2f(sm_m[p][hh] - M);
         Ls += sm_l[p][hh] * w;
         O += sm_o[p][hh][d] * w;
       }
     }
-    const long base = (((long)b * a.Hq + hk * G + hh) * a.nsplit + sp);
-    a.ws[base * D + d] = O;
-    if (d == 0) {
-      a.ws_ml[base * 2] = M;
-      a.ws_ml[base * 2 + 1] = Ls;
+    if (direct) {
+      a.o[(long)b * a.o_stride + (long)(hk * G + hh) * D + d] = (bf16)(Ls > 0.f ? O / Ls : 0.f);
+    } else {
+      const long base = ((long)b * a.Hq + hk * G + hh) * a.nsplit + sp;
+      a.ws[base * D + d] = O;
+      if (d == 0) {
+        a.ws_ml[base * 2] = M;
+        a.ws_ml[base * 2 + 1] = Ls;
+      }
     }
   }
 }
 
+// merge the splits of one (b, q-head): block of D threads; the (m, l) of every split are read
+// once into LDS (one round trip), then each thread's O loads are issued 8 at a time
 template <int D>
-__global__ __launch_bounds__(D) void decode_combine_kernel(const DecodeArgs a) {
+__global__ __launch_bounds__(D) void decode_combine_kernel(const DecodeArgs a, int chunk) {
+  __shared__ float sw[1024];
+  __shared__ float s_inv;
   const int bh = blockIdx.x;  // b * Hq + h
   const int b = bh / a.Hq, h = bh % a.Hq;
   const int d = threadIdx.x;
-  const int ns = min(a.nsplit, (a.lens[b] + a.chunk - 1) / a.chunk);
-  float M = -INFINITY;
-  for (int s = 0; s < ns; ++s) M = fmaxf(M, a.ws_ml[((long)bh * a.nsplit + s) * 2]);
-  float Ls = 0.f, O = 0.f;
-  if (M != -INFINITY) {
-    for (int s = 0; s < ns; ++s) {
-      const long base = (long)bh * a.nsplit + s;
-      const float w = __builtin_amdgcn_exp2f(a.ws_ml[base * 2] - M);
-      Ls += a.ws_ml[base * 2 + 1] * w;
-      O += a.ws[base * D + d] * w;
-    }
+  const int L = a.lens[b];
+  const int ns = min(a.nsplit, (L + chunk - 1) / chunk);
+  if (ns <= 1) return;  // the split kernel wrote this row directly
+  const long rec = (long)bh * a.nsplit;
+  float mloc = -INFINITY;
+  for (int s = d; s < ns; s += D) mloc = fmaxf(mloc, a.ws_ml[(rec + s) * 2]);
+  __shared__ float red[D / 64];
+  mloc = wave_max(mloc);
+  if ((d & 63) == 0) red[d >> 6] = mloc;
+  __syncthreads();
+  float M = red[0];
+#pragma unroll
+  for (int w = 1; w < D / 64; ++w) M = fmaxf(M, red[w]);
+  float lloc = 0.f;
+  for (int s = d; s < ns; s += D) {
+    const float w = M == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(a.ws_ml[(rec + s) * 2] - M);
+    sw[s] = w;
+    lloc += a.ws_ml[(rec + s) * 2 + 1] * w;
   }
-  a.o[(long)b * a.o_stride + (long)h * D + d] = (bf16)(Ls > 0.f ? O / Ls : 0.f);
+  lloc = wave_sum(lloc);
+  __syncthreads();
+  if ((d & 63) == 0) red[d >> 6] = lloc;
+  __syncthreads();
+  if (d == 0) {
+    float Ls = 0.f;
+#pragma unroll
+    for (int w = 0; w < D / 64; ++w) Ls += red[w];
+    s_inv = Ls > 0.f ? 1.f / Ls : 0.f;
+  }
+  __syncthreads();
+  float O = 0.f;
+  int s = 0;
+  for (; s + 8 <= ns; s += 8) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = a.ws[(rec + s + j) * D + d];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) O += v[j] * sw[s + j];
+  }
+  for (; s < ns; ++s) O += a.ws[(rec + s) * D + d] * sw[s];
+  a.o[(long)b * a.o_stride + (long)h * D + d] = (bf16)(O * s_inv);
 }
 
 }  // namespace
@@ -346,43 +479,61 @@ int mls_flash_attention(const void* q, const void* k, const void* v, void* o, in
   return (int)hipGetLastError();
 }
 
-// workspace: ws >= B*Hq*nsplit*D floats, ws_ml >= B*Hq*nsplit*2 floats; nsplit = ceil(max_len/chunk)
-int mls_decode_attention(const void* q, const void* k_cache, const void* v_cache, void* o, float* ws, float* ws_ml,
-                         int q_stride, int o_stride, long seq_stride, const int* lens, int B, int Hq, int Hkv, int D,
-                         int max_len, int chunk, float scale, void* stream) {
+// workspace: ws >= B*Hq*nsplit*D floats, ws_ml >= B*Hq*nsplit*2 floats, nsplit = ceil(max_len/chunk);
+// counters: B*Hkv zero-initialised ints.  chunk: rows per split (D=128: 16/32/64/128; D=64: 32..256).
+// positions/cos/sin non-null: rope mode (q = the fused QKV rows, positions[b] == lens[b] - 1).
+int mls_decode_attention(const void* q, void* k_cache, void* v_cache, void* o, float* ws, float* ws_ml, int* counters,
+                         int q_stride, int o_stride, long seq_stride, const int* lens, const int* positions,
+                         const float* cos_t, const float* sin_t, int B, int Hq, int Hkv, int D, int max_len, int chunk,
+                         float scale, void* stream) {
   if (B <= 0 || Hq % Hkv || chunk <= 0 || max_len <= 0) return MLS_BAD_ARG;
+  (void)counters;  // reserved (in-launch merge variants); the combine runs as its own launch
+  if (positions && (!cos_t || !sin_t)) return MLS_BAD_ARG;
   DecodeArgs a{};
   a.q = (const bf16*)q;
-  a.kc = (const bf16*)k_cache;
-  a.vc = (const bf16*)v_cache;
+  a.kc = (bf16*)k_cache;
+  a.vc = (bf16*)v_cache;
   a.o = (bf16*)o;
   a.ws = ws;
   a.ws_ml = ws_ml;
+  a.counters = counters;
   a.q_stride = q_stride;
   a.o_stride = o_stride;
   a.seq_stride = seq_stride;
   a.lens = lens;
+  a.positions = positions;
+  a.cos_t = cos_t;
+  a.sin_t = sin_t;
   a.Hq = Hq;
   a.Hkv = Hkv;
-  a.chunk = chunk;
   a.nsplit = (max_len + chunk - 1) / chunk;
   a.scale_log2 = scale * 1.4426950408889634f;
   const int G = Hq / Hkv;
+  const int rows = D == 128 ? 16 : 32;  // rows per block pass
+  const int nit = chunk / rows;
+  if (chunk % rows || (nit != 1 && nit != 2 && nit != 4 && nit != 8)) return MLS_BAD_ARG;
+  if (a.nsplit > 1024) return MLS_UNSUPPORTED;  // combine keeps one weight per split in LDS
   dim3 grid(a.nsplit, Hkv, B);
   hipStream_t st = (hipStream_t)stream;
-#define DEC(DD, GG) hipLaunchKernelGGL((decode_split_kernel<DD, GG>), grid, dim3(256), 0, st, a)
+#define DEC(DD, GG)                                                                                        \
+  switch (nit) {                                                                                           \
+    case 1: hipLaunchKernelGGL((decode_attn_kernel<DD, GG, 1>), grid, dim3(256), 0, st, a); break;        \
+    case 2: hipLaunchKernelGGL((decode_attn_kernel<DD, GG, 2>), grid, dim3(256), 0, st, a); break;        \
+    case 4: hipLaunchKernelGGL((decode_attn_kernel<DD, GG, 4>), grid, dim3(256), 0, st, a); break;        \
+    default: hipLaunchKernelGGL((decode_attn_kernel<DD, GG, 8>), grid, dim3(256), 0, st, a); break;       \
+  }
   if (D == 128) {
-    if (G == 1) DEC(128, 1);
-    else if (G == 2) DEC(128, 2);
-    else if (G == 4) DEC(128, 4);
-    else if (G == 8) DEC(128, 8);
+    if (G == 1) { DEC(128, 1) }
+    else if (G == 2) { DEC(128, 2) }
+    else if (G == 4) { DEC(128, 4) }
+    else if (G == 8) { DEC(128, 8) }
     else return MLS_UNSUPPORTED;
-    hipLaunchKernelGGL(decode_combine_kernel<128>, dim3(B * Hq), dim3(128), 0, st, a);
+    if (a.nsplit > 1) hipLaunchKernelGGL(decode_combine_kernel<128>, dim3(B * Hq), dim3(128), 0, st, a, chunk);
   } else if (D == 64) {
-    if (G == 1) DEC(64, 1);
-    else if (G == 4) DEC(64, 4);
+    if (G == 1) { DEC(64, 1) }
+    else if (G == 4) { DEC(64, 4) }
     else return MLS_UNSUPPORTED;
-    hipLaunchKernelGGL(decode_combine_kernel<64>, dim3(B * Hq), dim3(64), 0, st, a);
+    if (a.nsplit > 1) hipLaunchKernelGGL(decode_combine_kernel<64>, dim3(B * Hq), dim3(64), 0, st, a, chunk);
   } else {
     return MLS_UNSUPPORTED;
   }

@@ -35,6 +35,15 @@ MLS_DEV uint4 bload16(rsrc_t r, int byte_off) {
 MLS_DEV uint2 bload8(rsrc_t r, int byte_off) {
   return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(r, byte_off, 0, 0));
 }
+// write-through (sc1) 4-byte store / L1-bypassing (sc1) load: an in-launch hand-off between
+// workgroups with no release fence (whose L2 write-back serialises per XCD) and no acquire --
+// cdna_hip_programming.md §6 Guideline 16, R1
+MLS_DEV void bstore_f32_sc1(rsrc_t r, int byte_off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, byte_off, 0, 16);
+}
+MLS_DEV float bload_f32_sc1(rsrc_t r, int byte_off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 16));
+}
 MLS_DEV uint32_t clamp_bytes(size_t n) { return n > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)n; }
 
 MLS_DEV uint4 ld16(const void* p) { return *reinterpret_cast<const uint4*>(p); }

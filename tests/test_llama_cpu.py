@@ -50,6 +50,7 @@ def _tp_worker(rank, world, port, cfg_kw, q):
 
     from mlmicroservicetemplate_amd.models.llama import TPComm
 
+    torch.set_num_threads(1)  # fixed summation order: exact token equality across runs
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         cfg = tiny_config(**cfg_kw)
@@ -67,6 +68,7 @@ def _tp_worker(rank, world, port, cfg_kw, q):
 @pytest.mark.timeout(240)
 def test_tp_matches_tp1(world, kv):
     cfg_kw = dict(CFG, kv_heads=kv)
+    torch.set_num_threads(1)
     cfg = tiny_config(**cfg_kw)
     p = init_llama_shard(cfg, 1, 0, seed=1)
     ids, lens = _prompts()

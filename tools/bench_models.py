@@ -83,12 +83,12 @@ def bench_llama(args):
         tok = torch.randint(1000, 100000, (B, 1), device=dev, dtype=torch.int32)
         cur = lens.view(B, 1).clone()
         for _ in range(3):
-            m.decode_step(tok, cur, 1)
+            m.decode_step(tok, cur, 1, max_ctx=S + 1)
         torch.cuda.synchronize()
         t2 = time.perf_counter()
         n = args.steps
         for _ in range(n):
-            m.decode_step(tok, cur, 1)
+            m.decode_step(tok, cur, 1, max_ctx=S + 1)
         torch.cuda.synchronize()
         dec = (time.perf_counter() - t2) / n
         print(json.dumps({"bench": "llama3-8b", "tp": 1, "batch": B, "prompt": S,
