@@ -69,9 +69,10 @@ def main(argv=None) -> int:
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=32)
-    ap.add_argument("--inflight", type=int, default=2)
+    ap.add_argument("--inflight", type=int, default=3)
     ap.add_argument("--backend", default="fused", choices=["fused", "eager"])
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--serial", action="store_true", help="one compute stream (no concurrent in-flight batches)")
     ap.add_argument("--seed", type=int, default=0)
     args = ap.parse_args(argv)
 
@@ -95,7 +96,7 @@ def main(argv=None) -> int:
 
     fwd = build_model(args.backend, device, args.batch, params)
     engine = GpuEngine(fwd, device, (224, 224, 3), torch.uint8, buckets=[args.batch], inflight=args.inflight,
-                       use_graphs=not args.no_graphs, name=f"resnet50.r{info.rank}")
+                       use_graphs=not args.no_graphs, name=f"resnet50.r{info.rank}", concurrent=not args.serial)
     engine.warmup(capture=not args.no_graphs)
 
     rng = np.random.default_rng(1234 + info.rank)
@@ -146,7 +147,8 @@ def main(argv=None) -> int:
             "data": "synthetic uint8 224x224x3 images, random-init weights",
             "config": {"model": "resnet50-v1.5", "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "seq_len": None, "image_size": 224, "parallelism": f"dp{world}",
-                       "backend": args.backend, "hipgraph": not args.no_graphs, "inflight": args.inflight},
+                       "backend": args.backend, "hipgraph": not args.no_graphs, "inflight": args.inflight,
+                           "concurrent_slots": not args.serial},
             "p50_latency_ms": round(p50_max, 3),
             "p99_latency_ms": round(p99_max, 3),
             "per_gpu_requests_per_s": round(value / world, 1),

@@ -13,6 +13,10 @@ One :class:`GpuEngine` owns one model replica on one device and runs fixed-shape
   i+1's compute -- event-ordered across three HIP streams, no device-wide syncs.
 * The host thread only blocks on a *blocking-sync* event of its own slot, so concurrent
   callers (the batcher's executor threads) keep the GPU fed.
+* **Concurrent slots** (``concurrent=True``): each slot replays its graphs on its own compute
+  stream from its own graph memory pool, so two batches' kernels co-run -- the small
+  latency-bound layers of one batch fill the CUs the other leaves idle.  The model must then
+  keep per-stream scratch (``ResNet50Fused`` keys its split-K workspace by stream).
 
 The engine is model-agnostic: a model adapter provides ``sample_shape``/``sample_dtype`` of
 one request and ``forward(device_batch) -> tuple[Tensor, ...]`` (fixed-shape outputs whose
@@ -24,6 +28,7 @@ import logging
 import queue
 import threading
 import time
+from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
@@ -53,6 +58,8 @@ class _Slot:
     outs: Dict[int, Tuple[torch.Tensor, ...]] = field(default_factory=dict)  # bucket -> device outputs
     host_out: Dict[int, Tuple[torch.Tensor, ...]] = field(default_factory=dict)  # bucket -> pinned outputs
     graphs: Dict[int, torch.cuda.CUDAGraph] = field(default_factory=dict)
+    s_comp: Optional[torch.cuda.Stream] = None  # this slot's compute stream (concurrent mode)
+    pool: Optional[tuple] = None  # this slot's graph memory pool (concurrent mode)
     ev_h2d: Optional[torch.cuda.Event] = None
     ev_comp: Optional[torch.cuda.Event] = None
     ev_done: Optional[torch.cuda.Event] = None
@@ -88,6 +95,8 @@ class GpuEngine:
         inflight: int = 2,
         use_graphs: bool = True,
         name: str = "engine",
+        concurrent: bool = False,
+        stage_workers: int = 4,
     ):
         self.forward = forward
         self.device = torch.device(device)
@@ -97,6 +106,12 @@ class GpuEngine:
         self.max_batch = self.buckets[-1]
         self.inflight = max(1, int(inflight))
         self.use_graphs = use_graphs
+        self.concurrent = bool(concurrent) and self.inflight > 1
+        # host staging (request arrays -> pinned slot) split over a few threads: numpy releases the
+        # GIL for bulk copies, and one thread's ~5-8 GB/s memcpy is what a 4.8 MB ResNet batch
+        # every 0.9 ms needs
+        self._stage_pool = (ThreadPoolExecutor(max_workers=stage_workers, thread_name_prefix=f"{name}-stage")
+                            if stage_workers > 1 else None)
         self.name = name
         self._enqueue_lock = threading.Lock()
         self._free: "queue.Queue[_Slot]" = queue.Queue()
@@ -121,6 +136,12 @@ class GpuEngine:
                     ev_comp=torch.cuda.Event(),
                     ev_done=torch.cuda.Event(blocking=True),
                 )
+                if self.concurrent:
+                    slot.s_comp = torch.cuda.Stream(self.device)
+                    slot.pool = torch.cuda.graph_pool_handle() if use_graphs else None
+                else:
+                    slot.s_comp = self.s_comp
+                    slot.pool = self._pool
                 self.slots.append(slot)
                 self._free.put(slot)
 
@@ -130,9 +151,9 @@ class GpuEngine:
         with torch.cuda.device(self.device), torch.no_grad():
             for slot in self.slots:
                 for b in self.buckets:
-                    with torch.cuda.stream(self.s_comp):
+                    with torch.cuda.stream(slot.s_comp):
                         outs = self.forward(slot.dev_in[:b])
-                    self.s_comp.synchronize()
+                    slot.s_comp.synchronize()
                     if not (self.use_graphs and capture):
                         slot.outs[b] = tuple(outs)
                     self._alloc_host_out(slot, b, outs)
@@ -141,7 +162,7 @@ class GpuEngine:
                 for slot in self.slots:
                     for b in self.buckets:
                         g = torch.cuda.CUDAGraph()
-                        with torch.cuda.graph(g, pool=self._pool, stream=self.s_comp):
+                        with torch.cuda.graph(g, pool=slot.pool, stream=slot.s_comp):
                             outs = self.forward(slot.dev_in[:b])
                         slot.graphs[b] = g
                         slot.outs[b] = tuple(outs)
@@ -168,6 +189,15 @@ class GpuEngine:
                     dst[:n] = samples
                 elif isinstance(samples, torch.Tensor):
                     slot.host_in[:n].copy_(samples)
+                elif self._stage_pool is not None and n >= 8 and dst is not None:
+                    step = -(-n // self._stage_pool._max_workers)
+
+                    def _copy(lo, dst=dst, samples=samples, step=step):
+                        for i in range(lo, min(n, lo + step)):
+                            dst[i] = samples[i]
+
+                    for f in [self._stage_pool.submit(_copy, lo) for lo in range(0, n, step)]:
+                        f.result()
                 else:
                     for i, s in enumerate(samples):
                         dst[i] = s
@@ -176,8 +206,8 @@ class GpuEngine:
                     with torch.cuda.stream(self.s_h2d):
                         slot.dev_in[:bucket].copy_(slot.host_in[:bucket], non_blocking=True)
                         slot.ev_h2d.record(self.s_h2d)
-                    self.s_comp.wait_event(slot.ev_h2d)
-                    with torch.cuda.stream(self.s_comp):
+                    slot.s_comp.wait_event(slot.ev_h2d)
+                    with torch.cuda.stream(slot.s_comp):
                         if self.use_graphs and bucket in slot.graphs:
                             slot.graphs[bucket].replay()
                             outs = slot.outs[bucket]
@@ -187,7 +217,7 @@ class GpuEngine:
                             slot.outs[bucket] = outs
                             if bucket not in slot.host_out:
                                 self._alloc_host_out(slot, bucket, outs)
-                        slot.ev_comp.record(self.s_comp)
+                        slot.ev_comp.record(slot.s_comp)
                     self.s_d2h.wait_event(slot.ev_comp)
                     with torch.cuda.stream(self.s_d2h):
                         for h, d in zip(slot.host_out[bucket], outs):
@@ -222,5 +252,6 @@ class GpuEngine:
     def stats(self) -> dict:
         return {"name": self.name, "device": str(self.device), "batches": self.batches, "samples": self.samples,
                 "inflight": self.inflight, "buckets": self.buckets, "graphs": self.use_graphs,
+                "concurrent": self.concurrent,
                 "healthy": self.healthy, "last_error": self.last_error,
                 "free_slots": self._free.qsize()}

@@ -205,7 +205,7 @@ class BertFused:
         cb = torch.full((Cp,), -1e30, device=self.device, dtype=torch.float32)
         cb[:C] = self.w["cls.b"]
         self.cls_w, self.cls_b = cw, cb
-        self.workspace = torch.empty(16 << 20, device=self.device, dtype=torch.float32)
+        self._ws = ops.StreamWorkspace(16 << 20, self.device)  # per stream: concurrent engine slots
 
     def forward(self, ids: torch.Tensor, type_ids: Optional[torch.Tensor], lens: torch.Tensor) -> torch.Tensor:
         """ids/type_ids int32 ``[B, S]``, lens int32 ``[B]`` -> bf16 logits ``[B, Cpad]``."""
@@ -216,7 +216,7 @@ class BertFused:
         tt_f = type_ids.reshape(-1) if type_ids is not None else None
         x = ops.embed_layernorm(ids_f, tt_f, w["emb.word"], w["emb.pos"], w["emb.type"], w["emb.ln.g"], w["emb.ln.b"],
                                 S, eps=cfg.eps)
-        ws = self.workspace
+        ws = self._ws.get()
         for i in range(cfg.layers):
             # large token counts: library GEMMs with the residual folded into the LayerNorm;
             # small ones: native GEMMs with the residual in the epilogue

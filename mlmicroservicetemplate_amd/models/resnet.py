@@ -241,9 +241,9 @@ class ResNet50Fused:
 
     Per conv: weights pre-multiplied by the BN scale (bf16, ``[Cout][KH][KW][Cin]``), the BN
     bias applied in fp32 in the GEMM epilogue together with the residual add and ReLU.  One
-    split-K workspace is shared by all layers (they run back-to-back on one stream), sized at
-    construction for ``max_batch`` so nothing is allocated inside a hipGraph capture besides
-    the activations (which the capture's private pool then owns).
+    split-K workspace per stream is shared by all layers (they run back-to-back on it), sized for
+    ``max_batch`` and allocated at the first (eager) call on a stream, so nothing besides the
+    activations is allocated inside a hipGraph capture (the capture's private pool owns those).
 
     ``tuning`` maps a layer name to an explicit ``(cfg, splitk)`` (see ``ops.autotune``);
     layers without an entry use the C++ heuristic.
@@ -271,8 +271,11 @@ class ResNet50Fused:
         self.mean = IMAGENET_MEAN
         self.std = IMAGENET_STD
         self.max_batch = max_batch
-        self.workspace = torch.empty(self._workspace_bytes(max_batch) // 4 + 1, device=self.device,
-                                     dtype=torch.float32)
+        self._ws = ops.StreamWorkspace(self._workspace_bytes(max_batch) // 4 + 1, self.device)
+
+    @property
+    def workspace(self) -> torch.Tensor:
+        return self._ws.get()
 
     # -- planning ---------------------------------------------------------------------------
     def layer_gemm_shapes(self, batch: int) -> List[Tuple[str, int, int, int]]:

@@ -45,6 +45,25 @@ def _act(a) -> int:
     return _ACTS[a]
 
 
+class StreamWorkspace:
+    """fp32 scratch (split-K slabs) per HIP stream: batches that run concurrently on different
+    streams (GpuEngine concurrent slots) must not share it.  A stream's buffer is allocated on
+    its first use -- the engine's eager warm-up, before any graph capture."""
+
+    def __init__(self, elems: int, device):
+        self.elems = int(elems)
+        self.device = torch.device(device)
+        self._bufs: dict = {}
+
+    def get(self) -> torch.Tensor:
+        key = torch.cuda.current_stream(self.device).cuda_stream if self.device.type == "cuda" else 0
+        buf = self._bufs.get(key)
+        if buf is None:
+            buf = torch.empty(self.elems, device=self.device, dtype=torch.float32)
+            self._bufs[key] = buf
+        return buf
+
+
 def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
     return None if t is None else t.data_ptr()
 

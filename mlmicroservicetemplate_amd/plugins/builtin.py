@@ -134,7 +134,8 @@ class ResNet50Plugin(ModelPlugin):
         for dev in devices:
             fwd = self._build_forward(s.BACKEND, dev, max(buckets), params)
             eng = GpuEngine(fwd, dev, (224, 224, 3), torch.uint8, buckets=buckets, inflight=int(s.INFLIGHT),
-                            use_graphs=bool(s.USE_GRAPHS), name=f"resnet50.{dev}")
+                            use_graphs=bool(s.USE_GRAPHS), name=f"resnet50.{dev}",
+                            concurrent=bool(s.CONCURRENT_SLOTS))
             eng.warmup(capture=bool(s.USE_GRAPHS))
             self.engines.append(eng)
         logger.info("resnet50 ready on %s (backend=%s buckets=%s)", devices, s.BACKEND, buckets)

@@ -71,7 +71,8 @@ class BertPlugin(ModelPlugin):
                     return v, i.to(torch.int32)
 
                 eng = GpuEngine(fwd, dev, (2 * S + 1,), torch.int32, buckets=buckets, inflight=int(s.INFLIGHT),
-                                use_graphs=bool(s.USE_GRAPHS), name=f"bert.s{S}.{dev}")
+                                use_graphs=bool(s.USE_GRAPHS), name=f"bert.s{S}.{dev}",
+                                concurrent=bool(s.CONCURRENT_SLOTS))
                 eng.warmup(capture=bool(s.USE_GRAPHS))
                 per[S] = eng
             self.engines[dev] = per

@@ -38,7 +38,7 @@ def bench_bert(args):
                     v, i = torch.topk(logits.float(), 2, dim=-1)
                     return v, i.to(torch.int32)
 
-                eng = GpuEngine(fwd, dev, (2 * S + 1,), torch.int32, buckets=[B], inflight=2)
+                eng = GpuEngine(fwd, dev, (2 * S + 1,), torch.int32, buckets=[B], inflight=3, concurrent=True)
                 eng.warmup(capture=True)
                 for _ in range(5):
                     eng.run(packed)
@@ -48,7 +48,7 @@ def bench_bert(args):
                 pend = []
                 for _ in range(n):
                     pend.append(eng.submit(packed))
-                    if len(pend) >= 2:
+                    if len(pend) >= 3:
                         pend.pop(0).wait()
                 for t in pend:
                     t.wait()
