@@ -37,6 +37,7 @@ from .. import discovery
 from ..config import Settings, load_dotenv
 from ..plugins.base import ModelPlugin, PluginContext, load_plugin
 from ..scheduler.batcher import BatcherClosed, DynamicBatcher, QueueFull, ReplicaRouter
+from ..scheduler.watchdog import ReplicaWatchdog
 from ..utils.metrics import CONTENT_TYPE_LATEST, Metrics, gpu_memory_collector
 from .multipart import MultipartError, Part, parse_multipart
 from .state import OverloadedException, PredictionException, ServiceState
@@ -59,6 +60,7 @@ class ServingRuntime:
         self.metrics = metrics
         self.ctx = ctx or PluginContext(settings=settings)
         self.router: Optional[ReplicaRouter] = None
+        self.watchdog: Optional[ReplicaWatchdog] = None
         self.loop: Optional[asyncio.AbstractEventLoop] = None
 
     # ---------------------------------------------------------------- lifecycle
@@ -97,16 +99,26 @@ class ServingRuntime:
             batchers.append(b)
         self.router = ReplicaRouter(batchers)
         await self.router.start()
+        if float(s.WATCHDOG_INTERVAL_S) > 0:
+            self.watchdog = ReplicaWatchdog(
+                self.router, stall_s=float(s.WATCHDOG_STALL_S), max_failures=int(s.WATCHDOG_MAX_FAILURES),
+                interval_s=float(s.WATCHDOG_INTERVAL_S), cooldown_s=float(s.WATCHDOG_COOLDOWN_S),
+                probes=self.plugin.replica_probes(),
+                on_change=lambda i, ok, why: (None if ok else self.metrics.replica_drains.labels(str(i)).inc()))
+            self.watchdog.start()
 
         def collect_queues():
             for i, b in enumerate(self.router.batchers):
                 self.metrics.queue_depth.labels(str(i)).set(b.queue_depth)
+                self.metrics.replica_healthy.labels(str(i)).set(1 if b.healthy else 0)
 
         self.metrics.add_collector(collect_queues)
 
     async def shutdown(self) -> None:
         self.state.ready_to_predict = False
         self.metrics.ready.set(0)
+        if self.watchdog is not None:
+            await self.watchdog.stop()
         if self.router is not None:
             await self.router.stop()
         self.state.shutdown.set()
@@ -225,6 +237,10 @@ def create_app(settings: Optional[Settings] = None, plugin: Optional[ModelPlugin
                 return JSONResponse(status_code=503, content={"status": "failure", "detail": NOT_READY,
                                                               "error": state.init_error})
             raise PredictionException()
+        router = runtime.router
+        if router is not None and router.healthy_count == 0:
+            return JSONResponse(status_code=503, content={"status": "failure", "detail": NOT_READY,
+                                                          "error": "no healthy replica"})
         return {"status": "success", "detail": READY}
 
     @app.get("/health")
@@ -236,6 +252,7 @@ def create_app(settings: Optional[Settings] = None, plugin: Optional[ModelPlugin
             "init_error": state.init_error,
             "model": plugin.name,
             "replicas": runtime.router.stats() if runtime.router else [],
+            "watchdog_events": runtime.watchdog.events[-20:] if runtime.watchdog else [],
         }
 
     @app.get("/info")

@@ -164,6 +164,10 @@ class Settings:
     INFLIGHT: int = 3  # batches in flight per GPU worker (H2D/compute/D2H overlap)
     CONCURRENT_SLOTS: bool = True  # in-flight batches co-run on per-slot streams (+26 % ResNet-50 req/s)
     REQUEST_TIMEOUT_S: float = 30.0
+    WATCHDOG_INTERVAL_S: float = 1.0  # replica liveness check period (0 disables the watchdog)
+    WATCHDOG_STALL_S: float = 30.0  # a batch running longer than this drains its replica
+    WATCHDOG_MAX_FAILURES: int = 3  # consecutive failed batches that drain a replica
+    WATCHDOG_COOLDOWN_S: float = 30.0  # failure-drained replica re-admitted on probation after this
     HBM_FRACTION: float = 0.9  # of free HBM the batch-size cap may plan for
     # --- generate (Llama) ---
     MAX_NEW_TOKENS: int = 64

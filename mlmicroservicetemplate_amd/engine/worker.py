@@ -232,7 +232,12 @@ class GpuEngine:
     def _finish(self, t: Ticket) -> Tuple[np.ndarray, ...]:
         slot = t.slot
         try:
-            slot.ev_done.synchronize()
+            try:
+                slot.ev_done.synchronize()
+            except RuntimeError as e:  # device fault surfaced at the sync: this worker is dead
+                self.healthy = False
+                self.last_error = f"{type(e).__name__}: {e}"
+                raise
             res = []
             for h in slot.host_out[t.bucket]:
                 if h.dtype == torch.bfloat16:

@@ -67,6 +67,10 @@ class ModelPlugin:
     def generate(self, request: dict) -> dict:
         raise NotImplementedError(f"model {self.name!r} does not support /generate")
 
+    def replica_probes(self) -> List[Optional[Callable[[], bool]]]:
+        """Optional per-replica health probes for the watchdog (same order as :meth:`replicas`)."""
+        return []
+
     def describe(self) -> dict:
         return {"name": self.name, "task": self.task, "batched": self.batched}
 

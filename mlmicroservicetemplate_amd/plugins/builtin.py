@@ -165,6 +165,9 @@ class ResNet50Plugin(ModelPlugin):
     def preprocess(self, part: Part) -> Any:
         return decode_image(part.data, part.content_type or "")
 
+    def replica_probes(self):
+        return [lambda e=e: e.healthy for e in self.engines]
+
     def replicas(self):
         out = []
         for eng in self.engines:

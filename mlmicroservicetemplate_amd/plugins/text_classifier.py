@@ -82,6 +82,9 @@ class BertPlugin(ModelPlugin):
         text = part.data.decode("utf-8", errors="replace")
         return self.tokenizer.encode(text, self.max_seq)
 
+    def replica_probes(self):
+        return [lambda per=per: all(e.healthy for e in per.values()) for per in self.engines.values()]
+
     def replicas(self):
         from ..models import bert
 

@@ -73,6 +73,12 @@ class DynamicBatcher:
         self._inflight_now = 0
         self.on_batch = on_batch
         self.healthy = True
+        self.unhealthy_reason: Optional[str] = None
+        # liveness signals read by the watchdog (scheduler.watchdog)
+        self._running: dict = {}  # batch id -> dispatch time
+        self._next_id = 0
+        self.consecutive_failures = 0
+        self.last_success = time.perf_counter()
         # stats
         self.batches = 0
         self.requests = 0
@@ -145,6 +151,24 @@ class DynamicBatcher:
             return await fut
         return await asyncio.wait_for(fut, timeout)
 
+    def evict_queued(self) -> List[Tuple[Any, "asyncio.Future", float]]:
+        """Remove and return every queued (not yet dispatched) request -- a drained replica's
+        backlog, which the router hands to healthy replicas."""
+        items = list(self._q)
+        self._q.clear()
+        if self._full is not None:
+            self._full.clear()
+        return items
+
+    def adopt(self, items) -> None:
+        """Append requests evicted from another replica (their futures keep their waiters)."""
+        for it in items:
+            self._q.append(it)
+        if self._q and self._wake is not None:
+            self._wake.set()
+            if len(self._q) >= self.max_batch:
+                self._full.set()
+
     # ----------------------------------------------------------------- internals
     def _take(self) -> List[Tuple[Any, asyncio.Future, float]]:
         batch = []
@@ -181,20 +205,31 @@ class DynamicBatcher:
             self._inflight_now += 1
             self._dispatch(batch)
 
+    @property
+    def oldest_running_s(self) -> float:
+        """Age of the longest-running dispatched batch (0 if none) -- a hung GPU worker shows here."""
+        if not self._running:
+            return 0.0
+        return time.perf_counter() - min(self._running.values())
+
     def _dispatch(self, batch) -> None:
         samples = [b[0] for b in batch]
         t0 = time.perf_counter()
+        bid = self._next_id
+        self._next_id += 1
+        self._running[bid] = t0
         cfut = self._executor.submit(self.run_batch, samples)
 
         def done(f: cf.Future) -> None:
             try:
-                self._loop.call_soon_threadsafe(self._resolve, batch, f, t0)
+                self._loop.call_soon_threadsafe(self._resolve, batch, f, t0, bid)
             except RuntimeError:  # loop already closed (shutdown raced a running batch)
                 pass
 
         cfut.add_done_callback(done)
 
-    def _resolve(self, batch, f: cf.Future, t0: float) -> None:
+    def _resolve(self, batch, f: cf.Future, t0: float, bid: int = -1) -> None:
+        self._running.pop(bid, None)
         self._inflight_now -= 1
         self._sem.release()
         n = len(batch)
@@ -207,6 +242,11 @@ class DynamicBatcher:
             except Exception:  # metrics must never break serving
                 pass
         exc = f.exception()
+        if exc is None:
+            self.consecutive_failures = 0
+            self.last_success = time.perf_counter()
+        else:
+            self.consecutive_failures += 1
         if exc is not None:
             self.failed += n
             logger.warning("%s: batch of %d failed: %s", self.name, n, exc)
@@ -241,6 +281,9 @@ class DynamicBatcher:
             "rejected": self.rejected,
             "mean_batch": (self.requests / self.batches) if self.batches else 0.0,
             "healthy": self.healthy,
+            "unhealthy_reason": self.unhealthy_reason,
+            "consecutive_failures": self.consecutive_failures,
+            "oldest_running_s": round(self.oldest_running_s, 3),
         }
 
 
@@ -275,8 +318,27 @@ class ReplicaRouter:
     async def submit(self, sample: Any, timeout: Optional[float] = None) -> Any:
         return await self.pick().submit(sample, timeout)
 
-    def mark_unhealthy(self, idx: int) -> None:
-        self.batchers[idx].healthy = False
+    def mark_unhealthy(self, idx: int, reason: str = "marked unhealthy") -> None:
+        """Drain replica ``idx``: no new requests, and its queued backlog moves to the healthy
+        replicas (or fails with QueueFull when none is left)."""
+        b = self.batchers[idx]
+        b.healthy = False
+        b.unhealthy_reason = reason
+        backlog = b.evict_queued()
+        live = [x for x in self.batchers if x.healthy]
+        for j, item in enumerate(backlog):
+            if live:
+                live[j % len(live)].adopt([item])
+            elif not item[1].done():
+                item[1].set_exception(QueueFull(f"replica {idx} drained ({reason}); no healthy replica"))
+
+    def mark_healthy(self, idx: int) -> None:
+        self.batchers[idx].healthy = True
+        self.batchers[idx].unhealthy_reason = None
+
+    @property
+    def healthy_count(self) -> int:
+        return sum(1 for b in self.batchers if b.healthy)
 
     def stats(self) -> List[dict]:
         return [b.stats() for b in self.batchers]
