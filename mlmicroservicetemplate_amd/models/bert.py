@@ -45,6 +45,58 @@ BERT_BASE = BertConfig()
 CLS_ID, SEP_ID, PAD_ID, UNK_ID = 101, 102, 0, 100
 
 
+_HF_BERT_FIXED = {
+    "embeddings.word_embeddings.weight": "emb.word", "embeddings.position_embeddings.weight": "emb.pos",
+    "embeddings.token_type_embeddings.weight": "emb.type", "embeddings.LayerNorm.weight": "emb.ln.g",
+    "embeddings.LayerNorm.bias": "emb.ln.b", "pooler.dense.weight": "pooler.w", "pooler.dense.bias": "pooler.b",
+    "classifier.weight": "cls.w", "classifier.bias": "cls.b",
+}
+_HF_BERT_LAYER = {
+    "attention.self.query": "q", "attention.self.key": "k", "attention.self.value": "v",
+    "attention.output.dense": "o", "attention.output.LayerNorm": "ln1", "intermediate.dense": "ffn1",
+    "output.dense": "ffn2", "output.LayerNorm": "ln2",
+}
+
+
+def hf_bert_name(k: str) -> Optional[str]:
+    """Hugging Face ``BertForSequenceClassification`` key -> this model's name (q/k/v kept apart
+    here and fused into ``qkv`` by :func:`_fuse_qkv`)."""
+    k = k[5:] if k.startswith("bert.") else k
+    k = k.replace("LayerNorm.gamma", "LayerNorm.weight").replace("LayerNorm.beta", "LayerNorm.bias")
+    if k.endswith("position_ids"):
+        return None
+    if k in _HF_BERT_FIXED:
+        return _HF_BERT_FIXED[k]
+    if k.startswith("encoder.layer."):
+        rest = k[len("encoder.layer."):]
+        i, sub = rest.split(".", 1)
+        mod, leaf = sub.rsplit(".", 1)
+        short = _HF_BERT_LAYER.get(mod)
+        if short is None:
+            return k
+        if short.startswith("ln"):
+            return f"l{i}.{short}.{'g' if leaf == 'weight' else 'b'}"
+        return f"l{i}.{short}.{'w' if leaf == 'weight' else 'b'}"
+    return k
+
+
+def _fuse_qkv(state: Dict[str, torch.Tensor]) -> None:
+    i = 0
+    while f"l{i}.q.w" in state:
+        for leaf in ("w", "b"):
+            parts = [state.pop(f"l{i}.{n}.{leaf}") for n in ("q", "k", "v")]
+            state[f"l{i}.qkv.{leaf}"] = torch.cat(parts, 0)
+        i += 1
+
+
+def load_bert(path: str, cfg: "BertConfig") -> Dict[str, torch.Tensor]:
+    """fp32 parameters from a safetensors checkpoint in this model's names or Hugging Face's."""
+    from ..utils.checkpoint import load_validated
+
+    spec = {k: (shape, torch.float32) for k, (shape, _dt) in bert_spec(cfg).items()}
+    return load_validated(path, spec, rename=lambda k: k if k in spec else hf_bert_name(k), combine=_fuse_qkv)
+
+
 def init_bert(cfg: BertConfig = BERT_BASE, seed: int = 0, device="cpu", dtype=torch.float32) -> Dict[str, torch.Tensor]:
     g = torch.Generator(device=device).manual_seed(seed)
 

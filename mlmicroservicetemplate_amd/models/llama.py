@@ -101,47 +101,123 @@ def _full(seed, name, shape, device, kind="normal"):
     return torch.randn(*shape, generator=g, device=device) * 0.02
 
 
+class RandomSource:
+    """Deterministic random-init weights: every full tensor is generated from (seed, name), so
+    any TP shard of it is identical to the same slice at tp=1."""
+
+    def __init__(self, seed: int = 0, device="cpu"):
+        self.seed, self.device = seed, device
+
+    def region(self, name: str, shape, kind: str = "normal", rows: Optional[slice] = None,
+               cols: Optional[slice] = None) -> torch.Tensor:
+        t = _full(self.seed, name, shape, self.device, kind)
+        if rows is not None:
+            t = t[rows]
+        if cols is not None:
+            t = t[:, cols]
+        return t
+
+
+def hf_llama_name(name: str) -> str:
+    """Canonical name (``l3.q``, ``embed``, ...) -> Hugging Face Llama safetensors key."""
+    fixed = {"embed": "model.embed_tokens.weight", "lm_head": "lm_head.weight", "final_norm": "model.norm.weight"}
+    if name in fixed:
+        return fixed[name]
+    layer, part = name[1:].split(".", 1)
+    sub = {"q": "self_attn.q_proj", "k": "self_attn.k_proj", "v": "self_attn.v_proj", "o": "self_attn.o_proj",
+           "gate": "mlp.gate_proj", "up": "mlp.up_proj", "down": "mlp.down_proj",
+           "attn_norm": "input_layernorm", "mlp_norm": "post_attention_layernorm"}[part]
+    return f"model.layers.{layer}.{sub}.weight"
+
+
+class CheckpointSource:
+    """Weights from a safetensors file / shard directory, canonical or Hugging Face names.  Each
+    TP rank reads only its slice of every matrix (memory-mapped region reads); a checkpoint
+    without ``lm_head`` (tied embeddings) reuses ``embed``."""
+
+    def __init__(self, path: str, device="cpu"):
+        from ..utils.checkpoint import Checkpoint
+
+        self.ck = Checkpoint(path)
+        self.device = device
+
+    def _key(self, name: str) -> str:
+        from ..utils.checkpoint import CheckpointError
+
+        for k in (name, hf_llama_name(name)):
+            if k in self.ck:
+                return k
+        if name == "lm_head":
+            return self._key("embed")
+        raise CheckpointError(f"{self.ck.path}: no tensor for {name!r} (or {hf_llama_name(name)!r})")
+
+    def region(self, name: str, shape, kind: str = "normal", rows: Optional[slice] = None,
+               cols: Optional[slice] = None) -> torch.Tensor:
+        from ..utils.checkpoint import CheckpointError
+
+        key = self._key(name)
+        have = self.ck.shape(key)
+        if tuple(have) != tuple(shape):
+            raise CheckpointError(f"{self.ck.path}: {key} has shape {tuple(have)}, config expects {tuple(shape)}")
+        return self.ck.get_region(key, rows, cols).to(device=self.device, dtype=torch.float32)
+
+
 def init_llama_shard(cfg: LlamaConfig, tp: int = 1, rank: int = 0, seed: int = 0, device="cpu",
-                     dtype=torch.bfloat16) -> Dict[str, torch.Tensor]:
-    """This rank's shard of a random-init Llama (the same full model for every tp)."""
+                     dtype=torch.bfloat16, source=None) -> Dict[str, torch.Tensor]:
+    """This rank's shard of a Llama: from ``source`` (:class:`CheckpointSource`) or a
+    deterministic random init (:class:`RandomSource`, the same full model for every tp)."""
+    src = source if source is not None else RandomSource(seed, device)
     sd = shard_dims(cfg, tp, rank)
     H, D = cfg.hidden, cfg.head_dim
     kv_rep = cfg.kv_heads < tp  # more ranks than KV heads: replicate a head over tp/kv_heads ranks
     p: Dict[str, torch.Tensor] = {}
 
     def vocab_rows(name):
-        full = _full(seed, name, (cfg.vocab, H), device)
         lo, hi = sd.vocab_lo, min(cfg.vocab, sd.vocab_lo + sd.vocab_shard)
         out = torch.zeros(sd.vocab_shard, H, device=device)
         if hi > lo:
-            out[: hi - lo] = full[lo:hi]
+            out[: hi - lo] = src.region(name, (cfg.vocab, H), rows=slice(lo, hi)).to(device)
         return out.to(dtype)
 
     p["embed"] = vocab_rows("embed")
     p["lm_head"] = vocab_rows("lm_head")
-    p["final_norm"] = _full(seed, "final_norm", (H,), device, "norm").to(dtype)
+    p["final_norm"] = src.region("final_norm", (H,), "norm").to(device=device, dtype=dtype)
+    qs = slice(rank * sd.hq * D, (rank + 1) * sd.hq * D)
+    kvh = (rank * cfg.kv_heads) // tp if kv_rep else rank * sd.hkv
+    ks = slice(kvh * D, (kvh + sd.hkv) * D)
+    sl = slice(rank * sd.inter, (rank + 1) * sd.inter)
     for i in range(cfg.layers):
-        wq = _full(seed, f"l{i}.q", (cfg.heads * D, H), device)
-        wk = _full(seed, f"l{i}.k", (cfg.kv_heads * D, H), device)
-        wv = _full(seed, f"l{i}.v", (cfg.kv_heads * D, H), device)
-        q = wq[rank * sd.hq * D: (rank + 1) * sd.hq * D]
-        kvh = (rank * cfg.kv_heads) // tp if kv_rep else rank * sd.hkv
-        k = wk[kvh * D: (kvh + sd.hkv) * D]
-        v = wv[kvh * D: (kvh + sd.hkv) * D]
-        p[f"l{i}.qkv"] = torch.cat([q, k, v]).to(dtype).contiguous()
-        wo = _full(seed, f"l{i}.o", (H, cfg.heads * D), device)
-        p[f"l{i}.o"] = wo[:, rank * sd.hq * D: (rank + 1) * sd.hq * D].to(dtype).contiguous()
-        wg = _full(seed, f"l{i}.gate", (cfg.intermediate, H), device)
-        wu = _full(seed, f"l{i}.up", (cfg.intermediate, H), device)
-        sl = slice(rank * sd.inter, (rank + 1) * sd.inter)
-        p[f"l{i}.gate"] = wg[sl].to(dtype).contiguous()
-        p[f"l{i}.up"] = wu[sl].to(dtype).contiguous()
-        wd = _full(seed, f"l{i}.down", (H, cfg.intermediate), device)
-        p[f"l{i}.down"] = wd[:, sl].to(dtype).contiguous()
-        p[f"l{i}.attn_norm"] = _full(seed, f"l{i}.attn_norm", (H,), device, "norm").to(dtype)
-        p[f"l{i}.mlp_norm"] = _full(seed, f"l{i}.mlp_norm", (H,), device, "norm").to(dtype)
-        del wq, wk, wv, wo, wg, wu, wd
+        q = src.region(f"l{i}.q", (cfg.heads * D, H), rows=qs)
+        k = src.region(f"l{i}.k", (cfg.kv_heads * D, H), rows=ks)
+        v = src.region(f"l{i}.v", (cfg.kv_heads * D, H), rows=ks)
+        p[f"l{i}.qkv"] = torch.cat([q, k, v]).to(device=device, dtype=dtype).contiguous()
+        p[f"l{i}.o"] = src.region(f"l{i}.o", (H, cfg.heads * D), cols=qs).to(device=device, dtype=dtype).contiguous()
+        p[f"l{i}.gate"] = src.region(f"l{i}.gate", (cfg.intermediate, H), rows=sl).to(device=device,
+                                                                                      dtype=dtype).contiguous()
+        p[f"l{i}.up"] = src.region(f"l{i}.up", (cfg.intermediate, H), rows=sl).to(device=device,
+                                                                                  dtype=dtype).contiguous()
+        p[f"l{i}.down"] = src.region(f"l{i}.down", (H, cfg.intermediate), cols=sl).to(device=device,
+                                                                                      dtype=dtype).contiguous()
+        p[f"l{i}.attn_norm"] = src.region(f"l{i}.attn_norm", (H,), "norm").to(device=device, dtype=dtype)
+        p[f"l{i}.mlp_norm"] = src.region(f"l{i}.mlp_norm", (H,), "norm").to(device=device, dtype=dtype)
+        del q, k, v
     return p
+
+
+def full_llama_state(cfg: LlamaConfig, seed: int = 0, dtype=torch.bfloat16) -> Dict[str, torch.Tensor]:
+    """The unsharded random-init model under canonical names (what ``export-weights`` writes)."""
+    src = RandomSource(seed)
+    H, D = cfg.hidden, cfg.head_dim
+    out = {"embed": src.region("embed", (cfg.vocab, H)), "lm_head": src.region("lm_head", (cfg.vocab, H)),
+           "final_norm": src.region("final_norm", (H,), "norm")}
+    for i in range(cfg.layers):
+        for n, shp, kind in (("q", (cfg.heads * D, H), "normal"), ("k", (cfg.kv_heads * D, H), "normal"),
+                             ("v", (cfg.kv_heads * D, H), "normal"), ("o", (H, cfg.heads * D), "normal"),
+                             ("gate", (cfg.intermediate, H), "normal"), ("up", (cfg.intermediate, H), "normal"),
+                             ("down", (H, cfg.intermediate), "normal"), ("attn_norm", (H,), "norm"),
+                             ("mlp_norm", (H,), "norm")):
+            out[f"l{i}.{n}"] = src.region(f"l{i}.{n}", shp, kind)
+    return {k: v.to(dtype) for k, v in out.items()}
 
 
 # --------------------------------------------------------------------------- tokenizer

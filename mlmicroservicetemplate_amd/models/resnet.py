@@ -84,6 +84,40 @@ def init_resnet50(seed: int = 0, num_classes: int = NUM_CLASSES) -> Dict[str, to
     return params
 
 
+_BN = {"weight": "gamma", "bias": "beta", "running_mean": "mean", "running_var": "var"}
+
+
+def torchvision_name(k: str) -> Optional[str]:
+    """torchvision ``resnet50().state_dict()`` key -> this model's name (None: not a parameter)."""
+    if k.endswith("num_batches_tracked"):
+        return None
+    p = k.split(".")
+    if p[0] == "conv1":
+        return "stem.w"
+    if p[0] == "bn1":
+        return f"stem.bn.{_BN[p[1]]}"
+    if p[0] == "fc":
+        return {"weight": "fc.w", "bias": "fc.b"}[p[1]]
+    if p[0].startswith("layer") and len(p) >= 4:
+        blk = f"{p[0]}.{p[1]}"
+        if p[2].startswith("conv"):
+            return f"{blk}.{p[2]}.w"
+        if p[2].startswith("bn"):
+            return f"{blk}.conv{p[2][2:]}.bn.{_BN[p[3]]}"
+        if p[2] == "downsample":
+            return f"{blk}.down.w" if p[3] == "0" else f"{blk}.down.bn.{_BN[p[4]]}"
+    return k
+
+
+def load_resnet50(path: str, num_classes: int = NUM_CLASSES) -> Dict[str, torch.Tensor]:
+    """fp32 parameters from a safetensors checkpoint in this model's names or torchvision's
+    (validated name by name, shape by shape)."""
+    from ..utils.checkpoint import load_validated
+
+    spec = {k: (tuple(v.shape), torch.float32) for k, v in init_resnet50_spec(num_classes).items()}
+    return load_validated(path, spec, rename=lambda k: k if k in spec else torchvision_name(k))
+
+
 def init_resnet50_spec(num_classes: int = NUM_CLASSES) -> Dict[str, torch.Tensor]:
     """Meta tensors with the shapes/dtypes of :func:`init_resnet50` (what non-source ranks need
     to receive the X1 weight broadcast without generating weights themselves)."""

@@ -122,11 +122,7 @@ class ResNet50Plugin(ModelPlugin):
         # X1: rank 0 builds (or loads) the weights, every other rank receives them over RCCL
         params = None
         if ctx.rank == 0:
-            params = resnet.init_resnet50(int(s.SEED))
-            if s.WEIGHTS:
-                from safetensors.torch import load_file
-
-                params.update(load_file(s.WEIGHTS))
+            params = resnet.load_resnet50(s.WEIGHTS) if s.WEIGHTS else resnet.init_resnet50(int(s.SEED))
         if ctx.world_size > 1:
             spec = {k: (tuple(v.shape), v.dtype) for k, v in resnet.init_resnet50_spec().items()}
             params = mdist.broadcast_state(params, src=0, device=torch.device(devices[0]), spec=spec)

@@ -53,7 +53,9 @@ class LlamaPlugin(ModelPlugin):
         dev = ctx.devices[0] if on_gpu else "cpu"
         backend = s.BACKEND if (on_gpu and s.BACKEND == "fused") else "reference"
         self.comm_dev = torch.device(dev)
-        params = llama.init_llama_shard(cfg, tp, ctx.rank, int(s.SEED), device=dev)
+        # every TP rank reads just its own slices from the checkpoint (no weight broadcast needed)
+        source = llama.CheckpointSource(s.WEIGHTS, device=dev) if s.WEIGHTS else None
+        params = llama.init_llama_shard(cfg, tp, ctx.rank, int(s.SEED), device=dev, source=source)
         self.model = llama.LlamaTP(params, cfg, tp=tp, rank=ctx.rank, comm=llama.TPComm(None, tp), backend=backend,
                                    device=dev, max_batch=int(s.MAX_BATCH), max_seq=int(extra.get("max_seq", 2048)))
         self.tok = llama.LlamaTokenizer(cfg, extra.get("tokenizer_file"))

@@ -49,7 +49,9 @@ class BertPlugin(ModelPlugin):
         devices = ctx.devices or (["cuda:0"] if torch.cuda.is_available() else [])
         if not devices:
             raise RuntimeError("bert plugin needs a GPU")
-        params = bert.init_bert(cfg, int(s.SEED)) if ctx.rank == 0 else None
+        params = None
+        if ctx.rank == 0:
+            params = bert.load_bert(s.WEIGHTS, cfg) if s.WEIGHTS else bert.init_bert(cfg, int(s.SEED))
         if ctx.world_size > 1:
             spec = bert.bert_spec(cfg)
             params = mdist.broadcast_state(params, src=0, device=torch.device(devices[0]), spec=spec)

@@ -185,7 +185,33 @@ def build_parser() -> argparse.ArgumentParser:
     b = sub.add_parser("build", help="compile the HIP kernels for gfx950")
     b.add_argument("--force", action="store_true")
     sub.add_parser("plugins", help="list registered model plugins")
+    e = sub.add_parser("export-weights", help="write a model's random-init weights as .safetensors")
+    e.add_argument("--model", required=True, choices=["resnet50", "bert", "llama-tiny", "llama-8b"])
+    e.add_argument("--out", required=True)
+    e.add_argument("--seed", type=int, default=0)
     return ap
+
+
+def export_weights(model: str, out: str, seed: int = 0) -> str:
+    """The exact weights a ``SEED=seed`` server would random-initialise, under canonical names --
+    a ``WEIGHTS=out`` server then loads them through the validated checkpoint path."""
+    from .utils.checkpoint import save_state
+
+    if model == "resnet50":
+        from .models import resnet
+
+        state = resnet.init_resnet50(seed)
+    elif model == "bert":
+        from .models import bert
+
+        state = bert.init_bert(bert.BERT_BASE, seed)
+    else:
+        from .models import llama
+
+        cfg = llama.LLAMA3_8B if model == "llama-8b" else llama.tiny_config()
+        state = llama.full_llama_state(cfg, seed)
+    save_state(out, state, metadata={"model": model, "seed": str(seed)})
+    return out
 
 
 def main(argv: Optional[List[str]] = None) -> int:
@@ -201,6 +227,9 @@ def main(argv: Optional[List[str]] = None) -> int:
         from .plugins.base import available_plugins
 
         print("\n".join(available_plugins()))
+        return 0
+    if args.cmd == "export-weights":
+        print(export_weights(args.model, args.out, args.seed))
         return 0
     if args.cmd in ("serve", None):
         if args.cmd is None:
