@@ -479,16 +479,17 @@ class LlamaTP:
 
     def _decode_graph(self, B: int, k: int, ctx: int):
         """Captured decode step for batch B and context bound ctx (static token / position / length
-        buffers).  The warm-up runs at position max_seq - 1, which no generation ever reads (and
-        which the split grid of ctx < max_seq does not even reach), so graphs can be captured while
+        buffers).  The warm-up steps run at position ctx - 1: for a sequence being decoded under
+        this bound that row is either the one the step about to replay writes anyway, or a future
+        row that will be overwritten before anything reads it -- so graphs can be captured while
         sequences are in flight."""
         key = (B, k, ctx)
         if key in self._graphs:
             return self._graphs[key]
         dev = self.device
         tok = torch.zeros(B, 1, dtype=torch.int32, device=dev)
-        pos = torch.full((B, 1), self.max_seq - 1, dtype=torch.int32, device=dev)
-        lens = torch.full((B,), self.max_seq, dtype=torch.int32, device=dev)
+        pos = torch.full((B, 1), ctx - 1, dtype=torch.int32, device=dev)
+        lens = torch.full((B,), ctx, dtype=torch.int32, device=dev)
         self._dec_ctx = ctx
         try:
             side = torch.cuda.Stream(dev)

@@ -501,7 +501,8 @@ def rope_kv_(qkv: torch.Tensor, positions: torch.Tensor, cos: torch.Tensor, sin:
     T = positions.numel()
     rc = lib().mls_rope_kv(qkv.data_ptr(), positions.data_ptr(), cos.data_ptr(), sin.data_ptr(), T, qkv.shape[-1],
                            n_q_heads, n_kv_heads, head_dim, _ptr(slots), _ptr(k_cache), _ptr(v_cache), _ptr(lens),
-                           seq, max_seq, stream_ptr(dev))
+                           seq, max_seq, k_cache.numel() // (n_kv_heads * head_dim) if k_cache is not None else 0,
+                           cos.shape[0], stream_ptr(dev))
     check(rc, "mls_rope_kv")
     return qkv
 
@@ -570,8 +571,9 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
         _need(positions, "positions", torch.int32, dev)
     rc = lib().mls_decode_attention(q.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), out.data_ptr(),
                                     ws.data_ptr(), ws_ml.data_ptr(), counters.data_ptr(), q.stride(0), out.stride(0),
-                                    k_cache.stride(0), lens.data_ptr(), _ptr(positions), _ptr(cos), _ptr(sin), B,
-                                    n_q_heads, n_kv_heads, head_dim, max_len, chunk, float(scale), stream_ptr(dev))
+                                    k_cache.stride(0), lens.data_ptr(), _ptr(positions), _ptr(cos), _ptr(sin),
+                                    cos.shape[0] if cos is not None else 0, B, n_q_heads, n_kv_heads, head_dim, max_len,
+                                    chunk, float(scale), stream_ptr(dev))
     check(rc, "mls_decode_attention")
     return out
 

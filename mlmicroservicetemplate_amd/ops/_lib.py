@@ -47,12 +47,12 @@ _SIGS = {
     "mls_embed_ln": [P, P, P, P, P, P, P, P, L, I, I, I, F, P],
     "mls_embedding": [P, P, P, L, I, I, I, P],
     "mls_rope": [P, P, P, P, L, I, I, I, P],
-    "mls_rope_kv": [P, P, P, P, L, I, I, I, I, P, P, P, P, I, I, P],
+    "mls_rope_kv": [P, P, P, P, L, I, I, I, I, P, P, P, P, I, I, L, I, P],
     "mls_kv_append": [P, I, I, I, P, P, P, L, I, I, P],
     "mls_flash_attention": [P, P, P, P, I, I, I, I, I, I, I, I, I, P, I, F, P],
     "mls_skinny_gemm": [P, P, P, P, P, P, SZ, I, I, I, I, I, P],
     "mls_skinny_gemm_norm": [P, P, P, P, P, P, P, P, SZ, I, I, I, I, I, I, F, P],
-    "mls_decode_attention": [P, P, P, P, P, P, P, I, I, L, P, P, P, P, I, I, I, I, I, I, F, P],
+    "mls_decode_attention": [P, P, P, P, P, P, P, I, I, L, P, P, P, P, I, I, I, I, I, I, I, F, P],
 }
 _OPTIONAL_SIGS: dict = {"mls_set_debug_flags": [I]}
 
@@ -79,6 +79,17 @@ def _bind(lib: ctypes.CDLL) -> None:
         fn.restype = _c.c_int
 
 
+DEBUG = os.environ.get("MLS_DEBUG", "0") == "1"
+DEBUG_TUS = ("attention", "norm_ops")  # translation units with MLS_CHECK bounds
+DEBUG_CODES = {
+    101: "rope/KV append: cache slot beyond the cache",
+    102: "rope/KV append: position beyond the RoPE table",
+    201: "decode attention: lens[b] exceeds the split grid (host context bound max_len too small)",
+    202: "decode attention (rope mode): position outside the RoPE table or != lens - 1",
+    301: "flash attention: kv_lens[b] > S",
+}
+
+
 def lib(build_if_missing: bool = True) -> ctypes.CDLL:
     global _LIB
     if _LIB is not None:
@@ -86,11 +97,11 @@ def lib(build_if_missing: bool = True) -> ctypes.CDLL:
     with _LOCK:
         if _LIB is not None:
             return _LIB
-        path = _build.lib_path()
+        path = _build.lib_path(DEBUG)
         if build_if_missing:
             # incremental: a no-op when the stamp matches the sources
             try:
-                path = _build.build()
+                path = _build.build(debug=DEBUG)
             except Exception as e:  # toolchain missing -> only OK if the .so already exists
                 if not os.path.exists(path):
                     raise NativeError(f"native kernels unavailable and build failed: {e}") from e
@@ -113,6 +124,27 @@ def available() -> bool:
 def check(rc: int, what: str) -> None:
     if rc != 0:
         raise NativeError(f"{what} failed with status {rc}")
+    if DEBUG and not torch.cuda.is_current_stream_capturing():
+        debug_check(what)
+
+
+def debug_check(what: str = "kernel") -> None:
+    """Debug builds: synchronise, then raise on the first bound a kernel recorded (and clear it)."""
+    if not DEBUG:
+        return
+    torch.cuda.synchronize()
+    buf = (_c.c_int * 4)()
+    for tu in DEBUG_TUS:
+        fn = getattr(lib(), f"mls_debug_read_{tu}", None)
+        if fn is None:
+            raise NativeError(f"{lib()._name} is not a debug build")
+        fn.argtypes = [_c.c_void_p]
+        fn.restype = _c.c_int
+        if fn(_c.cast(buf, _c.c_void_p)) != 0:
+            raise NativeError("mls_debug_read failed")
+        if buf[0]:
+            raise NativeError(f"{what}: bound violated [{buf[0]}] {DEBUG_CODES.get(buf[0], '?')} "
+                              f"(block {buf[1]},{buf[2]} thread {buf[3]})")
 
 
 def stream_ptr(device: Optional[torch.device] = None) -> int:

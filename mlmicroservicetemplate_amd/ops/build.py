@@ -26,6 +26,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "_native")
 LIB_NAME = "libmls_kernels.so"
+DEBUG_LIB_NAME = "libmls_kernels_debug.so"  # -DMLS_DEBUG: bounds-checked variant (MLS_DEBUG=1)
 ARCH = os.environ.get("MLS_OFFLOAD_ARCH", "gfx950")
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
 
@@ -54,16 +55,21 @@ def _digest(paths: List[str], extra: str = "") -> str:
     return h.hexdigest()[:16]
 
 
-def lib_path() -> str:
-    return os.path.join(OUT_DIR, LIB_NAME)
+def lib_path(debug: bool = False) -> str:
+    return os.path.join(OUT_DIR, DEBUG_LIB_NAME if debug else LIB_NAME)
 
 
-def _compile(src: str, hdr_hash: str, obj_dir: str, verbose: bool) -> str:
-    key = _digest([src], hdr_hash + " ".join(CXXFLAGS))
+def _flags(debug: bool) -> List[str]:
+    return CXXFLAGS + (["-DMLS_DEBUG"] if debug else [])
+
+
+def _compile(src: str, hdr_hash: str, obj_dir: str, verbose: bool, debug: bool = False) -> str:
+    flags = _flags(debug)
+    key = _digest([src], hdr_hash + " ".join(flags))
     obj = os.path.join(obj_dir, os.path.basename(src).replace(".hip", f".{key}.o"))
     if os.path.exists(obj):
         return obj
-    cmd = [hipcc(), *CXXFLAGS, "-I", CSRC, "-c", src, "-o", obj + ".tmp"]
+    cmd = [hipcc(), *flags, "-I", CSRC, "-c", src, "-o", obj + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -73,14 +79,14 @@ def _compile(src: str, hdr_hash: str, obj_dir: str, verbose: bool) -> str:
     return obj
 
 
-def build(force: bool = False, verbose: bool = False, jobs: Optional[int] = None) -> str:
+def build(force: bool = False, verbose: bool = False, jobs: Optional[int] = None, debug: bool = False) -> str:
     os.makedirs(OUT_DIR, exist_ok=True)
-    obj_dir = os.path.join(OUT_DIR, "obj")
+    obj_dir = os.path.join(OUT_DIR, "obj_debug" if debug else "obj")
     os.makedirs(obj_dir, exist_ok=True)
     srcs = sources()
     hdr_hash = _digest(headers())
-    stamp = _digest(srcs + headers(), " ".join(CXXFLAGS))
-    out = lib_path()
+    stamp = _digest(srcs + headers(), " ".join(_flags(debug)))
+    out = lib_path(debug)
     stamp_file = out + ".stamp"
     if not force and os.path.exists(out) and os.path.exists(stamp_file):
         with open(stamp_file) as f:
@@ -88,7 +94,7 @@ def build(force: bool = False, verbose: bool = False, jobs: Optional[int] = None
                 return out
     jobs = jobs or min(len(srcs), max(1, min(8, os.cpu_count() or 1)))
     with cf.ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, hdr_hash, obj_dir, verbose), srcs))
+        objs = list(ex.map(lambda s: _compile(s, hdr_hash, obj_dir, verbose, debug), srcs))
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", out + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)
@@ -114,8 +120,9 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--debug", action="store_true", help="the bounds-checked -DMLS_DEBUG variant")
     args = ap.parse_args(argv)
-    path = build(force=args.force, verbose=args.verbose)
+    path = build(force=args.force, verbose=args.verbose, debug=args.debug)
     print(path)
     return 0
 

@@ -62,6 +62,7 @@ __global__ __launch_bounds__(256) void flash_fwd_kernel(const AttnArgs a) {
   const int hk = h / (a.Hq / a.Hkv);
   const int q0 = blockIdx.x * BQ;
   const int qw = q0 + wid * 16;
+  MLS_CHECK(!a.kv_lens || a.kv_lens[b] <= a.S, 301);
   const int L = a.kv_lens ? min(a.kv_lens[b], a.S) : a.S;
   const long tok0 = (long)b * a.S;
 
@@ -210,7 +211,7 @@ struct DecodeArgs {
   const int* positions;  // rope mode: query position per sequence (== lens[b] - 1)
   const float* cos_t;    // [max_pos][D/2]
   const float* sin_t;
-  int Hq, Hkv, nsplit;
+  int Hq, Hkv, nsplit, max_pos;
   float scale_log2;
 };
 
@@ -251,7 +252,10 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(const DecodeArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int grp = lane / LPR, gl = lane % LPR, glp = gl ^ (LPR / 2);
   const int b = blockIdx.z, hk = blockIdx.y, sp = blockIdx.x;
-  const int L = a.lens[b];
+  const int L0 = a.lens[b];
+  // keys past the split grid are never visited: a host context bound below lens is a caller bug
+  MLS_CHECK(sp != 0 || L0 <= a.nsplit * CHUNK, 201);
+  const int L = min(L0, a.nsplit * CHUNK);
   const int start = sp * CHUNK;
   if (start >= L) {
     if (L <= 0 && sp == 0)
@@ -261,6 +265,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(const DecodeArgs a) {
   const int end = min(L, start + CHUNK);
   const bool rope = a.positions != nullptr;
   const int pos = rope ? a.positions[b] : 0;
+  MLS_CHECK(!rope || (pos >= 0 && pos < a.max_pos && pos == L0 - 1), 202);
   const bf16* qrow = a.q + (long)b * a.q_stride;
   const long rstride = (long)a.Hkv * D;
   const long cbase = (long)b * a.seq_stride + (long)hk * D + gl * 8;
@@ -484,8 +489,8 @@ int mls_flash_attention(const void* q, const void* k, const void* v, void* o, in
 // positions/cos/sin non-null: rope mode (q = the fused QKV rows, positions[b] == lens[b] - 1).
 int mls_decode_attention(const void* q, void* k_cache, void* v_cache, void* o, float* ws, float* ws_ml, int* counters,
                          int q_stride, int o_stride, long seq_stride, const int* lens, const int* positions,
-                         const float* cos_t, const float* sin_t, int B, int Hq, int Hkv, int D, int max_len, int chunk,
-                         float scale, void* stream) {
+                         const float* cos_t, const float* sin_t, int max_pos, int B, int Hq, int Hkv, int D,
+                         int max_len, int chunk, float scale, void* stream) {
   if (B <= 0 || Hq % Hkv || chunk <= 0 || max_len <= 0) return MLS_BAD_ARG;
   (void)counters;  // reserved (in-launch merge variants); the combine runs as its own launch
   if (positions && (!cos_t || !sin_t)) return MLS_BAD_ARG;
@@ -504,6 +509,7 @@ int mls_decode_attention(const void* q, void* k_cache, void* v_cache, void* o, f
   a.positions = positions;
   a.cos_t = cos_t;
   a.sin_t = sin_t;
+  a.max_pos = max_pos;
   a.Hq = Hq;
   a.Hkv = Hkv;
   a.nsplit = (max_len + chunk - 1) / chunk;
@@ -542,3 +548,5 @@ int mls_decode_attention(const void* q, void* k_cache, void* v_cache, void* o, f
 }
 
 }  // extern "C"
+
+MLS_DEBUG_EXPORT(attention)

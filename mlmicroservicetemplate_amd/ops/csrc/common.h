@@ -22,6 +22,35 @@ enum MlsStatus : int {
 MLS_DEV float bf2f(bf16 x) { return (float)x; }
 MLS_DEV bf16 f2bf(float x) { return (bf16)x; }
 
+// ---- bounds-checked debug builds: `MLS_DEBUG=1` loads a variant compiled with
+// -DMLS_DEBUG in which MLS_CHECK records the first violated data-dependent bound (code, block,
+// thread) in a per-translation-unit device word instead of letting the access fault the GPU;
+// the kernels keep their guards in release builds too, MLS_CHECK only adds the report.  The host
+// reads / clears the words through mls_debug_read_<tu> after synchronising (ops._lib.check).
+#ifdef MLS_DEBUG
+static __device__ int g_mls_dbg[4];
+#define MLS_CHECK(cond, code)                                              \
+  do {                                                                     \
+    if (!(cond)) {                                                         \
+      if (atomicCAS(&g_mls_dbg[0], 0, (code)) == 0) {                      \
+        g_mls_dbg[1] = (int)blockIdx.x;                                    \
+        g_mls_dbg[2] = (int)blockIdx.y;                                    \
+        g_mls_dbg[3] = (int)threadIdx.x;                                   \
+      }                                                                    \
+    }                                                                      \
+  } while (0)
+#define MLS_DEBUG_EXPORT(tu)                                               \
+  extern "C" int mls_debug_read_##tu(int* out) {                           \
+    int zero[4] = {0, 0, 0, 0};                                            \
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mls_dbg), 16);    \
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(g_mls_dbg), zero, 16); \
+    return (int)e;                                                         \
+  }
+#else
+#define MLS_CHECK(cond, code) ((void)0)
+#define MLS_DEBUG_EXPORT(tu)
+#endif
+
 // ---- buffer (SRD) loads: hardware range check returns 0 for an out-of-range offset, which is
 // how the implicit-GEMM gather zero-fills conv padding without branches or pointer selects.
 typedef __amdgpu_buffer_rsrc_t rsrc_t;

@@ -158,10 +158,13 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(bf16* __restrict__ qkv, co
                                                       int row_stride, int Hq, int Hkv, int D,
                                                       const int* __restrict__ slots, bf16* __restrict__ kc,
                                                       bf16* __restrict__ vc, const int* __restrict__ lens, int S,
-                                                      int max_seq) {
+                                                      int max_seq, long cache_rows, int max_pos) {
   const long t = blockIdx.x;
   const int half = D >> 1, quads = half >> 2;
   const int p = positions[t];
+  const bool p_ok = p >= 0 && p < max_pos;
+  MLS_CHECK(p_ok, 102);
+  if (!p_ok) return;  // no RoPE row for this position: leave the token untouched
   bf16* row = qkv + t * row_stride;
   const int nrot = Hq + Hkv;
   for (int q = threadIdx.x; q < nrot * quads; q += blockDim.x) {
@@ -192,6 +195,8 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(bf16* __restrict__ qkv, co
     if (p < max_seq && (!lens || p < lens[b])) slot = b * max_seq + p;
   }
   if (slot < 0 || !kc) return;
+  MLS_CHECK(slot < cache_rows, 101);
+  if (slot >= cache_rows) return;
   __syncthreads();  // rotated K visible to the copy below (LDS-free: same block, global memory)
   __threadfence_block();
   const int nch = (Hkv * D) >> 3;
@@ -322,10 +327,11 @@ int mls_rope(void* qkv, const int* positions, const float* cos_t, const float* s
 
 int mls_rope_kv(void* qkv, const int* positions, const float* cos_t, const float* sin_t, long tokens, int row_stride,
                 int Hq, int Hkv, int D, const int* slots, void* k_cache, void* v_cache, const int* lens, int S,
-                int max_seq, void* stream) {
+                int max_seq, long cache_rows, int max_pos, void* stream) {
   if (D % 8 || tokens <= 0 || row_stride % 8 || (!slots && max_seq > 0 && S <= 0)) return MLS_BAD_ARG;
   hipLaunchKernelGGL(rope_kv_kernel, dim3((unsigned)tokens), dim3(256), 0, (hipStream_t)stream, (bf16*)qkv, positions,
-                     cos_t, sin_t, row_stride, Hq, Hkv, D, slots, (bf16*)k_cache, (bf16*)v_cache, lens, S, max_seq);
+                     cos_t, sin_t, row_stride, Hq, Hkv, D, slots, (bf16*)k_cache, (bf16*)v_cache, lens, S, max_seq,
+                     cache_rows, max_pos);
   return (int)hipGetLastError();
 }
 
@@ -340,3 +346,5 @@ int mls_kv_append(const void* qkv, int row_stride, int k_col, int v_col, const i
 }
 
 }  // extern "C"
+
+MLS_DEBUG_EXPORT(norm_ops)
