@@ -251,12 +251,24 @@ class LlamaTokenizer:
 class TPComm:
     """Tensor-parallel collectives over a torch.distributed group (RCCL on GPU, gloo on CPU)."""
 
-    def __init__(self, group=None, tp: int = 1):
+    def __init__(self, group=None, tp: int = 1, device=None, custom_ar: Optional[bool] = None):
+        import os
+
         self.group = group
         self.tp = tp
+        self.car = None
+        if custom_ar is None:
+            custom_ar = os.environ.get("MLS_CUSTOM_AR", "0") == "1"
+        if custom_ar and tp > 1 and device is not None and torch.device(device).type == "cuda":
+            from ..parallel.custom_ar import CustomAllReduce
+
+            car = CustomAllReduce(group, device)
+            self.car = car if car.enabled else None
 
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         if self.tp > 1:
+            if self.car is not None and self.car.eligible(t):
+                return self.car.all_reduce_(t)  # one-shot IPC path for small (decode) messages
             dist.all_reduce(t, group=self.group)
         return t
 

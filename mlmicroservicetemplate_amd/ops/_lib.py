@@ -47,6 +47,13 @@ _SIGS = {
     "mls_embed_ln": [P, P, P, P, P, P, P, P, L, I, I, I, F, P],
     "mls_embedding": [P, P, P, L, I, I, I, P],
     "mls_rope": [P, P, P, P, L, I, I, I, P],
+    "mls_ar_create": [I, I, L, P],
+    "mls_ar_handle": [P, P],
+    "mls_ar_handle_size": [],
+    "mls_ar_open": [P, P],
+    "mls_ar_allreduce": [P, P, P, L, _c.c_longlong, P],
+    "mls_ar_error": [P, P],
+    "mls_ar_destroy": [P],
     "mls_rope_kv": [P, P, P, P, L, I, I, I, I, P, P, P, P, I, I, L, I, P],
     "mls_kv_append": [P, I, I, I, P, P, P, L, I, I, P],
     "mls_flash_attention": [P, P, P, P, I, I, I, I, I, I, I, I, I, P, I, F, P],

@@ -1,0 +1,225 @@
+// X2: one-shot all-reduce over HIP IPC for the small, latency-bound
+// tensor-parallel messages of Llama decode (8 KiB per all-reduce at T = 1, 65 of them per token).
+//
+// A ring all-reduce over point-to-point xGMI pays 2(N-1) dependent link hops per call; here every
+// rank reads every peer's buffer directly -- all 7 links at once, one hop -- and sums locally:
+//
+//   1. each block b stages its chunk of the local input into this rank's IPC buffer (half
+//      `parity` = epoch & 1), then publishes `ready[rank][b] = epoch` in every peer's flag array;
+//   2. it waits until every peer has published chunk b of this epoch, reads chunk b from all
+//      ranks' buffers over xGMI, sums in fp32 and writes the output;
+//   3. it publishes `done[rank][b] = epoch` everywhere; before restaging a buffer half (two
+//      epochs later) a block first waits for every peer's `done` of that half's last epoch.
+//
+// The epoch lives on the device, one counter per block, so a captured hipGraph replays correctly
+// (every rank issues the same sequence of calls, hence the same per-block epochs).  Buffers and
+// flags are uncached device memory; flags are system-scope atomics, peer data is read with
+// system-coherent (sc0 sc1) loads.  Every spin-wait is bounded: on timeout the block records an
+// error (read by mls_ar_error) and finishes, so a missing peer can never hang the GPU; the Python
+// side self-tests the path at start-up against RCCL and keeps RCCL if anything is off.
+#include <cstring>
+
+#include "common.h"
+
+namespace {
+
+constexpr int AR_MAX_RANKS = 8;
+constexpr int AR_THREADS = 256;
+constexpr int AR_ELEMS_PER_BLOCK = AR_THREADS * 8;  // 4 KiB of bf16 per block per call
+
+struct ArCtx {
+  int rank, world, max_blocks;
+  size_t cap;                    // bytes per buffer half
+  char* local;                   // this rank's allocation
+  char* peers[AR_MAX_RANKS];     // every rank's allocation mapped here (peers[rank] == local)
+  int* epochs;                   // [max_blocks] device-side per-block epoch (local)
+  int* err;                      // local error word
+  bool opened;
+};
+
+// allocation layout: [2][cap] staging | ready[AR_MAX_RANKS][max_blocks] | done[...] | epochs | err
+__host__ __device__ inline size_t ar_flags_off(size_t cap) { return 2 * cap; }
+
+struct ArArgs {
+  const bf16* in;
+  bf16* out;
+  long n;
+  int rank, world, max_blocks;
+  size_t cap;
+  char* bufs[AR_MAX_RANKS];
+  int* epochs;
+  int* err;
+  long long timeout;  // spin iterations
+};
+
+MLS_DEV int* ar_ready(char* base, size_t cap, int max_blocks, int src, int b) {
+  return reinterpret_cast<int*>(base + ar_flags_off(cap)) + src * max_blocks + b;
+}
+MLS_DEV int* ar_done(char* base, size_t cap, int max_blocks, int src, int b) {
+  return reinterpret_cast<int*>(base + ar_flags_off(cap)) + (AR_MAX_RANKS + src) * max_blocks + b;
+}
+
+MLS_DEV bool ar_wait_ge(int* flag, int want, long long timeout) {
+  for (long long i = 0; i < timeout; ++i) {
+    if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >= want) return true;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return false;
+}
+
+MLS_DEV uint4 load_sys16(const void* p) {  // system-coherent 16-B load (peer memory over xGMI)
+  const rsrc_t r = make_rsrc(p, 16);
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, 0, 0, 17));
+}
+
+__global__ __launch_bounds__(AR_THREADS) void oneshot_allreduce_kernel(const ArArgs a) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  __shared__ int s_epoch, s_ok;
+  if (tid == 0) {
+    s_epoch = a.epochs[b] + 1;
+    s_ok = 1;
+  }
+  __syncthreads();
+  const int e = s_epoch;
+  const int parity = e & 1;
+  const long lo = (long)b * AR_ELEMS_PER_BLOCK;
+  const long i0 = lo + tid * 8;
+  const bool mine = i0 < a.n;  // n % 8 == 0 (host-checked)
+  // (3 of the previous use of this half) every peer finished reading it
+  if (tid < a.world && e > 2) {
+    if (!ar_wait_ge(ar_done(a.bufs[a.rank], a.cap, a.max_blocks, tid, b), e - 2, a.timeout)) s_ok = 0;
+  }
+  __syncthreads();
+  // (1) stage, publish
+  bf16* stage = reinterpret_cast<bf16*>(a.bufs[a.rank] + parity * a.cap);
+  if (mine) st16(stage + i0, ld16(a.in + i0));
+  __threadfence_system();
+  __syncthreads();
+  if (tid < a.world)
+    __hip_atomic_store(ar_ready(a.bufs[tid], a.cap, a.max_blocks, a.rank, b), e, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  // (2) wait for every peer's chunk, reduce
+  if (tid < a.world) {
+    if (!ar_wait_ge(ar_ready(a.bufs[a.rank], a.cap, a.max_blocks, tid, b), e, a.timeout)) s_ok = 0;
+  }
+  __syncthreads();
+  if (mine) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < a.world; ++r) {
+      const int src = (a.rank + r) % a.world;  // stagger the peers each rank hits first
+      float x[8];
+      unpack8(load_sys16(reinterpret_cast<const bf16*>(a.bufs[src] + parity * a.cap) + i0), x);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += x[k];
+    }
+    st16(a.out + i0, pack8(acc));
+  }
+  __syncthreads();
+  // (3) done reading this half
+  if (tid < a.world)
+    __hip_atomic_store(ar_done(a.bufs[tid], a.cap, a.max_blocks, a.rank, b), e, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  if (tid == 0) {
+    a.epochs[b] = e;
+    if (!s_ok) atomicOr(a.err, 1);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// cap: bytes per message (messages above it use RCCL); returns an opaque context
+int mls_ar_create(int rank, int world, long cap, void** ctx_out) {
+  if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world || cap <= 0 || cap % 4096) return MLS_BAD_ARG;
+  ArCtx* c = new ArCtx{};
+  c->rank = rank;
+  c->world = world;
+  c->cap = (size_t)cap;
+  c->max_blocks = (int)((cap / 2 + AR_ELEMS_PER_BLOCK - 1) / AR_ELEMS_PER_BLOCK);
+  const size_t flags = (size_t)2 * AR_MAX_RANKS * c->max_blocks * sizeof(int);
+  const size_t bytes = 2 * c->cap + flags + (size_t)c->max_blocks * sizeof(int) + 64;
+  if (hipExtMallocWithFlags((void**)&c->local, bytes, hipDeviceMallocUncached) != hipSuccess) {
+    delete c;
+    return MLS_UNSUPPORTED;
+  }
+  if (hipMemset(c->local, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    hipFree(c->local);
+    delete c;
+    return MLS_UNSUPPORTED;
+  }
+  c->epochs = reinterpret_cast<int*>(c->local + 2 * c->cap + flags);
+  c->err = c->epochs + c->max_blocks;
+  for (int i = 0; i < AR_MAX_RANKS; ++i) c->peers[i] = nullptr;
+  c->peers[rank] = c->local;
+  *ctx_out = c;
+  return 0;
+}
+
+int mls_ar_handle(void* ctx, void* handle_out /* HIP_IPC_HANDLE_SIZE bytes */) {
+  ArCtx* c = (ArCtx*)ctx;
+  hipIpcMemHandle_t h;
+  if (hipIpcGetMemHandle(&h, c->local) != hipSuccess) return MLS_UNSUPPORTED;
+  memcpy(handle_out, &h, sizeof(h));
+  return 0;
+}
+
+int mls_ar_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
+
+// handles: world * handle_size bytes (this rank's entry is ignored)
+int mls_ar_open(void* ctx, const void* handles) {
+  ArCtx* c = (ArCtx*)ctx;
+  for (int r = 0; r < c->world; ++r) {
+    if (r == c->rank) continue;
+    hipIpcMemHandle_t h;
+    memcpy(&h, (const char*)handles + (size_t)r * sizeof(h), sizeof(h));
+    void* p = nullptr;
+    if (hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) return MLS_UNSUPPORTED;
+    c->peers[r] = (char*)p;
+  }
+  c->opened = true;
+  return 0;
+}
+
+// in/out: n bf16 elements (n % 8 == 0, n * 2 <= cap); in may alias out
+int mls_ar_allreduce(void* ctx, const void* in, void* out, long n, long long timeout, void* stream) {
+  ArCtx* c = (ArCtx*)ctx;
+  if (!c->opened && c->world > 1) return MLS_BAD_ARG;
+  if (n <= 0 || n % 8 || (size_t)n * 2 > c->cap) return MLS_BAD_ARG;
+  ArArgs a{};
+  a.in = (const bf16*)in;
+  a.out = (bf16*)out;
+  a.n = n;
+  a.rank = c->rank;
+  a.world = c->world;
+  a.max_blocks = c->max_blocks;
+  a.cap = c->cap;
+  for (int r = 0; r < AR_MAX_RANKS; ++r) a.bufs[r] = c->peers[r];
+  a.epochs = c->epochs;
+  a.err = c->err;
+  a.timeout = timeout > 0 ? timeout : (1LL << 24);
+  const int blocks = (int)((n + AR_ELEMS_PER_BLOCK - 1) / AR_ELEMS_PER_BLOCK);
+  hipLaunchKernelGGL(oneshot_allreduce_kernel, dim3(blocks), dim3(AR_THREADS), 0, (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}
+
+// error word (1 = a wait timed out since the last reset); resets it
+int mls_ar_error(void* ctx, int* out) {
+  ArCtx* c = (ArCtx*)ctx;
+  if (hipMemcpy(out, c->err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return MLS_UNSUPPORTED;
+  const int zero = 0;
+  return (int)hipMemcpy(c->err, &zero, sizeof(int), hipMemcpyHostToDevice);
+}
+
+int mls_ar_destroy(void* ctx) {
+  ArCtx* c = (ArCtx*)ctx;
+  if (!c) return 0;
+  hipDeviceSynchronize();
+  for (int r = 0; r < c->world; ++r)
+    if (r != c->rank && c->peers[r]) hipIpcCloseMemHandle(c->peers[r]);
+  hipFree(c->local);
+  delete c;
+  return 0;
+}
+
+}  // extern "C"

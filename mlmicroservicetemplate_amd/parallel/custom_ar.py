@@ -1,0 +1,117 @@
+"""One-shot IPC all-reduce for tensor-parallel decode (X2).
+
+The kernel lives in ``ops/csrc/custom_allreduce.hip``: every rank reads every peer's staging
+buffer over xGMI in one hop (all 7 links at once) instead of RCCL's 2(N-1)-step ring, which
+is what an 8 KiB decode message pays for.  This module does the bootstrap -- allocate, export
+the IPC handle, all-gather the handles over the existing process group, open the peers -- and
+a start-up self-test against the group's own all-reduce.  Anything unexpected (IPC
+unavailable, a timeout, a wrong sum) leaves :attr:`CustomAllReduce.enabled` False and callers
+keep RCCL; messages larger than ``cap`` always use RCCL (bandwidth-bound: the ring wins there).
+
+``TPComm`` uses it when ``MLS_CUSTOM_AR=1`` (opt-in until measured on an 8-GPU node).
+"""
+from __future__ import annotations
+
+import ctypes
+import logging
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+logger = logging.getLogger("mlsamd.custom_ar")
+
+
+class CustomAllReduce:
+    def __init__(self, group=None, device=None, cap_bytes: int = 1 << 20, self_test: bool = True,
+                 timeout_iters: int = 1 << 24):
+        from ..ops import _lib
+
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.device = torch.device(device or torch.cuda.current_device())
+        self.cap = int(cap_bytes)
+        self.timeout = int(timeout_iters)
+        self.enabled = False
+        self.reason = ""
+        self._lib = _lib.lib()
+        self._ctx = ctypes.c_void_p()
+        try:
+            self._setup()
+            if self_test:
+                self._self_test()
+            self.enabled = True
+        except Exception as e:  # keep RCCL
+            self.reason = f"{type(e).__name__}: {e}"
+            logger.warning("custom all-reduce disabled: %s", self.reason)
+
+    def _setup(self) -> None:
+        L = self._lib
+        with torch.cuda.device(self.device):
+            rc = L.mls_ar_create(self.rank, self.world, self.cap, ctypes.byref(self._ctx))
+            if rc != 0:
+                raise RuntimeError(f"mls_ar_create failed ({rc})")
+            hs = L.mls_ar_handle_size()
+            mine = (ctypes.c_char * hs)()
+            if L.mls_ar_handle(self._ctx, ctypes.cast(mine, ctypes.c_void_p)) != 0:
+                raise RuntimeError("hipIpcGetMemHandle failed")
+            handles = [None] * self.world
+            dist.all_gather_object(handles, bytes(mine), group=self.group)
+            blob = (ctypes.c_char * (hs * self.world)).from_buffer_copy(b"".join(handles))
+            if L.mls_ar_open(self._ctx, ctypes.cast(blob, ctypes.c_void_p)) != 0:
+                raise RuntimeError("hipIpcOpenMemHandle failed")
+
+    def _errors(self) -> int:
+        out = ctypes.c_int(0)
+        self._lib.mls_ar_error(self._ctx, ctypes.byref(out))
+        return out.value
+
+    def _self_test(self) -> None:
+        g = torch.Generator().manual_seed(1234 + self.rank)
+        ok = True
+        for n in (8, 4096, 4096 * 3 + 8, self.cap // 2):
+            x = torch.randn(n, generator=g).to(torch.bfloat16)
+            ref = x.float().clone()
+            if dist.get_backend(self.group) == "nccl":
+                ref = ref.to(self.device)
+            dist.all_reduce(ref, group=self.group)  # the group's own backend (RCCL, or gloo on CPU)
+            ref = ref.cpu()
+            y = self._run(x.to(self.device))
+            torch.cuda.synchronize(self.device)
+            err = (y.float().cpu() - ref).abs().max().item() / (ref.abs().max().item() + 1e-6)
+            ok = ok and err < 2e-2
+        if self._errors():
+            raise RuntimeError("a peer wait timed out during the self-test")
+        # every rank must agree before anyone uses the path
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+        if dist.get_backend(self.group) == "nccl":
+            flag = flag.to(self.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+        if not int(flag.item()):
+            raise RuntimeError("self-test mismatch against the group all-reduce")
+
+    def _run(self, t: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        out = t if out is None else out
+        rc = self._lib.mls_ar_allreduce(self._ctx, t.data_ptr(), out.data_ptr(), t.numel(), self.timeout,
+                                        torch.cuda.current_stream(self.device).cuda_stream)
+        if rc != 0:
+            raise RuntimeError(f"mls_ar_allreduce failed ({rc})")
+        return out
+
+    def eligible(self, t: torch.Tensor) -> bool:
+        return (self.enabled and t.dtype == torch.bfloat16 and t.is_contiguous() and t.device == self.device
+                and t.numel() % 8 == 0 and t.numel() * 2 <= self.cap)
+
+    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+        """In-place sum across the group (one-shot path when eligible, else the group's backend)."""
+        if self.eligible(t):
+            return self._run(t)
+        dist.all_reduce(t, group=self.group)
+        return t
+
+    def close(self) -> None:
+        if self._ctx:
+            self._lib.mls_ar_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+            self.enabled = False

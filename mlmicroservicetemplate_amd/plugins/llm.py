@@ -56,7 +56,7 @@ class LlamaPlugin(ModelPlugin):
         # every TP rank reads just its own slices from the checkpoint (no weight broadcast needed)
         source = llama.CheckpointSource(s.WEIGHTS, device=dev) if s.WEIGHTS else None
         params = llama.init_llama_shard(cfg, tp, ctx.rank, int(s.SEED), device=dev, source=source)
-        self.model = llama.LlamaTP(params, cfg, tp=tp, rank=ctx.rank, comm=llama.TPComm(None, tp), backend=backend,
+        self.model = llama.LlamaTP(params, cfg, tp=tp, rank=ctx.rank, comm=llama.TPComm(None, tp, device=dev), backend=backend,
                                    device=dev, max_batch=int(s.MAX_BATCH), max_seq=int(extra.get("max_seq", 2048)))
         self.tok = llama.LlamaTokenizer(cfg, extra.get("tokenizer_file"))
         self.cfg = cfg

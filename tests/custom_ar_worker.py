@@ -1,0 +1,55 @@
+"""Child process for test_custom_ar_gpu.py: rank r of a gloo group whose ranks all drive cuda:0
+(one GPU box); exercises the IPC one-shot all-reduce eagerly and inside a captured hipGraph."""
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+
+def main():
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mlmicroservicetemplate_amd.parallel.custom_ar import CustomAllReduce
+
+    dev = torch.device("cuda:0")
+    car = CustomAllReduce(None, dev, cap_bytes=1 << 20)
+    assert car.enabled, car.reason
+    g = torch.Generator().manual_seed(rank)
+    fails = 0
+    for n in (8, 4096, 4104, 65536, 300000):
+        x = torch.randn(n, generator=g).to(torch.bfloat16)
+        ref = x.float().clone()
+        dist.all_reduce(ref)
+        y = car.all_reduce_(x.to(dev))
+        torch.cuda.synchronize()
+        err = (y.float().cpu() - ref).abs().max().item() / ref.abs().max().item()
+        fails += err > 2e-2
+    # captured in a graph: three all-reduces per replay, replayed twice (device-side epochs)
+    bufs = [torch.zeros(4096, device=dev, dtype=torch.bfloat16) for _ in range(3)]
+    s = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s):
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=s):
+            for b in bufs:
+                car.all_reduce_(b)
+    for it in range(2):
+        vals = [torch.full((4096,), float(rank + 1 + i + it), dtype=torch.bfloat16) for i in range(3)]
+        for b, v in zip(bufs, vals):
+            b.copy_(v.to(dev))
+        torch.cuda.synchronize()
+        dist.barrier()
+        graph.replay()
+        torch.cuda.synchronize()
+        for i, b in enumerate(bufs):
+            want = sum(r + 1 + i + it for r in range(world))
+            fails += int(not torch.all(b.float() == want).item())
+    fails += car._errors()
+    car.close()
+    dist.destroy_process_group()
+    print(f"rank {rank} fails {fails}")
+    sys.exit(1 if fails else 0)
+
+
+if __name__ == "__main__":
+    main()
