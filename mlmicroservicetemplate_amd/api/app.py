@@ -293,11 +293,16 @@ def create_app(settings: Optional[Settings] = None, plugin: Optional[ModelPlugin
                 part = Part(name=plugin.form_field, data=data, content_type="text/plain")
             elif isinstance(payload, dict) and filename is None:
                 filename = payload.get("filename")
-        elif filename is None and ctype.lower().startswith("application/x-www-form-urlencoded"):
+        elif ctype.lower().startswith("application/x-www-form-urlencoded"):
             form = await request.body()
             from urllib.parse import parse_qs
 
-            filename = (parse_qs(form.decode("latin-1")).get("filename") or [None])[0]
+            q = parse_qs(form.decode("utf-8", errors="replace"), keep_blank_values=True)
+            if q.get(plugin.form_field):  # e.g. text=... for the text classifier
+                part = Part(name=plugin.form_field, data=q[plugin.form_field][0].encode("utf-8"),
+                            content_type="text/plain")
+            elif filename is None:
+                filename = (q.get("filename") or [None])[0]
         if part is None and filename is not None:
             # legacy shared-volume flow: validate readiness first, then the file
             if not state.ready_to_predict:

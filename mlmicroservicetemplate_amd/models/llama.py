@@ -542,6 +542,9 @@ class LlamaTP:
         B, S = ids.shape
         if B > self.max_batch or S + gp.max_new_tokens > self.max_seq:
             raise ValueError("batch / sequence exceed the KV cache")
+        lens_host = lens.detach().to("cpu")
+        if lens_host.numel() != B or int(lens_host.min()) < 1 or int(lens_host.max()) > S:
+            raise ValueError(f"lens must be in [1, {S}] for each of the {B} sequences")
         dev = self.device
         ids = ids.to(dev)
         lens = lens.to(dev).to(torch.int32)

@@ -46,8 +46,53 @@ def _time(fn, iters: int = 20, warmup: int = 3) -> float:
     return start.elapsed_time(end) / iters
 
 
+def _time_multi(fns, iters: int = 20, warmup: int = 3) -> float:
+    """ms per call when ``len(fns)`` independent copies of a layer co-run on their own streams
+    (each captured in its own hipGraph): the per-call cost under the engine's concurrent slots,
+    where a throughput-efficient tile beats a latency-optimal one."""
+    if len(fns) == 1:
+        return _time(fns[0], iters, warmup)
+    main = torch.cuda.current_stream()
+    streams = [torch.cuda.Stream() for _ in fns]
+    graphs = []
+    for fn, st in zip(fns, streams):
+        st.wait_stream(main)
+        with torch.cuda.stream(st):
+            for _ in range(warmup):
+                fn()
+    torch.cuda.synchronize()
+    for fn, st in zip(fns, streams):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=st):
+            for _ in range(iters):
+                fn()
+        graphs.append(g)
+    torch.cuda.synchronize()
+
+    def replay_all():
+        for g, st in zip(graphs, streams):
+            st.wait_stream(main)
+            with torch.cuda.stream(st):
+                g.replay()
+        for st in streams:
+            main.wait_stream(st)
+
+    replay_all()  # warm
+    torch.cuda.synchronize()
+    start = torch.cuda.Event(enable_timing=True)
+    end = torch.cuda.Event(enable_timing=True)
+    start.record(main)
+    replay_all()
+    end.record(main)
+    end.synchronize()
+    del graphs
+    return start.elapsed_time(end) / (iters * len(fns))
+
+
 def tune_resnet50(batch: int, device="cuda:0", iters: int = 20, compare_torch: bool = True,
-                  candidates: Optional[List[Tuple[int, int]]] = None) -> Dict[str, dict]:
+                  candidates: Optional[List[Tuple[int, int]]] = None, concurrency: int = 1) -> Dict[str, dict]:
+    """Per-layer (cfg, splitk) search.  ``concurrency`` > 1 scores each candidate by its
+    per-batch cost with that many batches co-running (the serving engine's concurrent slots)."""
     from . import conv2d_nhwc, gemm, pack_conv_weight
     from ..models.resnet import conv_shapes
 
@@ -64,6 +109,9 @@ def tune_resnet50(batch: int, device="cuda:0", iters: int = 20, compare_torch: b
         bias = torch.randn(s.cout, device=dev)
         res = torch.randn(batch, ho, ho, s.cout, device=dev).to(torch.bfloat16) if s.name.endswith("conv3") else None
         out = torch.empty(batch, ho, ho, s.cout, device=dev, dtype=torch.bfloat16)
+        # per-stream copies for concurrent scoring (inputs shared read-only; outputs/scratch not)
+        outs = [out] + [torch.empty_like(out) for _ in range(concurrency - 1)]
+        wss = [ws] + [torch.empty_like(ws) for _ in range(concurrency - 1)]
         k = s.k * 32 if s.name == "stem" else s.k * s.k * s.cin
         flops = 2.0 * batch * ho * ho * s.cout * s.cin * s.k * s.k
         best = (1e9, 0, 0)
@@ -72,17 +120,21 @@ def tune_resnet50(batch: int, device="cuda:0", iters: int = 20, compare_torch: b
             if sk > 1 and k // sk < 128:
                 continue
 
-            def run(cfg=cfg, sk=sk):
-                conv2d_nhwc(x, wp, bias, kernel=s.k, stride=s.stride, pad=0 if s.name == "stem" else s.pad,
-                            residual=res, act=1, out=out,
-                            workspace=ws, cfg=cfg, splitk=sk)
+            def mk(o, wsc, cfg=cfg, sk=sk):
+                def run():
+                    conv2d_nhwc(x, wp, bias, kernel=s.k, stride=s.stride, pad=0 if s.name == "stem" else s.pad,
+                                residual=res, act=1, out=o, workspace=wsc, cfg=cfg, splitk=sk)
+                return run
 
-            t = _time(run, iters)
+            try:
+                t = _time_multi([mk(o, wsc) for o, wsc in zip(outs, wss)], iters)
+            except Exception:  # e.g. split-K slabs beyond a per-stream scratch: not a candidate
+                continue
             tried[f"{cfg},{sk}"] = round(t * 1e3, 2)
             if (cfg, sk) != (0, 0) and t < best[0]:
                 best = (t, cfg, sk)
         entry = {"M": batch * ho * ho, "N": s.cout, "K": k, "best_cfg": best[1], "best_splitk": best[2],
-                 "best_us": round(best[0] * 1e3, 2), "heuristic_us": tried["0,0"],
+                 "best_us": round(best[0] * 1e3, 2), "heuristic_us": tried.get("0,0"),
                  "tflops": round(flops / (best[0] * 1e-3) / 1e12, 1)}
         if compare_torch:
             xt = x[:, 3:-3, 3:-3, :3] if s.name == "stem" else x
@@ -123,7 +175,13 @@ SHIPPED_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned")
 
 
 def load_tuning(model: str, batch: int, arch: str = "gfx950") -> Dict[str, Tuple[int, int]]:
-    """Shipped (measured on MI355X, committed) or cached tuning table; {} -> C++ heuristic."""
+    """Shipped (measured on MI355X, committed) or cached tuning table; {} -> C++ heuristic.
+    ``MLS_TUNING_FILE`` overrides both (A/B runs of alternative tables)."""
+    override = os.environ.get("MLS_TUNING_FILE")
+    if override:
+        with open(override) as f:
+            data = json.load(f)
+        return {k: (v["best_cfg"], v["best_splitk"]) for k, v in data.items()}
     for d in (SHIPPED_DIR, CACHE_DIR):
         path = os.path.join(d, f"{model}_{arch}_b{batch}.json")
         if os.path.exists(path):
@@ -152,11 +210,13 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--out", default="")
+    ap.add_argument("--concurrency", type=int, default=1)
+    ap.add_argument("--no-torch", action="store_true")
     args = ap.parse_args()
     t0 = time.time()
-    res = tune_resnet50(args.batch)
+    res = tune_resnet50(args.batch, compare_torch=not args.no_torch, concurrency=args.concurrency)
     tot_best = sum(v["best_us"] for v in res.values())
-    tot_heur = sum(v.get("heuristic_us", v["best_us"]) for v in res.values())
+    tot_heur = sum(v.get("heuristic_us") or v["best_us"] for v in res.values())
     tot_torch = sum(v.get("torch_us", 0) for v in res.values())
     for name, v in res.items():
         print(json.dumps({"layer": name, **v}))

@@ -126,6 +126,73 @@ __global__ __launch_bounds__(256) void softmax_topk_wave_kernel(const Tin* __res
   }
 }
 
+// Register-resident variant for bf16 rows with N % 8 == 0, N <= 512 * CPL (the ResNet / BERT
+// classifier heads): a wave owns a row, every lane issues all its 16-B loads up front (one memory
+// round trip, where the strided scalar loop above paid one per element group), and the k selection
+// rounds scan registers + wave shuffles -- no LDS at all.
+template <int CPL>
+__global__ __launch_bounds__(256) void softmax_topk_reg_kernel(const bf16* __restrict__ x, float* __restrict__ vals,
+                                                               int* __restrict__ idx, int rows, int N, int k,
+                                                               int apply_softmax, float temperature) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const long r = (long)blockIdx.x * 4 + wid;
+  if (r >= rows) return;
+  const int nch = N >> 3;
+  const bf16* src = x + r * (long)N;
+  const float invt = 1.f / temperature;
+  float v[CPL][8];
+  uint4 raw[CPL];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int ch = lane + 64 * c;
+    raw[c] = ch < nch ? ld16(src + ch * 8) : make_uint4(0, 0, 0, 0);
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const bool ok = lane + 64 * c < nch;
+    unpack8(raw[c], v[c]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      v[c][e] = ok ? v[c][e] * invt : -INFINITY;
+      mx = fmaxf(mx, v[c][e]);
+    }
+  }
+  float denom = 1.f;
+  if (apply_softmax) {
+    mx = wave_max(mx);
+    float sum = 0.f;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sum += v[c][e] == -INFINITY ? 0.f : __expf(v[c][e] - mx);
+    denom = wave_sum(sum);
+  }
+  for (int j = 0; j < k; ++j) {
+    KV best{-INFINITY, -1};
+#pragma unroll
+    for (int c = 0; c < CPL; ++c)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int i = (lane + 64 * c) * 8 + e;
+        if (lane + 64 * c < nch) best = better(best, KV{v[c][e], i});
+      }
+    best = wave_argmax(best);
+    if (lane == 0) {
+      vals[r * k + j] = apply_softmax ? __expf(best.v - mx) / denom : best.v;
+      idx[r * k + j] = best.i;
+    }
+    if (best.i >= 0 && ((best.i >> 3) & 63) == lane) {  // owner lane retires the winner
+      const int c = (best.i >> 3) >> 6, e = best.i & 7;
+#pragma unroll
+      for (int cc = 0; cc < CPL; ++cc)
+#pragma unroll
+        for (int ee = 0; ee < 8; ++ee)
+          if (cc == c && ee == e) v[cc][ee] = -INFINITY;
+    }
+  }
+}
+
 // y = softmax(x * scale + mask) row-wise, bf16 in/out; mask (fp32, additive) is indexed
 // [row / rows_per_mask][N] (e.g. one padding mask per sequence shared by all heads/queries).
 __global__ __launch_bounds__(256) void softmax_rows_kernel(const bf16* __restrict__ x, bf16* __restrict__ y,
@@ -163,6 +230,19 @@ extern "C" {
 int mls_softmax_topk(const void* x, int dtype, float* vals, int* idx, int rows, int N, int k, int apply_softmax,
                      float temperature, void* stream) {
   if (rows <= 0 || N <= 0 || k <= 0 || k > N || N > 32768 || temperature <= 0.f) return MLS_BAD_ARG;
+  if (dtype == 0 && N % 8 == 0 && N <= 2048 && k <= 64) {
+    dim3 g((rows + 3) / 4);
+    if (N <= 512)
+      hipLaunchKernelGGL(softmax_topk_reg_kernel<1>, g, dim3(256), 0, (hipStream_t)stream, (const bf16*)x, vals, idx,
+                         rows, N, k, apply_softmax, temperature);
+    else if (N <= 1024)
+      hipLaunchKernelGGL(softmax_topk_reg_kernel<2>, g, dim3(256), 0, (hipStream_t)stream, (const bf16*)x, vals, idx,
+                         rows, N, k, apply_softmax, temperature);
+    else
+      hipLaunchKernelGGL(softmax_topk_reg_kernel<4>, g, dim3(256), 0, (hipStream_t)stream, (const bf16*)x, vals, idx,
+                         rows, N, k, apply_softmax, temperature);
+    return (int)hipGetLastError();
+  }
   if (N <= 4096) {
     const size_t lds4 = (size_t)4 * N * sizeof(float);
     dim3 g((rows + 3) / 4);

@@ -210,3 +210,17 @@ def test_module_plugin_reference_contract(tmp_path, monkeypatch):
         assert wait_ready(c)
         r = c.post("/predict", **upload(b"12345", filename="f.bin"))
         assert r.json() == {"status": "success", "result": {"n": 5, "name": "f.bin"}}
+
+
+def test_urlencoded_text_field():
+    """A url-encoded form carrying the plugin's field is a prediction input (text plugins)."""
+    import zlib
+
+    app = create_app(settings(), IdentityPlugin())
+    with TestClient(app, raise_server_exceptions=False) as c:
+        assert wait_ready(c)
+        r = c.post("/predict", content=b"image_file=hello+world&x=1",
+                   headers={"content-type": "application/x-www-form-urlencoded"})
+        assert r.status_code == 200, r.text
+        assert r.json()["result"]["result"]["crc32"] == zlib.crc32(b"hello world") & 0xFFFFFFFF
+

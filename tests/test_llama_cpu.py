@@ -88,3 +88,12 @@ def test_tp_matches_tp1(world, kv):
     for _rank, g, s in res:
         assert torch.equal(g, ref_g), (g, ref_g)
         assert torch.equal(s, ref_s)
+
+
+def test_generate_rejects_bad_lengths():
+    cfg = tiny_config(**CFG)
+    m = LlamaTP(init_llama_shard(cfg, 1, 0, seed=1), cfg, max_batch=4, max_seq=64)
+    ids = torch.randint(3, 2000, (2, 10))
+    for lens in ([11, 3], [0, 3], [5]):
+        with pytest.raises(ValueError):
+            m.generate(ids, torch.tensor(lens), GenParams(max_new_tokens=2))

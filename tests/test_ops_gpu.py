@@ -187,3 +187,21 @@ def test_resnet50_fused_matches_reference():
     assert rel_err(logits, ref) < 5e-2
     vals, idx = model.classify(imgs, 5)
     assert (idx[:, 0].long() == ref.argmax(-1)).float().mean().item() >= 0.75
+
+
+@pytest.mark.parametrize("rows,N,k", [(32, 1000, 5), (5, 8, 3), (7, 512, 50), (3, 2048, 10), (9, 1032, 1)])
+@pytest.mark.parametrize("softmax", [True, False])
+def test_softmax_topk_register_path(rows, N, k, softmax):
+    """The register-resident bf16 head kernel (N % 8 == 0, N <= 2048) vs torch.topk."""
+    from mlmicroservicetemplate_amd import ops
+
+    torch.manual_seed(N + k)
+    logits = (torch.randn(rows, N, device=DEV) * 3).to(torch.bfloat16)
+    vals, idx = ops.softmax_topk(logits, k, softmax=softmax)
+    ref = torch.softmax(logits.float(), -1) if softmax else logits.float()
+    rv, _ri = torch.topk(ref, k, dim=-1)
+    assert torch.allclose(vals, rv, rtol=1e-3, atol=1e-6)
+    assert torch.allclose(ref.gather(1, idx.long()), rv, rtol=1e-3, atol=1e-6)
+    assert (idx >= 0).all() and (idx < N).all()
+    for r in range(rows):  # no index repeats
+        assert len(set(idx[r].tolist())) == k
