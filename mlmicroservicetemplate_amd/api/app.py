@@ -35,7 +35,7 @@ from starlette.responses import JSONResponse, Response
 
 from .. import discovery
 from ..config import Settings, load_dotenv
-from ..plugins.base import ModelPlugin, PluginContext, load_plugin
+from ..plugins.base import ModelPlugin, PluginContext, default_devices, load_plugin
 from ..scheduler.batcher import BatcherClosed, DynamicBatcher, QueueFull, ReplicaRouter
 from ..scheduler.watchdog import ReplicaWatchdog
 from ..utils.metrics import CONTENT_TYPE_LATEST, Metrics, gpu_memory_collector
@@ -58,7 +58,7 @@ class ServingRuntime:
         self.plugin = plugin
         self.state = state
         self.metrics = metrics
-        self.ctx = ctx or PluginContext(settings=settings)
+        self.ctx = ctx or PluginContext(settings=settings, devices=default_devices(settings))
         self.router: Optional[ReplicaRouter] = None
         self.watchdog: Optional[ReplicaWatchdog] = None
         self.loop: Optional[asyncio.AbstractEventLoop] = None

@@ -40,6 +40,23 @@ class PluginContext:
     extra: Dict[str, Any] = field(default_factory=dict)
 
 
+def default_devices(settings, world_size: int = 1, local_rank: int = 0) -> List[str]:
+    """The devices a process drives: its own GPU when it is one rank of several, else the first
+    ``GPUS`` GPUs; none for CPU models (stub / identity / user modules) or ``GPUS=0``."""
+    try:
+        import torch
+
+        ngpu = torch.cuda.device_count()
+    except Exception:
+        ngpu = 0
+    model = str(getattr(settings, "MODEL", ""))
+    if not ngpu or int(getattr(settings, "GPUS", 1)) <= 0 or model in ("stub", "identity") or "." in model:
+        return []
+    if world_size > 1:
+        return [f"cuda:{local_rank}"]
+    return [f"cuda:{i}" for i in range(min(int(settings.GPUS), ngpu))]
+
+
 class ModelPlugin:
     name: str = "plugin"
     batched: bool = False

@@ -69,25 +69,15 @@ def run_rank(args) -> int:
 
     from .api.app import create_app
     from .parallel import dist as mdist
-    from .plugins.base import PluginContext, load_plugin
+    from .plugins.base import default_devices, PluginContext, load_plugin
 
     load_dotenv(args.env_file)
     settings = Settings.load(env_file=args.env_file, overrides=_overrides_from_args(args))
     logging.basicConfig(level=getattr(logging, settings.LOG_LEVEL.upper(), logging.INFO),
                         format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     info = mdist.env_info()
-    devices: List[str] = []
-    try:
-        import torch
-
-        ngpu = torch.cuda.device_count()
-    except Exception:
-        ngpu = 0
-    if ngpu and settings.MODEL not in ("stub", "identity") and "." not in settings.MODEL:
-        if info.world_size > 1:
-            devices = [f"cuda:{info.local_rank}"]
-        else:
-            devices = [f"cuda:{i}" for i in range(max(1, min(settings.GPUS, ngpu)))]
+    devices = default_devices(settings, info.world_size, info.local_rank)
+    ngpu = len(devices)
     if info.world_size > 1:
         mdist.init_distributed(device_id=info.local_rank if ngpu else None)
     ctx = PluginContext(settings=settings, rank=info.rank, world_size=info.world_size, local_rank=info.local_rank,
