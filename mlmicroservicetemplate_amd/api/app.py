@@ -253,6 +253,9 @@ def create_app(settings: Optional[Settings] = None, plugin: Optional[ModelPlugin
             "model": plugin.name,
             "replicas": runtime.router.stats() if runtime.router else [],
             "watchdog_events": runtime.watchdog.events[-20:] if runtime.watchdog else [],
+            "pid": os.getpid(),
+            "worker": int(os.environ.get("MLS_WORKER_INDEX", "0")),
+            "devices": list(runtime.ctx.devices),
         }
 
     @app.get("/info")

@@ -155,6 +155,7 @@ class Settings:
     TOPK: int = 5
     # --- GPU execution ---
     GPUS: int = 1
+    WORKERS_PER_GPU: int = 1  # HTTP worker processes per GPU (DP models): front-end CPU scales, each owns an engine
     TP: int = 1
     MAX_BATCH: int = 32
     MAX_WAIT_US: int = 2000

@@ -52,6 +52,10 @@ def default_devices(settings, world_size: int = 1, local_rank: int = 0) -> List[
     model = str(getattr(settings, "MODEL", ""))
     if not ngpu or int(getattr(settings, "GPUS", 1)) <= 0 or model in ("stub", "identity") or "." in model:
         return []
+    import os
+
+    if os.environ.get("MLS_DEVICE"):  # a launcher-assigned GPU (several workers per GPU)
+        return [f"cuda:{int(os.environ['MLS_DEVICE'])}"]
     if world_size > 1:
         return [f"cuda:{local_rank}"]
     return [f"cuda:{i}" for i in range(min(int(settings.GPUS), ngpu))]

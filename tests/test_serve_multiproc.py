@@ -59,3 +59,37 @@ def test_two_rank_identity_service():
             proc.wait(30)
         except subprocess.TimeoutExpired:
             os.killpg(proc.pid, signal.SIGKILL)
+
+
+@pytest.mark.timeout(120)
+def test_workers_per_gpu_share_the_port():
+    """WORKERS_PER_GPU: independent serving processes on one port (front-end CPU scaling)."""
+    port = _port()
+    env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    proc = subprocess.Popen([sys.executable, "-m", "mlmicroservicetemplate_amd", "serve", "--model", "identity",
+                             "--workers-per-gpu", "3", "--port", str(port), "--host", "127.0.0.1", "--no-register",
+                             "--env-file", "/nonexistent"], cwd=ROOT, env=env, start_new_session=True)
+    try:
+        url = f"http://127.0.0.1:{port}"
+        deadline = time.time() + 90
+        pids, workers = set(), set()
+        while time.time() < deadline and len(workers) < 3:
+            try:
+                if requests.get(url + "/status", timeout=1).status_code != 200:
+                    time.sleep(0.1)
+                    continue
+                h = requests.get(url + "/health", timeout=2).json()
+                pids.add(h["pid"])
+                workers.add(h["worker"])
+                body, ct = encode_multipart({"image_file": ("x", b"abc", "application/octet-stream")})
+                r = requests.post(url + "/predict", data=body, headers={"content-type": ct}, timeout=5)
+                assert r.status_code == 200
+            except requests.RequestException:
+                time.sleep(0.1)
+        assert workers == {0, 1, 2} and len(pids) == 3, (workers, pids)
+    finally:
+        os.killpg(proc.pid, signal.SIGTERM)
+        try:
+            proc.wait(30)
+        except subprocess.TimeoutExpired:
+            os.killpg(proc.pid, signal.SIGKILL)

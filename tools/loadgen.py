@@ -94,6 +94,11 @@ async def run(url: str, duration: float, concurrency: int, rate: float, payloads
     return lat, errors, codes
 
 
+def _client_proc(url, duration, concurrency, rate, jpeg, warmup, seed):
+    payloads = [make_payload(jpeg, 8 * seed + s) for s in range(8)]
+    return asyncio.run(run(url, duration, concurrency, rate, payloads, warmup))
+
+
 def wait_ready(base: str, timeout: float = 600) -> bool:
     import requests
 
@@ -120,6 +125,7 @@ def main(argv=None) -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--max-batch", type=int, default=32)
     ap.add_argument("--extra", default="", help="extra args for the spawned server")
+    ap.add_argument("--procs", type=int, default=1, help="client processes (one asyncio loop each)")
     args = ap.parse_args(argv)
     proc = None
     if args.spawn:
@@ -134,9 +140,23 @@ def main(argv=None) -> int:
             print(json.dumps({"error": "server did not become ready"}))
             return 1
     try:
-        payloads = [make_payload(args.jpeg, s) for s in range(8)]
-        lat, errors, codes = asyncio.run(run(args.url + "/predict", args.duration, args.concurrency, args.rate,
-                                             payloads, args.warmup))
+        if args.procs > 1:
+            import multiprocessing as mp
+
+            with mp.get_context("spawn").Pool(args.procs) as pool:
+                parts = pool.starmap(_client_proc, [(args.url + "/predict", args.duration,
+                                                     max(1, args.concurrency // args.procs), args.rate / args.procs,
+                                                     args.jpeg, args.warmup, i) for i in range(args.procs)])
+            lat = [x for p in parts for x in p[0]]
+            errors = sum(p[1] for p in parts)
+            codes = {}
+            for p in parts:
+                for k, v in p[2].items():
+                    codes[k] = codes.get(k, 0) + v
+        else:
+            payloads = [make_payload(args.jpeg, s) for s in range(8)]
+            lat, errors, codes = asyncio.run(run(args.url + "/predict", args.duration, args.concurrency, args.rate,
+                                                 payloads, args.warmup))
     finally:
         if proc is not None:
             os.killpg(proc.pid, signal.SIGTERM)
@@ -148,7 +168,8 @@ def main(argv=None) -> int:
     out = {
         "metric": "http requests/sec + latency", "model": args.spawn or "external", "url": args.url,
         "mode": "open" if args.rate > 0 else "closed", "concurrency": args.concurrency, "rate": args.rate,
-        "payload": "jpeg" if args.jpeg else "raw-rgb8", "gpus": args.gpus,
+        "payload": "jpeg" if args.jpeg else "raw-rgb8", "gpus": args.gpus, "client_procs": args.procs,
+        "server_extra": args.extra,
         "requests_per_s": round(len(lat) / args.duration, 1), "p50_ms": round(float(np.percentile(lat_ms, 50)), 3),
         "p90_ms": round(float(np.percentile(lat_ms, 90)), 3), "p99_ms": round(float(np.percentile(lat_ms, 99)), 3),
         "ok": len(lat), "errors": errors, "status_codes": {str(k): v for k, v in codes.items()},
