@@ -264,23 +264,41 @@ class TPComm:
 
             car = CustomAllReduce(group, device)
             self.car = car if car.enabled else None
+        # gloo with device tensors (TP rehearsal: several ranks sharing one GPU, where RCCL refuses
+        # duplicate devices): stage the collectives through host memory
+        self.host_staged = tp > 1 and dist.is_initialized() and dist.get_backend(group) == "gloo"
 
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         if self.tp > 1:
             if self.car is not None and self.car.eligible(t):
                 return self.car.all_reduce_(t)  # one-shot IPC path for small (decode) messages
+            if self.host_staged and t.is_cuda:
+                h = t.float().cpu()
+                dist.all_reduce(h, group=self.group)
+                t.copy_(h)
+                return t
             dist.all_reduce(t, group=self.group)
         return t
 
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
         if self.tp == 1:
             return t.unsqueeze(0)
+        if self.host_staged and t.is_cuda:
+            h = t.contiguous().cpu()
+            out = [torch.empty_like(h) for _ in range(self.tp)]
+            dist.all_gather(out, h, group=self.group)
+            return torch.stack(out).to(t.device)
         out = [torch.empty_like(t) for _ in range(self.tp)]
         dist.all_gather(out, t.contiguous(), group=self.group)
         return torch.stack(out)
 
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if self.tp > 1:
+            if self.host_staged and t.is_cuda:
+                h = t.cpu()
+                dist.broadcast(h, src=src, group=self.group)
+                t.copy_(h)
+                return t
             dist.broadcast(t, src=src, group=self.group)
         return t
 
@@ -335,7 +353,7 @@ class LlamaTP:
         import os
 
         self.use_graphs = backend == "fused" and self.device.type == "cuda" and (
-            tp == 1 or os.environ.get("MLS_TP_GRAPHS", "0") == "1")
+            tp == 1 or (os.environ.get("MLS_TP_GRAPHS", "0") == "1" and not getattr(self.comm, "host_staged", False)))
         self._graphs: Dict[Tuple[int, int, int], tuple] = {}
         self._dec_ctx: Optional[int] = None  # host bound on decode context (sizes the split grid)
 

@@ -1,0 +1,32 @@
+"""Child process for test_llama_tp_gpu.py: one TP rank of the fused (native-kernel) Llama; all
+ranks share cuda:0 and talk over gloo (host-staged collectives)."""
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+
+def main():
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mlmicroservicetemplate_amd.models.llama import GenParams, LlamaTP, TPComm, init_llama_shard, tiny_config
+
+    cfg = tiny_config(layers=2, hidden=512, heads=8, kv_heads=2, head_dim=128, intermediate=1024)
+    p = init_llama_shard(cfg, world, rank, seed=3, device="cuda")
+    m = LlamaTP(p, cfg, tp=world, rank=rank, comm=TPComm(None, world, device="cuda"), backend="fused",
+                device="cuda", max_batch=4, max_seq=256)
+    g = torch.Generator().manual_seed(7)
+    ids = torch.randint(3, cfg.vocab - 1, (3, 24), generator=g)
+    lens = torch.tensor([24, 11, 3])
+    pos = torch.arange(24, dtype=torch.int32).unsqueeze(0).expand(3, 24).contiguous().cuda()
+    vals, idx = m.step(ids.cuda(), pos, lens.cuda(), decode=False, k=8)
+    allv = m.comm.all_gather(vals)
+    alli = m.comm.all_gather(idx)
+    out = m.generate(ids, lens, GenParams(max_new_tokens=8))
+    torch.save({"tokens": out.cpu(), "vals": allv.cpu(), "idx": alli.cpu()}, os.environ["OUT"] + f".{rank}.pt")
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    sys.exit(main())
