@@ -199,6 +199,121 @@ __global__ __launch_bounds__(NWV * 64) void skinny_gemm_kernel(const SkArgs s) {
   }
 }
 
+// Few-row variant (M <= 4, whole K per block): the activation rows -- with the fused prologue,
+// a + a2 rounded to the bf16 residual stream -- are staged ONCE per block into LDS (M*K*2 bytes,
+// dynamic) together with their square sums, so the k loop is the plain weight stream with the
+// A fragments read from LDS; the block's first weight loads are issued before that prologue and
+// every later trip's loads are in flight while the previous trip's MFMAs run (register double
+// buffer).  Measured motivation: the register-path fused kernel streamed gate_up ~20 % slower
+// than the plain one (profiles/r1_decode_cold_weight_stream_probe.jsonl).
+template <int UNROLL, int NWV, int FUSE, int NT>
+__global__ __launch_bounds__(NWV * 64) void skinny_lds_kernel(const SkArgs s) {
+  extern __shared__ __attribute__((aligned(16))) uint4 a_lds[];  // [M][K/8]
+  __shared__ float red[NWV][16][NT * 16 + 1];
+  __shared__ float ssq_s[4];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nr = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.x * 16 * NT;
+  const int ksteps = s.K >> 5;
+  const int kch = s.K >> 3;  // 16-B chunks per row
+  const rsrc_t wr = make_rsrc(s.w, s.w_bytes);
+  int wbase[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) wbase[j] = ((n0 + 16 * j + nr) * s.K + 8 * g) * 2;
+
+  auto load_trip = [&](int ks0, uint4 (&wv)[UNROLL][NT]) {
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int ks = ks0 + NWV * u;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) wv[u][j] = bload16(wr, ks < ksteps ? wbase[j] + ks * 64 : OOB);
+    }
+  };
+  uint4 wnext[UNROLL][NT];
+  int ks = wid;
+  load_trip(ks, wnext);  // in flight during the prologue
+
+  // prologue: A (+ A2) -> LDS, residual write-back (column-tile-0 blocks), square sums
+  if (tid < 4) ssq_s[tid] = 0.f;
+  __syncthreads();
+  float part[4] = {0.f, 0.f, 0.f, 0.f};
+  const bool wr_res = FUSE == FUSE_ADD_NORM && s.a_out && blockIdx.x == 0;
+  for (int q = tid; q < s.M * kch; q += NWV * 64) {
+    const int m = q / kch, c = q - m * kch;
+    uint4 v = ld16(s.a + (size_t)m * s.lda + c * 8);
+    if constexpr (FUSE == FUSE_ADD_NORM) {
+      v = add_round(v, ld16(s.a2 + (size_t)m * s.lda + c * 8));
+      if (wr_res) st16(s.a_out + (size_t)m * s.lda + c * 8, v);
+    }
+    a_lds[q] = v;
+    if constexpr (FUSE != FUSE_NONE) {
+      const float sq = sumsq8(v);
+#pragma unroll
+      for (int mm = 0; mm < 4; ++mm) part[mm] += mm == m ? sq : 0.f;
+    }
+  }
+  if constexpr (FUSE != FUSE_NONE) {
+#pragma unroll
+    for (int mm = 0; mm < 4; ++mm) {
+      const float t = wave_sum(part[mm]);
+      if (lane == 0 && mm < s.M) atomicAdd(&ssq_s[mm], t);
+    }
+  }
+  __syncthreads();
+
+  f32x4 acc[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool arow = nr < s.M;
+  for (; ks < ksteps; ks += NWV * UNROLL) {
+    uint4 wv[UNROLL][NT];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) wv[u][j] = wnext[u][j];
+    if (ks + NWV * UNROLL < ksteps) load_trip(ks + NWV * UNROLL, wnext);
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int k = ks + NWV * u;
+      const uint4 av = (arow && k < ksteps) ? a_lds[nr * kch + k * 4 + g] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, av),
+                                                         __builtin_bit_cast(bf16x8, wv[u][j]), acc[j], 0, 0, 0);
+    }
+  }
+  // reduce the waves' partial sums; C layout: acc[j][i] = out[m = 4g + i][n = n0 + 16j + nr]
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[wid][4 * g + i][16 * j + nr] = acc[j][i];
+  __syncthreads();
+  const bool glu = s.act == ACT_SILU_MUL;
+  constexpr int COLS = NT * 16;
+  for (int q = tid; q < s.M * COLS; q += NWV * 64) {
+    const int m = q / COLS, c = q % COLS;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) v += red[w][m][c];
+    const float rs = FUSE != FUSE_NONE ? rsqrtf(ssq_s[m] / (float)s.K + s.eps) : 1.f;
+    const int n = n0 + c;
+    v *= rs;
+    if (glu) {
+      if ((c & 15) < 8) {
+        float up = 0.f;
+#pragma unroll
+        for (int w = 0; w < NWV; ++w) up += red[w][m][c + 8];
+        up *= rs;
+        s.out[(size_t)m * s.ldo + (n >> 4) * 8 + (n & 7)] = (bf16)(silu(epi(v, n, s)) * epi(up, n + 8, s));
+      }
+      continue;
+    }
+    float o = epi(v, n, s);
+    if (s.res) o += (float)s.res[(size_t)m * s.N + n];
+    s.out[(size_t)m * s.ldo + n] = (bf16)apply_act(o, s.act);
+  }
+}
+
 __global__ __launch_bounds__(256) void skinny_finish_kernel(const SkArgs s) {
   const bool glu = s.act == ACT_SILU_MUL;
   const int ncols = glu ? s.N / 2 : s.N;
@@ -231,7 +346,14 @@ __global__ __launch_bounds__(256) void skinny_finish_kernel(const SkArgs s) {
 
 }  // namespace
 
+int g_skinny_no_lds = 0;  // A/B switch for probes (mls_skinny_set_variant)
+
 extern "C" {
+
+int mls_skinny_set_variant(int no_lds) {
+  g_skinny_no_lds = no_lds;
+  return 0;
+}
 
 // M <= 32, N % 16 == 0, K % 8 == 0.  nsplit <= 0: auto (fill the chip).  ws: >= nsplit*M*(N+1) floats.
 // A2 / A_out / norm: the fused residual-add + RMSNorm prologue (header comment); A_out must not alias A/A2.
@@ -277,6 +399,28 @@ int mls_skinny_gemm_norm(const void* A, const void* A2, void* A_out, const void*
   hipStream_t st = (hipStream_t)stream;
   if ((A2 || A_out) && !norm) return MLS_UNSUPPORTED;  // the residual add exists only as the norm prologue
   const int mode = A2 ? FUSE_ADD_NORM : norm ? FUSE_NORM : FUSE_NONE;
+  const size_t a_lds_bytes = (size_t)M * K * 2;
+  if (M <= 4 && nsplit == 1 && K % 32 == 0 && a_lds_bytes <= 65536 && !g_skinny_no_lds) {
+#define MLS_SKL(UN, NT_)                                                                                        \
+  switch (mode) {                                                                                               \
+    case FUSE_NONE:                                                                                             \
+      hipLaunchKernelGGL((skinny_lds_kernel<UN, 8, FUSE_NONE, NT_>), grid, dim3(512), a_lds_bytes, st, s); break; \
+    case FUSE_NORM:                                                                                             \
+      hipLaunchKernelGGL((skinny_lds_kernel<UN, 8, FUSE_NORM, NT_>), grid, dim3(512), a_lds_bytes, st, s); break; \
+    default:                                                                                                    \
+      hipLaunchKernelGGL((skinny_lds_kernel<UN, 8, FUSE_ADD_NORM, NT_>), grid, dim3(512), a_lds_bytes, st, s);    \
+      break;                                                                                                    \
+  }
+    if (nt == 4) {
+      MLS_SKL(4, 4)
+    } else if (nt == 2) {
+      MLS_SKL(4, 2)
+    } else {
+      MLS_SKL(8, 1)
+    }
+#undef MLS_SKL
+    return (int)hipGetLastError();
+  }
 #define MLS_SKINNY_F(TMS, UN, NT_)                                                                             \
   switch (mode) {                                                                                              \
     case FUSE_NONE:                                                                                            \

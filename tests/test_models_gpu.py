@@ -27,7 +27,7 @@ def test_gemm_silu_mul():
         assert rel(out, ref) < 2e-2, (cfg, sk)
 
 
-@pytest.mark.parametrize("M", [1, 5, 16, 17, 32])
+@pytest.mark.parametrize("M", [1, 3, 4, 5, 16, 17, 32])
 @pytest.mark.parametrize("nsplit", [0, 1, 3])
 def test_skinny_gemm(M, nsplit):
     from mlmicroservicetemplate_amd import ops
@@ -51,7 +51,7 @@ def test_skinny_gemm(M, nsplit):
     assert out.shape == (M, 512) and rel(out, ref) < 2e-2
 
 
-@pytest.mark.parametrize("M", [1, 7, 16, 32])
+@pytest.mark.parametrize("M", [1, 2, 4, 7, 16, 32])
 @pytest.mark.parametrize("nsplit", [0, 1, 4])
 def test_gemm_rmsnorm_fused(M, nsplit):
     """Skinny GEMM with the residual add + RMSNorm prologue vs fp32 (gain folded into W)."""
@@ -79,6 +79,34 @@ def test_gemm_rmsnorm_fused(M, nsplit):
     out = ops.gemm_rmsnorm(x, wi, d, None, act="silu_mul", eps=1e-5, workspace=ws, splitk=nsplit)
     ref = torch.nn.functional.silu(xn.float() @ g.float().T) * (xn.float() @ u.float().T)
     assert out.shape == (M, 384) and rel(out, ref) < 2e-2
+
+
+@pytest.mark.parametrize("M", [1, 3, 4])
+@pytest.mark.parametrize("fused", [False, True])
+def test_skinny_lds_wide_n(M, fused):
+    """The few-row LDS-staged skinny kernel with NT = 2 / 4 column tiles per block (N >= 24576)."""
+    from mlmicroservicetemplate_amd import ops
+    from mlmicroservicetemplate_amd.ops import reference as R
+
+    torch.manual_seed(20 + M)
+    N, K = 24576 + 1024, 512
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    d = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) / K**0.5).to(torch.bfloat16)
+    ws = torch.empty(8 << 20, device=DEV, dtype=torch.float32)
+    if fused:
+        gain = (torch.rand(K, device=DEV) + 0.5).to(torch.bfloat16)
+        r_out = torch.empty_like(x)
+        y = ops.gemm_rmsnorm(x, ops.fold_norm(w, gain), d, r_out, eps=1e-5, workspace=ws, splitk=1)
+        xn, hs = R.layernorm(x, gain, None, residual=d, eps=1e-5, rms=True)
+        assert rel(y, xn.float() @ w.float().T) < 2e-2 and rel(r_out, hs) < 1e-2
+    else:
+        y = ops.gemm(x, w, workspace=ws, splitk=1)
+        assert rel(y, x.float() @ w.float().T) < 2e-2
+    g, u = w[: N // 2].contiguous(), w[N // 2:].contiguous()
+    out = ops.gemm(x, ops.interleave_gate_up(g, u), act="silu_mul", workspace=ws, splitk=1)
+    ref = torch.nn.functional.silu(x.float() @ g.float().T) * (x.float() @ u.float().T)
+    assert rel(out, ref) < 2e-2
 
 
 @pytest.mark.parametrize("impl", ["blas", "native"])

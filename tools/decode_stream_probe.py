@@ -1,0 +1,57 @@
+"""Cold-weight decode GEMM streaming: 32 distinct weight matrices per shape (as the 32 layers of a
+decode step), replayed back-to-back in one hipGraph, so every call reads its weights from HBM
+(the single-matrix probe is flattered by the 256 MB Infinity Cache).  Skinny kernel variants vs
+hipBLASLt; µs per call and HBM TB/s."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+SHAPES = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336)}
+
+
+def main():
+    from mlmicroservicetemplate_amd import ops
+    from mlmicroservicetemplate_amd.ops.autotune import _time
+
+    dev = torch.device("cuda:0")
+    ws = torch.empty(64 << 20, device=dev)
+    M = int(os.environ.get("M", "1"))
+    for name, (N, K) in SHAPES.items():
+        ws_list = [(torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16) for _ in range(32)]
+        x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        d = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        r_out = torch.empty_like(x)
+        act = "silu_mul" if name == "gate_up" else "none"
+        impls = {
+            "skinny": lambda: [ops.gemm(x, w, act=act, workspace=ws) for w in ws_list],
+            "hipblaslt": lambda: [torch.mm(x, w.t()) for w in ws_list],
+        }
+        if K == 4096 and name != "o":
+            impls["fused_norm_skinny"] = lambda: [ops.gemm_rmsnorm(x, w, d, r_out, act=act, workspace=ws)
+                                                  for w in ws_list]
+        lib = ops.lib()
+
+        def variant(fn, no_lds):
+            def run():
+                lib.mls_skinny_set_variant(no_lds)
+                fn()
+                lib.mls_skinny_set_variant(0)
+            return run
+
+        if hasattr(lib, "mls_skinny_set_variant"):
+            for k in [k for k in impls if "skinny" in k]:
+                impls[k + "_reg"] = variant(impls[k], 1)
+        for impl, fn in impls.items():
+            t = _time(fn, iters=3) * 1e-3 / 32
+            print(json.dumps({"shape": name, "M": M, "impl": impl, "us_per_call": round(t * 1e6, 2),
+                              "hbm_tb_s": round(N * K * 2 / t / 1e12, 2)}), flush=True)
+        del ws_list
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
