@@ -485,7 +485,7 @@ int mls_flash_attention(const void* q, const void* k, const void* v, void* o, in
 }
 
 // workspace: ws >= B*Hq*nsplit*D floats, ws_ml >= B*Hq*nsplit*2 floats, nsplit = ceil(max_len/chunk);
-// counters: B*Hkv zero-initialised ints.  chunk: rows per split (D=128: 16/32/64/128; D=64: 32..256).
+// counters: B*Hkv zero-initialised ints.  chunk: rows per split (D=128: 16..256; D=64: 32..512).
 // positions/cos/sin non-null: rope mode (q = the fused QKV rows, positions[b] == lens[b] - 1).
 int mls_decode_attention(const void* q, void* k_cache, void* v_cache, void* o, float* ws, float* ws_ml, int* counters,
                          int q_stride, int o_stride, long seq_stride, const int* lens, const int* positions,
@@ -517,7 +517,7 @@ int mls_decode_attention(const void* q, void* k_cache, void* v_cache, void* o, f
   const int G = Hq / Hkv;
   const int rows = D == 128 ? 16 : 32;  // rows per block pass
   const int nit = chunk / rows;
-  if (chunk % rows || (nit != 1 && nit != 2 && nit != 4 && nit != 8)) return MLS_BAD_ARG;
+  if (chunk % rows || (nit != 1 && nit != 2 && nit != 4 && nit != 8 && nit != 16)) return MLS_BAD_ARG;
   if (a.nsplit > 1024) return MLS_UNSUPPORTED;  // combine keeps one weight per split in LDS
   dim3 grid(a.nsplit, Hkv, B);
   hipStream_t st = (hipStream_t)stream;
@@ -526,7 +526,8 @@ int mls_decode_attention(const void* q, void* k_cache, void* v_cache, void* o, f
     case 1: hipLaunchKernelGGL((decode_attn_kernel<DD, GG, 1>), grid, dim3(256), 0, st, a); break;        \
     case 2: hipLaunchKernelGGL((decode_attn_kernel<DD, GG, 2>), grid, dim3(256), 0, st, a); break;        \
     case 4: hipLaunchKernelGGL((decode_attn_kernel<DD, GG, 4>), grid, dim3(256), 0, st, a); break;        \
-    default: hipLaunchKernelGGL((decode_attn_kernel<DD, GG, 8>), grid, dim3(256), 0, st, a); break;       \
+    case 8: hipLaunchKernelGGL((decode_attn_kernel<DD, GG, 8>), grid, dim3(256), 0, st, a); break;        \
+    default: hipLaunchKernelGGL((decode_attn_kernel<DD, GG, 16>), grid, dim3(256), 0, st, a); break;      \
   }
   if (D == 128) {
     if (G == 1) { DEC(128, 1) }

@@ -134,7 +134,7 @@ def test_flash_attention_spike_rescale(ops):
 
 
 @pytest.mark.parametrize("Hq,Hkv,D", [(4, 1, 128), (32, 8, 128), (12, 12, 64)])
-@pytest.mark.parametrize("chunk", [64, 128])
+@pytest.mark.parametrize("chunk", [64, 128, 256])
 def test_decode_attention(ops, Hq, Hkv, D, chunk):
     torch.manual_seed(5)
     B, max_len = 4, 1024
