@@ -207,6 +207,11 @@ def create_app(settings: Optional[Settings] = None, plugin: Optional[ModelPlugin
                             content={"status": "failure", "detail": "Server overloaded; retry later."},
                             headers={"Retry-After": "1"})
 
+    @app.exception_handler(asyncio.TimeoutError)
+    async def timeout_handler(request: Request, exc: asyncio.TimeoutError):
+        # REQUEST_TIMEOUT_S elapsed while the request waited in (or ran through) its replica
+        return JSONResponse(status_code=504, content={"status": "failure", "detail": "Prediction timed out."})
+
     @app.exception_handler(MultipartError)
     async def multipart_handler(request: Request, exc: MultipartError):
         return JSONResponse(status_code=400, content={"status": "failure", "detail": f"Malformed upload: {exc}"})

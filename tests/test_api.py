@@ -224,3 +224,34 @@ def test_urlencoded_text_field():
         assert r.status_code == 200, r.text
         assert r.json()["result"]["result"]["crc32"] == zlib.crc32(b"hello world") & 0xFFFFFFFF
 
+
+def test_request_timeout_is_504():
+    import threading
+
+    from mlmicroservicetemplate_amd.plugins.base import ModelPlugin
+
+    release = threading.Event()
+
+    class Slow(ModelPlugin):
+        name = "slow"
+        batched = True
+
+        def preprocess(self, part):
+            return part.data
+
+        def replicas(self):
+            def run_batch(samples):
+                release.wait(5)
+                return [{"n": len(x)} for x in samples]
+            return [run_batch]
+
+        def postprocess(self, out):
+            return out
+
+    app = create_app(settings(REQUEST_TIMEOUT_S=0.2, WATCHDOG_INTERVAL_S=0), Slow())
+    with TestClient(app, raise_server_exceptions=False) as c:
+        assert wait_ready(c)
+        r = c.post("/predict", **upload(b"abc", ctype="application/octet-stream"))
+        assert r.status_code == 504 and r.json()["detail"] == "Prediction timed out."
+        release.set()
+
