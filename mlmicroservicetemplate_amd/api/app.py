@@ -142,6 +142,17 @@ class ServingRuntime:
 
     async def generate(self, req: dict) -> dict:
         plugin = self.plugin
+        if hasattr(plugin, "submit_generate") and getattr(plugin, "engine", None) is not None:
+            # continuous batching: the plugin's scheduler owns admission and batching
+            from ..models.llama_serving import EngineFull
+
+            sample = await run_in_threadpool(plugin.prepare_generate, req)
+            try:
+                fut = plugin.submit_generate(sample)
+            except EngineFull as e:
+                raise OverloadedException(str(e)) from e
+            out = await asyncio.wait_for(asyncio.wrap_future(fut), float(self.settings.REQUEST_TIMEOUT_S))
+            return plugin.finish_generate(out)
         if plugin.batched and hasattr(plugin, "prepare_generate"):
             if self.router is None:
                 raise PredictionException()

@@ -172,6 +172,7 @@ class Settings:
     HBM_FRACTION: float = 0.9  # of free HBM the batch-size cap may plan for
     # --- generate (Llama) ---
     MAX_NEW_TOKENS: int = 64
+    CONTINUOUS_BATCHING: bool = True  # /generate: sequences join / leave the decode batch every step
     MAX_SEQ_LEN: int = 8192
     # --- HTTP ---
     CORS_ORIGINS: List[str] = field(default_factory=lambda: list(DEFAULT_CORS_ORIGINS))

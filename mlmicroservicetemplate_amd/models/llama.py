@@ -416,7 +416,8 @@ class LlamaTP:
         valid = positions < self.max_seq
         if not decode:
             valid = valid & (positions < lens.long()[b_of])
-        bi, pi = b_of[valid], positions[valid].long()
+        rows = b_of if slots_b is None else slots_b.long()[b_of]  # batch row -> cache row
+        bi, pi = rows[valid], positions[valid].long()
         self.k_cache[i][bi, pi] = k[valid].to(self.k_cache[i].dtype)
         self.v_cache[i][bi, pi] = v[valid].to(self.v_cache[i].dtype)
         if decode:
@@ -433,10 +434,10 @@ class LlamaTP:
         return x + d
 
     def _ref_forward(self, ids: torch.Tensor, positions: torch.Tensor, lens: torch.Tensor, B: int, S: int,
-                     decode: bool, k: int):
+                     decode: bool, k: int, slot_ids: Optional[torch.Tensor] = None):
         x = self._embed(ids.reshape(-1))
         for i in range(self.cfg.layers):
-            x = self._ref_layer(i, x, B, S, positions.reshape(-1), lens, None, decode)
+            x = self._ref_layer(i, x, B, S, positions.reshape(-1), lens, slot_ids, decode)
         xn = R.layernorm(x, self.p["final_norm"], None, eps=self.cfg.eps, rms=True)[0]
         if not decode:
             last = (torch.arange(B, device=x.device) * S + lens.long() - 1)
@@ -446,7 +447,7 @@ class LlamaTP:
 
     # ---------------------------------------------------------------- fused backend
     def _fused_forward(self, ids: torch.Tensor, positions: torch.Tensor, lens: torch.Tensor, B: int, S: int,
-                       decode: bool, k: int):
+                       decode: bool, k: int, slot_ids: Optional[torch.Tensor] = None):
         """Native-kernel forward.  The RMSNorm gains are folded into the following projections, so
         for decode-shaped token counts (<= 16) each pre-norm + residual add rides inside the skinny
         GEMM (``ops.gemm_rmsnorm``: 7 launches per layer); larger counts run a gain-free RMSNorm and
@@ -456,6 +457,12 @@ class LlamaTP:
         ws = self.workspace
         fuse = B * S <= 16
         pos = positions.reshape(-1)
+        explicit_slots = None
+        if slot_ids is not None and not decode:  # prefill into arbitrary cache rows (continuous batching)
+            b = torch.arange(B, device=ids.device, dtype=torch.int64).repeat_interleave(S)
+            pl = pos.long()
+            explicit_slots = torch.where(pl < lens.long()[b], slot_ids.long()[b] * self.max_seq + pl,
+                                         torch.full_like(pl, -1)).to(torch.int32)
         # decode split size: 64 rows measured best from batch 1 to 32 (a single 256-row split per
         # kv head, which skips the combine launch, was 1.6 % slower at batch 1)
         dec_chunk = 64
@@ -478,7 +485,7 @@ class LlamaTP:
                                          workspace=self.dec_ws, counters=self.dec_cnt, positions=pos, cos=self.cos,
                                          sin=self.sin, max_len=self._dec_ctx, chunk=dec_chunk)
             else:
-                ops.rope_kv_(qkv, pos, self.cos, self.sin, sd.hq, sd.hkv, D, None, self.k_cache[i],
+                ops.rope_kv_(qkv, pos, self.cos, self.sin, sd.hq, sd.hkv, D, explicit_slots, self.k_cache[i],
                              self.v_cache[i], lens=lens, seq=S, max_seq=self.max_seq)
                 a = ops.flash_attention(qkv, B, S, sd.hq, sd.hkv, D, kv_lens=lens, causal=True)
             o = self.comm.all_reduce_(ops.linear(a, p[f"l{i}.o"], workspace=ws))
@@ -496,13 +503,38 @@ class LlamaTP:
 
     # ---------------------------------------------------------------- public
     @torch.no_grad()
-    def step(self, ids: torch.Tensor, positions: torch.Tensor, lens: torch.Tensor, decode: bool, k: int):
+    def step(self, ids: torch.Tensor, positions: torch.Tensor, lens: torch.Tensor, decode: bool, k: int,
+             slot_ids: Optional[torch.Tensor] = None):
+        """One forward.  ``slot_ids`` (prefill only): cache row of each batch row (default: the
+        batch row itself) -- how continuous batching prefills new requests into free slots."""
         B, S = ids.shape
         ids, positions, lens = ids.contiguous(), positions.contiguous(), lens.contiguous()
+        if slot_ids is not None:
+            slot_ids = slot_ids.to(self.device).contiguous()
         if self.backend == "fused":
             return self._fused_forward(ids.to(torch.int32), positions.to(torch.int32), lens.to(torch.int32), B, S,
-                                       decode, k)
-        return self._ref_forward(ids, positions, lens, B, S, decode, k)
+                                       decode, k, slot_ids)
+        return self._ref_forward(ids, positions, lens, B, S, decode, k, slot_ids)
+
+    def gather_candidates(self, vals: torch.Tensor, idx: torch.Tensor):
+        """X4 all-gather of every rank's local top-k -> ``[B, tp*k]`` values / ids (host tensors)."""
+        allv = self.comm.all_gather(vals)
+        alli = self.comm.all_gather(idx)
+        B = vals.shape[0]
+        return (allv.permute(1, 0, 2).reshape(B, -1).float().cpu(), alli.permute(1, 0, 2).reshape(B, -1).cpu())
+
+    @staticmethod
+    def pick_token(cv: torch.Tensor, ci: torch.Tensor, gp: GenParams, step: int) -> int:
+        """One row's next token from its merged candidates -- the same rule (and the same seeded
+        generator per (seed, step)) as a batch-of-one :meth:`generate`."""
+        if gp.top_k <= 1:
+            return int(ci[int(cv.argmax())])
+        k = min(gp.top_k, cv.shape[0])
+        tv, tpos = torch.topk(cv, k)
+        probs = torch.softmax(tv / max(gp.temperature, 1e-5), dim=-1).view(1, -1)
+        g = torch.Generator().manual_seed(gp.seed * 1000003 + step)
+        pick = int(torch.multinomial(probs, 1, generator=g)[0, 0])
+        return int(ci[int(tpos[pick])])
 
     def ctx_bucket(self, max_ctx: Optional[int]) -> int:
         """Power-of-two context bound (>= 256, <= max_seq) a decode graph is captured for."""
@@ -573,13 +605,18 @@ class LlamaTP:
         pos = torch.arange(S, device=dev, dtype=torch.int32).unsqueeze(0).expand(B, S).contiguous()
         vals, idx = self.step(ids, pos, lens, decode=False, k=k)
         out = []
-        tok = self._merge_sample(vals, idx, gp, 0)
+        tok = self._sample_rows(vals, idx, gp, 0)
         out.append(tok)
         cur = lens.clone()
         for t in range(1, gp.max_new_tokens):
             # the new token sits at position cur; attention covers cur + 1 keys
-            vals, idx = self.decode_step(tok.to(torch.int32), cur, k, max_ctx=S + t)
-            tok = self._merge_sample(vals, idx, gp, t)
+            vals, idx = self.decode_step(tok.to(dev), cur, k, max_ctx=S + t)
+            tok = self._sample_rows(vals, idx, gp, t)
             out.append(tok)
             cur = cur + 1
         return torch.stack(out, dim=1)
+
+    def _sample_rows(self, vals, idx, gp: GenParams, step: int) -> torch.Tensor:
+        cv, ci = self.gather_candidates(vals, idx)
+        return torch.tensor([self.pick_token(cv[b], ci[b], gp, step) for b in range(cv.shape[0])],
+                            dtype=torch.int32)

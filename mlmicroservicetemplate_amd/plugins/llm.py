@@ -1,9 +1,10 @@
 """``llama`` plugin: ``POST /generate`` on Llama-3-8B, tensor-parallel over the node (config 5).
 
 Request: ``{"prompt": str | "input_ids": [int], "max_new_tokens": int, "top_k": int,
-"temperature": float, "seed": int}``.  Concurrent requests are micro-batched (same batcher as
-``/predict``); a batch is right-padded and generated together (batched prefill with per-sequence
-lengths, then lockstep decode steps over the KV cache).
+"temperature": float, "seed": int}``.  With ``CONTINUOUS_BATCHING`` (default) requests join and
+leave the running decode batch at every step (``models/llama_serving.py``); otherwise
+concurrent requests are micro-batched (same batcher as ``/predict``), right-padded and generated
+together (batched prefill with per-sequence lengths, then lockstep decode steps).
 
 Multi-GPU: rank 0 owns HTTP.  For each batch it broadcasts a small command header and the
 token ids to the other ranks (X5); every rank then runs the same TP forward, and the
@@ -22,7 +23,7 @@ from .base import ModelPlugin, PluginContext, register
 
 logger = logging.getLogger("mlsamd.plugin")
 
-OP_STOP, OP_GENERATE = 0, 1
+OP_STOP, OP_GENERATE, OP_ITER = 0, 1, 2
 
 
 @register("llama")
@@ -60,6 +61,14 @@ class LlamaPlugin(ModelPlugin):
                                    device=dev, max_batch=int(s.MAX_BATCH), max_seq=int(extra.get("max_seq", 2048)))
         self.tok = llama.LlamaTokenizer(cfg, extra.get("tokenizer_file"))
         self.cfg = cfg
+        self.engine = None
+        if bool(getattr(s, "CONTINUOUS_BATCHING", True)):
+            from ..models.llama_serving import ContinuousLlama
+
+            self.engine = ContinuousLlama(self.model, max_queue=int(s.MAX_QUEUE),
+                                          broadcast=self._broadcast_iter if tp > 1 else None)
+            if ctx.rank == 0:
+                self.engine.start()
         logger.info("llama ready: tp=%d rank=%d backend=%s device=%s", tp, ctx.rank, backend, dev)
 
     # ------------------------------------------------------------------ request path
@@ -78,6 +87,26 @@ class LlamaPlugin(ModelPlugin):
         if gp.max_new_tokens < 1:
             raise ValueError("max_new_tokens must be >= 1")
         return ids, gp
+
+    def submit_generate(self, sample):
+        """Continuous batching: enqueue into the scheduler; a concurrent.futures.Future of the
+        ``(prompt_len, tokens)`` pair :meth:`finish_generate` formats (None: no engine)."""
+        if self.engine is None:
+            return None
+        ids, gp = sample
+        fut = self.engine.submit(ids, gp)
+        import concurrent.futures as cf
+
+        out: cf.Future = cf.Future()
+
+        def done(f, n=len(ids)):
+            if f.exception() is not None:
+                out.set_exception(f.exception())
+            else:
+                out.set_result((n, f.result()))
+
+        fut.add_done_callback(done)
+        return out
 
     def finish_generate(self, out: Any) -> dict:
         prompt_len, toks = out
@@ -132,6 +161,27 @@ class LlamaPlugin(ModelPlugin):
             out = self.model.generate(ids, lens, gp)
         return out.cpu().tolist()
 
+    def _broadcast_iter(self, admit) -> None:
+        """Rank 0, continuous mode: publish one iteration's admissions (None = stop)."""
+        import torch.distributed as dist
+
+        hdr = torch.zeros(7, dtype=torch.int64, device=self.comm_dev)
+        if admit is None:
+            dist.broadcast(hdr, src=0)  # OP_STOP
+            return
+        n = len(admit)
+        S = max((len(a.ids) for a in admit), default=0)
+        hdr[:3] = torch.tensor([OP_ITER, n, S])
+        dist.broadcast(hdr, src=0)
+        if n:
+            meta = torch.tensor([[a.slot, len(a.ids), a.gp.max_new_tokens, a.gp.top_k, int(a.gp.temperature * 1000),
+                                  a.gp.seed] for a in admit], dtype=torch.int64, device=self.comm_dev)
+            ids = torch.zeros(n, S, dtype=torch.int64, device=self.comm_dev)
+            for j, a in enumerate(admit):
+                ids[j, : len(a.ids)] = torch.tensor(a.ids, dtype=torch.int64)
+            dist.broadcast(meta, src=0)
+            dist.broadcast(ids, src=0)
+
     def follower_loop(self) -> int:
         """Ranks > 0: execute rank 0's generate commands until STOP."""
         import torch.distributed as dist
@@ -145,6 +195,21 @@ class LlamaPlugin(ModelPlugin):
             if op == OP_STOP:
                 logger.info("rank %d: stop", self.ctx.rank)
                 return 0
+            if op == OP_ITER:  # continuous batching: replay rank 0's iteration
+                from ..models.llama_serving import _Seq
+
+                admit = []
+                if B:
+                    meta = torch.zeros(B, 6, dtype=torch.int64, device=self.comm_dev)
+                    ids = torch.zeros(B, S, dtype=torch.int64, device=self.comm_dev)
+                    dist.broadcast(meta, src=0)
+                    dist.broadcast(ids, src=0)
+                    for j, (slot, n, mnt_j, topk_j, temp_j, seed_j) in enumerate(meta.tolist()):
+                        seq = _Seq(ids[j, :n].tolist(), GenParams(mnt_j, topk_j, temp_j / 1000.0, seed_j), None)
+                        seq.slot = slot
+                        admit.append(seq)
+                self.engine.iteration(admit)
+                continue
             ids = torch.zeros(B, S, dtype=torch.int32, device=self.comm_dev)
             lens = torch.zeros(B, dtype=torch.int32, device=self.comm_dev)
             dist.broadcast(ids, src=0)
@@ -152,6 +217,10 @@ class LlamaPlugin(ModelPlugin):
             self.model.generate(ids, lens, GenParams(mnt, topk, temp / 1000.0, seed))
 
     def close(self) -> None:
+        if self.engine is not None and self.ctx.rank == 0:
+            self.engine.stop()  # in TP mode its scheduler announces STOP to the followers
+            if self.model.tp > 1:
+                return
         if self.model is not None and self.model.tp > 1 and self.ctx.rank == 0:
             try:
                 self._broadcast_cmd(OP_STOP)

@@ -96,15 +96,47 @@ def bench_llama(args):
                           "decode_ms_per_step": round(dec * 1e3, 3), "decode_tok_s": round(B / dec, 1)}), flush=True)
 
 
+def bench_llama_serve(args):
+    """Continuous batching throughput: ``--requests`` generate requests (prompt ``--prompt``,
+    ``--new`` tokens each) submitted at once to a ``max_batch = batches[0]`` engine."""
+    from mlmicroservicetemplate_amd.models.llama import LLAMA3_8B, GenParams, LlamaTP, init_llama_shard
+    from mlmicroservicetemplate_amd.models.llama_serving import ContinuousLlama
+
+    dev = torch.device("cuda:0")
+    B = args.batches[0]
+    p = init_llama_shard(LLAMA3_8B, 1, 0, seed=0, device=dev)
+    m = LlamaTP(p, LLAMA3_8B, backend="fused", device=dev, max_batch=B, max_seq=2048)
+    eng = ContinuousLlama(m).start()
+    rng = np.random.default_rng(0)
+    warm = [eng.submit(rng.integers(1000, 100000, args.prompt).tolist(), GenParams(4)) for _ in range(B)]
+    [f.result() for f in warm]
+    t0 = time.perf_counter()
+    futs = [eng.submit(rng.integers(1000, 100000, args.prompt).tolist(), GenParams(args.new))
+            for _ in range(args.requests)]
+    lat = []
+    for f in futs:
+        f.result()
+        lat.append(time.perf_counter() - t0)
+    dt = time.perf_counter() - t0
+    toks = sum(len(f.result()) for f in futs)
+    eng.stop()
+    print(json.dumps({"bench": "llama3-8b-continuous", "max_batch": B, "requests": args.requests,
+                      "prompt": args.prompt, "new_tokens": args.new, "tokens_per_s": round(toks / dt, 1),
+                      "requests_per_s": round(args.requests / dt, 2), "p50_latency_s": round(float(np.median(lat)), 3),
+                      "iterations": eng.iterations}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("which", choices=["bert", "llama"])
+    ap.add_argument("which", choices=["bert", "llama", "llama-serve"])
+    ap.add_argument("--requests", type=int, default=128)
+    ap.add_argument("--new", type=int, default=64)
     ap.add_argument("--batches", type=int, nargs="+", default=[1, 8, 32])
     ap.add_argument("--seqs", type=int, nargs="+", default=[128])
     ap.add_argument("--prompt", type=int, default=512)
     ap.add_argument("--steps", type=int, default=30)
     args = ap.parse_args()
-    {"bert": bench_bert, "llama": bench_llama}[args.which](args)
+    {"bert": bench_bert, "llama": bench_llama, "llama-serve": bench_llama_serve}[args.which](args)
 
 
 if __name__ == "__main__":
