@@ -80,7 +80,10 @@ def main(argv=None) -> int:
     world = info.world_size
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    device = torch.device("cuda", info.local_rank)
+    # one GPU per rank; with fewer visible GPUs than ranks (a gloo rehearsal on a 1-GPU box,
+    # MLS_DIST_BACKEND=gloo) ranks share them round-robin
+    ndev = max(1, torch.cuda.device_count())
+    device = torch.device("cuda", info.local_rank % ndev)
     torch.cuda.set_device(device)
 
     from mlmicroservicetemplate_amd.engine.worker import GpuEngine

@@ -55,13 +55,15 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0, de
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     # dmabuf IPC only on this pool's host driver (RCCL / tensor sharing across processes)
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend is None:  # MLS_DIST_BACKEND=gloo: rehearse several ranks on one GPU (RCCL refuses that)
+        backend = os.environ.get("MLS_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     kwargs = {}
     if backend == "nccl":
         dev = info.local_rank if device_id is None else device_id
         torch.cuda.set_device(dev)
         kwargs["device_id"] = torch.device("cuda", dev)
+    elif torch.cuda.is_available():
+        torch.cuda.set_device(info.local_rank % max(1, torch.cuda.device_count()))
     dist.init_process_group(backend=backend, rank=info.rank, world_size=info.world_size,
                             timeout=datetime.timedelta(seconds=timeout_s), **kwargs)
     info.backend = backend
