@@ -25,7 +25,7 @@ import contextlib
 import logging
 import os
 import time
-from typing import Any, Dict, List, Optional
+from typing import Optional
 
 from fastapi import FastAPI, Request, status
 from fastapi.exceptions import RequestValidationError

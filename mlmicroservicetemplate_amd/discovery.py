@@ -21,7 +21,6 @@ Defects of the reference that are fixed (SURVEY.md C9, §2.A race notes):
 from __future__ import annotations
 
 import logging
-import threading
 from typing import Callable, Optional
 
 import requests

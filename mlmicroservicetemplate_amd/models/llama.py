@@ -23,10 +23,9 @@ same full model, without any rank materialising the whole 8B model.
 from __future__ import annotations
 
 import hashlib
-import math
 import re
 import zlib
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch

@@ -15,7 +15,7 @@ from typing import Optional, Tuple
 
 import torch
 
-from . import _lib
+from . import _lib  # noqa: F401  (re-exported: ops._lib.DEBUG, register_signatures)
 from ._lib import NativeError, available, check, lib, stream_ptr
 
 ACT_NONE, ACT_RELU, ACT_GELU, ACT_TANH, ACT_SILU, ACT_SILU_MUL = 0, 1, 2, 3, 4, 5

@@ -2,7 +2,6 @@
 on CPU for the CPU test suite and on GPU as the numerics reference of the HIP kernels)."""
 from __future__ import annotations
 
-import math
 from typing import Optional, Tuple
 
 import torch

@@ -10,7 +10,6 @@ from __future__ import annotations
 import logging
 from typing import Any, List
 
-import numpy as np
 
 from ..api.multipart import Part
 from .base import ModelPlugin, PluginContext, register

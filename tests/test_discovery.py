@@ -5,7 +5,6 @@ import threading
 import time
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 
-import pytest
 
 from mlmicroservicetemplate_amd.api.state import ServiceState
 from mlmicroservicetemplate_amd.discovery import register_model_to_server, registration_payload
