@@ -299,6 +299,16 @@ class ResNet50Fused:
             w = params[s.name + ".w"] * scale.view(-1, 1, 1, 1)
             self.w[s.name] = ops.pack_conv_weight(w).to(self.device)
             self.b[s.name] = bias.to(device=self.device, dtype=torch.float32).contiguous()
+        # block 0 of each stage: conv3 + downsample projection as one GEMM over [y | x] (the identity
+        # branch never goes to HBM): concatenated folded weights, summed biases
+        self.dual_w: Dict[str, torch.Tensor] = {}
+        self.dual_b: Dict[str, torch.Tensor] = {}
+        for si, (_nb, _m, _c, _s) in enumerate(STAGES):
+            p0 = f"layer{si + 1}.0"
+            w3, wd = self.w[p0 + ".conv3"], self.w[p0 + ".down"]
+            self.dual_w[p0] = torch.cat([w3.reshape(w3.shape[0], -1), wd.reshape(wd.shape[0], -1)], 1).contiguous()
+            self.dual_b[p0] = (self.b[p0 + ".conv3"] + self.b[p0 + ".down"]).contiguous()
+        self.fuse_down = True
         self.fc_w = params["fc.w"].to(device=self.device, dtype=torch.bfloat16).contiguous()
         self.fc_b = params["fc.b"].to(device=self.device, dtype=torch.float32).contiguous()
         self.num_classes = self.fc_w.shape[0]
@@ -318,6 +328,9 @@ class ResNet50Fused:
         for s, _hin, ho in conv_shapes(self.image_size):
             k = s.k * 32 if s.name == "stem" else s.k * s.k * s.cin
             out.append((s.name, batch * ho * ho, s.cout, k))
+            if s.name.endswith(".0.down"):  # the fused conv3 + downsample GEMM of this block
+                c3 = self.specs[s.name[: -len("down")] + "conv3"]
+                out.append((s.name[: -len("down")] + "dual", batch * ho * ho, s.cout, c3.cin + s.cin))
         out.append(("fc", batch, self.num_classes, 2048))
         return out
 
@@ -357,10 +370,15 @@ class ResNet50Fused:
         for si, (nblocks, _m, _c, _s) in enumerate(STAGES):
             for bi in range(nblocks):
                 p = f"layer{si + 1}.{bi}"
-                identity = self._conv(x, p + ".down", ops.ACT_NONE) if bi == 0 else x
                 y = self._conv(x, p + ".conv1", ops.ACT_RELU)
                 y = self._conv(y, p + ".conv2", ops.ACT_RELU)
-                x = self._conv(y, p + ".conv3", ops.ACT_RELU, residual=identity)
+                if bi == 0 and self.fuse_down:
+                    cfg, sk = self.tuning.get(p + ".dual", (0, 0))
+                    x = ops.conv1x1_dual(y, x, self.dual_w[p], self.dual_b[p], stride2=self.specs[p + ".down"].stride,
+                                         act=ops.ACT_RELU, workspace=self.workspace, cfg=cfg, splitk=sk)
+                else:
+                    identity = self._conv(x, p + ".down", ops.ACT_NONE) if bi == 0 else x
+                    x = self._conv(y, p + ".conv3", ops.ACT_RELU, residual=identity)
         pooled = ops.avgpool_global_nhwc(x)
         cfg, sk = self.tuning.get("fc", (0, 0))
         return ops.gemm(pooled, self.fc_w, self.fc_b, workspace=self.workspace, cfg=cfg, splitk=sk)

@@ -153,6 +153,34 @@ def conv2d_nhwc(
     return out
 
 
+def conv1x1_dual(y: torch.Tensor, x: torch.Tensor, w_cat: torch.Tensor, bias: Optional[torch.Tensor] = None, *,
+                 stride2: int = 1, act=ACT_NONE, out: Optional[torch.Tensor] = None,
+                 workspace: Optional[torch.Tensor] = None, cfg: int = 0, splitk: int = 0) -> torch.Tensor:
+    """``act(conv1x1(y, W_y) + conv1x1_stride2(x, W_x) + bias)`` as ONE GEMM over the concatenated
+    reduction (``w_cat`` = ``[Cout][Cin_y + Cin_x]``): a ResNet bottleneck's last conv fused with its
+    downsample projection, so the identity branch is never materialised."""
+    dev = y.device
+    _need(y, "y", torch.bfloat16, dev)
+    _need(x, "x", torch.bfloat16, dev)
+    _need(w_cat, "w_cat", torch.bfloat16, dev)
+    B, Ho, Wo, C1 = y.shape
+    B2, H2, W2, C2 = x.shape
+    cout = w_cat.shape[0]
+    if B2 != B or tuple(w_cat.shape) != (cout, C1 + C2) or conv_out_hw(H2, W2, 1, stride2, 0) != (Ho, Wo):
+        raise ValueError("conv1x1_dual: inconsistent shapes")
+    if C1 % 64 or C2 % 8 or cout % 8:
+        raise ValueError("conv1x1_dual needs Cin_y % 64 == 0, Cin_x % 8 == 0, Cout % 8 == 0")
+    if bias is not None:
+        _need(bias, "bias", torch.float32, dev)
+    if out is None:
+        out = torch.empty(B, Ho, Wo, cout, device=dev, dtype=torch.bfloat16)
+    wsp, wsb = _workspace_args(workspace)
+    rc = lib().mls_conv2d_dual(y.data_ptr(), x.data_ptr(), w_cat.data_ptr(), _ptr(bias), out.data_ptr(), wsp, wsb,
+                               B, Ho, Wo, C1, H2, W2, C2, stride2, cout, _act(act), cfg, splitk, stream_ptr(dev))
+    check(rc, "mls_conv2d_dual")
+    return out
+
+
 def gemm(
     a: torch.Tensor,
     w: torch.Tensor,

@@ -148,6 +148,42 @@ def tune_resnet50(batch: int, device="cuda:0", iters: int = 20, compare_torch: b
 
             entry["torch_us"] = round(_time(trun, iters) * 1e3, 2)
         results[s.name] = entry
+    # fused conv3 + downsample GEMMs (block 0 of each stage)
+    from . import conv1x1_dual
+    from ..models.resnet import STAGES
+
+    shapes = {s.name: (s, hin, ho) for s, hin, ho in conv_shapes()}
+    for si in range(len(STAGES)):
+        p0 = f"layer{si + 1}.0"
+        sd, hin_d, ho = shapes[p0 + ".down"]
+        s3 = shapes[p0 + ".conv3"][0]
+        y = torch.randn(batch, ho, ho, s3.cin, device=dev).to(torch.bfloat16)
+        xx = torch.randn(batch, hin_d, hin_d, sd.cin, device=dev).to(torch.bfloat16)
+        wcat = (torch.randn(sd.cout, s3.cin + sd.cin, device=dev) * 0.05).to(torch.bfloat16)
+        bias = torch.randn(sd.cout, device=dev)
+        outs = [torch.empty(batch, ho, ho, sd.cout, device=dev, dtype=torch.bfloat16) for _ in range(concurrency)]
+        wss = [ws] + [torch.empty_like(ws) for _ in range(concurrency - 1)]
+        best = (1e9, 0, 0)
+        tried = {}
+        for cfg, sk in [(0, 0)] + cands:
+            if cfg >= 20:
+                continue
+
+            def mk(o, wsc, cfg=cfg, sk=sk):
+                return lambda: conv1x1_dual(y, xx, wcat, bias, stride2=sd.stride, act=1, out=o, workspace=wsc,
+                                            cfg=cfg, splitk=sk)
+
+            try:
+                t = _time_multi([mk(o, wsc) for o, wsc in zip(outs, wss)], iters)
+            except Exception:
+                continue
+            tried[f"{cfg},{sk}"] = round(t * 1e3, 2)
+            if (cfg, sk) != (0, 0) and t < best[0]:
+                best = (t, cfg, sk)
+        flops = 2.0 * batch * ho * ho * sd.cout * (s3.cin + sd.cin)
+        results[p0 + ".dual"] = {"M": batch * ho * ho, "N": sd.cout, "K": s3.cin + sd.cin, "best_cfg": best[1],
+                                 "best_splitk": best[2], "best_us": round(best[0] * 1e3, 2),
+                                 "heuristic_us": tried.get("0,0"), "tflops": round(flops / (best[0] * 1e-3) / 1e12, 1)}
     # FC
     a = torch.randn(batch, 2048, device=dev).to(torch.bfloat16)
     w = torch.randn(1000, 2048, device=dev).to(torch.bfloat16)

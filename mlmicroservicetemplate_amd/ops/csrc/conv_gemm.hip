@@ -30,7 +30,12 @@ namespace {
 constexpr int BK = 64;
 constexpr int NTHREADS = 256;
 
-enum ConvMode : int { MODE_GENERIC = 0, MODE_1X1 = 1, MODE_STEM = 2 };
+enum ConvMode : int { MODE_GENERIC = 0, MODE_1X1 = 1, MODE_STEM = 2, MODE_DUAL = 3 };
+
+// MODE_DUAL: two 1x1 convolutions summed into one output, i.e. one GEMM over the concatenated
+// reduction  [y | x(strided)] . [W_y ; W_x]^T  -- a ResNet bottleneck's conv3 together with its
+// downsample projection.  k < K1 reads y (the block's 1x1 input, stride 1), k >= K1 reads x at
+// stride `stride2`; the identity branch is never written to or re-read from HBM.
 
 struct ConvArgs {
   const bf16* x;
@@ -48,6 +53,10 @@ struct ConvArgs {
   uint32_t o_bytes;
   uint32_t x_bytes, w_bytes, r_bytes;  // extents of x, w, res for the buffer-load range check
   int dbg;  // diagnostics only (ablation): 1 = skip MFMAs, 2 = skip output stores, 4 = skip operand DMA
+  // MODE_DUAL second operand: x2 [B][H2][W2][Cin2], sampled at stride2; reduction split at K1
+  const bf16* x2;
+  uint32_t x2_bytes;
+  int H2, W2, Cin2, stride2, K1;
 };
 
 int g_dbg_flags = 0;  // set via mls_set_debug_flags (tools/conv_ablate.py); 0 in production
@@ -95,7 +104,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_kernel(const ConvArgs 
   const int r8 = lane >> 3;
   const int lc = (lane & 7) ^ r8;
 
-  int a_v[AI];
+  int a_v[AI], a_v2[AI];
   uint32_t a_msk[AI];
   const int HoWo = a.Ho * a.Wo;
 #pragma unroll
@@ -103,12 +112,16 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_kernel(const ConvArgs 
     const int m = m0 + (wid * AI + j) * 8 + r8;
     a_msk[j] = 0u;
     a_v[j] = OOB;
+    a_v2[j] = OOB;
     if (m < a.M) {
       const int b = m / HoWo;
       const int rem = m - b * HoWo;
       const int oh = rem / a.Wo;
       const int ow = rem - oh * a.Wo;
-      if (MODE == MODE_1X1) {
+      if (MODE == MODE_DUAL) {
+        a_v[j] = (((b * a.H + oh) * a.W + ow) * a.Cin + lc * 8) * 2;
+        a_v2[j] = (((b * a.H2 + oh * a.stride2) * a.W2 + ow * a.stride2) * a.Cin2 + lc * 8) * 2;
+      } else if (MODE == MODE_1X1) {
         a_v[j] = (((b * a.H + oh * a.stride) * a.W + ow * a.stride) * a.Cin + lc * 8) * 2;
       } else if (MODE == MODE_STEM) {  // pre-padded image, Cin 4, chunk = 2 taps: kh = lc>>2, kw = 2*(lc&3)
         a_v[j] = (((b * a.H + oh * a.stride + (lc >> 2)) * a.W + ow * a.stride + 2 * (lc & 3)) * 4) * 2;
@@ -133,6 +146,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_kernel(const ConvArgs 
 
   const rsrc_t xr = make_rsrc(a.x, a.x_bytes);
   const rsrc_t wr = make_rsrc(a.w, a.w_bytes);
+  const rsrc_t xr2 = make_rsrc(a.x2, MODE == MODE_DUAL ? a.x2_bytes : 0);
 
   auto issue = [&](int kt, int buf) {
     const int k0 = kbeg + kt * BK;
@@ -140,7 +154,16 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_kernel(const ConvArgs 
     char* sB = sA + A_BYTES;
     const int left = kend - k0;  // < 64 only on a K tail
     const bool lane_kin = lc * 8 < left;
-    if (MODE == MODE_1X1) {
+    if (MODE == MODE_DUAL) {  // K1 % 64 == 0: a step lies wholly in one operand (wave-uniform branch)
+      if (k0 < a.K1) {
+#pragma unroll
+        for (int j = 0; j < AI; ++j) glds16(xr, sA + (wid * AI + j) * 1024, lane_kin ? a_v[j] : OOB, k0 * 2);
+      } else {
+#pragma unroll
+        for (int j = 0; j < AI; ++j)
+          glds16(xr2, sA + (wid * AI + j) * 1024, lane_kin ? a_v2[j] : OOB, (k0 - a.K1) * 2);
+      }
+    } else if (MODE == MODE_1X1) {
 #pragma unroll
       for (int j = 0; j < AI; ++j) glds16(xr, sA + (wid * AI + j) * 1024, lane_kin ? a_v[j] : OOB, k0 * 2);
     } else if (MODE == MODE_STEM) {
@@ -696,6 +719,7 @@ int launch_conv(ConvArgs a, int mode, int cfg, int splitk, size_t ws_bytes, hipS
     if (ob >= 0x7FFFFFFFull) return MLS_UNSUPPORTED;
     a.o_bytes = (uint32_t)ob;
   }
+  if (cfg >= 20 && cfg <= 22 && mode == MODE_DUAL) cfg = 0;  // persistent kernel: no dual mode
   if (cfg >= 20 && cfg <= 22) {
     if (a.act != ACT_SILU_MUL && (splitk <= 1)) {
       a.splitk = 1;
@@ -742,6 +766,7 @@ int launch_conv(ConvArgs a, int mode, int cfg, int splitk, size_t ws_bytes, hipS
     case MODE_1X1: launch_mode<MODE_1X1>(cfg, grid, st, a); break;
     case MODE_GENERIC: launch_mode<MODE_GENERIC>(cfg, grid, st, a); break;
     case MODE_STEM: launch_mode<MODE_STEM>(cfg, grid, st, a); break;
+    case MODE_DUAL: launch_mode<MODE_DUAL>(cfg, grid, st, a); break;
     default: return MLS_UNSUPPORTED;
   }
   if (splitk > 1) {
@@ -800,6 +825,35 @@ int mls_conv2d(const void* x, const void* w, const float* scale, const float* bi
   if (wb >= 0x7FFFFFFFull) return MLS_UNSUPPORTED;
   a.w_bytes = (uint32_t)wb;
   return launch_conv(a, mode, cfg, splitk, ws_bytes, (hipStream_t)stream);
+}
+
+// out = act(conv1x1(y, W[:, :Cin1]) + conv1x1_stride2(x, W[:, Cin1:]) + bias): y [B][Ho][Wo][Cin1],
+// x [B][H2][W2][Cin2] with Ho = ceil(H2 / stride2); W [Cout][Cin1 + Cin2]; Cin1 % 64 == 0.
+int mls_conv2d_dual(const void* y, const void* x, const void* w, const float* bias, void* out, void* ws,
+                    size_t ws_bytes, int B, int Ho, int Wo, int Cin1, int H2, int W2, int Cin2, int stride2, int Cout,
+                    int act, int cfg, int splitk, void* stream) {
+  if (Cin1 % 64 || Cin2 % 8 || stride2 < 1 || (Ho - 1) * stride2 >= H2 || (Wo - 1) * stride2 >= W2) return MLS_BAD_ARG;
+  ConvArgs a{};
+  a.x = (const bf16*)y;
+  a.x2 = (const bf16*)x;
+  a.w = (const bf16*)w;
+  a.bias = bias;
+  a.out = (bf16*)out;
+  a.ws = (float*)ws;
+  a.B = B; a.H = Ho; a.W = Wo; a.Cin = Cin1; a.Ho = Ho; a.Wo = Wo; a.N = Cout; a.KH = 1; a.KW = 1;
+  a.stride = 1; a.pad = 0;
+  a.H2 = H2; a.W2 = W2; a.Cin2 = Cin2; a.stride2 = stride2; a.K1 = Cin1;
+  a.M = B * Ho * Wo;
+  a.K = Cin1 + Cin2;
+  a.act = act;
+  a.ldo = Cout;
+  a.ldr = Cout;
+  const size_t yb = (size_t)a.M * Cin1 * 2, xb = (size_t)B * H2 * W2 * Cin2 * 2, wb = (size_t)Cout * a.K * 2;
+  if (yb >= 0x7FFFFFFFull || xb >= 0x7FFFFFFFull || wb >= 0x7FFFFFFFull) return MLS_UNSUPPORTED;
+  a.x_bytes = (uint32_t)yb;
+  a.x2_bytes = (uint32_t)xb;
+  a.w_bytes = (uint32_t)wb;
+  return launch_conv(a, MODE_DUAL, cfg, splitk, ws_bytes, (hipStream_t)stream);
 }
 
 // out[M][N] = act(A[M][K] . W[N][K]^T * scale + bias (+ res[M][N]))

@@ -205,3 +205,26 @@ def test_softmax_topk_register_path(rows, N, k, softmax):
     assert (idx >= 0).all() and (idx < N).all()
     for r in range(rows):  # no index repeats
         assert len(set(idx[r].tolist())) == k
+
+
+@pytest.mark.parametrize("shape", [(2, 14, 14, 64, 28, 28, 32, 2, 128), (3, 7, 7, 128, 7, 7, 64, 1, 256),
+                                   (2, 5, 5, 64, 9, 9, 24, 2, 64)])
+@pytest.mark.parametrize("cfg,splitk", [(0, 0), (4, 1), (1, 1), (9, 2)])
+def test_conv1x1_dual(shape, cfg, splitk):
+    """conv3 + downsample fused along K vs the two convolutions summed in fp32."""
+    from mlmicroservicetemplate_amd import ops
+
+    B, Ho, Wo, C1, H2, W2, C2, s2, cout = shape
+    torch.manual_seed(B + C1)
+    y = torch.randn(B, Ho, Wo, C1, device=DEV).to(torch.bfloat16)
+    x = torch.randn(B, H2, W2, C2, device=DEV).to(torch.bfloat16)
+    w1 = (torch.randn(cout, C1, device=DEV) / C1**0.5).to(torch.bfloat16)
+    w2 = (torch.randn(cout, C2, device=DEV) / C2**0.5).to(torch.bfloat16)
+    b = torch.randn(cout, device=DEV)
+    ws = torch.empty(8 << 20, device=DEV, dtype=torch.float32)
+    out = ops.conv1x1_dual(y, x, torch.cat([w1, w2], 1).contiguous(), b, stride2=s2, act="relu", workspace=ws,
+                           cfg=cfg, splitk=splitk)
+    xs = x[:, ::s2, ::s2, :][:, :Ho, :Wo, :]
+    ref = torch.relu(y.float() @ w1.float().T + xs.float() @ w2.float().T + b)
+    assert out.shape == (B, Ho, Wo, cout)
+    assert rel_err(out, ref) < 2e-2
