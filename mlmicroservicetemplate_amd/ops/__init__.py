@@ -274,10 +274,12 @@ def fold_norm(w: torch.Tensor, gain: torch.Tensor) -> torch.Tensor:
 
 
 # Plain library GEMMs go to hipBLASLt (through torch.addmm): on the transformer prefill shapes it
-# runs 1.4-1.5 PFLOP/s against 0.9-1.0 for the native 128x128-tile kernel (profiles/r1_gemm_probe.jsonl).
-# The native kernels keep the decode-shaped (skinny) products and every fused epilogue hipBLASLt
-# cannot express (residual+bias, SiLU-mul is done by a native elementwise pass after it).
-BLAS_MIN_M = int(os.environ.get("MLS_BLAS_MIN_M", "512"))
+# runs 1.4-1.5 PFLOP/s against 0.9-1.0 for the native 128x128-tile kernel (profiles/r1_gemm_probe.jsonl),
+# and from M = 64 up it wins or ties on every BERT / Llama shape measured
+# (profiles/r1_gemm_probe_small_m.jsonl).  The native kernels keep the decode-shaped products
+# (skinny M <= 16, tiled up to 32, where they tie and fuse SiLU-mul) and every fused epilogue
+# hipBLASLt cannot express (SiLU-mul runs as a native elementwise pass after it).
+BLAS_MIN_M = int(os.environ.get("MLS_BLAS_MIN_M", "33"))
 _BF16_BIAS: dict = {}
 
 

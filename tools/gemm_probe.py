@@ -15,6 +15,9 @@ SHAPES = {  # name: (M, N, K)
     "llama_down": (4096, 4096, 14336), "bert_qkv": (4096, 2304, 768), "bert_ffn1": (4096, 3072, 768),
     "bert_ffn2": (4096, 768, 3072), "dec16_qkv": (16, 6144, 4096), "dec16_gateup": (16, 28672, 4096),
     "dec1_down": (1, 4096, 14336), "dec8_down": (8, 4096, 14336), "dec32_gateup": (32, 28672, 4096),
+    "bert128_qkv": (128, 2304, 768), "bert128_ffn1": (128, 3072, 768), "bert128_ffn2": (128, 768, 3072),
+    "bert128_o": (128, 768, 768), "bert1024_qkv": (1024, 2304, 768), "bert1024_ffn2": (1024, 768, 3072),
+    "m64_qkv": (64, 6144, 4096), "m256_gateup": (256, 28672, 4096),
 }
 
 
