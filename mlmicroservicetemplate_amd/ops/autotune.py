@@ -16,7 +16,7 @@ import torch
 import torch.nn.functional as F
 
 CACHE_DIR = os.environ.get("MLS_TUNE_DIR", os.path.join(os.path.dirname(os.path.abspath(__file__)), "_native", "tune"))
-CANDIDATES: List[Tuple[int, int]] = [(c, s) for c in range(1, 13) for s in (1, 2, 4, 8)] + [(20, 1), (21, 1), (22, 1)]
+CANDIDATES: List[Tuple[int, int]] = [(c, s) for c in range(1, 19) for s in (1, 2, 4, 8)] + [(20, 1), (21, 1), (22, 1)]
 
 
 def _time(fn, iters: int = 20, warmup: int = 3) -> float:

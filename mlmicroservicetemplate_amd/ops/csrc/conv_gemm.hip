@@ -67,20 +67,38 @@ MLS_DEV void glds16(rsrc_t r, char* lds, int voff, int soff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS3 void*)lds, 16, voff, soff, 0, 0);
 }
 
+// LDS chunk swizzle of a tile row: BK = 64 (128-B rows, 8 chunks): chunk ^ (row & 7);
+// BK = 32 (64-B rows, 4 chunks): chunk ^ f(row & 15), f = (r0 | r2 << 1) -- conflict-free for the
+// gfx950 ds_read_b128 lane groups over the MFMA fragment rows (checked exhaustively, 96 such linear
+// maps exist; this is one of them).
+template <int BKT>
+MLS_DEV int row_swz(int r) {
+  if constexpr (BKT == 64) return r & 7;
+  else return (r & 1) | ((r >> 1) & 2);
+}
+
 // v2: LDS-DMA (buffer_load ... lds) into a STAGES-deep ring, counted vmcnt + raw s_barrier.
-template <int BM, int BN, int WM, int WN, int STAGES, int MODE>
+// BKT (64 or 32) is the K depth of a stage: 32 halves the LDS ring, and with the accumulators
+// parked for the epilogue in EPI_PASSES row blocks, a block's LDS can shrink to ~24 KB -- twice
+// the resident blocks per CU for the latency-bound layers (guide: residency hides DMA latency).
+template <int BM, int BN, int WM, int WN, int STAGES, int MODE, int BKT = 64, int EPI_PASSES = 1>
 __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_kernel(const ConvArgs a) {
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
-  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  constexpr int CPK = BKT / 8;   // 16-B chunks per tile row
+  constexpr int RPP = 64 / CPK;  // tile rows per 1-KiB DMA piece
+  constexpr int A_BYTES = BM * BKT * 2, B_BYTES = BN * BKT * 2;
   constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
-  constexpr int AI = BM / 8 / NW, BI = BN / 8 / NW;  // 1-KiB DMA pieces per wave per stage
-  static_assert(AI * 8 * NW == BM && BI * 8 * NW == BN, "tile / wave mismatch");
+  constexpr int AI = BM / RPP / NW, BI = BN / RPP / NW;  // 1-KiB DMA pieces per wave per stage
+  static_assert(AI * RPP * NW == BM && BI * RPP * NW == BN, "tile / wave mismatch");
   static_assert(TM >= 1 && TN >= 1, "wave tile too small");
+  static_assert(BKT == 64 || BKT == 32, "BK");
   constexpr int LPS = AI + BI;  // vmcnt units per stage
   constexpr int C_LD = BN + 4;
-  constexpr int EPI_BYTES = BM * C_LD * 4;
+  constexpr int PASS_ROWS = BM / EPI_PASSES;
+  static_assert(PASS_ROWS % 16 == 0 && PASS_ROWS * EPI_PASSES == BM, "epilogue passes");
+  constexpr int EPI_BYTES = PASS_ROWS * C_LD * 4;
   constexpr int LDS_BYTES = (STAGES * STAGE_BYTES > EPI_BYTES) ? STAGES * STAGE_BYTES : EPI_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
 
@@ -96,20 +114,20 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_kernel(const ConvArgs 
   const int m0 = tmi * BM, n0 = tn * BN;
   const int kbeg = split * a.kchunk;
   const int kend = min(a.K, kbeg + a.kchunk);
-  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  const int nk = kend > kbeg ? (kend - kbeg + BKT - 1) / BKT : 0;
 
-  // lane -> (row within an 8-row DMA piece, logical 16-B chunk).  The DMA writes LDS lane-
+  // lane -> (row within an RPP-row DMA piece, logical 16-B chunk).  The DMA writes LDS lane-
   // linearly (base + 16*lane), so the XOR swizzle is applied to the SOURCE chunk instead:
-  // physical chunk (lane & 7) of row r holds logical chunk (lane & 7) ^ (r & 7).
-  const int r8 = lane >> 3;
-  const int lc = (lane & 7) ^ r8;
+  // physical chunk (lane % CPK) of row r holds logical chunk (lane % CPK) ^ row_swz(r).
+  const int r8 = lane / CPK;
+  const int lc = (lane % CPK) ^ row_swz<BKT>(r8);
 
   int a_v[AI], a_v2[AI];
   uint32_t a_msk[AI];
   const int HoWo = a.Ho * a.Wo;
 #pragma unroll
   for (int j = 0; j < AI; ++j) {
-    const int m = m0 + (wid * AI + j) * 8 + r8;
+    const int m = m0 + (wid * AI + j) * RPP + r8;
     a_msk[j] = 0u;
     a_v[j] = OOB;
     a_v2[j] = OOB;
@@ -140,7 +158,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_kernel(const ConvArgs 
   int b_v[BI];
 #pragma unroll
   for (int j = 0; j < BI; ++j) {
-    const int n = n0 + (wid * BI + j) * 8 + r8;
+    const int n = n0 + (wid * BI + j) * RPP + r8;
     b_v[j] = n < a.N ? (n * a.K + lc * 8) * 2 : OOB;
   }
 
@@ -149,10 +167,10 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_kernel(const ConvArgs 
   const rsrc_t xr2 = make_rsrc(a.x2, MODE == MODE_DUAL ? a.x2_bytes : 0);
 
   auto issue = [&](int kt, int buf) {
-    const int k0 = kbeg + kt * BK;
+    const int k0 = kbeg + kt * BKT;
     char* sA = smem + buf * STAGE_BYTES;
     char* sB = sA + A_BYTES;
-    const int left = kend - k0;  // < 64 only on a K tail
+    const int left = kend - k0;  // < BKT only on a K tail
     const bool lane_kin = lc * 8 < left;
     if (MODE == MODE_DUAL) {  // K1 % 64 == 0: a step lies wholly in one operand (wave-uniform branch)
       if (k0 < a.K1) {
@@ -171,7 +189,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_kernel(const ConvArgs 
 #pragma unroll
       for (int j = 0; j < AI; ++j) glds16(xr, sA + (wid * AI + j) * 1024, a_v[j], soff);
     } else {
-      const int tap = k0 / a.Cin;  // the whole 64-wide step is inside one tap
+      const int tap = k0 / a.Cin;  // the whole BKT-wide step is inside one tap
       const int c0 = k0 - tap * a.Cin;
       const int kh = tap / a.KW;
       const int kw = tap - kh * a.KW;
@@ -259,18 +277,18 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_kernel(const ConvArgs 
     const uint4* As = reinterpret_cast<const uint4*>(smem + cur * STAGE_BYTES);
     const uint4* Bs = reinterpret_cast<const uint4*>(smem + cur * STAGE_BYTES + A_BYTES);
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int kk = 0; kk < BKT / 32; ++kk) {
       const int ch = fq + 4 * kk;
       bf16x8 af[TM], bfv[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int r = wm * WTM + i * 16 + fr;
-        af[i] = __builtin_bit_cast(bf16x8, As[r * 8 + (ch ^ (r & 7))]);
+        af[i] = __builtin_bit_cast(bf16x8, As[r * CPK + (ch ^ row_swz<BKT>(r))]);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int r = wn * WTN + j * 16 + fr;
-        bfv[j] = __builtin_bit_cast(bf16x8, Bs[r * 8 + (ch ^ (r & 7))]);
+        bfv[j] = __builtin_bit_cast(bf16x8, Bs[r * CPK + (ch ^ row_swz<BKT>(r))]);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -282,21 +300,20 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_kernel(const ConvArgs 
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
 
-  // ---- epilogue: park fp32 accumulators in LDS, then emit 16-B rows ----
+  // ---- epilogue: park fp32 accumulators in LDS (EPI_PASSES row blocks), then emit 16-B rows ----
   float* Cs = reinterpret_cast<float*>(smem);
+  if (EPI_PASSES == 1 && a.act == ACT_SILU_MUL && a.splitk == 1) {
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wm * WTM + i * 16 + fq * 4 + r;
-        const int col = wn * WTN + j * 16 + fr;
-        Cs[row * C_LD + col] = acc[i][j][r];
-      }
-  __syncthreads();
-
-  if (a.act == ACT_SILU_MUL && a.splitk == 1) {
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * WTM + i * 16 + fq * 4 + r;
+          const int col = wn * WTN + j * 16 + fr;
+          Cs[row * C_LD + col] = acc[i][j][r];
+        }
+    __syncthreads();
     // gate/up interleaved in 8-column groups: chunk 2p = gate, 2p+1 = up -> 8 outputs at n/2
     for (int q = tid; q < BM * (CPR / 2); q += NT) {
       const int row = q / (CPR / 2), p = q - (q / (CPR / 2)) * (CPR / 2);
@@ -318,35 +335,55 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_kernel(const ConvArgs 
     return;
   }
 #pragma unroll
-  for (int it = 0; it < EPI_IT; ++it) {
-    const int q = tid + it * NT;
-    const int row = q / CPR, c8 = q - (q / CPR) * CPR;
-    const int m = m0 + row, n = n0 + c8 * 8;
-    if (q >= BM * CPR || m >= a.M || n >= a.N) continue;
-    const float4 v0 = *reinterpret_cast<const float4*>(Cs + row * C_LD + c8 * 8);
-    const float4 v1 = *reinterpret_cast<const float4*>(Cs + row * C_LD + c8 * 8 + 4);
-    if (a.splitk > 1) {
-      float* dst = a.ws + ((size_t)split * a.M + m) * a.N + n;
-      *reinterpret_cast<float4*>(dst) = v0;
-      *reinterpret_cast<float4*>(dst + 4) = v1;
-      continue;
-    }
-    float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+  for (int pass = 0; pass < EPI_PASSES; ++pass) {
+    const int row_lo = pass * PASS_ROWS;
+    if (pass > 0) __syncthreads();  // the previous pass's rows have been read
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = v[e] * scale8[e] + bias8[e];
-    if (pre_res) {
-      float r[8];
-      unpack8(resv[it], r);
+    for (int i = 0; i < TM; ++i) {
+      const int frag_row = wm * WTM + i * 16;  // a fragment's 16 rows fall in one pass
+      if (EPI_PASSES > 1 && (frag_row < row_lo || frag_row >= row_lo + PASS_ROWS)) continue;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += r[e];
-    }
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], a.act);
-    if (a.dbg & 2) {
-      if (v[0] == 12345.678f) st16(a.out, pack8(v));  // keep the value live, never true
-      continue;
+        for (int r = 0; r < 4; ++r) {
+          const int row = frag_row + fq * 4 + r - row_lo;
+          const int col = wn * WTN + j * 16 + fr;
+          Cs[row * C_LD + col] = acc[i][j][r];
+        }
     }
-    st16(a.out + (size_t)m * a.ldo + n, pack8(v));
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < EPI_IT; ++it) {
+      const int q = tid + it * NT;
+      const int row = q / CPR, c8 = q - (q / CPR) * CPR;
+      if (EPI_PASSES > 1 && (row < row_lo || row >= row_lo + PASS_ROWS)) continue;
+      const int m = m0 + row, n = n0 + c8 * 8;
+      if (q >= BM * CPR || m >= a.M || n >= a.N) continue;
+      const float4 v0 = *reinterpret_cast<const float4*>(Cs + (row - row_lo) * C_LD + c8 * 8);
+      const float4 v1 = *reinterpret_cast<const float4*>(Cs + (row - row_lo) * C_LD + c8 * 8 + 4);
+      if (a.splitk > 1) {
+        float* dst = a.ws + ((size_t)split * a.M + m) * a.N + n;
+        *reinterpret_cast<float4*>(dst) = v0;
+        *reinterpret_cast<float4*>(dst + 4) = v1;
+        continue;
+      }
+      float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = v[e] * scale8[e] + bias8[e];
+      if (pre_res) {
+        float r[8];
+        unpack8(resv[it], r);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += r[e];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], a.act);
+      if (a.dbg & 2) {
+        if (v[0] == 12345.678f) st16(a.out, pack8(v));  // keep the value live, never true
+        continue;
+      }
+      st16(a.out + (size_t)m * a.ldo + n, pack8(v));
+    }
   }
 }
 
@@ -642,8 +679,11 @@ struct TileCfg {
 constexpr TileCfg kCfgs[] = {{0, 0, 0},       {128, 128, 256}, {128, 64, 256}, {64, 128, 256},
                              {64, 64, 256},   {128, 128, 512}, {64, 64, 256},  {128, 64, 512},
                              {64, 128, 512},  {64, 128, 512},  {128, 64, 512}, {64, 64, 256},
-                             {128, 128, 512}};
-constexpr int kNumCfgs = 13;
+                             {128, 128, 512}, {128, 128, 512}, {128, 128, 512}, {64, 64, 256},
+                             {128, 64, 256},  {64, 128, 256},  {128, 128, 256}};
+constexpr int kNumCfgs = 19;
+// cfgs 13..18 stage K in 32-deep steps (BK = 32): not for the stem layout or the SiLU-mul epilogue
+constexpr bool cfg_bk32(int c) { return c >= 13 && c <= 18; }
 
 template <int MODE>
 void launch_mode(int cfg, dim3 grid, hipStream_t st, const ConvArgs& a) {
@@ -660,13 +700,21 @@ void launch_mode(int cfg, dim3 grid, hipStream_t st, const ConvArgs& a) {
     case 10: hipLaunchKernelGGL((conv_gemm_kernel<128, 64, 4, 2, 2, MODE>), grid, dim3(512), 0, st, a); break;
     case 11: hipLaunchKernelGGL((conv_gemm_kernel<64, 64, 2, 2, 2, MODE>), grid, dim3(256), 0, st, a); break;
     case 12: hipLaunchKernelGGL((conv_gemm_kernel<128, 128, 4, 2, 2, MODE>), grid, dim3(512), 0, st, a); break;
+    // BK = 32 + multi-pass epilogue: 24-48 KB of LDS per block instead of 48-68 KB
+    case 13: hipLaunchKernelGGL((conv_gemm_kernel<128, 128, 4, 2, 2, MODE, 32, 4>), grid, dim3(512), 0, st, a); break;
+    case 14: hipLaunchKernelGGL((conv_gemm_kernel<128, 128, 4, 2, 3, MODE, 32, 2>), grid, dim3(512), 0, st, a); break;
+    case 15: hipLaunchKernelGGL((conv_gemm_kernel<64, 64, 2, 2, 3, MODE, 32, 1>), grid, dim3(256), 0, st, a); break;
+    case 16: hipLaunchKernelGGL((conv_gemm_kernel<128, 64, 2, 2, 3, MODE, 32, 1>), grid, dim3(256), 0, st, a); break;
+    case 17: hipLaunchKernelGGL((conv_gemm_kernel<64, 128, 2, 2, 3, MODE, 32, 1>), grid, dim3(256), 0, st, a); break;
+    case 18: hipLaunchKernelGGL((conv_gemm_kernel<128, 128, 2, 2, 3, MODE, 32, 2>), grid, dim3(256), 0, st, a); break;
     default: hipLaunchKernelGGL((conv_gemm_kernel<64, 64, 2, 2, 3, MODE>), grid, dim3(256), 0, st, a); break;
   }
 }
 
 // Heuristic tile choice: fill 256 CUs x 2 resident blocks, penalise padding waste and small tiles.
 void choose_cfg(int M, int N, int K, int& cfg, int& splitk) {
-  const float tile_eff[kNumCfgs] = {0.f, 1.0f, 0.86f, 0.86f, 0.68f, 1.0f, 0.68f, 0.86f, 0.86f, 0.86f, 0.86f, 0.68f, 1.0f};
+  const float tile_eff[kNumCfgs] = {0.f,  1.0f, 0.86f, 0.86f, 0.68f, 1.0f, 0.68f, 0.86f, 0.86f, 0.86f,
+                                    0.86f, 0.68f, 1.0f, 1.0f, 1.0f, 0.68f, 0.86f, 0.86f, 1.0f};
   float best = -1.f;
   int bc = 4;
   for (int c = 1; c <= 4; ++c) {
@@ -741,6 +789,7 @@ int launch_conv(ConvArgs a, int mode, int cfg, int splitk, size_t ws_bytes, hipS
   int acfg = 0, asplit = 1;
   choose_cfg(a.M, a.N, a.K, acfg, asplit);
   if (cfg <= 0 || cfg >= kNumCfgs) cfg = acfg;
+  if (cfg_bk32(cfg) && (mode == MODE_STEM || a.act == ACT_SILU_MUL)) cfg = acfg;
   if (splitk <= 0) splitk = asplit;
   // K per split: multiple of BK (so MODE_GENERIC steps never straddle a tap)
   int kchunk = ((a.K + splitk - 1) / splitk + BK - 1) / BK * BK;

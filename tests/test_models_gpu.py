@@ -21,7 +21,7 @@ def test_gemm_silu_mul():
     w = ops.interleave_gate_up(g, u)
     ref = torch.nn.functional.silu(x.float() @ g.float().T) * (x.float() @ u.float().T)
     ws = torch.empty(8 << 20, device=DEV, dtype=torch.float32)
-    for cfg, sk in ((0, 0), (1, 1), (4, 1), (4, 4), (2, 2)):
+    for cfg, sk in ((0, 0), (1, 1), (4, 1), (4, 4), (2, 2), (13, 1), (15, 2)):
         out = ops.gemm(x, w, act="silu_mul", workspace=ws, cfg=cfg, splitk=sk)
         assert out.shape == (M, I)
         assert rel(out, ref) < 2e-2, (cfg, sk)

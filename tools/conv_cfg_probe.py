@@ -26,7 +26,7 @@ def main():
         res = torch.randn(32, ho, ho, s.cout, device=dev).to(torch.bfloat16) if name.endswith("conv3") else None
         outs = [torch.empty(32, ho, ho, s.cout, device=dev, dtype=torch.bfloat16) for _ in range(2)]
         wss = [torch.empty(64 << 20, device=dev) for _ in range(2)]
-        for cfg in list(range(1, 13)) + [20, 21, 22]:
+        for cfg in list(range(1, 19)) + [20, 21, 22]:
             row = {"layer": name, "cfg": cfg}
             for conc in (1, 2):
                 fns = [lambda o=o, wsc=wsc: ops.conv2d_nhwc(x, w, b, kernel=s.k, stride=s.stride, pad=s.pad,
