@@ -143,6 +143,7 @@ class Settings:
     REGISTER: bool = True
     HEARTBEAT_S: float = 10.0  # dependency.WAIT_TIME
     REGISTER_TIMEOUT_S: float = 5.0  # the reference had none (a hung POST blocked shutdown)
+    REGISTER_LEGACY: bool = False  # old-rev {"modelName","modelPort"} body, no api_key header
     POOL_WORKERS: int = 10  # dependency.pool size
     # --- model / plugin ---
     MODEL: str = "stub"  # stub | identity | resnet50 | bert | llama | <python.module.path>

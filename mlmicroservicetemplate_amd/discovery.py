@@ -108,5 +108,6 @@ def start_heartbeat(state: ServiceState, settings) -> "threading.Thread | None":
         settings.ADVERTISE_HOST,
         settings.HEARTBEAT_S,
         settings.REGISTER_TIMEOUT_S,
+        bool(getattr(settings, "REGISTER_LEGACY", False)),
     )
     return None

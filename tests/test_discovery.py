@@ -116,3 +116,24 @@ def test_invalid_url_does_not_kill_thread():
 
 def test_legacy_payload():
     assert registration_payload("m", "h", 5005, legacy=True) == {"modelName": "m", "modelPort": 5005}
+
+
+def test_legacy_payload_via_settings():
+    """REGISTER_LEGACY=1 makes the heartbeat send the old-rev body without the api_key header."""
+    from mlmicroservicetemplate_amd.config import Settings
+    from mlmicroservicetemplate_amd.discovery import start_heartbeat
+
+    orch = FakeOrchestrator()
+    s = Settings.load(env_file=None, environ={"SERVER_PORT": str(orch.port), "SERVER_HOST": "127.0.0.1",
+                                               "REGISTER_LEGACY": "1", "HEARTBEAT_S": "0.05", "API_KEY": "k3y"})
+    state = ServiceState(pool_workers=1)
+    start_heartbeat(state, s)
+    deadline = time.time() + 5
+    while not orch.requests and time.time() < deadline:
+        time.sleep(0.02)
+    state.begin_shutdown(wait=True)
+    orch.close()
+    path, headers, body, _ = orch.requests[0]
+    assert path == "/model/register"
+    assert body == {"modelName": s.NAME, "modelPort": s.PORT}
+    assert "api_key" not in {k.lower() for k in headers}
