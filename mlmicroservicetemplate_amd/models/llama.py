@@ -23,6 +23,7 @@ same full model, without any rank materialising the whole 8B model.
 from __future__ import annotations
 
 import hashlib
+import os
 import re
 import zlib
 from dataclasses import dataclass
@@ -251,8 +252,6 @@ class TPComm:
     """Tensor-parallel collectives over a torch.distributed group (RCCL on GPU, gloo on CPU)."""
 
     def __init__(self, group=None, tp: int = 1, device=None, custom_ar: Optional[bool] = None):
-        import os
-
         self.group = group
         self.tp = tp
         self.car = None
@@ -302,6 +301,29 @@ class TPComm:
         return t
 
 
+class ShardEmulationComm:
+    """One TP rank's shard with every collective replaced by a local no-op -- a measurement tool:
+    it times exactly the per-rank kernel work of a TP=tp decode / prefill step on one GPU (the
+    all-reduce / all-gather cost is measured separately).  Outputs are not the model's."""
+
+    graph_safe = True
+    host_staged = False
+    car = None
+
+    def __init__(self, tp: int):
+        self.tp = tp
+        self.group = None
+
+    def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
+        return t
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        return t.unsqueeze(0).expand(self.tp, *t.shape)
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        return t
+
+
 @dataclass
 class GenParams:
     max_new_tokens: int = 16
@@ -339,6 +361,7 @@ class LlamaTP:
             self.p["lm_head"] = ops.fold_norm(self.p["lm_head"], self.p.pop("final_norm"))
             self.ones = torch.ones(cfg.hidden, device=self.device, dtype=torch.bfloat16)
             self.workspace = torch.empty(32 << 20, device=self.device, dtype=torch.float32)
+            self.dec_chunk = int(os.environ.get("MLS_DEC_CHUNK", "0"))  # 0: auto (see _fused_forward)
             self.dec_ws = torch.empty(max_batch * self.sd.hq * (-(-max_seq // 64)) * (D + 2) + 16,
                                       device=self.device, dtype=torch.float32)
             self.dec_cnt = torch.zeros(max_batch * self.sd.hkv, device=self.device, dtype=torch.int32)
@@ -349,10 +372,9 @@ class LlamaTP:
         self.cos, self.sin = R.rope_tables(max_seq, D, cfg.rope_theta, self.device)
         # hipGraph capture of the decode step (P4): removes ~300 host launches per token.  With
         # tp > 1 the RCCL all-reduces are captured too (opt-in: MLS_TP_GRAPHS=1).
-        import os
-
         self.use_graphs = backend == "fused" and self.device.type == "cuda" and (
-            tp == 1 or (os.environ.get("MLS_TP_GRAPHS", "0") == "1" and not getattr(self.comm, "host_staged", False)))
+            tp == 1 or getattr(self.comm, "graph_safe", False)
+            or (os.environ.get("MLS_TP_GRAPHS", "0") == "1" and not getattr(self.comm, "host_staged", False)))
         self._graphs: Dict[Tuple[int, int, int], tuple] = {}
         self._dec_ctx: Optional[int] = None  # host bound on decode context (sizes the split grid)
 
@@ -462,9 +484,11 @@ class LlamaTP:
             pl = pos.long()
             explicit_slots = torch.where(pl < lens.long()[b], slot_ids.long()[b] * self.max_seq + pl,
                                          torch.full_like(pl, -1)).to(torch.int32)
-        # decode split size: 64 rows measured best from batch 1 to 32 (a single 256-row split per
-        # kv head, which skips the combine launch, was 1.6 % slower at batch 1)
-        dec_chunk = 64
+        # decode split size: 64 rows measured best from batch 1 to 32, at TP = 1 and on an emulated
+        # TP = 8 rank (one KV head).  A single 256-row split per KV head (no combine launch) was
+        # 1.6 % slower at batch 1, and one 8-wave block walking a whole <= 1024 context in passes
+        # was 26 % slower at TP = 8 (latency-bound on one CU) -- profiles/r1_llama_decode_sweep.jsonl.
+        dec_chunk = self.dec_chunk if self.dec_chunk > 0 else 64
         r = self._embed(ids.reshape(-1))  # residual stream (bf16)
         delta = None
 

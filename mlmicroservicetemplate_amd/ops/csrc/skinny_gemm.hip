@@ -346,12 +346,18 @@ __global__ __launch_bounds__(256) void skinny_finish_kernel(const SkArgs s) {
 
 }  // namespace
 
-int g_skinny_no_lds = 0;  // A/B switch for probes (mls_skinny_set_variant)
+int g_skinny_no_lds = 0;     // A/B switch for probes (mls_skinny_set_variant)
+int g_skinny_max_split = 0;  // cap on the automatic cross-block K split (0: none)
 
 extern "C" {
 
 int mls_skinny_set_variant(int no_lds) {
   g_skinny_no_lds = no_lds;
+  return 0;
+}
+
+int mls_skinny_set_max_split(int cap) {
+  g_skinny_max_split = cap;
   return 0;
 }
 
@@ -390,7 +396,12 @@ int mls_skinny_gemm_norm(const void* A, const void* A2, void* A_out, const void*
   const int ksteps = (K + 31) / 32;
   if (nsplit <= 0) {  // 8 waves split K inside a block; split across blocks only below 256 blocks
     nsplit = 1;
-    while (tiles * nsplit < 256 && ksteps / (nsplit * 2) >= 32) nsplit *= 2;
+    // M <= 4 with >= 32 column tiles: never split -- the finish launch costs more than the idle
+    // CUs (emulated TP = 8 rank, batch 1: 1.55 -> 1.44 ms/token; TP = 1 unchanged, its GEMMs
+    // already have >= 256 tiles).  At M = 8 the split still wins (1.67 vs 1.73 ms/token).
+    const bool no_split = M <= 4 && tiles >= 32;
+    while (!no_split && tiles * nsplit < 256 && ksteps / (nsplit * 2) >= 32) nsplit *= 2;
+    if (g_skinny_max_split > 0 && nsplit > g_skinny_max_split) nsplit = g_skinny_max_split;
   }
   if (nsplit > 1 && (ws == nullptr || ws_bytes < (size_t)nsplit * M * (N + 1) * 4)) nsplit = 1;
   s.nsplit = nsplit;

@@ -97,3 +97,17 @@ def test_generate_rejects_bad_lengths():
     for lens in ([11, 3], [0, 3], [5]):
         with pytest.raises(ValueError):
             m.generate(ids, torch.tensor(lens), GenParams(max_new_tokens=2))
+
+
+def test_shard_emulation_comm_runs_one_rank_of_tp():
+    """The bench-only stub comm drives one TP shard through prefill + decode without a process
+    group (shapes of a tp=4 rank; outputs are in-vocab ids)."""
+    from mlmicroservicetemplate_amd.models.llama import ShardEmulationComm
+
+    cfg = tiny_config(**CFG)
+    p = init_llama_shard(cfg, 4, 0, seed=1)
+    m = LlamaTP(p, cfg, tp=4, rank=0, comm=ShardEmulationComm(4), max_batch=4, max_seq=64)
+    ids, lens = _prompts()
+    out = m.generate(ids, lens, GenParams(max_new_tokens=4))
+    assert out.shape == (3, 4)
+    assert int(out.min()) >= 0 and int(out.max()) < cfg.vocab

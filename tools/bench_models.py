@@ -60,13 +60,20 @@ def bench_bert(args):
 
 
 def bench_llama(args):
-    from mlmicroservicetemplate_amd.models.llama import LLAMA3_8B, LlamaTP, init_llama_shard
+    """``--emulate-tp N``: rank 0's shard of a TP=N model with the collectives stubbed out
+    (:class:`ShardEmulationComm`) -- the per-rank kernel time of config 5 on one GPU."""
+    from mlmicroservicetemplate_amd.models.llama import LLAMA3_8B, LlamaTP, ShardEmulationComm, init_llama_shard
 
     dev = torch.device("cuda:0")
     t0 = time.time()
-    p = init_llama_shard(LLAMA3_8B, 1, 0, seed=0, device=dev)
-    m = LlamaTP(p, LLAMA3_8B, backend="fused", device=dev, max_batch=max(args.batches), max_seq=2048)
-    print(json.dumps({"bench": "llama3-8b", "init_s": round(time.time() - t0, 1)}), flush=True)
+    tp = args.emulate_tp
+    p = init_llama_shard(LLAMA3_8B, tp, 0, seed=0, device=dev)
+    comm = ShardEmulationComm(tp) if tp > 1 else None
+    m = LlamaTP(p, LLAMA3_8B, tp=tp, rank=0, comm=comm, backend="fused", device=dev, max_batch=max(args.batches),
+                max_seq=2048)
+    print(json.dumps({"bench": "llama3-8b", "tp": tp, "collectives": "stubbed" if tp > 1 else "none",
+                      "skinny_max_split": args.skinny_max_split,
+                      "init_s": round(time.time() - t0, 1)}), flush=True)
     for B in args.batches:
         S = args.prompt
         ids = torch.randint(1000, 100000, (B, S), device=dev, dtype=torch.int32)
@@ -91,7 +98,7 @@ def bench_llama(args):
             m.decode_step(tok, cur, 1, max_ctx=S + 1)
         torch.cuda.synchronize()
         dec = (time.perf_counter() - t2) / n
-        print(json.dumps({"bench": "llama3-8b", "tp": 1, "batch": B, "prompt": S,
+        print(json.dumps({"bench": "llama3-8b", "tp": tp, "batch": B, "prompt": S,
                           "prefill_ms": round(pre * 1e3, 2), "prefill_tok_s": round(B * S / pre, 1),
                           "decode_ms_per_step": round(dec * 1e3, 3), "decode_tok_s": round(B / dec, 1)}), flush=True)
 
@@ -135,7 +142,13 @@ def main():
     ap.add_argument("--seqs", type=int, nargs="+", default=[128])
     ap.add_argument("--prompt", type=int, default=512)
     ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--emulate-tp", type=int, default=1)
+    ap.add_argument("--skinny-max-split", type=int, default=0)
     args = ap.parse_args()
+    if args.skinny_max_split:
+        from mlmicroservicetemplate_amd.ops import _lib
+
+        _lib.lib().mls_skinny_set_max_split(args.skinny_max_split)
     {"bert": bench_bert, "llama": bench_llama, "llama-serve": bench_llama_serve}[args.which](args)
 
 
