@@ -176,6 +176,9 @@ class Settings:
     CONTINUOUS_BATCHING: bool = True  # /generate: sequences join / leave the decode batch every step
     MAX_SEQ_LEN: int = 8192
     # --- HTTP ---
+    FRONTEND: str = "python"  # python (FastAPI/uvicorn) | native (C++ epoll server + C++ batcher)
+    IO_THREADS: int = 4  # native front end: epoll I/O threads per serving process
+    DECODE_WORKERS: int = 4  # native front end: Python threads decoding non-raw uploads (JPEG/PNG)
     CORS_ORIGINS: List[str] = field(default_factory=lambda: list(DEFAULT_CORS_ORIGINS))
     MAX_UPLOAD_BYTES: int = 64 * 1024 * 1024
     LOG_LEVEL: str = "info"
@@ -245,6 +248,8 @@ class Settings:
             raise ValueError("GPUS must be >= 0 and TP >= 1")
         if self.DTYPE not in ("bf16", "fp32", "fp16"):
             raise ValueError(f"unsupported DTYPE {self.DTYPE}")
+        if self.FRONTEND not in ("python", "native"):
+            raise ValueError(f"FRONTEND must be python or native, not {self.FRONTEND!r}")
         self.GRAPH_BUCKETS = sorted(set(int(b) for b in self.GRAPH_BUCKETS if int(b) > 0))
         if not self.GRAPH_BUCKETS or self.GRAPH_BUCKETS[-1] < self.MAX_BATCH:
             self.GRAPH_BUCKETS = sorted(set(self.GRAPH_BUCKETS + [self.MAX_BATCH]))

@@ -180,7 +180,7 @@ class GpuEngine:
         n = len(samples)
         if n == 0:
             raise ValueError("empty batch")
-        bucket = pick_bucket(n, self.buckets)
+        pick_bucket(n, self.buckets)  # validate before taking a slot
         slot = self._free.get()  # blocks while `inflight` batches are outstanding
         try:
             with tracing.range(f"{self.name}.stage"):
@@ -201,6 +201,34 @@ class GpuEngine:
                 else:
                     for i, s in enumerate(samples):
                         dst[i] = s
+        except BaseException as e:
+            self._free.put(slot)
+            self.last_error = f"{type(e).__name__}: {e}"
+            raise
+        return self.launch(slot, n)
+
+    # -- zero-copy path: the caller fills the slot's pinned buffer itself (native front end) --
+    def acquire(self, timeout: Optional[float] = None) -> Optional[_Slot]:
+        """Take a free slot (``None`` on timeout); fill ``host_buffer(slot)[:n]`` then :meth:`launch`
+        it, or hand it back with :meth:`release`."""
+        try:
+            return self._free.get(timeout=timeout)
+        except queue.Empty:
+            return None
+
+    def release(self, slot: _Slot) -> None:
+        self._free.put(slot)
+
+    @staticmethod
+    def host_buffer(slot: _Slot) -> np.ndarray:
+        """The slot's pinned host input as a writable numpy view ``[max_batch, *sample_shape]``."""
+        return slot.host_in.numpy()
+
+    def launch(self, slot: _Slot, n: int) -> Ticket:
+        """Enqueue H2D -> graph replay -> D2H for the first ``n`` rows already in the slot's pinned
+        buffer.  Consumes the slot (returned to the free list by :meth:`Ticket.wait`)."""
+        try:
+            bucket = pick_bucket(n, self.buckets)
             with self._enqueue_lock, torch.cuda.device(self.device):
                 with tracing.range(f"{self.name}.enqueue"):
                     with torch.cuda.stream(self.s_h2d):

@@ -50,7 +50,7 @@ def default_devices(settings, world_size: int = 1, local_rank: int = 0) -> List[
     except Exception:
         ngpu = 0
     model = str(getattr(settings, "MODEL", ""))
-    if not ngpu or int(getattr(settings, "GPUS", 1)) <= 0 or model in ("stub", "identity") or "." in model:
+    if not ngpu or int(getattr(settings, "GPUS", 1)) <= 0 or model in ("stub", "identity", "toy_classifier") or "." in model:
         return []
     import os
 
@@ -87,6 +87,17 @@ class ModelPlugin:
     # --- /generate ---
     def generate(self, request: dict) -> dict:
         raise NotImplementedError(f"model {self.name!r} does not support /generate")
+
+    # --- native front end (FRONTEND=native, frontend/native.py) ---
+    def native_spec(self) -> Optional[dict]:
+        """``{"sample_bytes": int, "result": "topk" | "json"}`` when every request is one
+        fixed-size sample the C++ batcher can pack; ``None`` = Python front end only."""
+        return None
+
+    def native_replicas(self) -> List[Any]:
+        """After ``init``: one replica per engine, with ``acquire / release / buffer / run``
+        (``frontend.native.EngineReplica`` / ``HostReplica``)."""
+        raise NotImplementedError
 
     def replica_probes(self) -> List[Optional[Callable[[], bool]]]:
         """Optional per-replica health probes for the watchdog (same order as :meth:`replicas`)."""

@@ -175,14 +175,84 @@ class ResNet50Plugin(ModelPlugin):
         return out
 
     def postprocess(self, out: Any) -> dict:
-        vals, idx = out
-        names = [self.labels[int(i)] for i in idx]
-        return {"classes": names, "result": {n: float(v) for n, v in zip(names, vals)}}
+        return topk_result(self.labels, *out)
+
+    def native_spec(self) -> dict:
+        return {"sample_bytes": 224 * 224 * 3, "result": "topk"}
+
+    def native_replicas(self):
+        from ..frontend.native import EngineReplica
+
+        return [EngineReplica(e) for e in self.engines]
 
     def describe(self) -> dict:
         d = super().describe()
         d["engines"] = [e.stats() for e in self.engines]
         return d
+
+
+def topk_result(labels: List[str], vals, idx) -> dict:
+    """Classifier result dict (``classes`` + ``result`` map, the reference stub's shape,
+    reference ``model.py:31``) from one row of top-k probabilities / class ids."""
+    names = [labels[int(i)] if 0 <= int(i) < len(labels) else f"class_{int(i)}" for i in idx]
+    return {"classes": names, "result": {n: float(v) for n, v in zip(names, vals)}}
+
+
+@register("toy_classifier")
+class ToyClassifierPlugin(ModelPlugin):
+    """A CPU image classifier on tiny fixed-shape inputs (``TOY_SIZE``²x3 uint8 -> 10 classes,
+    fixed random linear layer + softmax + top-k): the batched fixed-shape serving path of
+    configs 2/4 -- either front end, micro-batching, raw and decoded uploads -- without a GPU."""
+
+    name = "toy_classifier"
+    batched = True
+    task = "image"
+    NUM_CLASSES = 10
+
+    def __init__(self, size: int = 8):
+        self.size = size
+        self.labels = [f"class_{i}" for i in range(self.NUM_CLASSES)]
+        self.topk = 5
+        self.w = None
+        self.max_batch = 32
+        self.inflight = 2
+
+    def init(self, ctx: PluginContext) -> None:
+        s = ctx.settings
+        self.topk = min(int(s.TOPK), self.NUM_CLASSES)
+        self.max_batch = int(s.MAX_BATCH)
+        self.inflight = int(s.INFLIGHT)
+        rng = np.random.default_rng(int(s.SEED))
+        self.w = (rng.standard_normal((self.NUM_CLASSES, self.size * self.size * 3)) / 8).astype(np.float32)
+
+    def scores(self, x: np.ndarray):
+        """uint8 ``[n, size, size, 3]`` -> (probs fp32 ``[n, k]``, ids int32 ``[n, k]``)."""
+        logits = (x.reshape(len(x), -1).astype(np.float32) / 255.0) @ self.w.T
+        p = np.exp(logits - logits.max(1, keepdims=True))
+        p /= p.sum(1, keepdims=True)
+        idx = np.argsort(-p, axis=1, kind="stable")[:, : self.topk].astype(np.int32)
+        return np.take_along_axis(p, idx, 1).astype(np.float32), idx
+
+    def preprocess(self, part: Part) -> Any:
+        return decode_image(part.data, part.content_type or "", size=self.size, resize=self.size)
+
+    def replicas(self):
+        def run_batch(samples):
+            v, i = self.scores(np.stack(samples))
+            return [(v[j], i[j]) for j in range(len(samples))]
+
+        return [run_batch]
+
+    def postprocess(self, out: Any) -> dict:
+        return topk_result(self.labels, *out)
+
+    def native_spec(self) -> dict:
+        return {"sample_bytes": self.size * self.size * 3, "result": "topk"}
+
+    def native_replicas(self):
+        from ..frontend.native import HostReplica
+
+        return [HostReplica(self.scores, (self.size, self.size, 3), self.max_batch, self.inflight)]
 
 
 def _register_optional() -> None:

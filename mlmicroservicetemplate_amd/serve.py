@@ -32,7 +32,7 @@ from .config import Settings, load_dotenv
 
 logger = logging.getLogger("mlsamd.serve")
 
-DP_MODELS = {"resnet50", "bert", "identity", "stub"}
+DP_MODELS = {"resnet50", "bert", "identity", "stub", "toy_classifier"}
 
 
 def free_port() -> int:
@@ -55,7 +55,7 @@ def reuseport_socket(host: str, port: int) -> socket.socket:
 def _overrides_from_args(args) -> Dict[str, object]:
     o = {}
     for k in ("MODEL", "PORT", "GPUS", "TP", "MAX_BATCH", "MAX_WAIT_US", "BACKEND", "NAME", "SERVER_PORT",
-              "WORKERS_PER_GPU"):
+              "WORKERS_PER_GPU", "FRONTEND", "IO_THREADS"):
         v = getattr(args, k.lower(), None)
         if v is not None:
             o[k] = v
@@ -89,11 +89,19 @@ def run_rank(args) -> int:
         plugin.init(ctx)
         mdist.all_reduce_health(True)  # matches rank 0's readiness all-reduce (X6)
         return plugin.follower_loop() if hasattr(plugin, "follower_loop") else 0
+    fd = os.environ.get("MLS_LISTEN_FD")
+    if settings.FRONTEND == "native":
+        from .frontend.native import NativeService, supports_native
+
+        if supports_native(plugin):
+            svc = NativeService(settings, plugin, ctx, host=args.host,
+                                listen_fd=int(fd) if fd is not None else None)
+            return svc.serve_forever()
+        logger.warning("model %s has no native front-end path; serving it with FRONTEND=python", plugin.name)
     app = create_app(settings, plugin, ctx)
     config = uvicorn.Config(app, host=args.host, port=settings.PORT, log_level=settings.LOG_LEVEL.lower(),
                             lifespan="on", timeout_graceful_shutdown=10)
     server = uvicorn.Server(config)
-    fd = os.environ.get("MLS_LISTEN_FD")
     if fd is not None:
         sock = socket.socket(fileno=int(fd))
         server.run(sockets=[sock])
@@ -227,6 +235,8 @@ def build_parser() -> argparse.ArgumentParser:
         p.add_argument("--max-batch", type=int)
         p.add_argument("--max-wait-us", type=int)
         p.add_argument("--backend")
+        p.add_argument("--frontend", choices=["python", "native"])
+        p.add_argument("--io-threads", type=int)
         p.add_argument("--name")
         p.add_argument("--server-port", type=int)
         p.add_argument("--no-register", action="store_true")

@@ -96,3 +96,64 @@ def test_llama_generate_service_fused(tmp_path):
         want = m.generate(torch.tensor([ids], device="cuda"), torch.tensor([len(ids)], device="cuda"),
                           GenParams(6))[0].tolist()
         assert res["token_ids"] == want[: res["num_tokens"]]
+
+
+def test_resnet50_native_frontend_matches_python_frontend():
+    """FRONTEND=native: C++ HTTP + C++ batcher writing straight into the engine slot's pinned
+    buffer -> same top-5 as the FastAPI path for raw and PNG uploads, and the C++ load generator
+    drives it without errors."""
+    import json
+    import subprocess
+
+    import requests
+
+    from mlmicroservicetemplate_amd.api.multipart import encode_multipart
+    from mlmicroservicetemplate_amd.config import Settings
+    from mlmicroservicetemplate_amd.frontend import build as fbuild
+    from mlmicroservicetemplate_amd.frontend.native import NativeService
+    from mlmicroservicetemplate_amd.plugins.base import PluginContext
+    from mlmicroservicetemplate_amd.plugins.builtin import ResNet50Plugin
+
+    rng = np.random.default_rng(0)
+    raws = [rng.integers(0, 256, (224, 224, 3), dtype=np.uint8) for _ in range(6)]
+    pngs = [_png(i) for i in range(3)]
+
+    def ups():
+        out = []
+        for a in raws:
+            out.append(encode_multipart({"image_file": ("x.rgb", a.tobytes(), "application/octet-stream")}))
+        for b in pngs:
+            out.append(encode_multipart({"image_file": ("x.png", b, "image/png")}))
+        return out
+
+    with _client(MODEL="resnet50", MAX_BATCH=8, GRAPH_BUCKETS=[1, 2, 4, 8]) as c:
+        _wait(c)
+        py = [c.post("/predict", content=b, headers={"content-type": ct}).json()["result"] for b, ct in ups()]
+    s = Settings.load(env_file=None, environ={}, overrides={"REGISTER": False, "GPUS": 1, "MODEL": "resnet50",
+                                                            "MAX_BATCH": 8, "GRAPH_BUCKETS": [1, 2, 4, 8],
+                                                            "MAX_WAIT_US": 2000, "IO_THREADS": 2})
+    svc = NativeService(s, ResNet50Plugin(), PluginContext(settings=s, devices=["cuda:0"]), host="127.0.0.1", port=0)
+    svc.start()
+    try:
+        url = f"http://127.0.0.1:{svc.port}"
+        t0 = time.time()
+        while requests.get(url + "/status").status_code != 200:
+            assert time.time() - t0 < 300 and "error" not in requests.get(url + "/status").json()
+            time.sleep(0.1)
+        with ThreadPoolExecutor(9) as ex:
+            outs = list(ex.map(lambda u: requests.post(url + "/predict", data=u[0], headers={"content-type": u[1]},
+                                                       timeout=60), ups()))
+        assert all(o.status_code == 200 for o in outs), [o.text for o in outs]
+        nat = [o.json()["result"] for o in outs]
+        for a, b in zip(py, nat):
+            assert a["classes"] == b["classes"]
+            for k in a["result"]:
+                assert abs(a["result"][k] - b["result"][k]) < 1e-5
+        lg = subprocess.run([fbuild.loadgen_path(), "--port", str(svc.port), "--conns", "32", "--threads", "2",
+                             "--duration", "2", "--warmup", "0.5"], capture_output=True, text=True, timeout=60)
+        res = json.loads(lg.stdout)
+        assert res["errors"] == 0 and res["ok"] > 100, res
+        st = svc.srv.stats()
+        assert st["samples"] > st["batches"]  # requests were micro-batched
+    finally:
+        svc.stop()

@@ -1,0 +1,82 @@
+"""End-to-end HTTP throughput of a serving process: starts ``python -m mlmicroservicetemplate_amd
+serve`` (any model / front end / workers), waits for ``/status``, drives ``POST /predict`` with the
+native closed-loop generator (``frontend/_native/mls_loadgen``) at each ``--conns`` level, and prints
+one JSON line per level (requests/s, p50/p90/p99 latency, server config).
+
+    python tools/http_bench.py --model resnet50 --frontend native --conns 64 256 --duration 10
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import signal
+import subprocess
+import sys
+import time
+
+import requests
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from mlmicroservicetemplate_amd.frontend import build as fbuild  # noqa: E402
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--frontend", default="native", choices=["native", "python"])
+    ap.add_argument("--workers-per-gpu", type=int, default=1)
+    ap.add_argument("--io-threads", type=int, default=4)
+    ap.add_argument("--port", type=int, default=5099)
+    ap.add_argument("--conns", type=int, nargs="+", default=[64, 256])
+    ap.add_argument("--client-threads", type=int, default=4)
+    ap.add_argument("--duration", type=float, default=10)
+    ap.add_argument("--warmup", type=float, default=2)
+    ap.add_argument("--bytes", type=int, default=224 * 224 * 3)
+    ap.add_argument("--ready-timeout", type=float, default=300)
+    args = ap.parse_args()
+    fbuild.build()
+    cmd = [sys.executable, "-m", "mlmicroservicetemplate_amd", "serve", "--model", args.model, "--frontend",
+           args.frontend, "--port", str(args.port), "--host", "127.0.0.1", "--no-register", "--env-file", "/nonexistent",
+           "--workers-per-gpu", str(args.workers_per_gpu), "--io-threads", str(args.io_threads)]
+    srv = subprocess.Popen(cmd, cwd=ROOT, env=dict(os.environ, PYTHONPATH=ROOT), start_new_session=True)
+    url = f"http://127.0.0.1:{args.port}"
+    try:
+        t0 = time.time()
+        while True:
+            if srv.poll() is not None:
+                raise SystemExit(f"server exited with {srv.returncode}")
+            try:
+                r = requests.get(url + "/status", timeout=2)
+                if r.status_code == 200:
+                    break
+                if "error" in r.json():
+                    raise SystemExit(f"init failed: {r.json()}")
+            except requests.RequestException:
+                pass
+            if time.time() - t0 > args.ready_timeout:
+                raise SystemExit("server not ready")
+            print(f"waiting for {url}/status ({time.time() - t0:.0f}s)", file=sys.stderr, flush=True)
+            time.sleep(1)
+        for conns in args.conns:
+            out = subprocess.run([fbuild.loadgen_path(), "--port", str(args.port), "--conns", str(conns),
+                                  "--threads", str(args.client_threads), "--duration", str(args.duration),
+                                  "--warmup", str(args.warmup), "--bytes", str(args.bytes)],
+                                 capture_output=True, text=True, timeout=args.duration + args.warmup + 60)
+            res = json.loads(out.stdout)
+            res.update({"model": args.model, "frontend": args.frontend, "workers_per_gpu": args.workers_per_gpu,
+                        "io_threads": args.io_threads, "gpus": 1})
+            print(json.dumps(res), flush=True)
+    finally:
+        os.killpg(srv.pid, signal.SIGTERM)
+        try:
+            srv.wait(30)
+        except subprocess.TimeoutExpired:
+            os.killpg(srv.pid, signal.SIGKILL)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
