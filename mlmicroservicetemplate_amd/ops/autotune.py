@@ -31,7 +31,7 @@ def _time(fn, iters: int = 20, warmup: int = 3) -> float:
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with torch.cuda.graph(g, stream=s):  # the warm-up stream: its split-K counters exist
         for _ in range(iters):
             fn()
     g.replay()  # warm

@@ -25,6 +25,10 @@
 //  * XCD-aware bijective block remap so neighbouring tiles share an XCD's L2.
 #include "common.h"
 
+#include <cstdlib>
+#include <mutex>
+#include <unordered_map>
+
 namespace {
 
 constexpr int BK = 64;
@@ -57,6 +61,10 @@ struct ConvArgs {
   const bf16* x2;
   uint32_t x2_bytes;
   int H2, W2, Cin2, stride2, K1;
+  // split-K arrival counters (one per output tile, zero between launches): non-null -> the last
+  // slice block of each tile sums the slabs and runs the epilogue in-launch (no reduce kernel)
+  int* cnt;
+  uint32_t ws_bytes;  // slab extent (sc1 buffer accesses of the in-launch reduction)
 };
 
 int g_dbg_flags = 0;  // set via mls_set_debug_flags (tools/conv_ablate.py); 0 in production
@@ -75,6 +83,69 @@ template <int BKT>
 MLS_DEV int row_swz(int r) {
   if constexpr (BKT == 64) return r & 7;
   else return (r & 1) | ((r >> 1) & 2);
+}
+
+// Split-K finish for 8 outputs of row m starting at column n: sum the fp32 slabs, then
+// act(sum * scale + bias (+ res)) -> bf16.  SiLU-mul (gate/up interleaved in 8-column groups):
+// columns n..n+15 -> 8 outputs at n / 2.  Used by the separate reduce kernel and by the in-launch
+// reducer (the last-arriving slice block of a tile).
+typedef unsigned int u32x4v __attribute__((__vector_size__(16)));
+
+// SC1: the slabs were written through (sc1 stores) by other workgroups of this launch -> read them
+// with sc1 loads through `wr` (no acquire fence); otherwise plain loads (a later launch).
+template <bool SC1>
+MLS_DEV float4 slab_ld(const ConvArgs& a, rsrc_t wr, size_t idx) {
+  if constexpr (SC1) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(wr, (int)(idx * 4), 0, 16));
+  } else {
+    return *reinterpret_cast<const float4*>(a.ws + idx);
+  }
+}
+
+template <bool SC1>
+MLS_DEV void splitk_finish_chunk(const ConvArgs& a, rsrc_t wr, int m, int n, bool glu) {
+  float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (glu) {
+    float u[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int s = 0; s < a.splitk; ++s) {
+      const size_t i0 = ((size_t)s * a.M + m) * a.N + n;
+      const float4 g0 = slab_ld<SC1>(a, wr, i0), g1 = slab_ld<SC1>(a, wr, i0 + 4);
+      const float4 u0 = slab_ld<SC1>(a, wr, i0 + 8), u1 = slab_ld<SC1>(a, wr, i0 + 12);
+      v[0] += g0.x; v[1] += g0.y; v[2] += g0.z; v[3] += g0.w; v[4] += g1.x; v[5] += g1.y; v[6] += g1.z; v[7] += g1.w;
+      u[0] += u0.x; u[1] += u0.y; u[2] += u0.z; u[3] += u0.w; u[4] += u1.x; u[5] += u1.y; u[6] += u1.z; u[7] += u1.w;
+    }
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float gt = v[e] + (a.bias ? a.bias[n + e] : 0.f);
+      const float up = u[e] + (a.bias ? a.bias[n + 8 + e] : 0.f);
+      o[e] = silu(gt) * up;
+    }
+    st16(a.out + (size_t)m * a.ldo + (n >> 1), pack8(o));
+    return;
+  }
+  for (int s = 0; s < a.splitk; ++s) {
+    const size_t i0 = ((size_t)s * a.M + m) * a.N + n;
+    const float4 x0 = slab_ld<SC1>(a, wr, i0), x1 = slab_ld<SC1>(a, wr, i0 + 4);
+    v[0] += x0.x; v[1] += x0.y; v[2] += x0.z; v[3] += x0.w; v[4] += x1.x; v[5] += x1.y; v[6] += x1.z; v[7] += x1.w;
+  }
+  if (a.scale) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] *= a.scale[n + e];
+  }
+  if (a.bias) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += a.bias[n + e];
+  }
+  if (a.res) {
+    float r[8];
+    unpack8(ld16(a.res + (size_t)m * a.ldr + n), r);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += r[e];
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], a.act);
+  st16(a.out + (size_t)m * a.ldo + n, pack8(v));
 }
 
 // v2: LDS-DMA (buffer_load ... lds) into a STAGES-deep ring, counted vmcnt + raw s_barrier.
@@ -334,6 +405,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_kernel(const ConvArgs 
     }
     return;
   }
+  const rsrc_t wsr = make_rsrc(a.ws, a.cnt != nullptr ? a.ws_bytes : 0u);
 #pragma unroll
   for (int pass = 0; pass < EPI_PASSES; ++pass) {
     const int row_lo = pass * PASS_ROWS;
@@ -362,9 +434,14 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_kernel(const ConvArgs 
       const float4 v0 = *reinterpret_cast<const float4*>(Cs + (row - row_lo) * C_LD + c8 * 8);
       const float4 v1 = *reinterpret_cast<const float4*>(Cs + (row - row_lo) * C_LD + c8 * 8 + 4);
       if (a.splitk > 1) {
-        float* dst = a.ws + ((size_t)split * a.M + m) * a.N + n;
-        *reinterpret_cast<float4*>(dst) = v0;
-        *reinterpret_cast<float4*>(dst + 4) = v1;
+        const size_t widx = ((size_t)split * a.M + m) * a.N + n;
+        if (a.cnt != nullptr) {  // write-through: visible to this tile's reducer with no release fence
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v0), wsr, (int)(widx * 4), 0, 16);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v1), wsr, (int)(widx * 4 + 16), 0, 16);
+        } else {
+          *reinterpret_cast<float4*>(a.ws + widx) = v0;
+          *reinterpret_cast<float4*>(a.ws + widx + 4) = v1;
+        }
         continue;
       }
       float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
@@ -383,6 +460,31 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_kernel(const ConvArgs 
         continue;
       }
       st16(a.out + (size_t)m * a.ldo + n, pack8(v));
+    }
+  }
+  if (a.splitk > 1 && a.cnt != nullptr) {
+    // In-launch split-K reduction (guide §5 item 2): publish this slice's slab with one agent-scope
+    // release, take a ticket; the tile's last arriver acquires once and finishes the tile.
+    // sc1 (write-through) slabs: drained stores need no release fence, sc1 loads no acquire (guide
+    // §5 item 2, §6 Guideline 16 R1).
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(smem);  // the one LDS array (no second __shared__ object)
+    if (tid == 0) {
+      const int prev = __hip_atomic_fetch_add(a.cnt + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = prev == a.splitk - 1;
+      if (last) __hip_atomic_store(a.cnt + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
+      flag[0] = last;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+    const bool glu = a.act == ACT_SILU_MUL;
+    const int cpr = glu ? CPR / 2 : CPR;  // output chunks of 8 per tile row
+    const int cw = glu ? 16 : 8;          // input columns per chunk
+    for (int q = tid; q < BM * cpr; q += NT) {
+      const int row = q / cpr, c = q - (q / cpr) * cpr;
+      const int m = m0 + row, n = n0 + c * cw;
+      if (m < a.M && n < a.N) splitk_finish_chunk<true>(a, wsr, m, n, glu);
     }
   }
 }
@@ -630,45 +732,7 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(const ConvArgs a) 
   const long total = (long)a.M * nc;
   for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
     const int m = (int)(q / nc), c = (int)(q - (q / nc) * nc);
-    const int n = glu ? c * 16 : c * 8;
-    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0}, u[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int s = 0; s < a.splitk; ++s) {
-      const float* src = a.ws + ((size_t)s * a.M + m) * a.N + n;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += src[e];
-      if (glu) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) u[e] += src[8 + e];
-      }
-    }
-    if (glu) {
-      float o[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float gt = v[e] + (a.bias ? a.bias[n + e] : 0.f);
-        const float up = u[e] + (a.bias ? a.bias[n + 8 + e] : 0.f);
-        o[e] = silu(gt) * up;
-      }
-      st16(a.out + (size_t)m * a.ldo + (n >> 1), pack8(o));
-      continue;
-    }
-    if (a.scale) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] *= a.scale[n + e];
-    }
-    if (a.bias) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += a.bias[n + e];
-    }
-    if (a.res) {
-      float r[8];
-      unpack8(ld16(a.res + (size_t)m * a.ldr + n), r);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += r[e];
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], a.act);
-    st16(a.out + (size_t)m * a.ldo + n, pack8(v));
+    splitk_finish_chunk<false>(a, make_rsrc(nullptr, 0), m, glu ? c * 16 : c * 8, glu);
   }
 }
 
@@ -759,6 +823,39 @@ void launch_persistent(int cfg, hipStream_t st, const ConvArgs& a) {
   }
 }
 
+// Split-K arrival counters: one zeroed array per HIP stream, reset by each tile's last arriver,
+// so it is zero again whenever the next launch on that stream starts.  A launch captured into a
+// hipGraph keeps the capture stream's array; that is safe under the same rule the split-K slabs
+// (StreamWorkspace, keyed by stream) already follow: graphs captured on one stream are replayed on
+// that stream only (the engine's per-slot streams).  Arrays are allocated outside capture only (the
+// eager warm-up); a stream without one uses the separate reduce kernel.  MLS_SPLITK_INLAUNCH=0
+// disables the in-launch path.
+constexpr int kStreamCounters = 1 << 16;
+
+int* splitk_counters(hipStream_t st, long ntiles) {
+  static std::mutex mu;
+  static std::unordered_map<hipStream_t, int*> arrays;
+  static const bool enabled = [] {
+    const char* e = getenv("MLS_SPLITK_INLAUNCH");
+    return !(e && e[0] == '0');
+  }();
+  if (!enabled || ntiles <= 0 || ntiles > kStreamCounters) return nullptr;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = arrays.find(st);
+  if (it != arrays.end()) return it->second;
+  if (cs != hipStreamCaptureStatusNone) return nullptr;  // no allocation inside a capture
+  int* p = nullptr;
+  if (hipMalloc(&p, kStreamCounters * sizeof(int)) != hipSuccess) return nullptr;
+  if (hipMemset(p, 0, kStreamCounters * sizeof(int)) != hipSuccess) {
+    (void)hipFree(p);
+    return nullptr;
+  }
+  arrays[st] = p;
+  return p;
+}
+
 int launch_conv(ConvArgs a, int mode, int cfg, int splitk, size_t ws_bytes, hipStream_t st) {
   if (a.act == ACT_SILU_MUL && a.N % 16 != 0) return MLS_BAD_ARG;
   if (a.N % 8 != 0 || a.M <= 0 || a.N <= 0 || a.K <= 0 || a.K % 8 != 0) return MLS_BAD_ARG;
@@ -808,8 +905,14 @@ int launch_conv(ConvArgs a, int mode, int cfg, int splitk, size_t ws_bytes, hipS
     a.r_bytes = (uint32_t)rb;
   }
   const int bm = kCfgs[cfg].bm, bn = kCfgs[cfg].bn;
-  const long ntiles = (long)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn) * splitk;
+  const long otiles = (long)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
+  const long ntiles = otiles * splitk;
   if (ntiles > 0x7fffffffL) return MLS_BAD_ARG;
+  a.cnt = nullptr;
+  if (splitk > 1 && (size_t)splitk * a.M * a.N * sizeof(float) < 0x7FFFFFF0ull) {
+    a.cnt = splitk_counters(st, otiles);
+    a.ws_bytes = (uint32_t)((size_t)splitk * a.M * a.N * sizeof(float));
+  }
   dim3 grid((unsigned)ntiles);
   switch (mode) {
     case MODE_1X1: launch_mode<MODE_1X1>(cfg, grid, st, a); break;
@@ -818,7 +921,7 @@ int launch_conv(ConvArgs a, int mode, int cfg, int splitk, size_t ws_bytes, hipS
     case MODE_DUAL: launch_mode<MODE_DUAL>(cfg, grid, st, a); break;
     default: return MLS_UNSUPPORTED;
   }
-  if (splitk > 1) {
+  if (splitk > 1 && a.cnt == nullptr) {
     const long total = (long)a.M * (a.N / 8);
     int blocks = (int)((total + 255) / 256);
     if (blocks > 4096) blocks = 4096;
