@@ -31,7 +31,7 @@ sys.path.insert(0, ROOT)
 
 from mlmicroservicetemplate_amd.parallel import dist as mdist  # noqa: E402
 
-EAGER_BASELINE_IMG_S = 7754.8  # stock PyTorch-ROCm (MIOpen) bs=32 bf16, 1x MI355X: profiles/r1_eager_baseline_miopen.jsonl
+EAGER_BASELINE_IMG_S = 11249.9  # stock PyTorch-ROCm (MIOpen) ops in the same engine, bs=32 bf16, 5 in flight, 1x MI355X: profiles/r1_bench_eager_inflight.jsonl
 
 
 def log(*a):

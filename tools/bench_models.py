@@ -38,7 +38,7 @@ def bench_bert(args):
                     v, i = torch.topk(logits.float(), 2, dim=-1)
                     return v, i.to(torch.int32)
 
-                eng = GpuEngine(fwd, dev, (2 * S + 1,), torch.int32, buckets=[B], inflight=3, concurrent=True)
+                eng = GpuEngine(fwd, dev, (2 * S + 1,), torch.int32, buckets=[B], inflight=args.inflight, concurrent=True)
                 eng.warmup(capture=True)
                 for _ in range(5):
                     eng.run(packed)
@@ -142,6 +142,7 @@ def main():
     ap.add_argument("--seqs", type=int, nargs="+", default=[128])
     ap.add_argument("--prompt", type=int, default=512)
     ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--inflight", type=int, default=5, help="bert: batches in flight (co-running engine slots)")
     ap.add_argument("--emulate-tp", type=int, default=1)
     ap.add_argument("--skinny-max-split", type=int, default=0)
     args = ap.parse_args()
