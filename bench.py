@@ -85,6 +85,9 @@ def main(argv=None) -> int:
     ndev = max(1, torch.cuda.device_count())
     device = torch.device("cuda", info.local_rank % ndev)
     torch.cuda.set_device(device)
+    from mlmicroservicetemplate_amd.parallel.affinity import bind_to_gpu
+
+    bind_to_gpu(device.index, world)  # host staging on the GPU's NUMA node (multi-rank runs)
 
     from mlmicroservicetemplate_amd.engine.worker import GpuEngine
     from mlmicroservicetemplate_amd.models import resnet

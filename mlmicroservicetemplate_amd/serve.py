@@ -79,6 +79,10 @@ def run_rank(args) -> int:
     info = mdist.env_info()
     devices = default_devices(settings, info.world_size, info.local_rank)
     ngpu = len(devices)
+    if ngpu == 1:
+        from .parallel.affinity import bind_to_gpu
+
+        bind_to_gpu(int(devices[0].split(":")[1]), max(info.world_size, int(settings.GPUS)))
     if info.world_size > 1:
         mdist.init_distributed(device_id=info.local_rank if ngpu else None)
     ctx = PluginContext(settings=settings, rank=info.rank, world_size=info.world_size, local_rank=info.local_rank,
