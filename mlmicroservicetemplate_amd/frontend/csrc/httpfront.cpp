@@ -344,7 +344,10 @@ class Server {
       t->ep = epoll_create1(EPOLL_CLOEXEC);
       t->efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
       epoll_event ev{};
-      ev.events = EPOLLIN | EPOLLEXCLUSIVE;  // one thread woken per incoming connection
+      // own socket: wake one I/O thread per connection.  A socket inherited from the launcher is
+      // shared by every serving process on the port: wake them all (new connections are rare with
+      // keep-alive) so the accepting process is random instead of always the same waiter.
+      ev.events = own_lfd_ ? (EPOLLIN | EPOLLEXCLUSIVE) : EPOLLIN;
       ev.data.u64 = 0;
       epoll_ctl(t->ep, EPOLL_CTL_ADD, lfd_, &ev);
       ev.events = EPOLLIN;

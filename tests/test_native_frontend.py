@@ -351,3 +351,40 @@ def test_launcher_serves_native_and_stops_on_sigterm():
     finally:
         if proc.poll() is None:
             os.killpg(proc.pid, signal.SIGKILL)
+
+
+@pytest.mark.timeout(120)
+def test_two_rank_native_service_shares_the_port():
+    """GPUS=2 (gloo on CPU): two ranks, each a native front end on the launcher's shared listening
+    socket (EPOLLEXCLUSIVE accept across processes)."""
+    port = _free_port()
+    env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    proc = subprocess.Popen([sys.executable, "-m", "mlmicroservicetemplate_amd", "serve", "--model", "toy_classifier",
+                             "--frontend", "native", "--gpus", "2", "--port", str(port), "--host", "127.0.0.1",
+                             "--no-register", "--env-file", "/nonexistent"], cwd=ROOT, env=env, start_new_session=True)
+    try:
+        url = f"http://127.0.0.1:{port}"
+        deadline = time.time() + 90
+        ready = False
+        while time.time() < deadline and not ready:
+            try:
+                ready = requests.get(url + "/status", timeout=1).status_code == 200
+            except requests.RequestException:
+                time.sleep(0.2)
+        assert ready
+        ranks = set()
+        for i in range(60):
+            info = requests.get(url + "/info", timeout=5).json()  # new connection each time
+            ranks.add(info["rank"])
+            assert info["world_size"] == 2
+            r = requests.post(url + "/predict", **raw_upload(img(i)), timeout=5)
+            assert r.status_code == 200
+            if len(ranks) == 2:
+                break
+        assert ranks == {0, 1}
+    finally:
+        os.killpg(proc.pid, signal.SIGTERM)
+        try:
+            proc.wait(30)
+        except subprocess.TimeoutExpired:
+            os.killpg(proc.pid, signal.SIGKILL)
