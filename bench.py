@@ -108,10 +108,14 @@ def main(argv=None) -> int:
     rng = np.random.default_rng(1234 + info.rank)
     pool = [[rng.integers(0, 256, (224, 224, 3), dtype=np.uint8) for _ in range(args.batch)] for _ in range(4)]
 
+    host_s = [0.0]  # host time spent inside submit() (staging copy + enqueue): diagnostics
+
     def run_steps(n, lat):
         pending = []
         for i in range(n):
+            t0 = time.perf_counter()
             pending.append(engine.submit(pool[i % len(pool)]))
+            host_s[0] += time.perf_counter() - t0
             if len(pending) >= args.inflight:
                 t = pending.pop(0)
                 t.wait()
@@ -121,6 +125,7 @@ def main(argv=None) -> int:
             lat.append(time.perf_counter() - t.t_submit)
 
     run_steps(args.warmup, [])
+    host_s[0] = 0.0
     lat: list = []
     mdist.barrier()
     torch.cuda.synchronize(device)
@@ -160,6 +165,7 @@ def main(argv=None) -> int:
             "per_gpu_requests_per_s": round(value / world, 1),
             "vs_pytorch_eager_per_gpu": round(value / world / EAGER_BASELINE_IMG_S, 3),
             "weight_broadcast_s": round(t_bcast, 3),
+            "host_submit_ms_per_step": round(host_s[0] * 1e3 / args.steps, 4),
         }
         print(json.dumps(out), flush=True)
     mdist.destroy()
