@@ -62,6 +62,7 @@ class ServingRuntime:
         self.router: Optional[ReplicaRouter] = None
         self.watchdog: Optional[ReplicaWatchdog] = None
         self.loop: Optional[asyncio.AbstractEventLoop] = None
+        self.reloader = None  # parallel.reload.ReloadCoordinator, after init
 
     # ---------------------------------------------------------------- lifecycle
     def init_model(self) -> None:
@@ -78,6 +79,10 @@ class ServingRuntime:
 
                 if not mdist.all_reduce_health(True):
                     raise RuntimeError("another rank failed to initialise")
+            if self.plugin.reload_spec() is not None:
+                from ..parallel.reload import ReloadCoordinator
+
+                self.reloader = ReloadCoordinator(self.plugin, self.ctx, self.settings)
         except BaseException as e:  # report, do not swallow (reference C6 defect)
             logger.exception("model init failed")
             self.state.mark_failed(e)
@@ -123,6 +128,8 @@ class ServingRuntime:
             await self.router.stop()
         self.state.shutdown.set()
         await run_in_threadpool(self.state.pool.shutdown, True)
+        if self.reloader is not None:
+            self.reloader.close()
         self.plugin.close()
 
     # ---------------------------------------------------------------- requests
@@ -342,6 +349,22 @@ def create_app(settings: Optional[Settings] = None, plugin: Optional[ModelPlugin
             raise PredictionException()
         result = await runtime.predict(part)
         return {"status": "success", "result": result}
+
+    @app.post("/admin/reload")
+    async def reload_weights(request: Request):
+        """Hot weight reload, in place under the captured hipGraphs; every DP rank over RCCL
+        (parallel/reload.py).  JSON ``{"weights": <safetensors path>}`` or ``{"seed": n}``."""
+        from ..parallel.reload import handle_reload_request
+
+        try:
+            payload = await request.json()
+        except Exception:
+            payload = None
+        if not state.ready_to_predict:
+            raise PredictionException()
+        code, body = await run_in_threadpool(handle_reload_request, runtime.reloader, settings,
+                                             dict(request.headers), payload)
+        return JSONResponse(status_code=code, content=body)
 
     @app.post("/generate")
     async def generate(request: Request):

@@ -24,6 +24,7 @@ first dim is the batch).
 """
 from __future__ import annotations
 
+import contextlib
 import logging
 import queue
 import threading
@@ -218,6 +219,26 @@ class GpuEngine:
 
     def release(self, slot: _Slot) -> None:
         self._free.put(slot)
+
+    @contextlib.contextmanager
+    def quiesce(self, timeout: Optional[float] = 120.0):
+        """Hold every slot: in-flight batches finish first, new ones wait until the block exits
+        (hot weight reload -- the captured graphs read the weights in place)."""
+        held: List[_Slot] = []
+        try:
+            deadline = None if timeout is None else time.monotonic() + timeout
+            while len(held) < len(self.slots):
+                left = None if deadline is None else max(0.0, deadline - time.monotonic())
+                try:
+                    held.append(self._free.get(timeout=left))
+                except queue.Empty:
+                    raise TimeoutError(f"{self.name}: in-flight batches did not drain") from None
+            torch.cuda.synchronize(self.device)
+            yield
+            torch.cuda.synchronize(self.device)
+        finally:
+            for sl in held:
+                self._free.put(sl)
 
     @staticmethod
     def host_buffer(slot: _Slot) -> np.ndarray:

@@ -148,6 +148,7 @@ class NativeService:
             form_field=plugin.form_field, cors_origins=list(settings.CORS_ORIGINS),
             request_timeout_s=float(settings.REQUEST_TIMEOUT_S), python_decode=True)
         self.replicas: List[Any] = []
+        self.reloader = None  # parallel.reload.ReloadCoordinator, after init
         self._stop = threading.Event()
         self._threads: List[threading.Thread] = []
         self._live_dispatchers = 0
@@ -185,6 +186,10 @@ class NativeService:
 
                 if not mdist.all_reduce_health(True):
                     raise RuntimeError("another rank failed to initialise")
+            if self.plugin.reload_spec() is not None:
+                from ..parallel.reload import ReloadCoordinator
+
+                self.reloader = ReloadCoordinator(self.plugin, self.ctx, self.settings)
             self.replicas = list(self.plugin.native_replicas())
             labels = getattr(self.plugin, "labels", None)
             if labels:
@@ -213,6 +218,8 @@ class NativeService:
         for t in self._threads:
             t.join(timeout=10)
         self.state.pool.shutdown(wait=True)
+        if self.reloader is not None:
+            self.reloader.close()
         self.plugin.close()
 
     def serve_forever(self) -> int:
@@ -286,7 +293,8 @@ class NativeService:
                 self.srv.respond(token, 500, _json({"status": "failure", "detail": f"{type(e).__name__}: {e}"}))
 
     # ---------------------------------------------------------------- Python-served routes
-    KNOWN = {"/": "GET", "/status": "GET", "/predict": "POST", "/health": "GET", "/info": "GET", "/metrics": "GET"}
+    KNOWN = {"/": "GET", "/status": "GET", "/predict": "POST", "/health": "GET", "/info": "GET", "/metrics": "GET",
+             "/admin/reload": "POST"}
 
     def _handle(self, token, method: str, path: str, query: str, headers: dict, body: bytes) -> None:
         srv = self.srv
@@ -300,6 +308,18 @@ class NativeService:
             srv.respond(token, 200, self.metrics_text().encode(), "text/plain; version=0.0.4; charset=utf-8")
         elif path == "/predict" and method == "POST":
             self._legacy_predict(token, query, headers, body)
+        elif path == "/admin/reload" and method == "POST":
+            from ..parallel.reload import handle_reload_request
+
+            if not self.state.ready_to_predict:
+                srv.respond(token, 503, _json({"status": "failure", "detail": "Model is not ready to receive predictions."}))
+                return
+            try:
+                payload = json.loads(body or b"null")
+            except ValueError:
+                payload = None
+            code, out = handle_reload_request(self.reloader, self.settings, headers, payload)
+            srv.respond(token, code, _json(out))
         elif path in self.KNOWN:
             srv.respond(token, 405, _json({"detail": "Method Not Allowed"}), headers=[("allow", self.KNOWN[path])])
         else:

@@ -216,6 +216,20 @@ class ResNet50Eager(torch.nn.Module):
         self.mean = torch.tensor(IMAGENET_MEAN, device=device, dtype=torch.float32)
         self.inv_std = 1.0 / torch.tensor(IMAGENET_STD, device=device, dtype=torch.float32)
 
+    @torch.no_grad()
+    def update_params(self, params: Dict[str, torch.Tensor]) -> None:
+        """Hot weight reload, in place (see :meth:`ResNet50Fused.update_params`)."""
+        for s in conv_specs():
+            w = params[s.name + ".w"]
+            scale, bias = fold_bn(params, s.name)
+            if self.fold:
+                w = w * scale.view(-1, 1, 1, 1)
+            self.w[s.name].copy_(w)
+            self.sb[s.name][0].copy_(scale)
+            self.sb[s.name][1].copy_(bias)
+        self.fc_w.copy_(params["fc.w"])
+        self.fc_b.copy_(params["fc.b"])
+
     def _cbr(self, x, name, relu=True, residual=None):
         s = self.specs[name]
         y = F.conv2d(x, self.w[name], stride=s.stride, padding=s.pad)
@@ -320,6 +334,26 @@ class ResNet50Fused:
     @property
     def workspace(self) -> torch.Tensor:
         return self._ws.get()
+
+    @torch.no_grad()
+    def update_params(self, params: Dict[str, torch.Tensor]) -> None:
+        """Hot weight reload: fold / pack the new parameters and copy them INTO the existing device
+        tensors, so every hipGraph already captured against them stays valid (no re-capture).
+        The caller quiesces the engine first (no batch may read the weights mid-copy)."""
+        from .. import ops
+
+        for s in conv_specs():
+            scale, bias = fold_bn(params, s.name)
+            w = ops.pack_conv_weight(params[s.name + ".w"] * scale.view(-1, 1, 1, 1))
+            self.w[s.name].copy_(w)
+            self.b[s.name].copy_(bias)
+        for si in range(len(STAGES)):
+            p0 = f"layer{si + 1}.0"
+            w3, wd = self.w[p0 + ".conv3"], self.w[p0 + ".down"]
+            self.dual_w[p0].copy_(torch.cat([w3.reshape(w3.shape[0], -1), wd.reshape(wd.shape[0], -1)], 1))
+            self.dual_b[p0].copy_(self.b[p0 + ".conv3"] + self.b[p0 + ".down"])
+        self.fc_w.copy_(params["fc.w"])
+        self.fc_b.copy_(params["fc.b"])
 
     # -- planning ---------------------------------------------------------------------------
     def layer_gemm_shapes(self, batch: int) -> List[Tuple[str, int, int, int]]:

@@ -1,0 +1,172 @@
+"""Hot weight reload (``POST /admin/reload``): X1 of SURVEY.md §2.E.2 "once at startup, and on hot
+weight reload".
+
+Single process: load (``WEIGHTS``-style safetensors path, or a ``seed`` for random weights), then
+``plugin.apply_params`` -- which quiesces each engine (in-flight batches drain, new ones wait) and
+copies the new parameters INTO the existing device tensors, so the captured hipGraphs keep
+pointing at valid weights and are replayed unchanged (no re-capture, no allocation).
+
+Data-parallel service (one process per GPU, any rank may receive the HTTP request): the receiving
+rank writes the request to a small control directory shared by the service's ranks
+(``/dev/shm/mls-reload-<PORT>-<MASTER_PORT>``); every rank's watcher thread picks it up, rank 0
+loads the checkpoint, broadcasts an ok flag and then the parameters as one flattened buffer per
+dtype over RCCL/xGMI (``dist.broadcast_state``), every rank applies them and acknowledges; the
+HTTP request returns once all ranks acknowledged.  The process group is otherwise idle in DP
+serving, so the reload collectives never interleave with other collectives.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+import shutil
+import tempfile
+import threading
+import time
+from typing import Any, Dict, Optional
+
+logger = logging.getLogger("mlsamd.reload")
+
+
+class ReloadError(ValueError):
+    """Bad request (unknown file, shape mismatch, unsupported model): HTTP 400."""
+
+
+def _atomic_write(path: str, obj: dict) -> None:
+    tmp = f"{path}.{os.getpid()}.tmp"
+    with open(tmp, "w") as f:
+        json.dump(obj, f)
+    os.replace(tmp, path)
+
+
+def _read(path: str) -> Optional[dict]:
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
+class ReloadCoordinator:
+    def __init__(self, plugin, ctx, settings, poll_s: float = 0.1):
+        self.plugin = plugin
+        self.ctx = ctx
+        self.settings = settings
+        self.poll_s = poll_s
+        self.generation = 0
+        self.last: Optional[dict] = None
+        self._lock = threading.Lock()
+        self._stop = threading.Event()
+        self._thread: Optional[threading.Thread] = None
+        self.ctl_dir: Optional[str] = None
+        if ctx.world_size > 1:
+            base = "/dev/shm" if os.path.isdir("/dev/shm") else tempfile.gettempdir()
+            self.ctl_dir = os.path.join(base, f"mls-reload-{settings.PORT}-{os.environ.get('MASTER_PORT', '0')}")
+            os.makedirs(self.ctl_dir, exist_ok=True)
+            self._thread = threading.Thread(target=self._watch, name="mls-reload-watch", daemon=True)
+            self._thread.start()
+
+    @property
+    def supported(self) -> bool:
+        return self.plugin.reload_spec() is not None
+
+    # ------------------------------------------------------------------ entry point (any rank)
+    def request(self, weights: Optional[str] = None, seed: Optional[int] = None, timeout: float = 300.0) -> dict:
+        if not self.supported:
+            raise ReloadError(f"model {self.plugin.name!r} does not support weight reload")
+        if weights is None and seed is None:
+            raise ReloadError("give 'weights' (a safetensors path on the server) or 'seed'")
+        if weights is not None and not os.path.exists(weights):
+            raise ReloadError(f"weights not found: {weights}")
+        t0 = time.perf_counter()
+        if self.ctl_dir is None:
+            with self._lock:
+                params = self.plugin.load_params(weights, seed)
+                self.plugin.apply_params(params)
+                self.generation += 1
+                self.last = {"generation": self.generation, "weights": weights, "seed": seed}
+            return {"generation": self.generation, "ranks": 1, "seconds": round(time.perf_counter() - t0, 3)}
+        with self._lock:
+            cur = _read(os.path.join(self.ctl_dir, "request.json")) or {}
+            gen = int(cur.get("generation", 0)) + 1
+            _atomic_write(os.path.join(self.ctl_dir, "request.json"), {"generation": gen, "weights": weights, "seed": seed})
+        deadline = time.monotonic() + timeout
+        while time.monotonic() < deadline:
+            acks = [_read(os.path.join(self.ctl_dir, f"ack-{gen}-{r}.json")) for r in range(self.ctx.world_size)]
+            if all(a is not None for a in acks):
+                errs = [a["error"] for a in acks if a.get("error")]
+                if errs:
+                    raise ReloadError(errs[0])
+                return {"generation": gen, "ranks": len(acks), "seconds": round(time.perf_counter() - t0, 3)}
+            time.sleep(self.poll_s)
+        raise TimeoutError(f"reload generation {gen}: not every rank acknowledged within {timeout} s")
+
+    # ------------------------------------------------------------------ per-rank watcher
+    def _watch(self) -> None:
+        req_path = os.path.join(self.ctl_dir, "request.json")
+        while not self._stop.is_set():
+            req = _read(req_path)
+            if req and int(req.get("generation", 0)) > self.generation:
+                self._apply_distributed(req)
+            self._stop.wait(self.poll_s)
+
+    def _apply_distributed(self, req: dict) -> None:
+        import torch
+        import torch.distributed as dist
+
+        from . import dist as mdist
+
+        gen = int(req["generation"])
+        err = ""
+        params = None
+        if self.ctx.rank == 0:
+            try:
+                params = self.plugin.load_params(req.get("weights"), req.get("seed"))
+            except Exception as e:  # validated on rank 0 before any rank commits
+                err = f"{type(e).__name__}: {e}"
+        backend = dist.get_backend()
+        dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
+        ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=dev)
+        dist.broadcast(ok, src=0)
+        if int(ok.item()):
+            try:
+                params = mdist.broadcast_state(params, src=0, device=None, spec=self.plugin.reload_spec())
+                with self._lock:
+                    self.plugin.apply_params(params)
+                    self.last = {"generation": gen, "weights": req.get("weights"), "seed": req.get("seed")}
+            except Exception as e:
+                logger.exception("reload generation %d failed on rank %d", gen, self.ctx.rank)
+                err = f"{type(e).__name__}: {e}"
+        elif not err:
+            err = "rank 0 could not load the weights"
+        self.generation = gen
+        _atomic_write(os.path.join(self.ctl_dir, f"ack-{gen}-{self.ctx.rank}.json"),
+                      {"rank": self.ctx.rank, "generation": gen, "error": err})
+
+    def close(self) -> None:
+        self._stop.set()
+        if self._thread is not None:
+            self._thread.join(timeout=5)
+        if self.ctl_dir and self.ctx.rank == 0:
+            shutil.rmtree(self.ctl_dir, ignore_errors=True)
+
+
+def handle_reload_request(coordinator: Optional[ReloadCoordinator], settings, headers: Dict[str, str],
+                          payload: Any) -> tuple:
+    """Shared by both front ends: ``(status, body_dict)``.  Auth: the ``api_key`` header must match
+    ``API_KEY`` when one is configured (the key the service registers with, reference C10)."""
+    key = getattr(settings, "API_KEY", "")
+    if key and headers.get("api_key") != key:
+        return 401, {"status": "failure", "detail": "invalid or missing api_key"}
+    if coordinator is None:
+        return 503, {"status": "failure", "detail": "Model is not ready to receive predictions."}
+    if not isinstance(payload, dict):
+        return 422, {"detail": [{"type": "dict_type", "loc": ["body"], "msg": "JSON object required", "input": None}]}
+    seed = payload.get("seed")
+    try:
+        out = coordinator.request(weights=payload.get("weights"), seed=None if seed is None else int(seed))
+    except (ReloadError, ValueError, KeyError) as e:
+        return 400, {"status": "failure", "detail": str(e)}
+    except TimeoutError as e:
+        return 504, {"status": "failure", "detail": str(e)}
+    return 200, {"status": "success", "result": out}

@@ -99,6 +99,20 @@ class ModelPlugin:
         (``frontend.native.EngineReplica`` / ``HostReplica``)."""
         raise NotImplementedError
 
+    # --- hot weight reload (POST /admin/reload, parallel/reload.py) ---
+    def reload_spec(self) -> Optional[Dict[str, tuple]]:
+        """``{name: (shape, dtype)}`` of the parameters ``load_params`` returns (what non-source
+        ranks receive in the X1 broadcast); ``None`` = reload unsupported."""
+        return None
+
+    def load_params(self, weights: Optional[str], seed: Optional[int]) -> Dict[str, Any]:
+        """Rank 0 side: parameters from a safetensors path, or random ones from ``seed``."""
+        raise NotImplementedError
+
+    def apply_params(self, params: Dict[str, Any]) -> None:
+        """Every rank: swap the serving weights (quiescing the engines; in place for graphs)."""
+        raise NotImplementedError
+
     def replica_probes(self) -> List[Optional[Callable[[], bool]]]:
         """Optional per-replica health probes for the watchdog (same order as :meth:`replicas`)."""
         return []

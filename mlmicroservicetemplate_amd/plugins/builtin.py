@@ -103,6 +103,7 @@ class ResNet50Plugin(ModelPlugin):
 
     def __init__(self):
         self.engines = []
+        self.models = []
         self.labels: List[str] = []
         self.topk = 5
 
@@ -147,9 +148,11 @@ class ResNet50Plugin(ModelPlugin):
 
             tuning = autotune.load_tuning("resnet50", max_batch)
             model = resnet.ResNet50Fused(params, dev, max_batch=max_batch, tuning=tuning)
+            self.models.append(model)
             return lambda x: model.classify(x, k)
         if backend == "eager":
             model = resnet.ResNet50Eager(params, dev)
+            self.models.append(model)
 
             def fwd(x):
                 v, i = torch.topk(torch.softmax(model(x).float(), -1), k, dim=-1)
@@ -179,6 +182,21 @@ class ResNet50Plugin(ModelPlugin):
 
     def native_spec(self) -> dict:
         return {"sample_bytes": 224 * 224 * 3, "result": "topk"}
+
+    def reload_spec(self):
+        from ..models import resnet
+
+        return {k: (tuple(v.shape), v.dtype) for k, v in resnet.init_resnet50_spec().items()}
+
+    def load_params(self, weights, seed):
+        from ..models import resnet
+
+        return resnet.load_resnet50(weights) if weights else resnet.init_resnet50(int(seed))
+
+    def apply_params(self, params) -> None:
+        for eng, model in zip(self.engines, self.models):
+            with eng.quiesce():
+                model.update_params(params)
 
     def native_replicas(self):
         from ..frontend.native import EngineReplica
@@ -248,6 +266,25 @@ class ToyClassifierPlugin(ModelPlugin):
 
     def native_spec(self) -> dict:
         return {"sample_bytes": self.size * self.size * 3, "result": "topk"}
+
+    def reload_spec(self):
+        import torch
+
+        return {"w": ((self.NUM_CLASSES, self.size * self.size * 3), torch.float32)}
+
+    def load_params(self, weights, seed):
+        import torch
+
+        if weights:
+            from ..utils.checkpoint import load_validated
+
+            return load_validated(weights, self.reload_spec())
+        rng = np.random.default_rng(int(seed))
+        w = (rng.standard_normal((self.NUM_CLASSES, self.size * self.size * 3)) / 8).astype(np.float32)
+        return {"w": torch.from_numpy(w)}
+
+    def apply_params(self, params) -> None:
+        self.w = params["w"].detach().cpu().float().numpy().copy()  # one reference swap: batches see old or new
 
     def native_replicas(self):
         from ..frontend.native import HostReplica

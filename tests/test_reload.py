@@ -1,0 +1,143 @@
+"""Hot weight reload (POST /admin/reload, parallel/reload.py) on CPU with the toy classifier:
+both front ends, auth, errors, safetensors source, and the 2-rank (gloo) broadcast path."""
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+import warnings
+
+import numpy as np
+import pytest
+import requests
+
+warnings.filterwarnings("ignore", category=DeprecationWarning)
+
+from fastapi.testclient import TestClient  # noqa: E402
+
+from mlmicroservicetemplate_amd.api.app import create_app  # noqa: E402
+from mlmicroservicetemplate_amd.api.multipart import encode_multipart  # noqa: E402
+from mlmicroservicetemplate_amd.config import Settings  # noqa: E402
+from mlmicroservicetemplate_amd.frontend.native import NativeService  # noqa: E402
+from mlmicroservicetemplate_amd.plugins.base import PluginContext  # noqa: E402
+from mlmicroservicetemplate_amd.plugins.builtin import ToyClassifierPlugin  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def settings(**kw):
+    base = {"MODEL": "toy_classifier", "REGISTER": False, "MAX_WAIT_US": 2000, "IO_THREADS": 2}
+    base.update(kw)
+    return Settings.load(env_file=None, environ={}, overrides=base)
+
+
+def img(seed=0):
+    return np.random.default_rng(seed).integers(0, 256, (8, 8, 3), dtype=np.uint8)
+
+
+def upload(a):
+    body, ct = encode_multipart({"image_file": ("x.rgb", a.tobytes(), "application/octet-stream")})
+    return body, {"content-type": ct}
+
+
+def expected_classes(seed, a):
+    p = ToyClassifierPlugin()
+    p.w = p.load_params(None, seed)["w"].numpy()
+    _, idx = p.scores(a[None])
+    return [f"class_{i}" for i in idx[0]]
+
+
+def _ready(get, timeout=10):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        if get("/status").status_code == 200:
+            return True
+        time.sleep(0.01)
+    return False
+
+
+def test_reload_python_frontend_seed_auth_and_errors(tmp_path):
+    a = img(1)
+    with TestClient(create_app(settings(API_KEY="sekret"), ToyClassifierPlugin())) as c:
+        assert _ready(c.get)
+        body, h = upload(a)
+        assert c.post("/predict", content=body, headers=h).json()["result"]["classes"] == expected_classes(0, a)
+        assert c.post("/admin/reload", json={"seed": 3}).status_code == 401
+        assert c.post("/admin/reload", json={"seed": 3}, headers={"api_key": "nope"}).status_code == 401
+        r = c.post("/admin/reload", json={"seed": 3}, headers={"api_key": "sekret"})
+        assert r.status_code == 200 and r.json()["result"]["generation"] == 1
+        assert c.post("/predict", content=body, headers=h).json()["result"]["classes"] == expected_classes(3, a)
+        bad = c.post("/admin/reload", json={"weights": str(tmp_path / "missing.safetensors")}, headers={"api_key": "sekret"})
+        assert bad.status_code == 400 and "not found" in bad.json()["detail"]
+        assert c.post("/admin/reload", json={}, headers={"api_key": "sekret"}).status_code == 400
+        # safetensors source, validated against the plugin's spec
+        from mlmicroservicetemplate_amd.utils.checkpoint import save_state
+
+        path = str(tmp_path / "toy.safetensors")
+        save_state(path, ToyClassifierPlugin().load_params(None, 11))
+        r = c.post("/admin/reload", json={"weights": path}, headers={"api_key": "sekret"})
+        assert r.status_code == 200 and r.json()["result"]["generation"] == 2
+        assert c.post("/predict", content=body, headers=h).json()["result"]["classes"] == expected_classes(11, a)
+
+
+def test_reload_native_frontend():
+    a = img(2)
+    s = settings()
+    svc = NativeService(s, ToyClassifierPlugin(), PluginContext(settings=s), host="127.0.0.1", port=0).start()
+    try:
+        url = f"http://127.0.0.1:{svc.port}"
+        assert _ready(lambda p: requests.get(url + p))
+        body, h = upload(a)
+        assert requests.post(url + "/predict", data=body, headers=h).json()["result"]["classes"] == expected_classes(0, a)
+        r = requests.post(url + "/admin/reload", json={"seed": 5})
+        assert r.status_code == 200 and r.json()["result"]["ranks"] == 1
+        assert requests.post(url + "/predict", data=body, headers=h).json()["result"]["classes"] == expected_classes(5, a)
+        assert requests.get(url + "/admin/reload").status_code == 405
+    finally:
+        svc.stop()
+
+
+def _free_port():
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+@pytest.mark.timeout(150)
+@pytest.mark.parametrize("frontend", ["python", "native"])
+def test_reload_two_ranks_broadcasts_to_every_rank(frontend):
+    port = _free_port()
+    env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    proc = subprocess.Popen([sys.executable, "-m", "mlmicroservicetemplate_amd", "serve", "--model", "toy_classifier",
+                             "--frontend", frontend, "--gpus", "2", "--port", str(port), "--host", "127.0.0.1",
+                             "--no-register", "--env-file", "/nonexistent"], cwd=ROOT, env=env, start_new_session=True)
+    try:
+        url = f"http://127.0.0.1:{port}"
+        deadline = time.time() + 90
+        ready = False
+        while time.time() < deadline and not ready:
+            try:
+                ready = requests.get(url + "/status", timeout=1).status_code == 200
+            except requests.RequestException:
+                time.sleep(0.2)
+        assert ready
+        r = requests.post(url + "/admin/reload", json={"seed": 9}, timeout=60)
+        assert r.status_code == 200, r.text
+        assert r.json()["result"]["ranks"] == 2
+        a = img(4)
+        want = expected_classes(9, a)
+        body, h = upload(a)
+        ranks = set()
+        for _ in range(60):  # fresh connections land on both ranks; every rank serves the new weights
+            ranks.add(requests.get(url + "/info", timeout=5).json()["rank"])
+            assert requests.post(url + "/predict", data=body, headers=h, timeout=5).json()["result"]["classes"] == want
+            if len(ranks) == 2:
+                break
+        assert ranks == {0, 1}
+    finally:
+        os.killpg(proc.pid, signal.SIGTERM)
+        try:
+            proc.wait(30)
+        except subprocess.TimeoutExpired:
+            os.killpg(proc.pid, signal.SIGKILL)
