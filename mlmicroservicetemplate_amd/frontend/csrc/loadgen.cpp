@@ -10,6 +10,7 @@
 //
 // usage: mls_loadgen --port P [--host 127.0.0.1] [--path /predict] [--conns 64] [--threads 4]
 //                    [--duration 10] [--warmup 2] [--bytes 150528] [--field image_file] [--raw]
+//                    [--file upload.jpg --ctype image/jpeg]   (a real file instead of random bytes)
 #include <arpa/inet.h>
 #include <errno.h>
 #include <fcntl.h>
@@ -44,6 +45,8 @@ struct Opts {
   long bytes = 224 * 224 * 3;
   std::string field = "image_file";
   bool raw = false;
+  std::string file;                            // send this file's bytes instead of random ones
+  std::string ctype = "application/octet-stream";  // the upload part's content type
 };
 
 struct ThreadStats {
@@ -213,23 +216,39 @@ int main(int argc, char** argv) {
     else if (a == "--bytes") o.bytes = atol(next());
     else if (a == "--field") o.field = next();
     else if (a == "--raw") o.raw = true;
+    else if (a == "--file") o.file = next();
+    else if (a == "--ctype") o.ctype = next();
     else {
       fprintf(stderr, "unknown option %s\n", a.c_str());
       return 2;
     }
   }
   o.threads = std::max(1, std::min(o.threads, o.conns));
-  std::mt19937 rng(1234);
-  std::string payload((size_t)o.bytes, '\0');
-  for (auto& ch : payload) ch = (char)(rng() & 0xff);
+  std::string payload;
+  if (!o.file.empty()) {
+    FILE* f = fopen(o.file.c_str(), "rb");
+    if (!f) {
+      fprintf(stderr, "cannot open %s\n", o.file.c_str());
+      return 2;
+    }
+    char buf[65536];
+    size_t n;
+    while ((n = fread(buf, 1, sizeof buf, f)) > 0) payload.append(buf, n);
+    fclose(f);
+    o.bytes = (long)payload.size();
+  } else {
+    std::mt19937 rng(1234);
+    payload.assign((size_t)o.bytes, '\0');
+    for (auto& ch : payload) ch = (char)(rng() & 0xff);
+  }
   std::string body, ctype;
   if (o.raw) {
     body = payload;
-    ctype = "application/octet-stream";
+    ctype = o.ctype;
   } else {
     const std::string bnd = "mlsloadgenboundary7d1f";
     body = "--" + bnd + "\r\nContent-Disposition: form-data; name=\"" + o.field +
-           "\"; filename=\"img.rgb\"\r\nContent-Type: application/octet-stream\r\n\r\n" + payload + "\r\n--" + bnd +
+           "\"; filename=\"upload\"\r\nContent-Type: " + o.ctype + "\r\n\r\n" + payload + "\r\n--" + bnd +
            "--\r\n";
     ctype = "multipart/form-data; boundary=" + bnd;
   }

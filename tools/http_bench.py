@@ -36,12 +36,30 @@ def main() -> int:
     ap.add_argument("--warmup", type=float, default=2)
     ap.add_argument("--bytes", type=int, default=224 * 224 * 3)
     ap.add_argument("--ready-timeout", type=float, default=300)
+    ap.add_argument("--jpeg", action="store_true", help="upload a 320x240 JPEG (server-side decode) instead of raw RGB8")
+    ap.add_argument("--decode-workers", type=int, default=4)
     args = ap.parse_args()
     fbuild.build()
     cmd = [sys.executable, "-m", "mlmicroservicetemplate_amd", "serve", "--model", args.model, "--frontend",
            args.frontend, "--port", str(args.port), "--host", "127.0.0.1", "--no-register", "--env-file", "/nonexistent",
            "--workers-per-gpu", str(args.workers_per_gpu), "--io-threads", str(args.io_threads)]
-    srv = subprocess.Popen(cmd, cwd=ROOT, env=dict(os.environ, PYTHONPATH=ROOT), start_new_session=True)
+    payload_args = ["--bytes", str(args.bytes)]
+    if args.jpeg:
+        import io
+
+        import numpy as np
+        from PIL import Image
+
+        buf = io.BytesIO()
+        img = np.random.default_rng(0).integers(0, 256, (240, 320, 3), dtype=np.uint8)
+        Image.fromarray(img).save(buf, format="JPEG", quality=90)
+        path = os.path.join(ROOT, "gpurun_out", "http_bench_upload.jpg")
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, "wb") as f:
+            f.write(buf.getvalue())
+        payload_args = ["--file", path, "--ctype", "image/jpeg"]
+    srv = subprocess.Popen(cmd, cwd=ROOT, env=dict(os.environ, PYTHONPATH=ROOT, DECODE_WORKERS=str(args.decode_workers)),
+                           start_new_session=True)
     url = f"http://127.0.0.1:{args.port}"
     try:
         t0 = time.time()
@@ -63,11 +81,12 @@ def main() -> int:
         for conns in args.conns:
             out = subprocess.run([fbuild.loadgen_path(), "--port", str(args.port), "--conns", str(conns),
                                   "--threads", str(args.client_threads), "--duration", str(args.duration),
-                                  "--warmup", str(args.warmup), "--bytes", str(args.bytes)],
+                                  "--warmup", str(args.warmup), *payload_args],
                                  capture_output=True, text=True, timeout=args.duration + args.warmup + 60)
             res = json.loads(out.stdout)
             res.update({"model": args.model, "frontend": args.frontend, "workers_per_gpu": args.workers_per_gpu,
-                        "io_threads": args.io_threads, "gpus": 1})
+                        "io_threads": args.io_threads, "gpus": 1, "payload": "jpeg320x240" if args.jpeg else "raw-rgb8",
+                        "decode_workers": args.decode_workers})
             print(json.dumps(res), flush=True)
     finally:
         os.killpg(srv.pid, signal.SIGTERM)
