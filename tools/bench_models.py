@@ -25,7 +25,8 @@ def bench_bert(args):
     dev = torch.device("cuda:0")
     cfg = bert.BertConfig()
     p = bert.init_bert(cfg, 0)
-    models = {"fused": bert.BertFused(p, dev, cfg), "eager": bert.BertEager(p, dev, cfg)}
+    models = {"fused": lambda: bert.BertFused(p, dev, cfg), "eager": lambda: bert.BertEager(p, dev, cfg)}
+    models = {k: v() for k, v in models.items() if k in args.backends}
     for S in args.seqs:
         for B in args.batches:
             rng = np.random.default_rng(0)
@@ -48,12 +49,12 @@ def bench_bert(args):
                 pend = []
                 for _ in range(n):
                     pend.append(eng.submit(packed))
-                    if len(pend) >= 3:
+                    if len(pend) >= args.inflight:
                         pend.pop(0).wait()
                 for t in pend:
                     t.wait()
                 dt = (time.perf_counter() - t0) / n
-                print(json.dumps({"bench": "bert-base", "backend": name, "batch": B, "seq": S,
+                print(json.dumps({"bench": "bert-base", "backend": name, "batch": B, "seq": S, "inflight": args.inflight,
                                   "ms_per_batch": round(dt * 1e3, 3), "seq_per_s": round(B / dt, 1),
                                   "tokens_per_s": round(B * S / dt, 1)}), flush=True)
                 del eng
@@ -143,6 +144,7 @@ def main():
     ap.add_argument("--prompt", type=int, default=512)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--inflight", type=int, default=5, help="bert: batches in flight (co-running engine slots)")
+    ap.add_argument("--backends", nargs="+", default=["fused", "eager"], help="bert: which implementations")
     ap.add_argument("--emulate-tp", type=int, default=1)
     ap.add_argument("--skinny-max-split", type=int, default=0)
     args = ap.parse_args()
