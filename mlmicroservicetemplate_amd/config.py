@@ -158,7 +158,9 @@ class Settings:
     GPUS: int = 1
     WORKERS_PER_GPU: int = 1  # HTTP worker processes per GPU (DP models): front-end CPU scales, each owns an engine
     TP: int = 1
-    MAX_BATCH: int = 32
+    MAX_BATCH: int = 32  # 0 = auto: planned from free HBM / per-sample activations and LATENCY_SLO_MS
+    MAX_BATCH_CAP: int = 1024  # ceiling of an auto-planned batch
+    LATENCY_SLO_MS: float = 50.0  # auto planning: GPU time budget of one batch
     MAX_WAIT_US: int = 2000
     MAX_QUEUE: int = 4096
     GRAPH_BUCKETS: List[int] = field(default_factory=lambda: [1, 2, 4, 8, 16, 32])
@@ -242,8 +244,8 @@ class Settings:
     def validate(self) -> None:
         if not (0 < self.PORT < 65536):
             raise ValueError(f"PORT out of range: {self.PORT}")
-        if self.MAX_BATCH < 1:
-            raise ValueError("MAX_BATCH must be >= 1")
+        if self.MAX_BATCH < 0:
+            raise ValueError("MAX_BATCH must be >= 1, or 0 for an HBM / latency-planned batch")
         if self.GPUS < 0 or self.TP < 1:
             raise ValueError("GPUS must be >= 0 and TP >= 1")
         if self.DTYPE not in ("bf16", "fp32", "fp16"):
@@ -251,7 +253,7 @@ class Settings:
         if self.FRONTEND not in ("python", "native"):
             raise ValueError(f"FRONTEND must be python or native, not {self.FRONTEND!r}")
         self.GRAPH_BUCKETS = sorted(set(int(b) for b in self.GRAPH_BUCKETS if int(b) > 0))
-        if not self.GRAPH_BUCKETS or self.GRAPH_BUCKETS[-1] < self.MAX_BATCH:
+        if self.MAX_BATCH and (not self.GRAPH_BUCKETS or self.GRAPH_BUCKETS[-1] < self.MAX_BATCH):
             self.GRAPH_BUCKETS = sorted(set(self.GRAPH_BUCKETS + [self.MAX_BATCH]))
 
     def to_dict(self, redact: bool = True) -> Dict[str, Any]:

@@ -143,7 +143,8 @@ class NativeService:
             host=host, port=int(settings.PORT if port is None else port),
             listen_fd=-1 if listen_fd is None else int(listen_fd),
             io_threads=int(settings.IO_THREADS), sample_bytes=int(spec["sample_bytes"]),
-            max_batch=int(settings.MAX_BATCH), max_wait_us=int(settings.MAX_WAIT_US),
+            max_batch=int(settings.MAX_BATCH) or 32,  # wake-up hint only: batches are sized by the replica
+            max_wait_us=int(settings.MAX_WAIT_US),
             max_queue=int(settings.MAX_QUEUE), max_upload=int(settings.MAX_UPLOAD_BYTES),
             form_field=plugin.form_field, cors_origins=list(settings.CORS_ORIGINS),
             request_timeout_s=float(settings.REQUEST_TIMEOUT_S), python_decode=True)

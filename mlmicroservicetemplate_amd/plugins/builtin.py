@@ -127,6 +127,8 @@ class ResNet50Plugin(ModelPlugin):
         if ctx.world_size > 1:
             spec = {k: (tuple(v.shape), v.dtype) for k, v in resnet.init_resnet50_spec().items()}
             params = mdist.broadcast_state(params, src=0, device=torch.device(devices[0]), spec=spec)
+        if int(s.MAX_BATCH) == 0:  # auto: plan from free HBM and the latency SLO (scheduler/capacity.py)
+            self.plan_batch(s, devices[0], params)
         buckets = [b for b in s.GRAPH_BUCKETS if b <= s.MAX_BATCH]
         for dev in devices:
             fwd = self._build_forward(s.BACKEND, dev, max(buckets), params)
@@ -136,6 +138,34 @@ class ResNet50Plugin(ModelPlugin):
             eng.warmup(capture=bool(s.USE_GRAPHS))
             self.engines.append(eng)
         logger.info("resnet50 ready on %s (backend=%s buckets=%s)", devices, s.BACKEND, buckets)
+
+    def plan_batch(self, s, dev: str, params) -> None:
+        """MAX_BATCH=0: measure this model's per-image activation bytes and time on ``dev`` and set
+        MAX_BATCH + GRAPH_BUCKETS from free HBM (all in-flight slots) and LATENCY_SLO_MS."""
+        import torch
+
+        from ..models import resnet
+        from ..scheduler.capacity import buckets_up_to, plan_for_device
+
+        fused = s.BACKEND == "fused"
+        probe = resnet.ResNet50Fused(params, dev, max_batch=32) if fused else resnet.ResNet50Eager(params, dev)
+        gen = torch.Generator(device="cpu").manual_seed(0)
+
+        def make(b):
+            return torch.randint(0, 256, (b, 224, 224, 3), dtype=torch.uint8, generator=gen).to(dev)
+
+        def fwd(x):
+            return probe.classify(x, self.topk) if fused else probe(x)
+
+        with torch.no_grad():
+            plan = plan_for_device(fwd, make, torch.device(dev), s)
+        del probe
+        torch.cuda.empty_cache()
+        self.capacity_plan = plan
+        s.MAX_BATCH = plan.max_batch
+        s.GRAPH_BUCKETS = buckets_up_to(plan.max_batch)
+        logger.info("auto batch: %d (bound by %s; %.1f MB/image, %.4f ms/image, %.1f GB free)", plan.max_batch,
+                    plan.limit, plan.per_sample_bytes / 1e6, plan.per_sample_ms, plan.free_bytes / 1e9)
 
     def _build_forward(self, backend: str, dev: str, max_batch: int, params):
         import torch
@@ -206,6 +236,9 @@ class ResNet50Plugin(ModelPlugin):
     def describe(self) -> dict:
         d = super().describe()
         d["engines"] = [e.stats() for e in self.engines]
+        plan = getattr(self, "capacity_plan", None)
+        if plan is not None:
+            d["capacity_plan"] = plan.to_dict()
         return d
 
 

@@ -58,7 +58,7 @@ class LlamaPlugin(ModelPlugin):
         source = llama.CheckpointSource(s.WEIGHTS, device=dev) if s.WEIGHTS else None
         params = llama.init_llama_shard(cfg, tp, ctx.rank, int(s.SEED), device=dev, source=source)
         self.model = llama.LlamaTP(params, cfg, tp=tp, rank=ctx.rank, comm=llama.TPComm(None, tp, device=dev), backend=backend,
-                                   device=dev, max_batch=int(s.MAX_BATCH), max_seq=int(extra.get("max_seq", 2048)))
+                                   device=dev, max_batch=int(s.MAX_BATCH) or 32, max_seq=int(extra.get("max_seq", 2048)))
         self.tok = llama.LlamaTokenizer(cfg, extra.get("tokenizer_file"))
         self.cfg = cfg
         self.engine = None

@@ -54,6 +54,8 @@ class BertPlugin(ModelPlugin):
         if ctx.world_size > 1:
             spec = bert.bert_spec(cfg)
             params = mdist.broadcast_state(params, src=0, device=torch.device(devices[0]), spec=spec)
+        if not int(s.MAX_BATCH):  # auto planning is implemented for resnet50; BERT keeps a fixed cap
+            s.MAX_BATCH = 32
         buckets = [b for b in s.GRAPH_BUCKETS if b <= s.MAX_BATCH]
         seqs = [q for q in SEQ_BUCKETS if q <= self.max_seq] or [self.max_seq]
         for dev in devices:

@@ -190,3 +190,23 @@ def test_resnet50_hot_reload_in_place_under_graphs():
     np.testing.assert_array_equal(i1, fi.cpu().numpy())
     np.testing.assert_allclose(v1, fv.cpu().numpy(), rtol=1e-3, atol=1e-4)
     assert not np.array_equal(i0, i1)
+
+
+def test_resnet50_auto_batch_plan():
+    """MAX_BATCH=0: the cap is planned from measured activation bytes / time, free HBM and the SLO."""
+    from mlmicroservicetemplate_amd.config import Settings
+    from mlmicroservicetemplate_amd.plugins.base import PluginContext
+    from mlmicroservicetemplate_amd.plugins.builtin import ResNet50Plugin
+
+    s = Settings.load(env_file=None, environ={}, overrides={"REGISTER": False, "GPUS": 1, "MODEL": "resnet50",
+                                                            "MAX_BATCH": 0, "LATENCY_SLO_MS": 3.0, "INFLIGHT": 2})
+    plugin = ResNet50Plugin()
+    plugin.init(PluginContext(settings=s, devices=["cuda:0"]))
+    plan = plugin.capacity_plan
+    assert plan.limit == "slo" and 1 <= plan.max_batch <= 1024  # 288 GB never binds for ResNet-50
+    assert plan.per_sample_bytes > 1e5 and plan.free_bytes > 1e11
+    assert s.MAX_BATCH == plan.max_batch and s.GRAPH_BUCKETS[-1] == plan.max_batch
+    assert plugin.engines[0].max_batch == plan.max_batch
+    x = np.random.default_rng(0).integers(0, 256, (plan.max_batch, 224, 224, 3), dtype=np.uint8)
+    v, i = plugin.engines[0].run(x)
+    assert v.shape == (plan.max_batch, 5) and np.all(np.isfinite(v))
