@@ -98,6 +98,7 @@ class GpuEngine:
         name: str = "engine",
         concurrent: bool = False,
         stage_workers: int = 4,
+        copies_on_slot_stream: Optional[bool] = None,
     ):
         self.forward = forward
         self.device = torch.device(device)
@@ -108,6 +109,13 @@ class GpuEngine:
         self.inflight = max(1, int(inflight))
         self.use_graphs = use_graphs
         self.concurrent = bool(concurrent) and self.inflight > 1
+        # concurrent slots: a slot's H2D and D2H may ride its own compute stream (fewer streams
+        # than hardware queues need sharing; MLS_SLOT_COPIES=1) instead of the shared copy streams
+        if copies_on_slot_stream is None:
+            import os
+
+            copies_on_slot_stream = os.environ.get("MLS_SLOT_COPIES", "0") == "1"
+        self.copies_on_slot_stream = bool(copies_on_slot_stream) and self.concurrent
         # host staging (request arrays -> pinned slot) split over a few threads: numpy releases the
         # GIL for bulk copies, and one thread's ~5-8 GB/s memcpy is what a 4.8 MB ResNet batch
         # every 0.9 ms needs
@@ -252,9 +260,11 @@ class GpuEngine:
             bucket = pick_bucket(n, self.buckets)
             with self._enqueue_lock, torch.cuda.device(self.device):
                 with tracing.range(f"{self.name}.enqueue"):
-                    with torch.cuda.stream(self.s_h2d):
+                    s_h2d = slot.s_comp if self.copies_on_slot_stream else self.s_h2d
+                    s_d2h = slot.s_comp if self.copies_on_slot_stream else self.s_d2h
+                    with torch.cuda.stream(s_h2d):
                         slot.dev_in[:bucket].copy_(slot.host_in[:bucket], non_blocking=True)
-                        slot.ev_h2d.record(self.s_h2d)
+                        slot.ev_h2d.record(s_h2d)
                     slot.s_comp.wait_event(slot.ev_h2d)
                     with torch.cuda.stream(slot.s_comp):
                         if self.use_graphs and bucket in slot.graphs:
@@ -267,11 +277,11 @@ class GpuEngine:
                             if bucket not in slot.host_out:
                                 self._alloc_host_out(slot, bucket, outs)
                         slot.ev_comp.record(slot.s_comp)
-                    self.s_d2h.wait_event(slot.ev_comp)
-                    with torch.cuda.stream(self.s_d2h):
+                    s_d2h.wait_event(slot.ev_comp)
+                    with torch.cuda.stream(s_d2h):
                         for h, d in zip(slot.host_out[bucket], outs):
                             h.copy_(d, non_blocking=True)
-                        slot.ev_done.record(self.s_d2h)
+                        slot.ev_done.record(s_d2h)
         except BaseException as e:
             self._free.put(slot)
             self.last_error = f"{type(e).__name__}: {e}"
