@@ -883,6 +883,10 @@ class Server {
         if (c.in.size() > MAX_HEAD) immediate(c, 431, failure_body("Request headers too large."), false);
         break;  // else: need more bytes
       }
+      if (h.head_len > MAX_HEAD) {
+        immediate(c, 431, failure_body("Request headers too large."), false);
+        break;
+      }
       if (h.method.empty()) {
         immediate(c, 400, failure_body("Malformed request line."), false);
         break;

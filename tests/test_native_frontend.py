@@ -388,3 +388,49 @@ def test_two_rank_native_service_shares_the_port():
             proc.wait(30)
         except subprocess.TimeoutExpired:
             os.killpg(proc.pid, signal.SIGKILL)
+
+
+def _raw_exchange(port, data, timeout=5.0):
+    with socket.create_connection(("127.0.0.1", port), timeout=timeout) as sk:
+        sk.sendall(data)
+        sk.shutdown(socket.SHUT_WR)
+        buf = b""
+        while True:
+            chunk = sk.recv(65536)
+            if not chunk:
+                break
+            buf += chunk
+    return buf
+
+
+def test_http_protocol_edges():
+    """HTTP/1.0 close, Expect: 100-continue, chunked -> 411, oversize -> 413, huge header -> 431,
+    bad Content-Length / request line -> 400."""
+    with Service(MAX_UPLOAD_BYTES=4096) as s:
+        assert s.wait_ready()
+        port = s.svc.port
+        r = _raw_exchange(port, b"GET / HTTP/1.0\r\n\r\n")
+        assert r.startswith(b"HTTP/1.1 200") and b"connection: close" in r.lower()
+        up = raw_upload(img(1))
+        head = (b"POST /predict HTTP/1.1\r\nHost: x\r\nExpect: 100-continue\r\nContent-Type: " +
+                up["headers"]["content-type"].encode() + b"\r\nContent-Length: " + str(len(up["data"])).encode() +
+                b"\r\n\r\n")
+        with socket.create_connection(("127.0.0.1", port), timeout=5) as sk:
+            sk.sendall(head)
+            first = sk.recv(1024)
+            assert first.startswith(b"HTTP/1.1 100 Continue")
+            sk.sendall(up["data"])
+            got = _recv_responses(sk, 1)
+            assert got[0][0] == 200
+        r = _raw_exchange(port, b"POST /predict HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n0\r\n\r\n")
+        assert r.startswith(b"HTTP/1.1 411")
+        r = _raw_exchange(port, b"POST /predict HTTP/1.1\r\nContent-Length: 999999\r\n\r\n")
+        assert r.startswith(b"HTTP/1.1 413")
+        r = _raw_exchange(port, b"GET / HTTP/1.1\r\nX-Big: " + b"a" * 70000 + b"\r\n\r\n")
+        assert r.startswith(b"HTTP/1.1 431")
+        r = _raw_exchange(port, b"POST /predict HTTP/1.1\r\nContent-Length: 12x\r\n\r\n")
+        assert r.startswith(b"HTTP/1.1 400")
+        r = _raw_exchange(port, b"GARBAGE\r\n\r\n")
+        assert r.startswith(b"HTTP/1.1 400")
+        # the server is still healthy after the abuse
+        assert requests.post(s.url + "/predict", **raw_upload(img(2))).status_code == 200
