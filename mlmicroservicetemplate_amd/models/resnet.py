@@ -19,6 +19,7 @@ non-trivial random running statistics so that BN folding is actually exercised.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
@@ -323,6 +324,8 @@ class ResNet50Fused:
             self.dual_w[p0] = torch.cat([w3.reshape(w3.shape[0], -1), wd.reshape(wd.shape[0], -1)], 1).contiguous()
             self.dual_b[p0] = (self.b[p0 + ".conv3"] + self.b[p0 + ".down"]).contiguous()
         self.fuse_down = True
+        # normalise + stem + max pool as one kernel (csrc/stem_pool.hip); MLS_FUSED_STEM=0 -> 3 kernels
+        self.fuse_stem = image_size == 224 and os.environ.get("MLS_FUSED_STEM", "1") != "0"
         self.fc_w = params["fc.w"].to(device=self.device, dtype=torch.bfloat16).contiguous()
         self.fc_b = params["fc.b"].to(device=self.device, dtype=torch.float32).contiguous()
         self.num_classes = self.fc_w.shape[0]
@@ -398,9 +401,12 @@ class ResNet50Fused:
         B = images_u8_nhwc.shape[0]
         if B > self.max_batch:
             raise ValueError(f"batch {B} > max_batch {self.max_batch}")
-        x = ops.normalize_u8(images_u8_nhwc, self.mean, self.std, pad=3)  # zero border = stem padding
-        x = self._conv(x, "stem", ops.ACT_RELU, pad=0)
-        x = ops.maxpool2d_nhwc(x, 3, 2, 1)
+        if self.fuse_stem:
+            x = ops.stem_pool_u8(images_u8_nhwc, self.w["stem"], self.b["stem"], self.mean, self.std)
+        else:
+            x = ops.normalize_u8(images_u8_nhwc, self.mean, self.std, pad=3)  # zero border = stem padding
+            x = self._conv(x, "stem", ops.ACT_RELU, pad=0)
+            x = ops.maxpool2d_nhwc(x, 3, 2, 1)
         for si, (nblocks, _m, _c, _s) in enumerate(STAGES):
             for bi in range(nblocks):
                 p = f"layer{si + 1}.{bi}"

@@ -372,6 +372,32 @@ def normalize_u8(images: torch.Tensor, mean, std, pad: int = 0, out: Optional[to
     return out
 
 
+def stem_pool_u8(images: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, mean, std,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """ResNet input block in one kernel: uint8 ``[B,224,224,3]`` -> normalise -> 7x7/2 conv
+    (packed ``[64,7,8,4]`` weights, BN folded) + bias -> ReLU -> 3x3/2 max pool -> bf16
+    ``[B,56,56,64]`` (csrc/stem_pool.hip)."""
+    dev = images.device
+    _need(images, "images", torch.uint8, dev)
+    _need(w, "w", torch.bfloat16, dev)
+    _need(bias, "bias", torch.float32, dev)
+    B, H, W, C = images.shape
+    if C != 3 or H != 224 or W != 224 or tuple(w.shape) != (64, 7, 8, 4) or bias.numel() != 64:
+        raise ValueError("stem_pool_u8: 224x224x3 images, [64,7,8,4] weights, 64 biases")
+    shape = (B, 56, 56, 64)
+    if out is None:
+        out = torch.empty(shape, device=dev, dtype=torch.bfloat16)
+    else:
+        _need(out, "out", torch.bfloat16, dev)
+        if tuple(out.shape) != shape:
+            raise ValueError(f"out must be {shape}")
+    m = (ctypes.c_float * 3)(*[float(v) for v in mean])
+    s = (ctypes.c_float * 3)(*[float(v) for v in std])
+    check(lib().mls_stem_pool(images.data_ptr(), w.data_ptr(), bias.data_ptr(), out.data_ptr(), B, H, W, m, s,
+                              stream_ptr(dev)), "mls_stem_pool")
+    return out
+
+
 def maxpool2d_nhwc(x: torch.Tensor, k: int = 3, s: int = 2, p: int = 1, out: Optional[torch.Tensor] = None):
     dev = x.device
     _need(x, "x", torch.bfloat16, dev)

@@ -39,6 +39,7 @@ _SIGS = {
     "mls_gemm_num_cfgs": [],
     "mls_normalize_u8": [P, P, I, I, I, I, FP, FP, P],
     "mls_maxpool2d": [P, P, I, I, I, I, I, I, I, P],
+    "mls_stem_pool": [P, P, P, P, I, I, I, FP, FP, P],
     "mls_avgpool_global": [P, P, I, I, I, P],
     "mls_bn_act": [P, P, P, P, L, I, I, P],
     "mls_silu_mul_interleaved": [P, P, L, I, P],
@@ -88,7 +89,7 @@ def _bind(lib: ctypes.CDLL) -> None:
 
 
 DEBUG = os.environ.get("MLS_DEBUG", "0") == "1"
-DEBUG_TUS = ("attention", "norm_ops")  # translation units with MLS_CHECK bounds
+DEBUG_TUS = ("attention", "norm_ops", "stem_pool")  # translation units with MLS_CHECK bounds
 DEBUG_CODES = {
     101: "rope/KV append: cache slot beyond the cache",
     102: "rope/KV append: position beyond the RoPE table",

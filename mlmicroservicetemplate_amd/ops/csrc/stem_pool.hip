@@ -1,0 +1,223 @@
+// ResNet-50 input block as ONE kernel: uint8 image -> normalise -> 7x7/2 stem conv (BN folded)
+// -> ReLU -> 3x3/2 max pool, bf16 NHWC [B][56][56][64] out.  Replaces three launches
+// (normalize_u8 -> conv_gemm_kernel MODE_STEM -> maxpool_kernel) and keeps the 112x112x64 stem
+// activation (51 MB per batch of 32, written once and re-read once) entirely on chip.
+//
+// Block = up to 4 consecutive 4 x 8 tiles of pooled outputs along one pooled-row strip (weights
+// loaded to VGPRs once per block; the next tile's image bytes are fetched during the current
+// tile's math).  A tile  Its pooling windows cover 9 x 17 stem pixels (one row /
+// column shared with the neighbouring tile, recomputed instead of exchanged), whose receptive
+// fields form one 23 x 40 pixel patch of the image: staged ONCE in LDS as normalised bf16 x 4
+// channels (zero outside the image = the conv padding), so every image pixel is read from memory
+// once per tile instead of once per tap (the implicit-GEMM stem re-gathers each ~12 times).
+// GEMM view per tile: M = 153 stem pixels (padded to 160 = 10 MFMA row blocks), N = 64, K = 7 kh
+// x 32 (kw padded 7 -> 8, Cin 3 -> 4: one v_mfma_f32_16x16x32_bf16 k-slab per kernel row, each
+// lane's 16-byte A fragment = 2 adjacent taps x 4 channels, one ds_read_b128 from the patch).
+// Weights (28 KB, L2-resident) go straight to VGPRs.  Epilogue: bias + ReLU -> bf16 tile in LDS
+// (stem pixels outside the image forced to 0, which cannot win a max of ReLU outputs), then each
+// thread max-reduces one pooled pixel x 8 channels and stores 16 bytes.  Rounding to bf16 before
+// the max equals rounding after it (monotone), so the result matches the three-kernel path.
+#include "common.h"
+
+#include <cstdlib>
+
+namespace {
+
+constexpr int TPH = 4, TPW = 8;                    // pooled outputs per block
+constexpr int SR = 2 * TPH + 1, SC = 2 * TPW + 1;  // stem pixels per block: 9 x 17
+constexpr int SP = SR * SC;                        // 153
+constexpr int MROWS = 160;                         // 10 row blocks of 16
+constexpr int PR = 2 * (SR - 1) + 7;               // patch rows: 23
+constexpr int PC = 2 * (SC - 1) + 8;               // patch cols: 40 (taps padded to 8)
+constexpr int COUT = 64, KTOT = 7 * 32;
+constexpr int PATCH_BYTES = PR * PC * 8;           // 7360
+constexpr int TSTR = COUT + 8;                      // stem tile row stride (bf16): 144 B spreads the
+                                                    // epilogue's 4 row groups and the pool's rows over banks
+constexpr int TILE_BYTES = MROWS * TSTR * 2;       // 23040
+
+// TILES_PER_BLOCK = consecutive tiles of one pooled-row strip per block
+template <int TILES_PER_BLOCK>
+__global__ __launch_bounds__(256, 3) void stem_pool_kernel(const uint8_t* __restrict__ img, const bf16* __restrict__ w,
+                                                        const float* __restrict__ bias, bf16* __restrict__ out, int B,
+                                                        int H, int W, int Po, float m0, float m1, float m2, float s0,
+                                                        float s1, float s2, int dbg) {
+  __shared__ __attribute__((aligned(16))) char smem[PATCH_BYTES + TILE_BYTES];
+  bf16* tile = reinterpret_cast<bf16*>(smem + PATCH_BYTES);  // [MROWS][TSTR]
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tw = Po / TPW, th = Po / TPH;
+  const int nparts = (tw + TILES_PER_BLOCK - 1) / TILES_PER_BLOCK;
+  int t = blockIdx.x;
+  const int part = t % nparts;
+  t /= nparts;
+  const int by = t % th;
+  const int b = t / th;
+  MLS_CHECK(b < B, 401);
+  const int bx0 = part * TILES_PER_BLOCK, bx1 = min(tw, bx0 + TILES_PER_BLOCK);
+  const int ph0 = by * TPH;
+  const int sr0 = 2 * ph0 - 1;     // first stem row of the strip (may be -1)
+  const int ir0 = 2 * sr0 - 3;     // first image row of the patch (stride 2, pad 3)
+
+  // weight fragments straight to registers, once per block (2 x 2 waves, a wave = 80 rows x 32 cols)
+  const int wm = wid >> 1, wn = wid & 1;
+  const int fr = lane & 15, fq = lane >> 4;
+  bf16x8 bw[2][7];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = wn * 32 + j * 16 + fr;
+#pragma unroll
+    for (int kh = 0; kh < 7; ++kh)
+      bw[j][kh] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(w + (long)n * KTOT + kh * 32 + fq * 8));
+  }
+  float bj[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) bj[j] = bias[wn * 32 + j * 16 + fr];
+  int abase[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const int p = min(wm * 80 + i * 16 + fr, SP - 1);  // padded rows read a valid pixel, never stored
+    const int sr = p / SC, sc = p - (p / SC) * SC;
+    abase[i] = ((2 * sr) * PC + 2 * sc + 2 * fq) * 8;
+  }
+
+  // epilogue row masks (bit i * 4 + r): padded rows, stem row 0, stem column 0 -- kept as bits so the
+  // tile loop does not hold 20 row / column pairs in registers
+  uint32_t m_pad = 0, m_sr0 = 0, m_sc0 = 0;
+#pragma unroll
+  for (int i = 0; i < 5; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = wm * 80 + i * 16 + fq * 4 + r;
+      const int sr = row / SC, sc = row - (row / SC) * SC;
+      m_pad |= (uint32_t)(row >= SP) << (i * 4 + r);
+      m_sr0 |= (uint32_t)(sr == 0) << (i * 4 + r);
+      m_sc0 |= (uint32_t)(sc == 0) << (i * 4 + r);
+    }
+
+  // image bytes of a tile's patch -> registers (issued a tile ahead: software pipelined)
+  constexpr int PIT = (PR * PC + 255) / 256;  // 4
+  uint8_t px[PIT][3];
+  bool in[PIT];
+  auto fetch = [&](int bx) {
+    const int ic0 = 2 * (2 * (bx * TPW) - 1) - 3;
+#pragma unroll
+    for (int it = 0; it < PIT; ++it) {
+      const int q = tid + it * 256;
+      const int pr = q / PC, pc = q - (q / PC) * PC;
+      const int iy = ir0 + pr, ix = ic0 + pc;
+      in[it] = q < PR * PC && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W && !(dbg & 1);
+      const uint8_t* p = img + (((long)b * H + (in[it] ? iy : 0)) * W + (in[it] ? ix : 0)) * 3;
+      px[it][0] = p[0];
+      px[it][1] = p[1];
+      px[it][2] = p[2];
+    }
+  };
+  fetch(bx0);
+  for (int bx = bx0; bx < bx1; ++bx) {
+    const int pw0 = bx * TPW;
+    const int sc0 = 2 * pw0 - 1;
+    __syncthreads();  // the previous tile's patch / tile reads are done
+    // patch: normalised bf16 x 4 channels, zero outside the image
+#pragma unroll
+    for (int it = 0; it < PIT; ++it) {
+      const int q = tid + it * 256;
+      if (q >= PR * PC) break;
+      bf16x4 v;
+      v[0] = (bf16)(in[it] ? ((float)px[it][0] - m0) * s0 : 0.f);
+      v[1] = (bf16)(in[it] ? ((float)px[it][1] - m1) * s1 : 0.f);
+      v[2] = (bf16)(in[it] ? ((float)px[it][2] - m2) * s2 : 0.f);
+      v[3] = (bf16)0.f;
+      *reinterpret_cast<uint2*>(smem + q * 8) = __builtin_bit_cast(uint2, v);
+    }
+    if (bx + 1 < bx1) fetch(bx + 1);  // next tile's bytes fly during this tile's math
+    __syncthreads();
+
+    // MFMA over the 7 kernel rows
+    f32x4 acc[5][2];
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kh = 0; kh < 7; ++kh) {
+      if (dbg & 2) break;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        const bf16x8 av = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(smem + abase[i] + kh * PC * 8));
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bw[j][kh], acc[i][j], 0, 0, 0);
+      }
+    }
+
+    // bias + ReLU -> bf16 stem tile in LDS; stem pixels outside the image (row / column -1) -> 0
+    const uint32_t zero = (sr0 < 0 ? m_sr0 : 0u) | (sc0 < 0 ? m_sc0 : 0u);
+    bf16* trow = tile + (wm * 80 + fq * 4) * TSTR + wn * 32 + fr;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 5; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int k = i * 4 + r;
+          if (!((m_pad >> k) & 1u))
+            trow[(i * 16 + r) * TSTR + j * 16] = (bf16)(((zero >> k) & 1u) ? 0.f : fmaxf(acc[i][j][r] + bj[j], 0.f));
+        }
+    __syncthreads();
+
+    // 3x3 / 2 max pool: thread = one pooled pixel x 8 channels
+    const int pp = tid >> 3, c8 = tid & 7;
+    const int pr = pp / TPW, pc = pp - (pp / TPW) * TPW;
+    float m[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        const int row = (2 * pr + dy) * SC + 2 * pc + dx;
+        float v[8];
+        unpack8(*reinterpret_cast<const uint4*>(tile + row * TSTR + c8 * 8), v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], v[e]);
+      }
+    if (dbg & 4) {
+      if (m[0] == 12345.f) st16(out, pack8(m));  // keep the work live; never true
+      continue;
+    }
+    st16(out + (((long)b * Po + ph0 + pr) * Po + pw0 + pc) * COUT + c8 * 8, pack8(m));
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// images uint8 [B][H][W][3]; w = the packed stem weights [64][7][8][4] bf16 (BN scale folded);
+// bias fp32 [64]; out bf16 [B][Po][Po][64] with Po = H / 4.  224 x 224 (ResNet) only.
+int mls_stem_pool(const void* images, const void* w, const float* bias, void* out, int B, int H, int W,
+                  const float* mean3, const float* std3, void* stream) {
+  if (B <= 0 || H != 224 || W != 224) return MLS_UNSUPPORTED;
+  const int Po = H / 4;  // stem 112 -> pool 56
+  if (Po % TPH || Po % TPW) return MLS_UNSUPPORTED;
+  static const int dbg = [] {  // ablation flags for tools/probe/stem_pool_probe.py: 1 no image loads, 2 no MFMA, 4 no stores
+    const char* e = getenv("MLS_STEM_DBG");
+    return e ? atoi(e) : 0;
+  }();
+  // tiles per block (1, 2, 4 or 7; MLS_STEM_TPB overrides for the probe).  7 = a whole pooled-row
+  // strip: 25.9 us vs 28.9 (1 tile) with 4 copies co-running, 35.0 vs 32.0 alone
+  // (profiles/r1_stem_pool_tiles_per_block.jsonl); the engine runs 5 batches in flight.
+  static const int tpb = [] {
+    const char* e = getenv("MLS_STEM_TPB");
+    const int v = e ? atoi(e) : 7;
+    return v == 1 || v == 2 || v == 4 ? v : 7;
+  }();
+  const long blocks = (long)B * (Po / TPH) * ((Po / TPW + tpb - 1) / tpb);
+  if (blocks > 0x7fffffffL) return MLS_BAD_ARG;
+  auto kernel = tpb == 1 ? stem_pool_kernel<1> : tpb == 2 ? stem_pool_kernel<2> : tpb == 7 ? stem_pool_kernel<7>
+                                                                                            : stem_pool_kernel<4>;
+  hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)images,
+                     (const bf16*)w, bias, (bf16*)out, B, H, W, Po, mean3[0], mean3[1], mean3[2], 1.f / std3[0],
+                     1.f / std3[1], 1.f / std3[2], dbg);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"
+
+MLS_DEBUG_EXPORT(stem_pool)

@@ -229,3 +229,38 @@ def test_conv1x1_dual(shape, cfg, splitk):
     ref = torch.relu(y.float() @ w1.float().T + xs.float() @ w2.float().T + b)
     assert out.shape == (B, Ho, Wo, cout)
     assert rel_err(out, ref) < 2e-2
+
+
+@pytest.mark.parametrize("B", [1, 3])
+def test_stem_pool_fused_matches_three_kernels(B):
+    """csrc/stem_pool.hip (normalise + 7x7/2 stem + ReLU + 3x3/2 max pool in one kernel) against the
+    three-kernel path it replaces, and against the fp32 PyTorch reference of the same ops."""
+    import torch.nn.functional as F
+
+    from mlmicroservicetemplate_amd import ops
+    from mlmicroservicetemplate_amd.models.resnet import IMAGENET_MEAN, IMAGENET_STD
+
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device="cpu").manual_seed(B)
+    imgs = torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8, generator=g).to(dev)
+    w = (torch.randn(64, 3, 7, 7, generator=g) * 0.05).to(dev)
+    bias = (torch.randn(64, generator=g) * 0.5).to(dev)
+    wp = ops.pack_conv_weight(w.to(torch.bfloat16))
+    fused = ops.stem_pool_u8(imgs, wp, bias, IMAGENET_MEAN, IMAGENET_STD)
+    x = ops.normalize_u8(imgs, IMAGENET_MEAN, IMAGENET_STD, pad=3)
+    y = ops.conv2d_nhwc(x, wp, bias, kernel=7, stride=2, pad=0, act=ops.ACT_RELU,
+                        workspace=torch.empty(1 << 20, device=dev, dtype=torch.float32))
+    three = ops.maxpool2d_nhwc(y, 3, 2, 1)
+    torch.cuda.synchronize()
+    assert fused.shape == three.shape == (B, 56, 56, 64)
+    diff = (fused.float() - three.float()).abs()
+    assert diff.max().item() <= 0.02 * three.float().abs().max().item()  # fp32 summation order only
+    assert (diff > 0).float().mean().item() < 0.02
+    # fp32 reference
+    mean = torch.tensor(IMAGENET_MEAN, device=dev).view(1, 3, 1, 1)
+    std = torch.tensor(IMAGENET_STD, device=dev).view(1, 3, 1, 1)
+    xr = ((imgs.permute(0, 3, 1, 2).float() - mean) / std).to(torch.bfloat16).float()
+    ref = F.max_pool2d(F.relu(F.conv2d(xr, w.to(torch.bfloat16).float(), bias, stride=2, padding=3)), 3, 2, 1)
+    ref = ref.permute(0, 2, 3, 1)
+    err = ((fused.float() - ref).abs().max() / ref.abs().max()).item()
+    assert err < 2e-2, err
