@@ -258,6 +258,8 @@ class BertFused:
         cb[:C] = self.w["cls.b"]
         self.cls_w, self.cls_b = cw, cb
         self._ws = ops.StreamWorkspace(16 << 20, self.device)  # per stream: concurrent engine slots
+        if self.device.type == "cuda":
+            ops.load_blas_tuning()  # TunableOp-measured hipBLASLt solutions (FFN-up)
 
     def forward(self, ids: torch.Tensor, type_ids: Optional[torch.Tensor], lens: torch.Tensor) -> torch.Tensor:
         """ids/type_ids int32 ``[B, S]``, lens int32 ``[B]`` -> bf16 logits ``[B, Cpad]``."""

@@ -239,6 +239,25 @@ def gemm(
     return out
 
 
+_TUNED_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned")
+def load_blas_tuning(path: Optional[str] = None) -> bool:
+    """Make hipBLASLt use the solutions PyTorch TunableOp measured fastest on MI355X for the shapes
+    in ``tuned/tunableop_gfx950.csv`` (BERT FFN-up + GELU: 26.4 vs 30.1 us at 4-way concurrency,
+    ``profiles/r1_bert_gemm_probe.jsonl``).  Lookup only -- tuning stays off, so nothing is timed or
+    written at run time, and untuned shapes keep the library default.  ``MLS_BLAS_TUNING=0``
+    disables it.  Returns whether the table was loaded."""
+    if os.environ.get("MLS_BLAS_TUNING", "1") == "0" or not torch.cuda.is_available():
+        return False
+    from torch.cuda import tunable
+
+    tunable.enable(True)
+    tunable.tuning_enable(False)
+    ok = bool(tunable.read_file(path or os.path.join(_TUNED_DIR, "tunableop_gfx950.csv")))
+    if not ok:
+        tunable.enable(False)
+    return ok
+
+
 def gemm_rmsnorm(x: torch.Tensor, w_folded: torch.Tensor, delta: Optional[torch.Tensor] = None,
                  resid_out: Optional[torch.Tensor] = None, *, act=ACT_NONE, eps: float = 1e-5,
                  workspace: Optional[torch.Tensor] = None, splitk: int = 0) -> torch.Tensor:

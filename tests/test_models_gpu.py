@@ -141,14 +141,18 @@ def test_topk_large():
     assert torch.allclose(v, rv) and torch.allclose(x.float().gather(1, i.long()), rv)
 
 
-@pytest.mark.parametrize("B", [4, 16])  # 256 tokens: native GEMMs; 1024: hipBLASLt + LN-fused residual
-def test_bert_fused_matches_reference(B):
+# 256 tokens: native GEMMs; 1024: hipBLASLt + LN-fused residual; 4096 (the benchmark shape):
+# + the TunableOp-chosen hipBLASLt FFN-up solution (ops/tuned/tunableop_gfx950.csv)
+@pytest.mark.parametrize("B,S", [(4, 64), (16, 64), (32, 128)])
+def test_bert_fused_matches_reference(B, S):
+    from mlmicroservicetemplate_amd import ops
     from mlmicroservicetemplate_amd.models import bert
 
     cfg = bert.BertConfig(num_labels=3)
     p = bert.init_bert(cfg, 0)
     torch.manual_seed(1)
-    S = 64
+    if B * S == 4096:
+        assert ops.load_blas_tuning()
     ids = torch.randint(1000, cfg.vocab, (B, S), device=DEV, dtype=torch.int32)
     tt = torch.zeros_like(ids)
     lens = torch.tensor(([64, 33, 10, 1] * (B // 4)), device=DEV, dtype=torch.int32)

@@ -1,0 +1,25 @@
+"""Shipped tuning tables (ops/tuned/): well-formed, and lookups behave on a host without a GPU."""
+import csv
+import json
+import os
+
+from mlmicroservicetemplate_amd import ops
+
+TUNED = os.path.join(os.path.dirname(ops.__file__), "tuned")
+
+
+def test_tunableop_table_and_cpu_noop():
+    with open(os.path.join(TUNED, "tunableop_gfx950.csv")) as f:
+        rows = list(csv.reader(f))
+    validators = {r[1] for r in rows if r[0] == "Validator"}
+    assert {"PT_VERSION", "GCN_ARCH_NAME", "HIPBLASLT_VERSION"} <= validators
+    entries = [r for r in rows if r[0] != "Validator"]
+    assert entries and all(len(r) == 4 and r[0].endswith("TunableOp_BFloat16_TN") for r in entries)
+    assert ops.load_blas_tuning() is False  # no GPU here: nothing enabled
+
+
+def test_resnet_table_loads():
+    from mlmicroservicetemplate_amd.ops import autotune
+
+    t = autotune.load_tuning("resnet50", 32)
+    assert "stem" in t and all(len(v) == 2 for v in t.values())

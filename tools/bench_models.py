@@ -33,10 +33,12 @@ def bench_bert(args):
             toks = [list(rng.integers(1000, 30000, S)) for _ in range(B)]
             packed = bert.pack_requests(toks, S).numpy()
             for name, model in models.items():
-                def fwd(x, model=model, S=S):
+                def fwd(x, model=model, S=S, name=name):
                     ids, tt, lens = bert.unpack_requests(x, S)
+                    if name == "fused":  # the serving head (plugins/text_classifier.py): fused softmax + top-k
+                        return model.classify(ids, tt, lens, 2)
                     logits = model(ids, tt, lens)
-                    v, i = torch.topk(logits.float(), 2, dim=-1)
+                    v, i = torch.topk(torch.softmax(logits.float(), -1), 2, dim=-1)
                     return v, i.to(torch.int32)
 
                 eng = GpuEngine(fwd, dev, (2 * S + 1,), torch.int32, buckets=[B], inflight=args.inflight, concurrent=True)
