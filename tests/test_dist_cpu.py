@@ -1,4 +1,4 @@
-"""X1 weight broadcast / X6 health / max-over-ranks on a gloo 'fake cluster' (world 2 and 4)."""
+"""X1 weight broadcast / X6 health / max-over-ranks on a gloo 'fake cluster' (world 2, 4 and 8)."""
 import os
 import socket
 
@@ -40,7 +40,7 @@ def _worker(rank, world, port, q):
         mdist.destroy()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 @pytest.mark.timeout(180)
 def test_collectives_gloo(world):
     ctx = mp.get_context("spawn")
