@@ -97,6 +97,11 @@ def _workspace_args(ws: Optional[torch.Tensor]):
     return ws.data_ptr(), ws.numel() * ws.element_size()
 
 
+# conv2d_nhwc ``cfg`` that selects the halo-tiled direct 3x3 kernel (csrc/conv3x3_halo.hip) instead
+# of an implicit-GEMM tile config; a tuning-table value like any other.
+CFG_HALO = 100
+
+
 def conv2d_nhwc(
     x: torch.Tensor,
     w: torch.Tensor,
@@ -129,6 +134,10 @@ def conv2d_nhwc(
     if cout % 8:
         raise ValueError("Cout must be a multiple of 8")
     ho, wo = conv_out_hw(H, W, kernel, stride, pad)
+    if cfg == CFG_HALO:
+        if kernel != 3 or stride != 1 or pad != 1 or scale is not None:
+            raise ValueError("CFG_HALO: 3x3 / stride 1 / pad 1 convolutions without a scale only")
+        return conv3x3_halo(x, w, bias, act=act, residual=residual, out=out)
     for name, t in (("bias", bias), ("scale", scale)):
         if t is not None:
             _need(t, name, torch.float32, dev)
@@ -415,6 +424,45 @@ def stem_pool_u8(images: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, mean
     check(lib().mls_stem_pool(images.data_ptr(), w.data_ptr(), bias.data_ptr(), out.data_ptr(), B, H, W, m, s,
                               stream_ptr(dev)), "mls_stem_pool")
     return out
+
+
+def conv3x3_halo(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, act=ACT_NONE,
+                 residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """3x3 / stride 1 / pad 1 NHWC conv on the halo-tiled direct kernel (csrc/conv3x3_halo.hip):
+    x ``[B,H,W,Cin]`` bf16, w packed ``[N,3,3,Cin]`` bf16, bias fp32 ``[N]`` -> ``[B,H,W,N]``
+    ``act(conv + bias (+ residual))``.  Cin % 32 == 0, N % 64 == 0."""
+    dev = x.device
+    _need(x, "x", torch.bfloat16, dev)
+    _need(w, "w", torch.bfloat16, dev)
+    B, H, W, C = x.shape
+    N = w.shape[0]
+    if tuple(w.shape) != (N, 3, 3, C) or C % 32 or N % 64:
+        raise ValueError("conv3x3_halo: w must be [N,3,3,Cin], Cin % 32 == 0, N % 64 == 0")
+    if bias is not None:
+        _need(bias, "bias", torch.float32, dev)
+        if bias.numel() != N:
+            raise ValueError("bias must have N elements")
+    shape = (B, H, W, N)
+    if residual is not None:
+        _need(residual, "residual", torch.bfloat16, dev)
+        if tuple(residual.shape) != shape:
+            raise ValueError(f"residual must be {shape}")
+    if out is None:
+        out = torch.empty(shape, device=dev, dtype=torch.bfloat16)
+    else:
+        _need(out, "out", torch.bfloat16, dev)
+        if tuple(out.shape) != shape:
+            raise ValueError(f"out must be {shape}")
+    check(lib().mls_conv3x3_halo(x.data_ptr(), w.data_ptr(), _ptr(bias), _ptr(residual), out.data_ptr(), B, H, W, C,
+                                 N, _act(act), stream_ptr(dev)), "mls_conv3x3_halo")
+    return out
+
+
+def conv3x3_halo_geometry(B: int, H: int, W: int) -> Optional[Tuple[int, int]]:
+    """(output rows per tile, images per tile) the halo kernel uses for this shape, or None."""
+    th, nb = ctypes.c_int(0), ctypes.c_int(0)
+    rc = lib().mls_conv3x3_halo_geometry(B, H, W, ctypes.byref(th), ctypes.byref(nb))
+    return (th.value, nb.value) if rc == 0 else None
 
 
 def maxpool2d_nhwc(x: torch.Tensor, k: int = 3, s: int = 2, p: int = 1, out: Optional[torch.Tensor] = None):

@@ -40,6 +40,8 @@ _SIGS = {
     "mls_normalize_u8": [P, P, I, I, I, I, FP, FP, P],
     "mls_maxpool2d": [P, P, I, I, I, I, I, I, I, P],
     "mls_stem_pool": [P, P, P, P, I, I, I, FP, FP, P],
+    "mls_conv3x3_halo": [P, P, P, P, P, I, I, I, I, I, I, P],
+    "mls_conv3x3_halo_geometry": [I, I, I, _c.POINTER(I), _c.POINTER(I)],
     "mls_avgpool_global": [P, P, I, I, I, P],
     "mls_bn_act": [P, P, P, P, L, I, I, P],
     "mls_silu_mul_interleaved": [P, P, L, I, P],
@@ -89,7 +91,7 @@ def _bind(lib: ctypes.CDLL) -> None:
 
 
 DEBUG = os.environ.get("MLS_DEBUG", "0") == "1"
-DEBUG_TUS = ("attention", "norm_ops", "stem_pool")  # translation units with MLS_CHECK bounds
+DEBUG_TUS = ("attention", "norm_ops", "stem_pool", "conv3x3_halo")  # translation units with MLS_CHECK bounds
 DEBUG_CODES = {
     101: "rope/KV append: cache slot beyond the cache",
     102: "rope/KV append: position beyond the RoPE table",

@@ -1,0 +1,297 @@
+// Halo-tiled direct 3x3 / stride 1 / pad 1 convolution, NHWC bf16, for the ResNet bottleneck conv2
+// layers (56x56x64, 28x28x128, 14x14x256, 7x7x512).
+//
+// Why not the implicit GEMM of conv_gemm.hip: there every k-step re-gathers a BM x 64 slice of the
+// input for ONE tap, so each input pixel crosses L2 -> LDS nine times, and a 128x128 tile at BK 64
+// needs ~150 GB/s per CU of L2 bandwidth to keep its MFMAs busy -- about what a CU gets
+// (docs/PERF_NOTES.md).  Here a block owns a whole spatial tile -- nb images x th output rows x the
+// full width W (<= 256 output pixels, contiguous in the NHWC output) -- and per 32-channel chunk
+// stages the input patch WITH its 1-pixel halo once ((th + 2) x (W + 2) pixels x 64 B) plus the
+// 9 taps' weights for 64 output channels (36 KB); all 9 taps then read their A fragments from the
+// same patch at a (kh, kw) pixel offset.  Per chunk: ~60 KB of LDS-DMA for 2 x 16 x 64 x 9 x 32
+// MACs -- ~2.5x the arithmetic intensity of the 128x128 implicit-GEMM tile.
+//
+// Layout: patch [pixel][4 x 16-B chunks] (a fragment row = one pixel's 64 B); weights
+// [tap][64 cols][4 chunks], chunk-swizzled so the B reads are conflict-free (the A reads of a row
+// block that wraps a patch row cannot be swizzled for every alignment and stay <= 2-way).  Both are
+// filled by buffer_load ... lds (LDS DMA; out-of-image halo pixels get an out-of-range offset and
+// read as zero = the conv padding).  One 60 KB stage per block so TWO blocks share a CU and
+// overlap each other's loads (the double-buffered 120 KB variant, MLS_HALO_STAGES=2, measured
+// slower under concurrency: profiles/r1_halo_probe_stages.jsonl).  8 waves: wave w owns MFMA row
+// blocks w and w + 8 (16 output pixels each) x all 4 column blocks; a tap's fragments are read
+// while the previous tap's MFMAs run.  Epilogue: bias + activation (+ optional residual) -> bf16
+// tile in LDS -> 16-B coalesced stores.
+//
+// Selected per layer by the tuning table (ops.CFG_HALO); at bs=32 under 4-way concurrency it wins
+// 12 of the 13 stride-1 3x3 layers (13.5 vs 19.1 us on layer1, profiles/r1_halo_vs_table_c4.jsonl)
+// and lifts bench.py from 48.0k to 49.6k req/s.
+#include "common.h"
+
+#include <cstdlib>
+
+namespace {
+
+constexpr int CK = 32;                        // input channels per chunk = one MFMA k-slab
+constexpr int BN = 64;                        // output channels per block
+constexpr int NWAVE = 8, NTHR = NWAVE * 64;
+constexpr int MAX_ROWS = 256;                 // output pixels per block (16 MFMA row blocks)
+constexpr int PATCH_MAX = 384;                // input pixels per patch
+constexpr int PATCH_BYTES = PATCH_MAX * CK * 2;  // 24576
+constexpr int W_BYTES = 9 * BN * CK * 2;         // 36864 = 36 DMA pieces of 1 KB
+constexpr int W_PIECES = W_BYTES / 1024;
+constexpr int STAGE = PATCH_BYTES + W_BYTES;     // 61440
+constexpr int EPI_LD = BN + 8;                   // bf16 row stride of the epilogue tile (144 B)
+static_assert(MAX_ROWS * EPI_LD * 2 <= STAGE, "epilogue tile fits a stage buffer");
+constexpr int PP_WAVE = (PATCH_MAX / 16 + NWAVE - 1) / NWAVE;  // patch pieces per wave (max)
+constexpr int WP_WAVE = (W_PIECES + NWAVE - 1) / NWAVE;        // weight pieces per wave (max)
+
+#define LDS3 __attribute__((address_space(3)))
+
+MLS_DEV void glds16(rsrc_t r, char* lds, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS3 void*)lds, 16, voff, soff, 0, 0);
+}
+
+struct HaloArgs {
+  const bf16* x;     // [B][H][W][Cin]
+  const bf16* w;     // [N][3][3][Cin]
+  const float* bias; // [N] fp32 or null
+  const bf16* res;   // [B][H][W][N] or null
+  bf16* out;         // [B][H][W][N]
+  int B, H, W, Cin, N, th, nb, act;
+  uint32_t x_bytes, w_bytes;
+};
+
+// Weight image swizzle: 16-B chunk ch of column n sits at ch ^ h((n >> 2) & 3), h = {0, 2, 3, 1}:
+// the four 16-lane groups of a ds_read_b128 ({0-3,12-15,20-27}, ...) then hit 16 distinct bank
+// quads (MI355X_MICROARCH.md, LDS table); unswizzled they conflict 2-way.
+MLS_DEV int wswz(int n) { return (0x78 >> (2 * ((n >> 2) & 3))) & 3; }
+
+// STAGES = 2: chunk c + 1 in flight during chunk c's MFMAs, 120 KB of LDS (one block per CU);
+// STAGES = 1: 60 KB, two blocks per CU overlap each other's loads (and other streams' blocks).
+template <int STAGES>
+__global__ __launch_bounds__(NTHR) void conv3x3_halo_kernel(const HaloArgs a) {
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int W2 = a.W + 2, TH2 = a.th + 2;
+  const int R = a.nb * a.th * a.W;  // output pixels of the tile
+  const int P = a.nb * TH2 * W2;    // patch pixels
+  const int tiles = (a.B / a.nb) * (a.H / a.th);
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int tn = t / tiles, tile = t - tn * tiles;  // column-block-major: neighbours share weights
+  MLS_CHECK(tn * BN < a.N, 501);
+  const int n0 = tn * BN;
+  const int tpi = a.H / a.th;  // tiles per image (nb == 1)
+  const int b0 = a.nb > 1 ? tile * a.nb : tile / tpi;
+  const int oh0 = a.nb > 1 ? 0 : (tile - (tile / tpi) * tpi) * a.th;
+  const long m_base = (long)tile * R;  // the tile's output pixels are contiguous rows
+
+  // A fragments: patch pixel of tap (0, 0) for this lane's row in each of the wave's row blocks
+  int pb[2];
+  bool rb_on[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int rb = wid + NWAVE * i;
+    rb_on[i] = rb * 16 < R;
+    const int r = min(rb * 16 + fr, R - 1);  // padded rows read a valid pixel, never stored
+    const int img = r / (a.th * a.W);
+    const int rem = r - img * (a.th * a.W);
+    const int ohl = rem / a.W, ow = rem - (rem / a.W) * a.W;
+    pb[i] = (img * TH2 + ohl) * W2 + ow;
+  }
+
+  // DMA source offsets without the chunk's channel base (added as the scalar offset)
+  const int npieces = (P + 15) / 16;
+  int xoff[PP_WAVE];
+#pragma unroll
+  for (int s = 0; s < PP_WAVE; ++s) {
+    const int j = wid + NWAVE * s;
+    const int px = j * 16 + (lane >> 2), ch = lane & 3;
+    xoff[s] = OOB;
+    if (px < P) {
+      const int img = px / (TH2 * W2);
+      const int rem = px - img * (TH2 * W2);
+      const int pr = rem / W2, pc = rem - (rem / W2) * W2;
+      const int b = b0 + img, ih = oh0 + pr - 1, iw = pc - 1;
+      if (b < a.B && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
+        xoff[s] = (((b * a.H + ih) * a.W + iw) * a.Cin + ch * 8) * 2;
+    }
+  }
+  const int K = 9 * a.Cin;
+  int woff[WP_WAVE];
+#pragma unroll
+  for (int s = 0; s < WP_WAVE; ++s) {
+    const int j = wid + NWAVE * s;
+    const int q = j * 64 + lane;
+    const int n = (q >> 2) & (BN - 1), tap = q >> 8;
+    const int ch = (q & 3) ^ wswz(n);  // LDS slot (q & 3) holds source chunk ch (DMA writes lane-linearly)
+    woff[s] = j < W_PIECES ? ((n0 + n) * K + tap * a.Cin + ch * 8) * 2 : OOB;
+  }
+  const rsrc_t xr = make_rsrc(a.x, a.x_bytes);
+  const rsrc_t wr = make_rsrc(a.w, a.w_bytes);
+
+  auto issue = [&](int c, int buf) {
+    char* sP = smem + buf * STAGE;
+    char* sW = sP + PATCH_BYTES;
+    const int cb = c * CK * 2;
+#pragma unroll
+    for (int s = 0; s < PP_WAVE; ++s) {
+      const int j = wid + NWAVE * s;
+      if (j < npieces) glds16(xr, sP + j * 1024, xoff[s], cb);
+    }
+#pragma unroll
+    for (int s = 0; s < WP_WAVE; ++s) {
+      const int j = wid + NWAVE * s;
+      if (j < W_PIECES) glds16(wr, sW + j * 1024, woff[s], cb);
+    }
+  };
+
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nchunks = a.Cin / CK;
+  const int bsw = (fq ^ wswz(fr)) * 16;  // this lane's B chunk slot (j * 16 keeps (n >> 2) & 3)
+  if (STAGES == 2) issue(0, 0);
+  for (int c = 0; c < nchunks; ++c) {
+    if (STAGES == 1) {
+      if (c > 0) __syncthreads();  // every wave is done reading chunk c - 1
+      issue(c, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // chunk c landed for every wave; every wave is done reading chunk c - 1
+    if (STAGES == 2 && c + 1 < nchunks) issue(c + 1, (c + 1) & 1);
+    const char* sP = smem + (STAGES == 2 ? (c & 1) * STAGE : 0);
+    const char* sW = sP + PATCH_BYTES;
+    // fragments of tap t + 1 are read while tap t's 8 MFMAs run (register double buffer); both
+    // row blocks are always computed (a padded row block reads clamped pixels and is not stored)
+    // so the tap loop has no branches for the scheduler to stop at
+    const char* pA0 = sP + (pb[0] * 4 + fq) * 16;
+    const char* pA1 = sP + (pb[1] * 4 + fq) * 16;
+    const char* pB = sW + fr * 64 + bsw;
+    bf16x8 af[2][2], bf[2][4];
+    auto load = [&](int tap, int slot) {
+      const int toff = ((tap / 3) * W2 + (tap % 3)) * 64;
+      af[slot][0] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(pA0 + toff));
+      af[slot][1] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(pA1 + toff));
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        bf[slot][j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(pB + (tap * BN + j * 16) * 64));
+    };
+    load(0, 0);
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int cur = tap & 1;
+      if (tap + 1 < 9) load(tap + 1, cur ^ 1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[cur][i], bf[cur][j], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  // epilogue: bias + act -> bf16 tile in LDS (reusing the stage buffers) -> 16-B stores
+  float bj[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bj[j] = a.bias ? a.bias[n0 + j * 16 + fr] : 0.f;
+  __syncthreads();  // every wave is done with the last chunk's buffers
+  bf16* to = reinterpret_cast<bf16*>(smem);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    if (!rb_on[i]) continue;
+    const int rb = wid + NWAVE * i;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = rb * 16 + fq * 4 + r;
+        float v = acc[i][j][r] + bj[j];
+        if (!a.res) v = apply_act(v, a.act);
+        to[row * EPI_LD + j * 16 + fr] = (bf16)v;
+      }
+  }
+  __syncthreads();
+  for (int q = tid; q < R * (BN / 8); q += NTHR) {
+    const int row = q >> 3, c8 = q & 7;
+    const long o = (m_base + row) * a.N + n0 + c8 * 8;
+    uint4 v = *reinterpret_cast<const uint4*>(to + row * EPI_LD + c8 * 8);
+    if (a.res) {  // act(conv + bias + residual)
+      float f[8], g[8];
+      unpack8(v, f);
+      unpack8(*reinterpret_cast<const uint4*>(a.res + o), g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = apply_act(f[e] + g[e], a.act);
+      v = pack8(f);
+    }
+    st16(a.out + o, v);
+  }
+}
+
+// Tile geometry for an H x W image: the largest th dividing H with th * W <= 256 output pixels
+// and (th + 2) * (W + 2) <= PATCH_MAX patch pixels; whole images (th == H) are packed nb per
+// block (nb | B).  Returns false when no geometry fits.
+bool halo_geometry(int B, int H, int W, int* th, int* nb) {
+  for (int t = H; t >= 1; --t) {
+    if (H % t || t * W > MAX_ROWS || (t + 2) * (W + 2) > PATCH_MAX) continue;
+    int n = 1;
+    if (t == H)
+      for (int c = 8; c >= 1; --c)
+        if (B % c == 0 && c * H * W <= MAX_ROWS && c * (H + 2) * (W + 2) <= PATCH_MAX) {
+          n = c;
+          break;
+        }
+    *th = t;
+    *nb = n;
+    return true;
+  }
+  return false;
+}
+
+}  // namespace
+
+extern "C" {
+
+// 3x3 / stride 1 / pad 1 conv: x [B][H][W][Cin] bf16, w [N][3][3][Cin] bf16 (the packed conv
+// layout), bias fp32 [N] (BN folded), optional residual [B][H][W][N]; out [B][H][W][N] bf16.
+// Cin % 32 == 0, N % 64 == 0.
+int mls_conv3x3_halo(const void* x, const void* w, const float* bias, const void* res, void* out, int B, int H, int W,
+                     int Cin, int N, int act, void* stream) {
+  if (B <= 0 || H <= 0 || W <= 0 || Cin % CK || Cin <= 0 || N % BN || N <= 0) return MLS_BAD_ARG;
+  int th = 0, nb = 0;
+  if (!halo_geometry(B, H, W, &th, &nb)) return MLS_UNSUPPORTED;
+  const long xb = (long)B * H * W * Cin * 2, wb = (long)N * 9 * Cin * 2;
+  if (xb >= 0x7fffffffL || wb >= 0x7fffffffL || (long)B * H * W * N >= 0x7fffffffL) return MLS_UNSUPPORTED;
+  HaloArgs a;
+  a.x = (const bf16*)x;
+  a.w = (const bf16*)w;
+  a.bias = bias;
+  a.res = (const bf16*)res;
+  a.out = (bf16*)out;
+  a.B = B, a.H = H, a.W = W, a.Cin = Cin, a.N = N, a.th = th, a.nb = nb, a.act = act;
+  a.x_bytes = (uint32_t)xb;
+  a.w_bytes = (uint32_t)wb;
+  const int tiles = (B / nb) * (H / th);
+  const long blocks = (long)tiles * (N / BN);
+  static const int stages = [] {  // MLS_HALO_STAGES=2: the double-buffered variant
+    const char* e = getenv("MLS_HALO_STAGES");
+    return e && atoi(e) == 2 ? 2 : 1;
+  }();
+  if (stages == 2)
+    hipLaunchKernelGGL(conv3x3_halo_kernel<2>, dim3((unsigned)blocks), dim3(NTHR), 0, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(conv3x3_halo_kernel<1>, dim3((unsigned)blocks), dim3(NTHR), 0, (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}
+
+// The geometry the kernel would use (for tests / the tuner): returns 0 and fills th, nb.
+int mls_conv3x3_halo_geometry(int B, int H, int W, int* th, int* nb) {
+  return halo_geometry(B, H, W, th, nb) ? 0 : MLS_UNSUPPORTED;
+}
+
+}  // extern "C"
+
+MLS_DEBUG_EXPORT(conv3x3_halo)

@@ -264,3 +264,31 @@ def test_stem_pool_fused_matches_three_kernels(B):
     ref = ref.permute(0, 2, 3, 1)
     err = ((fused.float() - ref).abs().max() / ref.abs().max()).item()
     assert err < 2e-2, err
+
+
+@pytest.mark.parametrize("B,H,W,cin,cout,resid", [
+    (2, 56, 56, 64, 64, False),   # layer1 conv2: 4 rows x 56 per tile
+    (2, 28, 28, 128, 128, False),  # layer2: 7 x 28
+    (2, 14, 14, 256, 256, False),  # layer3: whole image
+    (8, 7, 7, 512, 512, False),    # layer4: 4 images per tile
+    (3, 10, 12, 32, 64, True),     # odd geometry + residual epilogue
+])
+def test_conv3x3_halo_matches_reference(B, H, W, cin, cout, resid):
+    """csrc/conv3x3_halo.hip (halo-tiled direct 3x3 / s1 / p1) vs the fp32 PyTorch conv, and vs the
+    implicit-GEMM kernel it can replace."""
+    from mlmicroservicetemplate_amd import ops
+
+    g = torch.Generator(device="cpu").manual_seed(H * cin + B)
+    x = torch.randn(B, H, W, cin, generator=g).to(DEV).to(torch.bfloat16)
+    w = (torch.randn(cout, cin, 3, 3, generator=g) / (3 * cin ** 0.5)).to(DEV).to(torch.bfloat16)
+    bias = (torch.randn(cout, generator=g) * 0.1).to(DEV)
+    res = torch.randn(B, H, W, cout, generator=g).to(DEV).to(torch.bfloat16) if resid else None
+    assert ops.conv3x3_halo_geometry(B, H, W) is not None
+    out = ops.conv3x3_halo(x, ops.pack_conv_weight(w), bias, act=ops.ACT_RELU, residual=res)
+    ref = _conv_ref(x, w, bias, 1, 1, 1, res)
+    assert rel_err(out, ref) < 2e-2
+    if cin % 64:
+        return  # the implicit-GEMM kernel needs Cin % 64 == 0
+    gemm = ops.conv2d_nhwc(x, ops.pack_conv_weight(w), bias, kernel=3, stride=1, pad=1, act=ops.ACT_RELU,
+                           residual=res, workspace=torch.empty(8 << 20, device=DEV, dtype=torch.float32))
+    assert rel_err(out, gemm) < 2e-2
