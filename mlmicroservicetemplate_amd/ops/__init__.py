@@ -97,9 +97,10 @@ def _workspace_args(ws: Optional[torch.Tensor]):
     return ws.data_ptr(), ws.numel() * ws.element_size()
 
 
-# conv2d_nhwc ``cfg`` that selects the halo-tiled direct 3x3 kernel (csrc/conv3x3_halo.hip) instead
-# of an implicit-GEMM tile config; a tuning-table value like any other.
+# conv2d_nhwc ``cfg`` values that select the halo-tiled direct 3x3 kernel (csrc/conv3x3_halo.hip,
+# variant 0 / 1) instead of an implicit-GEMM tile config; tuning-table values like any other.
 CFG_HALO = 100
+CFG_HALO_N32 = 101
 
 
 def conv2d_nhwc(
@@ -134,10 +135,10 @@ def conv2d_nhwc(
     if cout % 8:
         raise ValueError("Cout must be a multiple of 8")
     ho, wo = conv_out_hw(H, W, kernel, stride, pad)
-    if cfg == CFG_HALO:
+    if cfg in (CFG_HALO, CFG_HALO_N32):
         if kernel != 3 or stride != 1 or pad != 1 or scale is not None:
             raise ValueError("CFG_HALO: 3x3 / stride 1 / pad 1 convolutions without a scale only")
-        return conv3x3_halo(x, w, bias, act=act, residual=residual, out=out)
+        return conv3x3_halo(x, w, bias, act=act, residual=residual, out=out, variant=cfg - CFG_HALO)
     for name, t in (("bias", bias), ("scale", scale)):
         if t is not None:
             _need(t, name, torch.float32, dev)
@@ -427,17 +428,19 @@ def stem_pool_u8(images: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, mean
 
 
 def conv3x3_halo(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, act=ACT_NONE,
-                 residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+                 variant: int = 0) -> torch.Tensor:
     """3x3 / stride 1 / pad 1 NHWC conv on the halo-tiled direct kernel (csrc/conv3x3_halo.hip):
     x ``[B,H,W,Cin]`` bf16, w packed ``[N,3,3,Cin]`` bf16, bias fp32 ``[N]`` -> ``[B,H,W,N]``
-    ``act(conv + bias (+ residual))``.  Cin % 32 == 0, N % 64 == 0."""
+    ``act(conv + bias (+ residual))``.  Cin % 32 == 0; ``variant`` 0 = 64 output channels x 8
+    waves per block (N % 64 == 0), 1 = 32 x 4 (N % 32 == 0)."""
     dev = x.device
     _need(x, "x", torch.bfloat16, dev)
     _need(w, "w", torch.bfloat16, dev)
     B, H, W, C = x.shape
     N = w.shape[0]
-    if tuple(w.shape) != (N, 3, 3, C) or C % 32 or N % 64:
-        raise ValueError("conv3x3_halo: w must be [N,3,3,Cin], Cin % 32 == 0, N % 64 == 0")
+    if tuple(w.shape) != (N, 3, 3, C) or C % 32 or N % (32 if variant == 1 else 64) or variant not in (0, 1):
+        raise ValueError("conv3x3_halo: w must be [N,3,3,Cin], Cin % 32 == 0, N % 64 (variant 1: 32) == 0")
     if bias is not None:
         _need(bias, "bias", torch.float32, dev)
         if bias.numel() != N:
@@ -454,7 +457,7 @@ def conv3x3_halo(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] 
         if tuple(out.shape) != shape:
             raise ValueError(f"out must be {shape}")
     check(lib().mls_conv3x3_halo(x.data_ptr(), w.data_ptr(), _ptr(bias), _ptr(residual), out.data_ptr(), B, H, W, C,
-                                 N, _act(act), stream_ptr(dev)), "mls_conv3x3_halo")
+                                 N, _act(act), variant, stream_ptr(dev)), "mls_conv3x3_halo")
     return out
 
 

@@ -93,7 +93,7 @@ def tune_resnet50(batch: int, device="cuda:0", iters: int = 20, compare_torch: b
                   candidates: Optional[List[Tuple[int, int]]] = None, concurrency: int = 1) -> Dict[str, dict]:
     """Per-layer (cfg, splitk) search.  ``concurrency`` > 1 scores each candidate by its
     per-batch cost with that many batches co-running (the serving engine's concurrent slots)."""
-    from . import CFG_HALO, conv2d_nhwc, gemm, pack_conv_weight
+    from . import CFG_HALO, CFG_HALO_N32, conv2d_nhwc, gemm, pack_conv_weight
     from ..models.resnet import conv_shapes
 
     dev = torch.device(device)
@@ -117,7 +117,7 @@ def tune_resnet50(batch: int, device="cuda:0", iters: int = 20, compare_torch: b
         best = (1e9, 0, 0)
         tried = {}
         halo = s.k == 3 and s.stride == 1 and s.cin % 32 == 0 and s.cout % 64 == 0
-        for cfg, sk in [(0, 0)] + cands + ([(CFG_HALO, 1)] if halo else []):
+        for cfg, sk in [(0, 0)] + cands + ([(CFG_HALO, 1), (CFG_HALO_N32, 1)] if halo else []):
             if sk > 1 and k // sk < 128:
                 continue
 

@@ -15,10 +15,9 @@
 // [tap][64 cols][4 chunks], chunk-swizzled so the B reads are conflict-free (the A reads of a row
 // block that wraps a patch row cannot be swizzled for every alignment and stay <= 2-way).  Both are
 // filled by buffer_load ... lds (LDS DMA; out-of-image halo pixels get an out-of-range offset and
-// read as zero = the conv padding).  One 60 KB stage per block so TWO blocks share a CU and
-// overlap each other's loads (the double-buffered 120 KB variant, MLS_HALO_STAGES=2, measured
-// slower under concurrency: profiles/r1_halo_probe_stages.jsonl).  8 waves: wave w owns MFMA row
-// blocks w and w + 8 (16 output pixels each) x all 4 column blocks; a tap's fragments are read
+// read as zero = the conv padding).  One stage per block so several blocks share a CU and
+// overlap each other's loads (a double-buffered 120 KB first version, one block per CU, measured
+// slower under concurrency: profiles/r1_halo_probe_stages.jsonl).  A tap's fragments are read
 // while the previous tap's MFMAs run.  Epilogue: bias + activation (+ optional residual) -> bf16
 // tile in LDS -> 16-B coalesced stores.
 //
@@ -27,23 +26,13 @@
 // and lifts bench.py from 48.0k to 49.6k req/s.
 #include "common.h"
 
-#include <cstdlib>
 
 namespace {
 
-constexpr int CK = 32;                        // input channels per chunk = one MFMA k-slab
-constexpr int BN = 64;                        // output channels per block
-constexpr int NWAVE = 8, NTHR = NWAVE * 64;
-constexpr int MAX_ROWS = 256;                 // output pixels per block (16 MFMA row blocks)
-constexpr int PATCH_MAX = 384;                // input pixels per patch
+constexpr int CK = 32;                           // input channels per chunk = one MFMA k-slab
+constexpr int MAX_ROWS = 256;                    // output pixels per block (16 MFMA row blocks)
+constexpr int PATCH_MAX = 384;                   // input pixels per patch
 constexpr int PATCH_BYTES = PATCH_MAX * CK * 2;  // 24576
-constexpr int W_BYTES = 9 * BN * CK * 2;         // 36864 = 36 DMA pieces of 1 KB
-constexpr int W_PIECES = W_BYTES / 1024;
-constexpr int STAGE = PATCH_BYTES + W_BYTES;     // 61440
-constexpr int EPI_LD = BN + 8;                   // bf16 row stride of the epilogue tile (144 B)
-static_assert(MAX_ROWS * EPI_LD * 2 <= STAGE, "epilogue tile fits a stage buffer");
-constexpr int PP_WAVE = (PATCH_MAX / 16 + NWAVE - 1) / NWAVE;  // patch pieces per wave (max)
-constexpr int WP_WAVE = (W_PIECES + NWAVE - 1) / NWAVE;        // weight pieces per wave (max)
 
 #define LDS3 __attribute__((address_space(3)))
 
@@ -66,11 +55,29 @@ struct HaloArgs {
 // quads (MI355X_MICROARCH.md, LDS table); unswizzled they conflict 2-way.
 MLS_DEV int wswz(int n) { return (0x78 >> (2 * ((n >> 2) & 3))) & 3; }
 
-// STAGES = 2: chunk c + 1 in flight during chunk c's MFMAs, 120 KB of LDS (one block per CU);
-// STAGES = 1: 60 KB, two blocks per CU overlap each other's loads (and other streams' blocks).
-template <int STAGES>
-__global__ __launch_bounds__(NTHR) void conv3x3_halo_kernel(const HaloArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE];
+// BN output channels per block, NW waves; wave w owns MFMA row blocks w, w + NW, ... (16 / NW of
+// them) x all BN / 16 column blocks.  <64, 8>: 60 KB of LDS (2 blocks per CU); <32, 4>: 42 KB
+// (3 per CU), half the MFMA work per staged patch.
+template <int BN, int NW>
+struct HaloCfg {
+  static constexpr int NTHR = NW * 64;
+  static constexpr int W_BYTES = 9 * BN * CK * 2;
+  static constexpr int W_PIECES = W_BYTES / 1024;
+  static constexpr int STAGE = PATCH_BYTES + W_BYTES;
+  static constexpr int EPI_LD = BN + 8;  // bf16 row stride of the epilogue tile
+  static constexpr int RBW = 16 / NW;    // row blocks per wave
+  static constexpr int CB = BN / 16;     // column blocks
+  static constexpr int PP_WAVE = (PATCH_MAX / 16 + NW - 1) / NW;
+  static constexpr int WP_WAVE = (W_PIECES + NW - 1) / NW;
+  static_assert(MAX_ROWS * EPI_LD * 2 <= STAGE, "epilogue tile fits the stage buffer");
+  static_assert(RBW * NW == 16 && CB * 16 == BN, "tile split");
+};
+
+template <int BN, int NW>
+__global__ __launch_bounds__(NW * 64) void conv3x3_halo_kernel(const HaloArgs a) {
+  using C = HaloCfg<BN, NW>;
+  constexpr int RBW = C::RBW, CB = C::CB;
+  __shared__ __attribute__((aligned(16))) char smem[C::STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fq = lane >> 4;
@@ -88,11 +95,11 @@ __global__ __launch_bounds__(NTHR) void conv3x3_halo_kernel(const HaloArgs a) {
   const long m_base = (long)tile * R;  // the tile's output pixels are contiguous rows
 
   // A fragments: patch pixel of tap (0, 0) for this lane's row in each of the wave's row blocks
-  int pb[2];
-  bool rb_on[2];
+  int pb[RBW];
+  bool rb_on[RBW];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int rb = wid + NWAVE * i;
+  for (int i = 0; i < RBW; ++i) {
+    const int rb = wid + NW * i;
     rb_on[i] = rb * 16 < R;
     const int r = min(rb * 16 + fr, R - 1);  // padded rows read a valid pixel, never stored
     const int img = r / (a.th * a.W);
@@ -103,10 +110,10 @@ __global__ __launch_bounds__(NTHR) void conv3x3_halo_kernel(const HaloArgs a) {
 
   // DMA source offsets without the chunk's channel base (added as the scalar offset)
   const int npieces = (P + 15) / 16;
-  int xoff[PP_WAVE];
+  int xoff[C::PP_WAVE];
 #pragma unroll
-  for (int s = 0; s < PP_WAVE; ++s) {
-    const int j = wid + NWAVE * s;
+  for (int s = 0; s < C::PP_WAVE; ++s) {
+    const int j = wid + NW * s;
     const int px = j * 16 + (lane >> 2), ch = lane & 3;
     xoff[s] = OOB;
     if (px < P) {
@@ -119,66 +126,55 @@ __global__ __launch_bounds__(NTHR) void conv3x3_halo_kernel(const HaloArgs a) {
     }
   }
   const int K = 9 * a.Cin;
-  int woff[WP_WAVE];
+  int woff[C::WP_WAVE];
 #pragma unroll
-  for (int s = 0; s < WP_WAVE; ++s) {
-    const int j = wid + NWAVE * s;
+  for (int s = 0; s < C::WP_WAVE; ++s) {
+    const int j = wid + NW * s;
     const int q = j * 64 + lane;
-    const int n = (q >> 2) & (BN - 1), tap = q >> 8;
+    const int n = (q >> 2) & (BN - 1), tap = q / (4 * BN);
     const int ch = (q & 3) ^ wswz(n);  // LDS slot (q & 3) holds source chunk ch (DMA writes lane-linearly)
-    woff[s] = j < W_PIECES ? ((n0 + n) * K + tap * a.Cin + ch * 8) * 2 : OOB;
+    woff[s] = j < C::W_PIECES ? ((n0 + n) * K + tap * a.Cin + ch * 8) * 2 : OOB;
   }
   const rsrc_t xr = make_rsrc(a.x, a.x_bytes);
   const rsrc_t wr = make_rsrc(a.w, a.w_bytes);
+  char* sP = smem;
+  char* sW = smem + PATCH_BYTES;
 
-  auto issue = [&](int c, int buf) {
-    char* sP = smem + buf * STAGE;
-    char* sW = sP + PATCH_BYTES;
-    const int cb = c * CK * 2;
+  f32x4 acc[RBW][CB];
 #pragma unroll
-    for (int s = 0; s < PP_WAVE; ++s) {
-      const int j = wid + NWAVE * s;
-      if (j < npieces) glds16(xr, sP + j * 1024, xoff[s], cb);
-    }
+  for (int i = 0; i < RBW; ++i)
 #pragma unroll
-    for (int s = 0; s < WP_WAVE; ++s) {
-      const int j = wid + NWAVE * s;
-      if (j < W_PIECES) glds16(wr, sW + j * 1024, woff[s], cb);
-    }
-  };
-
-  f32x4 acc[2][4];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < CB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nchunks = a.Cin / CK;
   const int bsw = (fq ^ wswz(fr)) * 16;  // this lane's B chunk slot (j * 16 keeps (n >> 2) & 3)
-  if (STAGES == 2) issue(0, 0);
   for (int c = 0; c < nchunks; ++c) {
-    if (STAGES == 1) {
-      if (c > 0) __syncthreads();  // every wave is done reading chunk c - 1
-      issue(c, 0);
+    if (c > 0) __syncthreads();  // every wave is done reading chunk c - 1
+    const int cb = c * CK * 2;
+#pragma unroll
+    for (int s = 0; s < C::PP_WAVE; ++s) {
+      const int j = wid + NW * s;
+      if (j < npieces) glds16(xr, sP + j * 1024, xoff[s], cb);
+    }
+#pragma unroll
+    for (int s = 0; s < C::WP_WAVE; ++s) {
+      const int j = wid + NW * s;
+      if (j < C::W_PIECES) glds16(wr, sW + j * 1024, woff[s], cb);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // chunk c landed for every wave; every wave is done reading chunk c - 1
-    if (STAGES == 2 && c + 1 < nchunks) issue(c + 1, (c + 1) & 1);
-    const char* sP = smem + (STAGES == 2 ? (c & 1) * STAGE : 0);
-    const char* sW = sP + PATCH_BYTES;
-    // fragments of tap t + 1 are read while tap t's 8 MFMAs run (register double buffer); both
-    // row blocks are always computed (a padded row block reads clamped pixels and is not stored)
-    // so the tap loop has no branches for the scheduler to stop at
-    const char* pA0 = sP + (pb[0] * 4 + fq) * 16;
-    const char* pA1 = sP + (pb[1] * 4 + fq) * 16;
+    __syncthreads();  // chunk c landed for every wave
+    // fragments of tap t + 1 are read while tap t's MFMAs run (register double buffer); every
+    // row block is computed (a padded one reads clamped pixels and is not stored) so the tap
+    // loop has no branches for the scheduler to stop at
     const char* pB = sW + fr * 64 + bsw;
-    bf16x8 af[2][2], bf[2][4];
+    bf16x8 af[2][RBW], bf[2][CB];
     auto load = [&](int tap, int slot) {
       const int toff = ((tap / 3) * W2 + (tap % 3)) * 64;
-      af[slot][0] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(pA0 + toff));
-      af[slot][1] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(pA1 + toff));
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int i = 0; i < RBW; ++i)
+        af[slot][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sP + (pb[i] * 4 + fq) * 16 + toff));
+#pragma unroll
+      for (int j = 0; j < CB; ++j)
         bf[slot][j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(pB + (tap * BN + j * 16) * 64));
     };
     load(0, 0);
@@ -187,38 +183,39 @@ __global__ __launch_bounds__(NTHR) void conv3x3_halo_kernel(const HaloArgs a) {
       const int cur = tap & 1;
       if (tap + 1 < 9) load(tap + 1, cur ^ 1);
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < RBW; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < CB; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[cur][i], bf[cur][j], acc[i][j], 0, 0, 0);
     }
   }
 
-  // epilogue: bias + act -> bf16 tile in LDS (reusing the stage buffers) -> 16-B stores
-  float bj[4];
+  // epilogue: bias + act -> bf16 tile in LDS (reusing the stage buffer) -> 16-B stores
+  float bj[CB];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) bj[j] = a.bias ? a.bias[n0 + j * 16 + fr] : 0.f;
-  __syncthreads();  // every wave is done with the last chunk's buffers
+  for (int j = 0; j < CB; ++j) bj[j] = a.bias ? a.bias[n0 + j * 16 + fr] : 0.f;
+  __syncthreads();  // every wave is done with the last chunk
   bf16* to = reinterpret_cast<bf16*>(smem);
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < RBW; ++i) {
     if (!rb_on[i]) continue;
-    const int rb = wid + NWAVE * i;
+    const int rb = wid + NW * i;
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < CB; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = rb * 16 + fq * 4 + r;
         float v = acc[i][j][r] + bj[j];
         if (!a.res) v = apply_act(v, a.act);
-        to[row * EPI_LD + j * 16 + fr] = (bf16)v;
+        to[row * C::EPI_LD + j * 16 + fr] = (bf16)v;
       }
   }
   __syncthreads();
-  for (int q = tid; q < R * (BN / 8); q += NTHR) {
-    const int row = q >> 3, c8 = q & 7;
+  constexpr int CPR = BN / 8;  // 16-B chunks per output row
+  for (int q = tid; q < R * CPR; q += C::NTHR) {
+    const int row = q / CPR, c8 = q - (q / CPR) * CPR;
     const long o = (m_base + row) * a.N + n0 + c8 * 8;
-    uint4 v = *reinterpret_cast<const uint4*>(to + row * EPI_LD + c8 * 8);
+    uint4 v = *reinterpret_cast<const uint4*>(to + row * C::EPI_LD + c8 * 8);
     if (a.res) {  // act(conv + bias + residual)
       float f[8], g[8];
       unpack8(v, f);
@@ -257,10 +254,13 @@ extern "C" {
 
 // 3x3 / stride 1 / pad 1 conv: x [B][H][W][Cin] bf16, w [N][3][3][Cin] bf16 (the packed conv
 // layout), bias fp32 [N] (BN folded), optional residual [B][H][W][N]; out [B][H][W][N] bf16.
-// Cin % 32 == 0, N % 64 == 0.
+// Cin % 32 == 0; variant 0: 64 output channels x 8 waves per block (N % 64 == 0), variant 1:
+// 32 x 4 (N % 32 == 0).
 int mls_conv3x3_halo(const void* x, const void* w, const float* bias, const void* res, void* out, int B, int H, int W,
-                     int Cin, int N, int act, void* stream) {
-  if (B <= 0 || H <= 0 || W <= 0 || Cin % CK || Cin <= 0 || N % BN || N <= 0) return MLS_BAD_ARG;
+                     int Cin, int N, int act, int variant, void* stream) {
+  const int bn = variant == 1 ? 32 : 64;
+  if (B <= 0 || H <= 0 || W <= 0 || Cin % CK || Cin <= 0 || N % bn || N <= 0 || variant < 0 || variant > 1)
+    return MLS_BAD_ARG;
   int th = 0, nb = 0;
   if (!halo_geometry(B, H, W, &th, &nb)) return MLS_UNSUPPORTED;
   const long xb = (long)B * H * W * Cin * 2, wb = (long)N * 9 * Cin * 2;
@@ -275,15 +275,11 @@ int mls_conv3x3_halo(const void* x, const void* w, const float* bias, const void
   a.x_bytes = (uint32_t)xb;
   a.w_bytes = (uint32_t)wb;
   const int tiles = (B / nb) * (H / th);
-  const long blocks = (long)tiles * (N / BN);
-  static const int stages = [] {  // MLS_HALO_STAGES=2: the double-buffered variant
-    const char* e = getenv("MLS_HALO_STAGES");
-    return e && atoi(e) == 2 ? 2 : 1;
-  }();
-  if (stages == 2)
-    hipLaunchKernelGGL(conv3x3_halo_kernel<2>, dim3((unsigned)blocks), dim3(NTHR), 0, (hipStream_t)stream, a);
+  const dim3 grid((unsigned)((long)tiles * (N / bn)));
+  if (variant == 1)
+    hipLaunchKernelGGL((conv3x3_halo_kernel<32, 4>), grid, dim3(256), 0, (hipStream_t)stream, a);
   else
-    hipLaunchKernelGGL(conv3x3_halo_kernel<1>, dim3((unsigned)blocks), dim3(NTHR), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL((conv3x3_halo_kernel<64, 8>), grid, dim3(512), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
 

@@ -284,9 +284,10 @@ def test_conv3x3_halo_matches_reference(B, H, W, cin, cout, resid):
     bias = (torch.randn(cout, generator=g) * 0.1).to(DEV)
     res = torch.randn(B, H, W, cout, generator=g).to(DEV).to(torch.bfloat16) if resid else None
     assert ops.conv3x3_halo_geometry(B, H, W) is not None
-    out = ops.conv3x3_halo(x, ops.pack_conv_weight(w), bias, act=ops.ACT_RELU, residual=res)
     ref = _conv_ref(x, w, bias, 1, 1, 1, res)
-    assert rel_err(out, ref) < 2e-2
+    for variant in (1, 0):
+        out = ops.conv3x3_halo(x, ops.pack_conv_weight(w), bias, act=ops.ACT_RELU, residual=res, variant=variant)
+        assert rel_err(out, ref) < 2e-2, variant
     if cin % 64:
         return  # the implicit-GEMM kernel needs Cin % 64 == 0
     gemm = ops.conv2d_nhwc(x, ops.pack_conv_weight(w), bias, kernel=3, stride=1, pad=1, act=ops.ACT_RELU,

@@ -29,16 +29,17 @@ for s, hin, ho in conv_shapes():
     wss = [torch.empty(64 << 20, device=dev, dtype=torch.float32) for _ in range(CONC)]
     ent = table[s.name]
     res = {}
-    for cfg, sk in ((ent["best_cfg"], ent["best_splitk"]), (ops.CFG_HALO, 1)):
+    cur = (ent["best_cfg"], ent["best_splitk"])
+    for cfg, sk in dict.fromkeys([cur, (ops.CFG_HALO, 1), (ops.CFG_HALO_N32, 1)]):
         fns = [lambda o=o, w_=w_, cfg=cfg, sk=sk: ops.conv2d_nhwc(x, wp, bias, kernel=3, stride=1, pad=1, act=1, out=o,
                                                                   workspace=w_, cfg=cfg, splitk=sk)
                for o, w_ in zip(outs, wss)]
         res[(cfg, sk)] = autotune._time_multi(fns, 20) * 1e3
     (cfg, sk), us = min(res.items(), key=lambda kv: kv[1])
-    print(json.dumps({"layer": s.name, "concurrency": CONC, "table_cfg": [ent["best_cfg"], ent["best_splitk"]],
-                      "table_us": round(res[(ent["best_cfg"], ent["best_splitk"])], 2),
-                      "halo_us": round(res[(ops.CFG_HALO, 1)], 2), "chosen": [cfg, sk]}), flush=True)
-    if cfg == ops.CFG_HALO:
+    print(json.dumps({"layer": s.name, "concurrency": CONC, "table_cfg": list(cur), "table_us": round(res[cur], 2),
+                      "halo64_us": round(res[(ops.CFG_HALO, 1)], 2), "halo32_us": round(res[(ops.CFG_HALO_N32, 1)], 2),
+                      "chosen": [cfg, sk]}), flush=True)
+    if (cfg, sk) != cur:
         ent.update(best_cfg=cfg, best_splitk=sk, best_us=round(us, 2),
                    tflops=round(2.0 * B * ho * ho * s.cout * s.cin * 9 / (us * 1e-3) / 1e12, 1))
 os.makedirs("gpurun_out", exist_ok=True)
