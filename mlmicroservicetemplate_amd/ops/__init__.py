@@ -138,7 +138,8 @@ def conv2d_nhwc(
     if cfg in (CFG_HALO, CFG_HALO_N32):
         if kernel != 3 or stride != 1 or pad != 1 or scale is not None:
             raise ValueError("CFG_HALO: 3x3 / stride 1 / pad 1 convolutions without a scale only")
-        return conv3x3_halo(x, w, bias, act=act, residual=residual, out=out, variant=cfg - CFG_HALO)
+        return conv3x3_halo(x, w, bias, act=act, residual=residual, out=out, variant=cfg - CFG_HALO,
+                            splitk=splitk, workspace=workspace)
     for name, t in (("bias", bias), ("scale", scale)):
         if t is not None:
             _need(t, name, torch.float32, dev)
@@ -429,11 +430,13 @@ def stem_pool_u8(images: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, mean
 
 def conv3x3_halo(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, act=ACT_NONE,
                  residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-                 variant: int = 0) -> torch.Tensor:
+                 variant: int = 0, splitk: int = 1, workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
     """3x3 / stride 1 / pad 1 NHWC conv on the halo-tiled direct kernel (csrc/conv3x3_halo.hip):
     x ``[B,H,W,Cin]`` bf16, w packed ``[N,3,3,Cin]`` bf16, bias fp32 ``[N]`` -> ``[B,H,W,N]``
     ``act(conv + bias (+ residual))``.  Cin % 32 == 0; ``variant`` 0 = 64 output channels x 8
-    waves per block (N % 64 == 0), 1 = 32 x 4 (N % 32 == 0)."""
+    waves per block (N % 64 == 0), 1 = 32 x 4 (N % 32 == 0).  ``splitk`` > 1 splits the input
+    channels over that many blocks per tile, reduced in the same launch through fp32 slabs in
+    ``workspace`` (>= splitk * B*H*W * N floats; otherwise, or on an uneven split, one slice)."""
     dev = x.device
     _need(x, "x", torch.bfloat16, dev)
     _need(w, "w", torch.bfloat16, dev)
@@ -456,8 +459,10 @@ def conv3x3_halo(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] 
         _need(out, "out", torch.bfloat16, dev)
         if tuple(out.shape) != shape:
             raise ValueError(f"out must be {shape}")
-    check(lib().mls_conv3x3_halo(x.data_ptr(), w.data_ptr(), _ptr(bias), _ptr(residual), out.data_ptr(), B, H, W, C,
-                                 N, _act(act), variant, stream_ptr(dev)), "mls_conv3x3_halo")
+    wsp, wsb = _workspace_args(workspace)
+    check(lib().mls_conv3x3_halo(x.data_ptr(), w.data_ptr(), _ptr(bias), _ptr(residual), out.data_ptr(), wsp, wsb,
+                                 B, H, W, C, N, _act(act), variant, max(1, int(splitk)), stream_ptr(dev)),
+          "mls_conv3x3_halo")
     return out
 
 

@@ -117,7 +117,8 @@ def tune_resnet50(batch: int, device="cuda:0", iters: int = 20, compare_torch: b
         best = (1e9, 0, 0)
         tried = {}
         halo = s.k == 3 and s.stride == 1 and s.cin % 32 == 0 and s.cout % 64 == 0
-        for cfg, sk in [(0, 0)] + cands + ([(CFG_HALO, 1), (CFG_HALO_N32, 1)] if halo else []):
+        halo_cands = [(CFG_HALO, 1), (CFG_HALO, 2), (CFG_HALO, 4), (CFG_HALO_N32, 1)] if halo else []
+        for cfg, sk in [(0, 0)] + cands + halo_cands:
             if sk > 1 and k // sk < 128:
                 continue
 

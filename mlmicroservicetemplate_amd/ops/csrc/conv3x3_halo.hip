@@ -27,6 +27,8 @@
 #include "common.h"
 
 
+int* mls_stream_splitk_counters(void* stream, long ntiles);  // conv_gemm.hip
+
 namespace {
 
 constexpr int CK = 32;                           // input channels per chunk = one MFMA k-slab
@@ -46,8 +48,10 @@ struct HaloArgs {
   const float* bias; // [N] fp32 or null
   const bf16* res;   // [B][H][W][N] or null
   bf16* out;         // [B][H][W][N]
-  int B, H, W, Cin, N, th, nb, act;
-  uint32_t x_bytes, w_bytes;
+  float* ws;         // split-K slabs [ksplit][B*H*W][N] fp32 (ksplit > 1)
+  int* cnt;          // per-tile arrival counters of this stream (ksplit > 1)
+  int B, H, W, Cin, N, th, nb, act, ksplit;
+  uint32_t x_bytes, w_bytes, ws_bytes;
 };
 
 // Weight image swizzle: 16-B chunk ch of column n sits at ch ^ h((n >> 2) & 3), h = {0, 2, 3, 1}:
@@ -85,7 +89,9 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_halo_kernel(const HaloArgs a)
   const int R = a.nb * a.th * a.W;  // output pixels of the tile
   const int P = a.nb * TH2 * W2;    // patch pixels
   const int tiles = (a.B / a.nb) * (a.H / a.th);
-  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = t % a.ksplit;  // split-K slices of a tile are neighbours (one XCD's L2)
+  t /= a.ksplit;
   const int tn = t / tiles, tile = t - tn * tiles;  // column-block-major: neighbours share weights
   MLS_CHECK(tn * BN < a.N, 501);
   const int n0 = tn * BN;
@@ -146,10 +152,11 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_halo_kernel(const HaloArgs a)
 #pragma unroll
     for (int j = 0; j < CB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nchunks = a.Cin / CK;
+  const int nchunks = a.Cin / CK / a.ksplit;  // host: divisible
+  const int cfirst = split * nchunks;
   const int bsw = (fq ^ wswz(fr)) * 16;  // this lane's B chunk slot (j * 16 keeps (n >> 2) & 3)
-  for (int c = 0; c < nchunks; ++c) {
-    if (c > 0) __syncthreads();  // every wave is done reading chunk c - 1
+  for (int c = cfirst; c < cfirst + nchunks; ++c) {
+    if (c > cfirst) __syncthreads();  // every wave is done reading chunk c - 1
     const int cb = c * CK * 2;
 #pragma unroll
     for (int s = 0; s < C::PP_WAVE; ++s) {
@@ -188,6 +195,63 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_halo_kernel(const HaloArgs a)
         for (int j = 0; j < CB; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[cur][i], bf[cur][j], acc[i][j], 0, 0, 0);
     }
+  }
+
+  const long M = (long)a.B * a.H * a.W;
+  if (a.ksplit > 1) {
+    // In-launch split-K: write this slice's fp32 partial through to the slabs (sc1), take a
+    // ticket on the tile's counter; the last arriver sums the slices and runs the epilogue
+    // (the conv_gemm.hip reducer's protocol).
+    const rsrc_t wsr = make_rsrc(a.ws, a.ws_bytes);
+#pragma unroll
+    for (int i = 0; i < RBW; ++i) {
+      const int rb = wid + NW * i;
+#pragma unroll
+      for (int j = 0; j < CB; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = rb * 16 + fq * 4 + r;
+          const long idx = ((long)split * M + m_base + row) * a.N + n0 + j * 16 + fr;
+          // (the element goes through a named float: __builtin_bit_cast of the vector element
+          // expression itself stored element 0 for every r with this compiler)
+          const float v = acc[i][j][r];
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), wsr, row < R ? (int)(idx * 4) : OOB, 0, 16);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(smem);
+    if (tid == 0) {
+      int* c = a.cnt + tn * tiles + tile;
+      const int prev = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = prev == a.ksplit - 1;
+      if (last) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
+      flag[0] = last;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+    constexpr int CPR8 = BN / 8;
+    for (int q = tid; q < R * CPR8; q += C::NTHR) {
+      const int row = q / CPR8, c8 = q - (q / CPR8) * CPR8;
+      const long o = (m_base + row) * a.N + n0 + c8 * 8;
+      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int sl = 0; sl < a.ksplit; ++sl) {
+        const int off = (int)(((long)sl * M * a.N + o) * 4);
+        const float4 x0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(wsr, off, 0, 16));
+        const float4 x1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(wsr, off + 16, 0, 16));
+        v[0] += x0.x; v[1] += x0.y; v[2] += x0.z; v[3] += x0.w;
+        v[4] += x1.x; v[5] += x1.y; v[6] += x1.z; v[7] += x1.w;
+      }
+      float g[8];
+      if (a.res) unpack8(*reinterpret_cast<const uint4*>(a.res + o), g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float bb = a.bias ? a.bias[n0 + c8 * 8 + e] : 0.f;
+        v[e] = apply_act(v[e] + bb + (a.res ? g[e] : 0.f), a.act);
+      }
+      st16(a.out + o, pack8(v));
+    }
+    return;
   }
 
   // epilogue: bias + act -> bf16 tile in LDS (reusing the stage buffer) -> 16-B stores
@@ -256,8 +320,9 @@ extern "C" {
 // layout), bias fp32 [N] (BN folded), optional residual [B][H][W][N]; out [B][H][W][N] bf16.
 // Cin % 32 == 0; variant 0: 64 output channels x 8 waves per block (N % 64 == 0), variant 1:
 // 32 x 4 (N % 32 == 0).
-int mls_conv3x3_halo(const void* x, const void* w, const float* bias, const void* res, void* out, int B, int H, int W,
-                     int Cin, int N, int act, int variant, void* stream) {
+int mls_conv3x3_halo(const void* x, const void* w, const float* bias, const void* res, void* out, void* ws,
+                     size_t ws_bytes, int B, int H, int W, int Cin, int N, int act, int variant, int splitk,
+                     void* stream) {
   const int bn = variant == 1 ? 32 : 64;
   if (B <= 0 || H <= 0 || W <= 0 || Cin % CK || Cin <= 0 || N % bn || N <= 0 || variant < 0 || variant > 1)
     return MLS_BAD_ARG;
@@ -275,7 +340,23 @@ int mls_conv3x3_halo(const void* x, const void* w, const float* bias, const void
   a.x_bytes = (uint32_t)xb;
   a.w_bytes = (uint32_t)wb;
   const int tiles = (B / nb) * (H / th);
-  const dim3 grid((unsigned)((long)tiles * (N / bn)));
+  // split-K over input-channel chunks: needs the slabs, this stream's counters (allocated outside
+  // graph capture, like conv_gemm's) and an even chunk split; otherwise one slice
+  a.ksplit = 1;
+  a.ws = nullptr;
+  a.cnt = nullptr;
+  a.ws_bytes = 0;
+  const long slab = (long)splitk * B * H * W * N * 4;
+  if (splitk > 1 && (Cin / CK) % splitk == 0 && ws && (long)ws_bytes >= slab && slab < 0x7fffffffL) {
+    int* cnt = mls_stream_splitk_counters(stream, (long)tiles * (N / bn));
+    if (cnt) {
+      a.ksplit = splitk;
+      a.ws = (float*)ws;
+      a.cnt = cnt;
+      a.ws_bytes = (uint32_t)slab;
+    }
+  }
+  const dim3 grid((unsigned)((long)tiles * (N / bn) * a.ksplit));
   if (variant == 1)
     hipLaunchKernelGGL((conv3x3_halo_kernel<32, 4>), grid, dim3(256), 0, (hipStream_t)stream, a);
   else

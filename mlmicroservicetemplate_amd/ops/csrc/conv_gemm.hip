@@ -932,6 +932,10 @@ int launch_conv(ConvArgs a, int mode, int cfg, int splitk, size_t ws_bytes, hipS
 
 }  // namespace
 
+// Per-stream split-K arrival counters for other translation units (conv3x3_halo.hip): the same
+// arrays, so kernels of different kinds on one stream share them (each launch leaves them zero).
+int* mls_stream_splitk_counters(void* stream, long ntiles) { return splitk_counters((hipStream_t)stream, ntiles); }
+
 extern "C" {
 
 // NHWC conv2d with fused epilogue. Weights [Cout][KH][KW][Cin] bf16; for the stem mode

@@ -285,9 +285,14 @@ def test_conv3x3_halo_matches_reference(B, H, W, cin, cout, resid):
     res = torch.randn(B, H, W, cout, generator=g).to(DEV).to(torch.bfloat16) if resid else None
     assert ops.conv3x3_halo_geometry(B, H, W) is not None
     ref = _conv_ref(x, w, bias, 1, 1, 1, res)
-    for variant in (1, 0):
-        out = ops.conv3x3_halo(x, ops.pack_conv_weight(w), bias, act=ops.ACT_RELU, residual=res, variant=variant)
-        assert rel_err(out, ref) < 2e-2, variant
+    ws = torch.empty(4 * B * H * W * cout, device=DEV, dtype=torch.float32)
+    for variant, sk in ((1, 1), (0, 1), (0, 2), (0, 4)):
+        if (cin // 32) % sk:
+            continue
+        for _ in range(2):  # the second launch checks the split-K counters were left at zero
+            out = ops.conv3x3_halo(x, ops.pack_conv_weight(w), bias, act=ops.ACT_RELU, residual=res,
+                                   variant=variant, splitk=sk, workspace=ws)
+            assert rel_err(out, ref) < 2e-2, (variant, sk)
     if cin % 64:
         return  # the implicit-GEMM kernel needs Cin % 64 == 0
     gemm = ops.conv2d_nhwc(x, ops.pack_conv_weight(w), bias, kernel=3, stride=1, pad=1, act=ops.ACT_RELU,
