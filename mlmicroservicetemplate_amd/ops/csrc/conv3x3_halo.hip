@@ -14,8 +14,10 @@
 // Layout: patch [pixel][4 x 16-B chunks] (a fragment row = one pixel's 64 B); weights
 // [tap][64 cols][4 chunks], chunk-swizzled so the B reads are conflict-free (the A reads of a row
 // block that wraps a patch row cannot be swizzled for every alignment and stay <= 2-way).  Both are
-// filled by buffer_load ... lds (LDS DMA; out-of-image halo pixels get an out-of-range offset and
-// read as zero = the conv padding).  One stage per block so several blocks share a CU and
+// staged through registers: chunk c + 1's buffer loads are in flight during chunk c's MFMAs and
+// land in LDS after the next barrier (MLS_HALO_RS=0: LDS DMA per chunk instead; level end to end,
+// faster per layer at c4 -- profiles/r1_halo_regstage_probe.jsonl); out-of-image halo pixels get
+// an out-of-range offset and read as zero = the conv padding.  One stage per block so several blocks share a CU and
 // overlap each other's loads (a double-buffered 120 KB first version, one block per CU, measured
 // slower under concurrency: profiles/r1_halo_probe_stages.jsonl).  A tap's fragments are read
 // while the previous tap's MFMAs run.  Epilogue: bias + activation (+ optional residual) -> bf16
@@ -26,6 +28,7 @@
 // and lifts bench.py from 48.0k to 49.6k req/s.
 #include "common.h"
 
+#include <cstdlib>
 
 int* mls_stream_splitk_counters(void* stream, long ntiles);  // conv_gemm.hip
 
@@ -77,7 +80,7 @@ struct HaloCfg {
   static_assert(RBW * NW == 16 && CB * 16 == BN, "tile split");
 };
 
-template <int BN, int NW>
+template <int BN, int NW, bool RS>
 __global__ __launch_bounds__(NW * 64) void conv3x3_halo_kernel(const HaloArgs a) {
   using C = HaloCfg<BN, NW>;
   constexpr int RBW = C::RBW, CB = C::CB;
@@ -155,21 +158,49 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_halo_kernel(const HaloArgs a)
   const int nchunks = a.Cin / CK / a.ksplit;  // host: divisible
   const int cfirst = split * nchunks;
   const int bsw = (fq ^ wswz(fr)) * 16;  // this lane's B chunk slot (j * 16 keeps (n >> 2) & 3)
-  for (int c = cfirst; c < cfirst + nchunks; ++c) {
-    if (c > cfirst) __syncthreads();  // every wave is done reading chunk c - 1
+  // RS: register-staged -- chunk c + 1's patch and weights are loaded into VGPRs while chunk c's
+  // MFMAs run and written to LDS after the next barrier, so the L2 / HBM latency hides behind
+  // the math instead of stalling every chunk; otherwise LDS-DMA issued and awaited per chunk.
+  uint4 px[C::PP_WAVE], pw[C::WP_WAVE];
+  auto fetch = [&](int c) {
     const int cb = c * CK * 2;
 #pragma unroll
-    for (int s = 0; s < C::PP_WAVE; ++s) {
-      const int j = wid + NW * s;
-      if (j < npieces) glds16(xr, sP + j * 1024, xoff[s], cb);
-    }
+    for (int s = 0; s < C::PP_WAVE; ++s) px[s] = bload16(xr, xoff[s] + cb);  // OOB (halo, tail) -> 0
 #pragma unroll
-    for (int s = 0; s < C::WP_WAVE; ++s) {
-      const int j = wid + NW * s;
-      if (j < C::W_PIECES) glds16(wr, sW + j * 1024, woff[s], cb);
+    for (int s = 0; s < C::WP_WAVE; ++s) pw[s] = bload16(wr, woff[s] + cb);
+  };
+  if (RS) fetch(cfirst);
+  for (int c = cfirst; c < cfirst + nchunks; ++c) {
+    if (c > cfirst) __syncthreads();  // every wave is done reading chunk c - 1
+    if (RS) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int s = 0; s < C::PP_WAVE; ++s) {
+        const int j = wid + NW * s;
+        if (j < npieces) *reinterpret_cast<uint4*>(sP + j * 1024 + lane * 16) = px[s];
+      }
+#pragma unroll
+      for (int s = 0; s < C::WP_WAVE; ++s) {
+        const int j = wid + NW * s;
+        if (j < C::W_PIECES) *reinterpret_cast<uint4*>(sW + j * 1024 + lane * 16) = pw[s];
+      }
+      __syncthreads();  // chunk c is in LDS for every wave
+      if (c + 1 < cfirst + nchunks) fetch(c + 1);
+    } else {
+      const int cb = c * CK * 2;
+#pragma unroll
+      for (int s = 0; s < C::PP_WAVE; ++s) {
+        const int j = wid + NW * s;
+        if (j < npieces) glds16(xr, sP + j * 1024, xoff[s], cb);
+      }
+#pragma unroll
+      for (int s = 0; s < C::WP_WAVE; ++s) {
+        const int j = wid + NW * s;
+        if (j < C::W_PIECES) glds16(wr, sW + j * 1024, woff[s], cb);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // chunk c landed for every wave
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // chunk c landed for every wave
     // fragments of tap t + 1 are read while tap t's MFMAs run (register double buffer); every
     // row block is computed (a padded one reads clamped pixels and is not stored) so the tap
     // loop has no branches for the scheduler to stop at
@@ -357,10 +388,19 @@ int mls_conv3x3_halo(const void* x, const void* w, const float* bias, const void
     }
   }
   const dim3 grid((unsigned)((long)tiles * (N / bn) * a.ksplit));
-  if (variant == 1)
-    hipLaunchKernelGGL((conv3x3_halo_kernel<32, 4>), grid, dim3(256), 0, (hipStream_t)stream, a);
-  else
-    hipLaunchKernelGGL((conv3x3_halo_kernel<64, 8>), grid, dim3(512), 0, (hipStream_t)stream, a);
+  static const bool rs = [] {  // MLS_HALO_RS=0: LDS-DMA staging (A/B)
+    const char* e = getenv("MLS_HALO_RS");
+    return !(e && e[0] == '0');
+  }();
+  // (a 64-channel x 4-wave variant -- 4 x 4 MFMA tiles per wave, half the LDS reads per MFMA --
+  // measured 15-25 % slower than <64, 8>: profiles/r1_halo_w4_probe.jsonl)
+  if (variant == 1) {
+    if (rs) hipLaunchKernelGGL((conv3x3_halo_kernel<32, 4, true>), grid, dim3(256), 0, (hipStream_t)stream, a);
+    else hipLaunchKernelGGL((conv3x3_halo_kernel<32, 4, false>), grid, dim3(256), 0, (hipStream_t)stream, a);
+  } else {
+    if (rs) hipLaunchKernelGGL((conv3x3_halo_kernel<64, 8, true>), grid, dim3(512), 0, (hipStream_t)stream, a);
+    else hipLaunchKernelGGL((conv3x3_halo_kernel<64, 8, false>), grid, dim3(512), 0, (hipStream_t)stream, a);
+  }
   return (int)hipGetLastError();
 }
 

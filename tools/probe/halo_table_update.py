@@ -30,7 +30,7 @@ for s, hin, ho in conv_shapes():
     ent = table[s.name]
     res = {}
     cur = (ent["best_cfg"], ent["best_splitk"])
-    cands = [cur, (ops.CFG_HALO, 1), (ops.CFG_HALO_N32, 1)] + [(ops.CFG_HALO, k) for k in (2, 4) if s.cin // 32 % k == 0]
+    cands = [cur, (ops.CFG_HALO, 1), (ops.CFG_HALO_N32, 1)]
     for cfg, sk in dict.fromkeys(cands):
         fns = [lambda o=o, w_=w_, cfg=cfg, sk=sk: ops.conv2d_nhwc(x, wp, bias, kernel=3, stride=1, pad=1, act=1, out=o,
                                                                   workspace=w_, cfg=cfg, splitk=sk)
@@ -39,8 +39,6 @@ for s, hin, ho in conv_shapes():
     (cfg, sk), us = min(res.items(), key=lambda kv: kv[1])
     print(json.dumps({"layer": s.name, "concurrency": CONC, "table_cfg": list(cur), "table_us": round(res[cur], 2),
                       "halo64_us": round(res[(ops.CFG_HALO, 1)], 2), "halo32_us": round(res[(ops.CFG_HALO_N32, 1)], 2),
-                      "halo64_sk2_us": round(res.get((ops.CFG_HALO, 2), 0), 2),
-                      "halo64_sk4_us": round(res.get((ops.CFG_HALO, 4), 0), 2),
                       "chosen": [cfg, sk]}), flush=True)
     if (cfg, sk) != cur:
         ent.update(best_cfg=cfg, best_splitk=sk, best_us=round(us, 2),
