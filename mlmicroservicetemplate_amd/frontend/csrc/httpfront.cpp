@@ -294,6 +294,9 @@ class Server {
     int listen_fd = -1;
     int io_threads = 4;
     long long sample_bytes = 0;
+    // false: every upload goes through the Python preprocess (a text model's packed sample must
+    // never be taken verbatim from a client body that happens to have the same size)
+    bool raw_samples = true;
     int max_batch = 32;
     int max_wait_us = 2000;
     int max_queue = 4096;
@@ -1060,7 +1063,8 @@ class Server {
       immediate(c, 503, NOT_READY_BODY, ref.keep_alive, cors);
       return;
     }
-    if (cfg_.sample_bytes > 0 && (long long)payload.size() == cfg_.sample_bytes && raw_content_type(pctype)) {
+    if (cfg_.raw_samples && cfg_.sample_bytes > 0 && (long long)payload.size() == cfg_.sample_bytes &&
+        raw_content_type(pctype)) {
       Pending p;
       p.ref = std::move(ref);
       p.off = (size_t)(payload.data() - body.data());
@@ -1096,7 +1100,8 @@ PYBIND11_MODULE(_httpfront, m) {
   py::class_<Server>(m, "Server")
       .def(py::init([](std::string host, int port, int listen_fd, int io_threads, long long sample_bytes,
                        int max_batch, int max_wait_us, int max_queue, long long max_upload, std::string form_field,
-                       std::vector<std::string> cors_origins, double request_timeout_s, bool python_decode) {
+                       std::vector<std::string> cors_origins, double request_timeout_s, bool python_decode,
+                       bool raw_samples) {
              Server::Config c;
              c.host = std::move(host);
              c.port = port;
@@ -1111,13 +1116,14 @@ PYBIND11_MODULE(_httpfront, m) {
              c.cors_origins = std::move(cors_origins);
              c.request_timeout_s = request_timeout_s;
              c.python_decode = python_decode;
+             c.raw_samples = raw_samples;
              return std::make_unique<Server>(std::move(c));
            }),
            py::arg("host") = "0.0.0.0", py::arg("port") = 0, py::arg("listen_fd") = -1, py::arg("io_threads") = 4,
            py::arg("sample_bytes") = 0, py::arg("max_batch") = 32, py::arg("max_wait_us") = 2000,
            py::arg("max_queue") = 4096, py::arg("max_upload") = 32 << 20, py::arg("form_field") = "image_file",
            py::arg("cors_origins") = std::vector<std::string>{}, py::arg("request_timeout_s") = 30.0,
-           py::arg("python_decode") = true)
+           py::arg("python_decode") = true, py::arg("raw_samples") = true)
       .def("start", &Server::start, py::call_guard<py::gil_scoped_release>())
       .def("stop", &Server::stop, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("port", &Server::port)

@@ -147,7 +147,8 @@ class NativeService:
             max_wait_us=int(settings.MAX_WAIT_US),
             max_queue=int(settings.MAX_QUEUE), max_upload=int(settings.MAX_UPLOAD_BYTES),
             form_field=plugin.form_field, cors_origins=list(settings.CORS_ORIGINS),
-            request_timeout_s=float(settings.REQUEST_TIMEOUT_S), python_decode=True)
+            request_timeout_s=float(settings.REQUEST_TIMEOUT_S), python_decode=True,
+            raw_samples=bool(spec.get("raw_samples", True)))
         self.replicas: List[Any] = []
         self.reloader = None  # parallel.reload.ReloadCoordinator, after init
         self._stop = threading.Event()
@@ -270,13 +271,16 @@ class NativeService:
 
     def _decode_loop(self) -> None:
         srv, plugin = self.srv, self.plugin
+        # plugins whose Python-path sample differs from the engine row (bert: token list vs the
+        # packed ids | type ids | length row) provide native_preprocess
+        prep = getattr(plugin, "native_preprocess", None) or plugin.preprocess
         while not self._stop.is_set():
             item = srv.next_decode(200)
             if item is None:
                 continue
             token, data, ctype = item
             try:
-                arr = plugin.preprocess(Part(name=plugin.form_field, data=data, content_type=ctype))
+                arr = prep(Part(name=plugin.form_field, data=data, content_type=ctype))
                 srv.submit_sample(token, np.ascontiguousarray(arr))
             except Exception as e:  # undecodable upload: 500, as PIL's error was in the reference
                 srv.respond(token, 500, _json({"status": "failure", "detail": f"{type(e).__name__}: {e}"}))
@@ -331,6 +335,26 @@ class NativeService:
         main.pyc@L119-152); everything else without the upload field is a 422 as in FastAPI."""
         srv, plugin = self.srv, self.plugin
         ctype = headers.get("content-type", "").lower()
+        prep = getattr(plugin, "native_preprocess", None) or plugin.preprocess
+        if getattr(plugin, "task", "") == "text":  # JSON / urlencoded text field (the bert plugin)
+            text = None
+            try:
+                if ctype.startswith("application/json"):
+                    payload = json.loads(body or b"null")
+                    if isinstance(payload, dict) and isinstance(payload.get(plugin.form_field), str):
+                        text = payload[plugin.form_field]
+                elif ctype.startswith("application/x-www-form-urlencoded"):
+                    text = (parse_qs(body.decode("utf-8", "replace")).get(plugin.form_field) or [None])[0]
+            except ValueError:
+                text = None
+            if text is not None:
+                if not self.state.ready_to_predict:
+                    srv.respond(token, 503, _json({"status": "failure",
+                                                   "detail": "Model is not ready to receive predictions."}))
+                    return
+                arr = prep(Part(name=plugin.form_field, data=text.encode("utf-8")))
+                srv.submit_sample(token, np.ascontiguousarray(arr))
+                return
         filename = (parse_qs(query).get("filename") or [None])[0]
         try:
             if filename is None and ctype.startswith("application/json"):
@@ -360,7 +384,7 @@ class NativeService:
             return
         with open(p, "rb") as f:
             data = f.read()
-        arr = plugin.preprocess(Part(name=plugin.form_field, data=data, filename=os.path.basename(p)))
+        arr = prep(Part(name=plugin.form_field, data=data, filename=os.path.basename(p)))
         srv.submit_sample(token, np.ascontiguousarray(arr))
 
     def health(self) -> dict:

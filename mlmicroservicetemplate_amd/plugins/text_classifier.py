@@ -85,6 +85,31 @@ class BertPlugin(ModelPlugin):
         text = part.data.decode("utf-8", errors="replace")
         return self.tokenizer.encode(text, self.max_seq)
 
+    # --- native front end: one fixed-size packed row per request at the largest seq bucket ---
+    def _native_seq(self) -> int:
+        return max(q for q in SEQ_BUCKETS if q <= self.max_seq) if self.max_seq >= SEQ_BUCKETS[0] else self.max_seq
+
+    def native_spec(self) -> dict:
+        # raw_samples False: a packed row is only ever built here, never taken from a client body
+        return {"sample_bytes": (2 * self._native_seq() + 1) * 4, "result": "topk", "raw_samples": False}
+
+    def native_preprocess(self, part: Part):
+        """Tokenise straight into the engine row layout (ids | type ids | length, int32)."""
+        import numpy as np
+
+        S = self._native_seq()
+        ids = self.preprocess(part)[:S]
+        row = np.zeros(2 * S + 1, dtype=np.int32)
+        row[: len(ids)] = ids
+        row[2 * S] = len(ids)
+        return row
+
+    def native_replicas(self):
+        from ..frontend.native import EngineReplica
+
+        S = self._native_seq()
+        return [EngineReplica(per[S]) for per in self.engines.values()]
+
     def replica_probes(self):
         return [lambda per=per: all(e.healthy for e in per.values()) for per in self.engines.values()]
 
@@ -106,9 +131,10 @@ class BertPlugin(ModelPlugin):
         return out
 
     def postprocess(self, out: Any) -> dict:
-        vals, idx = out
-        names = [self.labels[int(i)] for i in idx]
-        return {"classes": list(self.labels), "result": {n: float(v) for n, v in zip(names, vals)}}
+        # same body as the native front end's C++ top-k reply (classes in probability order)
+        from .builtin import topk_result
+
+        return topk_result(self.labels, *out)
 
     def describe(self) -> dict:
         d = super().describe()

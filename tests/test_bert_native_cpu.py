@@ -1,0 +1,33 @@
+"""bert plugin's native-front-end contract on CPU: packed row layout (ids | type ids | length at
+the largest seq bucket) equals the Python path's pack_requests, and raw client bodies are never
+accepted as rows (``raw_samples`` False)."""
+import numpy as np
+
+from mlmicroservicetemplate_amd.api.multipart import Part
+from mlmicroservicetemplate_amd.models import bert
+from mlmicroservicetemplate_amd.plugins.text_classifier import BertPlugin
+
+
+def _plugin(max_seq):
+    p = BertPlugin()
+    p.max_seq = max_seq
+    p.tokenizer = bert.HashTokenizer(30522)
+    return p
+
+
+def test_native_row_matches_pack_requests():
+    p = _plugin(128)
+    spec = p.native_spec()
+    assert spec == {"sample_bytes": (2 * 128 + 1) * 4, "result": "topk", "raw_samples": False}
+    for text in ["hello world", "word " * 300, ""]:
+        part = Part(name="text", data=text.encode())
+        row = p.native_preprocess(part)
+        assert row.dtype == np.int32 and row.nbytes == spec["sample_bytes"]
+        want = bert.pack_requests([p.preprocess(part)], 128).numpy()[0]
+        np.testing.assert_array_equal(row, want)
+
+
+def test_native_seq_is_largest_bucket_below_max_seq():
+    p = _plugin(100)  # buckets 32, 64 fit: rows are packed at 64, longer texts truncated like the Python path
+    row = p.native_preprocess(Part(name="text", data=("w " * 200).encode()))
+    assert row.shape == (2 * 64 + 1,) and row[-1] == 64

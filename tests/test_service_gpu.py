@@ -164,6 +164,58 @@ def test_resnet50_native_frontend_matches_python_frontend():
         svc.stop()
 
 
+def test_bert_native_frontend_matches_python_frontend():
+    """FRONTEND=native with the bert plugin (config 3): the Python decode thread tokenises straight
+    into the engine's packed row, the C++ batcher packs rows into the slot's pinned buffer; the
+    top class matches the FastAPI path (which may pick a shorter seq bucket: probabilities within
+    bf16 noise) for multipart, JSON and urlencoded texts, and a same-size text body is never taken
+    as a raw row."""
+    import json
+    import subprocess
+
+    import requests
+
+    from mlmicroservicetemplate_amd.config import Settings
+    from mlmicroservicetemplate_amd.frontend import build as fbuild
+    from mlmicroservicetemplate_amd.frontend.native import NativeService
+    from mlmicroservicetemplate_amd.plugins.base import PluginContext
+    from mlmicroservicetemplate_amd.plugins.text_classifier import BertPlugin
+
+    texts = ["the quick brown fox", "MI355X serving " * 20, "a", "x" * ((2 * 128 + 1) * 4)]
+    with _client(MODEL="bert", MAX_BATCH=8, GRAPH_BUCKETS=[1, 2, 4, 8]) as c:
+        _wait(c)
+        py = [c.post("/predict", data={"text": t}).json()["result"] for t in texts]
+    s = Settings.load(env_file=None, environ={}, overrides={"REGISTER": False, "GPUS": 1, "MODEL": "bert",
+                                                            "MAX_BATCH": 8, "GRAPH_BUCKETS": [1, 2, 4, 8],
+                                                            "MAX_WAIT_US": 2000, "IO_THREADS": 2})
+    svc = NativeService(s, BertPlugin(), PluginContext(settings=s, devices=["cuda:0"]), host="127.0.0.1", port=0)
+    svc.start()
+    try:
+        url = f"http://127.0.0.1:{svc.port}"
+        t0 = time.time()
+        while requests.get(url + "/status").status_code != 200:
+            assert time.time() - t0 < 300 and "error" not in requests.get(url + "/status").json()
+            time.sleep(0.1)
+        outs = [requests.post(url + "/predict", files={"text": (None, t)}, timeout=60) for t in texts]
+        outs += [requests.post(url + "/predict", json={"text": texts[0]}, timeout=60),
+                 requests.post(url + "/predict", data={"text": texts[1]}, timeout=60)]
+        assert all(o.status_code == 200 for o in outs), [o.text for o in outs]
+        nat = [o.json()["result"] for o in outs]
+        for a, b in zip(py + [py[0], py[1]], nat):
+            assert a["classes"][0] == b["classes"][0]
+            for k in a["result"]:
+                assert abs(a["result"][k] - b["result"][k]) < 2e-2
+        lg = subprocess.run([fbuild.loadgen_path(), "--port", str(svc.port), "--conns", "32", "--threads", "2",
+                             "--duration", "2", "--warmup", "0.5", "--field", "text", "--bytes", "400"],
+                            capture_output=True, text=True, timeout=60)
+        res = json.loads(lg.stdout)
+        assert res["errors"] == 0 and res["ok"] > 100, res
+        st = svc.srv.stats()
+        assert st["samples"] > st["batches"]  # requests were micro-batched
+    finally:
+        svc.stop()
+
+
 def test_resnet50_hot_reload_in_place_under_graphs():
     """POST /admin/reload's engine path: new weights copied INTO the tensors the captured hipGraphs
     read (pointers unchanged, no re-capture), outputs equal a model built from the new weights."""

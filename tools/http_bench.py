@@ -38,6 +38,8 @@ def main() -> int:
     ap.add_argument("--ready-timeout", type=float, default=300)
     ap.add_argument("--jpeg", action="store_true", help="upload a 320x240 JPEG (server-side decode) instead of raw RGB8")
     ap.add_argument("--decode-workers", type=int, default=4)
+    ap.add_argument("--text", action="store_true",
+                    help="upload an English text (~110 tokens) as multipart field `text` (the bert plugin)")
     args = ap.parse_args()
     fbuild.build()
     cmd = [sys.executable, "-m", "mlmicroservicetemplate_amd", "serve", "--model", args.model, "--frontend",
@@ -58,6 +60,14 @@ def main() -> int:
         with open(path, "wb") as f:
             f.write(buf.getvalue())
         payload_args = ["--file", path, "--ctype", "image/jpeg"]
+    if args.text:
+        words = ("the quick brown fox jumps over the lazy dog while a serving framework batches "
+                 "requests for the matrix cores of the accelerator").split()
+        path = os.path.join(ROOT, "gpurun_out", "http_bench_upload.txt")
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, "w") as f:
+            f.write(" ".join(words[i % len(words)] for i in range(100)))
+        payload_args = ["--file", path, "--ctype", "text/plain", "--field", "text"]
     srv = subprocess.Popen(cmd, cwd=ROOT, env=dict(os.environ, PYTHONPATH=ROOT, DECODE_WORKERS=str(args.decode_workers)),
                            start_new_session=True)
     url = f"http://127.0.0.1:{args.port}"
@@ -85,7 +95,7 @@ def main() -> int:
                                  capture_output=True, text=True, timeout=args.duration + args.warmup + 60)
             res = json.loads(out.stdout)
             res.update({"model": args.model, "frontend": args.frontend, "workers_per_gpu": args.workers_per_gpu,
-                        "io_threads": args.io_threads, "gpus": 1, "payload": "jpeg320x240" if args.jpeg else "raw-rgb8",
+                        "io_threads": args.io_threads, "gpus": 1, "payload": "text100w" if args.text else ("jpeg320x240" if args.jpeg else "raw-rgb8"),
                         "decode_workers": args.decode_workers})
             print(json.dumps(res), flush=True)
     finally:
