@@ -194,6 +194,64 @@ bool raw_content_type(std::string_view ct) {
   return ct.empty() || ieq(ct, "application/octet-stream") || ieq(ct, "application/x-rgb8");
 }
 
+// Hash tokenizer of models/bert.py:HashTokenizer for pure-ASCII texts, run on the I/O thread so a
+// text request never touches Python: lowercase, split into [a-z0-9]+ runs and single other
+// non-space characters (whitespace = Python's str.isspace() over ASCII: \t \n \v \f \r
+// \x1c-\x1f and space), id = 1000 + crc32(token) % (vocab - 1000), framed by CLS / SEP and cut
+// at max_len exactly as encode() does.  Non-ASCII texts go to the Python tokenizer (Unicode
+// lowercasing / whitespace), so both paths give the same ids.
+struct TextHash {
+  int vocab = 0, max_len = 0, seq = 0, cls = 101, sep = 102;
+};
+
+uint32_t crc32_bytes(const char* p, size_t n) {
+  static const auto table = [] {
+    std::vector<uint32_t> t(256);
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+      t[i] = c;
+    }
+    return t;
+  }();
+  uint32_t c = 0xFFFFFFFFu;
+  for (size_t i = 0; i < n; ++i) c = table[(c ^ (uint8_t)p[i]) & 0xFF] ^ (c >> 8);
+  return c ^ 0xFFFFFFFFu;
+}
+
+inline bool ascii_space(unsigned char c) { return c == ' ' || (c >= 9 && c <= 13) || (c >= 0x1c && c <= 0x1f); }
+inline bool ascii_alnum(unsigned char c) { return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z'); }
+
+// -> false when the text is not pure ASCII (caller falls back to Python); else ids (truncated to seq)
+bool hash_tokenize(std::string_view text, const TextHash& th, std::vector<int32_t>& ids) {
+  for (unsigned char c : text)
+    if (c >= 0x80) return false;
+  ids.clear();
+  ids.push_back(th.cls);
+  const uint32_t span = (uint32_t)(th.vocab - 1000);
+  std::string w;
+  size_t i = 0;
+  while (i < text.size()) {
+    const unsigned char c = text[i];
+    if (ascii_space(c)) { ++i; continue; }
+    w.clear();
+    if (ascii_alnum(c)) {
+      while (i < text.size() && ascii_alnum((unsigned char)text[i])) {
+        unsigned char d = text[i++];
+        w.push_back((char)((d >= 'A' && d <= 'Z') ? d + 32 : d));
+      }
+    } else {
+      w.push_back((char)c);
+      ++i;
+    }
+    ids.push_back((int32_t)(1000 + crc32_bytes(w.data(), w.size()) % span));
+    if ((int)ids.size() >= th.max_len - 1) break;
+  }
+  ids.push_back(th.sep);
+  if ((int)ids.size() > th.seq) ids.resize(th.seq);
+  return true;
+}
+
 struct ReqRef {
   int thread = -1;
   uint64_t conn = 0;
@@ -297,6 +355,7 @@ class Server {
     // false: every upload goes through the Python preprocess (a text model's packed sample must
     // never be taken verbatim from a client body that happens to have the same size)
     bool raw_samples = true;
+    TextHash text_hash;  // vocab > 0: tokenise ASCII texts in C++ into packed (2*seq+1) int32 rows
     int max_batch = 32;
     int max_wait_us = 2000;
     int max_queue = 4096;
@@ -1073,6 +1132,21 @@ class Server {
       enqueue_sample(std::move(p));
       return;
     }
+    if (cfg_.text_hash.vocab > 0) {
+      std::vector<int32_t> ids;
+      if (hash_tokenize(payload, cfg_.text_hash, ids)) {
+        const int S = cfg_.text_hash.seq;
+        std::vector<int32_t> row(2 * S + 1, 0);
+        std::copy(ids.begin(), ids.end(), row.begin());
+        row[2 * S] = (int32_t)ids.size();
+        Pending p;
+        p.ref = std::move(ref);
+        p.body.assign(reinterpret_cast<const char*>(row.data()), row.size() * sizeof(int32_t));
+        c.waiting = true;
+        enqueue_sample(std::move(p));
+        return;
+      }
+    }
     if (!cfg_.python_decode) {
       immediate(c, 415, failure_body("Only raw samples of the model's input size are accepted."), ref.keep_alive, cors);
       return;
@@ -1097,11 +1171,19 @@ py::bytes as_bytes(const std::string& s) { return py::bytes(s.data(), s.size());
 
 PYBIND11_MODULE(_httpfront, m) {
   m.doc() = "Native HTTP/1.1 front end: epoll I/O threads, multipart parsing, C++ dynamic batching";
+  m.def("hash_tokenize",
+        [](std::string text, int vocab, int max_len, int seq) -> py::object {
+          std::vector<int32_t> ids;
+          if (!hash_tokenize(text, TextHash{vocab, max_len, seq, 101, 102}, ids)) return py::none();
+          return py::cast(ids);
+        },
+        "C++ hash tokenizer of the bert plugin (None for non-ASCII text)", py::arg("text"), py::arg("vocab"),
+        py::arg("max_len"), py::arg("seq"));
   py::class_<Server>(m, "Server")
       .def(py::init([](std::string host, int port, int listen_fd, int io_threads, long long sample_bytes,
                        int max_batch, int max_wait_us, int max_queue, long long max_upload, std::string form_field,
                        std::vector<std::string> cors_origins, double request_timeout_s, bool python_decode,
-                       bool raw_samples) {
+                       bool raw_samples, std::vector<int> text_hash) {
              Server::Config c;
              c.host = std::move(host);
              c.port = port;
@@ -1117,13 +1199,20 @@ PYBIND11_MODULE(_httpfront, m) {
              c.request_timeout_s = request_timeout_s;
              c.python_decode = python_decode;
              c.raw_samples = raw_samples;
+             if (text_hash.size() == 5) {  // vocab, max_len, seq, cls, sep
+               c.text_hash = TextHash{text_hash[0], text_hash[1], text_hash[2], text_hash[3], text_hash[4]};
+               if (c.text_hash.vocab <= 1000 || c.text_hash.seq <= 0 || c.text_hash.max_len < 2 ||
+                   c.sample_bytes != (long long)(2 * c.text_hash.seq + 1) * 4)
+                 throw std::invalid_argument("text_hash does not match sample_bytes");
+             }
              return std::make_unique<Server>(std::move(c));
            }),
            py::arg("host") = "0.0.0.0", py::arg("port") = 0, py::arg("listen_fd") = -1, py::arg("io_threads") = 4,
            py::arg("sample_bytes") = 0, py::arg("max_batch") = 32, py::arg("max_wait_us") = 2000,
            py::arg("max_queue") = 4096, py::arg("max_upload") = 32 << 20, py::arg("form_field") = "image_file",
            py::arg("cors_origins") = std::vector<std::string>{}, py::arg("request_timeout_s") = 30.0,
-           py::arg("python_decode") = true, py::arg("raw_samples") = true)
+           py::arg("python_decode") = true, py::arg("raw_samples") = true,
+           py::arg("text_hash") = std::vector<int>{})
       .def("start", &Server::start, py::call_guard<py::gil_scoped_release>())
       .def("stop", &Server::stop, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("port", &Server::port)

@@ -8,6 +8,7 @@ run through one engine per sequence bucket (each with its own batch-bucket hipGr
 from __future__ import annotations
 
 import logging
+import os
 from typing import Any, List
 
 
@@ -91,7 +92,16 @@ class BertPlugin(ModelPlugin):
 
     def native_spec(self) -> dict:
         # raw_samples False: a packed row is only ever built here, never taken from a client body
-        return {"sample_bytes": (2 * self._native_seq() + 1) * 4, "result": "topk", "raw_samples": False}
+        spec = {"sample_bytes": (2 * self._native_seq() + 1) * 4, "result": "topk", "raw_samples": False}
+        if (os.environ.get("MLS_NATIVE_TOKENIZER", "0") == "1" and self.tokenizer is not None
+                and self.tokenizer._wp is None):
+            # opt-in: ASCII texts hash-tokenised on the C++ I/O threads (no Python per request).
+            # Measured slower end to end than the Python decode threads (15.6k vs 21.0k req/s at
+            # 64 connections, profiles/r1_http_bert_native_frontend.jsonl), hence off by default.
+            from ..models import bert
+
+            spec["text_hash"] = [self.tokenizer.vocab_size, self.max_seq, self._native_seq(), bert.CLS_ID, bert.SEP_ID]
+        return spec
 
     def native_preprocess(self, part: Part):
         """Tokenise straight into the engine row layout (ids | type ids | length, int32)."""

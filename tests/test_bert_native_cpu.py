@@ -2,6 +2,8 @@
 the largest seq bucket) equals the Python path's pack_requests, and raw client bodies are never
 accepted as rows (``raw_samples`` False)."""
 import numpy as np
+from hypothesis import given, settings
+from hypothesis import strategies as st
 
 from mlmicroservicetemplate_amd.api.multipart import Part
 from mlmicroservicetemplate_amd.models import bert
@@ -27,7 +29,33 @@ def test_native_row_matches_pack_requests():
         np.testing.assert_array_equal(row, want)
 
 
+def test_native_tokenizer_opt_in(monkeypatch):
+    monkeypatch.setenv("MLS_NATIVE_TOKENIZER", "1")
+    assert _plugin(128).native_spec()["text_hash"] == [30522, 128, 128, bert.CLS_ID, bert.SEP_ID]
+
+
 def test_native_seq_is_largest_bucket_below_max_seq():
     p = _plugin(100)  # buckets 32, 64 fit: rows are packed at 64, longer texts truncated like the Python path
     row = p.native_preprocess(Part(name="text", data=("w " * 200).encode()))
     assert row.shape == (2 * 64 + 1,) and row[-1] == 64
+
+
+ASCII = "".join(chr(i) for i in range(128))
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.text(alphabet=ASCII, max_size=400), st.sampled_from([(128, 128), (100, 64), (16, 16)]))
+def test_cpp_hash_tokenizer_matches_python(text, lens):
+    """The C++ tokenizer on the native front end's I/O threads == HashTokenizer (+ the row cut)."""
+    from mlmicroservicetemplate_amd.frontend.native import load_extension
+
+    max_len, seq = lens
+    ext = load_extension()
+    want = bert.HashTokenizer(30522).encode(text, max_len)[:seq]
+    assert ext.hash_tokenize(text, 30522, max_len, seq) == want
+
+
+def test_cpp_hash_tokenizer_defers_non_ascii():
+    from mlmicroservicetemplate_amd.frontend.native import load_extension
+
+    assert load_extension().hash_tokenize("caf\u00e9 na\u00efve", 30522, 128, 128) is None
