@@ -94,6 +94,12 @@ def main() -> int:
                                   "--warmup", str(args.warmup), *payload_args],
                                  capture_output=True, text=True, timeout=args.duration + args.warmup + 60)
             res = json.loads(out.stdout)
+            try:  # server-side batching (native front end): mean samples per engine batch so far
+                nat = requests.get(url + "/health", timeout=5).json().get("native") or {}
+                if nat.get("batches"):
+                    res["server_mean_batch"] = round(nat["samples"] / nat["batches"], 2)
+            except (requests.RequestException, ValueError):
+                pass
             res.update({"model": args.model, "frontend": args.frontend, "workers_per_gpu": args.workers_per_gpu,
                         "io_threads": args.io_threads, "gpus": 1, "payload": "text100w" if args.text else ("jpeg320x240" if args.jpeg else "raw-rgb8"),
                         "decode_workers": args.decode_workers})
