@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import asyncio
 import contextlib
+import json
 import logging
 import os
 import time
@@ -47,6 +48,39 @@ logger = logging.getLogger("api")
 ROOT_MESSAGE = "MLMicroserviceTemplate is Running!"
 NOT_READY = "Model is not ready to receive predictions."
 READY = "Model ready to receive prediction requests."
+
+
+class UploadTooLarge(Exception):
+    """Request body over ``MAX_UPLOAD_BYTES``: 413 (same body as the native front end)."""
+
+
+async def read_body(request: Request, limit: int) -> bytes:
+    """The request body, refusing (``UploadTooLarge``) anything over ``limit`` bytes: by the
+    declared Content-Length before reading, and by the streamed length while reading (chunked
+    bodies carry no length), so an oversized body is never buffered whole."""
+    declared = request.headers.get("content-length")
+    if declared is not None:
+        try:
+            if int(declared) > limit:
+                raise UploadTooLarge()
+        except ValueError:
+            pass
+    chunks, n = [], 0
+    async for chunk in request.stream():
+        n += len(chunk)
+        if n > limit:
+            raise UploadTooLarge()
+        chunks.append(chunk)
+    return b"".join(chunks)
+
+
+async def read_json(request: Request, limit: int):
+    """``read_body`` + JSON decode; ``None`` for an empty or invalid body."""
+    body = await read_body(request, limit)
+    try:
+        return json.loads(body) if body else None
+    except ValueError:
+        return None
 
 
 class ServingRuntime:
@@ -230,6 +264,10 @@ def create_app(settings: Optional[Settings] = None, plugin: Optional[ModelPlugin
         # REQUEST_TIMEOUT_S elapsed while the request waited in (or ran through) its replica
         return JSONResponse(status_code=504, content={"status": "failure", "detail": "Prediction timed out."})
 
+    @app.exception_handler(UploadTooLarge)
+    async def too_large_handler(request: Request, exc: UploadTooLarge):
+        return JSONResponse(status_code=413, content={"status": "failure", "detail": "Upload too large."})
+
     @app.exception_handler(MultipartError)
     async def multipart_handler(request: Request, exc: MultipartError):
         return JSONResponse(status_code=400, content={"status": "failure", "detail": f"Malformed upload: {exc}"})
@@ -298,10 +336,9 @@ def create_app(settings: Optional[Settings] = None, plugin: Optional[ModelPlugin
         ctype = request.headers.get("content-type", "")
         part: Optional[Part] = None
         filename = request.query_params.get("filename")
+        limit = int(settings.MAX_UPLOAD_BYTES)
         if ctype.lower().startswith("multipart/form-data"):
-            body = await request.body()
-            if len(body) > int(settings.MAX_UPLOAD_BYTES):
-                return JSONResponse(status_code=413, content={"status": "failure", "detail": "Upload too large."})
+            body = await read_body(request, limit)
             fields = parse_multipart(body, ctype)
             parts = fields.get(plugin.form_field) or []
             if parts:
@@ -309,10 +346,7 @@ def create_app(settings: Optional[Settings] = None, plugin: Optional[ModelPlugin
             elif "filename" in fields and filename is None:
                 filename = fields["filename"][0].text()
         elif ctype.lower().startswith("application/json"):
-            try:
-                payload = await request.json()
-            except Exception:
-                payload = None
+            payload = await read_json(request, limit)
             if isinstance(payload, dict) and payload.get(plugin.form_field) is not None:
                 val = payload[plugin.form_field]
                 data = val.encode("utf-8") if isinstance(val, str) else str(val).encode("utf-8")
@@ -320,7 +354,7 @@ def create_app(settings: Optional[Settings] = None, plugin: Optional[ModelPlugin
             elif isinstance(payload, dict) and filename is None:
                 filename = payload.get("filename")
         elif ctype.lower().startswith("application/x-www-form-urlencoded"):
-            form = await request.body()
+            form = await read_body(request, limit)
             from urllib.parse import parse_qs
 
             q = parse_qs(form.decode("utf-8", errors="replace"), keep_blank_values=True)
@@ -356,10 +390,7 @@ def create_app(settings: Optional[Settings] = None, plugin: Optional[ModelPlugin
         (parallel/reload.py).  JSON ``{"weights": <safetensors path>}`` or ``{"seed": n}``."""
         from ..parallel.reload import handle_reload_request
 
-        try:
-            payload = await request.json()
-        except Exception:
-            payload = None
+        payload = await read_json(request, int(settings.MAX_UPLOAD_BYTES))
         if not state.ready_to_predict:
             raise PredictionException()
         code, body = await run_in_threadpool(handle_reload_request, runtime.reloader, settings,
@@ -368,9 +399,8 @@ def create_app(settings: Optional[Settings] = None, plugin: Optional[ModelPlugin
 
     @app.post("/generate")
     async def generate(request: Request):
-        try:
-            req = await request.json()
-        except Exception:
+        req = await read_json(request, int(settings.MAX_UPLOAD_BYTES))
+        if req is None:
             raise RequestValidationError([{"type": "json_invalid", "loc": ("body",), "msg": "JSON body required",
                                            "input": None}])
         if not isinstance(req, dict) or ("prompt" not in req and "input_ids" not in req):

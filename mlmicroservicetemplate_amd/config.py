@@ -152,6 +152,7 @@ class Settings:
     DTYPE: str = "bf16"
     SEED: int = 0
     WEIGHTS: str = ""  # optional .safetensors path
+    WEIGHTS_DIR: str = ""  # POST /admin/reload may only load safetensors under this directory ("" = seed reloads only)
     IMAGE_DIR: str = "src/images"  # legacy /predict?filename= flow (old-rev main.pyc@L119-152)
     TOPK: int = 5
     # --- GPU execution ---

@@ -129,6 +129,8 @@ class NativeService:
 
     def __init__(self, settings, plugin, ctx, host: str = "0.0.0.0", port: Optional[int] = None,
                  listen_fd: Optional[int] = None):
+        if hasattr(plugin, "configure"):  # row geometry from the settings, before init() runs
+            plugin.configure(settings)
         spec = plugin.native_spec() if hasattr(plugin, "native_spec") else None
         if not spec:
             raise ValueError(f"model {plugin.name!r} has no native front-end support (use FRONTEND=python)")
@@ -424,5 +426,7 @@ def _json(obj) -> bytes:
     return json.dumps(obj).encode()
 
 
-def supports_native(plugin) -> bool:
+def supports_native(plugin, settings=None) -> bool:
+    if settings is not None and hasattr(plugin, "configure"):
+        plugin.configure(settings)
     return bool(getattr(plugin, "native_spec", None) and plugin.native_spec())

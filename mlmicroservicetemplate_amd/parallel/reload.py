@@ -13,9 +13,20 @@ loads the checkpoint, broadcasts an ok flag and then the parameters as one flatt
 dtype over RCCL/xGMI (``dist.broadcast_state``), every rank applies them and acknowledges; the
 HTTP request returns once all ranks acknowledged.  The process group is otherwise idle in DP
 serving, so the reload collectives never interleave with other collectives.
+
+Ordering: a new generation is only written (under an ``fcntl`` lock on the control directory)
+once every rank has acknowledged the previous one -- a second request meanwhile gets 409 -- so
+every watcher applies every generation, in order, and all ranks issue the same collectives.  Rank
+0 also broadcasts the generation it applies, and a rank that read another one fails loudly.
+
+Security: the endpoint is off unless ``API_KEY`` is set (403), the ``api_key`` header must match
+it, and ``weights`` may only name a file under ``WEIGHTS_DIR`` (same 400 whether a path is outside
+it or missing, so the endpoint does not reveal which paths exist).
 """
 from __future__ import annotations
 
+import fcntl
+import hmac
 import json
 import logging
 import os
@@ -30,6 +41,43 @@ logger = logging.getLogger("mlsamd.reload")
 
 class ReloadError(ValueError):
     """Bad request (unknown file, shape mismatch, unsupported model): HTTP 400."""
+
+
+class ReloadBusy(RuntimeError):
+    """Another reload generation is still being applied by some rank: HTTP 409."""
+
+
+class _DirLock:
+    """Exclusive ``flock`` on ``<dir>/lock``: serialises reload requests across the ranks."""
+
+    def __init__(self, directory: str):
+        self.path = os.path.join(directory, "lock")
+        self.fd = -1
+
+    def __enter__(self):
+        self.fd = os.open(self.path, os.O_CREAT | os.O_RDWR, 0o600)
+        fcntl.flock(self.fd, fcntl.LOCK_EX)
+        return self
+
+    def __exit__(self, *exc):
+        fcntl.flock(self.fd, fcntl.LOCK_UN)
+        os.close(self.fd)
+        self.fd = -1
+
+
+def resolve_weights(settings, weights: Any) -> str:
+    """``weights`` (relative to ``WEIGHTS_DIR``, or absolute inside it) -> a real file path under
+    ``WEIGHTS_DIR``.  One error message for "outside" and "missing"."""
+    base_setting = str(getattr(settings, "WEIGHTS_DIR", "") or "")
+    if not base_setting:
+        raise ReloadError("weights reload is disabled on this server (WEIGHTS_DIR is not set); use 'seed'")
+    if not isinstance(weights, str) or not weights or "\x00" in weights:
+        raise ReloadError("'weights' must be a file name under WEIGHTS_DIR")
+    base = os.path.realpath(base_setting)
+    path = os.path.realpath(os.path.join(base, weights))
+    if not path.startswith(base + os.sep) or not os.path.isfile(path):
+        raise ReloadError("'weights' must name an existing file under WEIGHTS_DIR")
+    return path
 
 
 def _atomic_write(path: str, obj: dict) -> None:
@@ -76,8 +124,6 @@ class ReloadCoordinator:
             raise ReloadError(f"model {self.plugin.name!r} does not support weight reload")
         if weights is None and seed is None:
             raise ReloadError("give 'weights' (a safetensors path on the server) or 'seed'")
-        if weights is not None and not os.path.exists(weights):
-            raise ReloadError(f"weights not found: {weights}")
         t0 = time.perf_counter()
         if self.ctl_dir is None:
             with self._lock:
@@ -86,9 +132,13 @@ class ReloadCoordinator:
                 self.generation += 1
                 self.last = {"generation": self.generation, "weights": weights, "seed": seed}
             return {"generation": self.generation, "ranks": 1, "seconds": round(time.perf_counter() - t0, 3)}
-        with self._lock:
+        with self._lock, _DirLock(self.ctl_dir):
             cur = _read(os.path.join(self.ctl_dir, "request.json")) or {}
-            gen = int(cur.get("generation", 0)) + 1
+            prev = int(cur.get("generation", 0))
+            if prev and not all(os.path.exists(os.path.join(self.ctl_dir, f"ack-{prev}-{r}.json"))
+                                for r in range(self.ctx.world_size)):
+                raise ReloadBusy(f"reload generation {prev} is still being applied; retry later")
+            gen = prev + 1
             _atomic_write(os.path.join(self.ctl_dir, "request.json"), {"generation": gen, "weights": weights, "seed": seed})
         deadline = time.monotonic() + timeout
         while time.monotonic() < deadline:
@@ -126,9 +176,12 @@ class ReloadCoordinator:
                 err = f"{type(e).__name__}: {e}"
         backend = dist.get_backend()
         dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
-        ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=dev)
+        ok = torch.tensor([0 if err else 1, gen], dtype=torch.int64, device=dev)
         dist.broadcast(ok, src=0)
-        if int(ok.item()):
+        flag, gen0 = (int(v) for v in ok.tolist())
+        if gen0 != gen:  # cannot happen with the 409 gate; never apply out of step with rank 0
+            raise RuntimeError(f"reload: rank {self.ctx.rank} read generation {gen}, rank 0 applies {gen0}")
+        if flag:
             try:
                 params = mdist.broadcast_state(params, src=0, device=None, spec=self.plugin.reload_spec())
                 with self._lock:
@@ -155,8 +208,10 @@ def handle_reload_request(coordinator: Optional[ReloadCoordinator], settings, he
                           payload: Any) -> tuple:
     """Shared by both front ends: ``(status, body_dict)``.  Auth: the ``api_key`` header must match
     ``API_KEY`` when one is configured (the key the service registers with, reference C10)."""
-    key = getattr(settings, "API_KEY", "")
-    if key and headers.get("api_key") != key:
+    key = str(getattr(settings, "API_KEY", "") or "")
+    if not key:
+        return 403, {"status": "failure", "detail": "admin endpoints are disabled (set API_KEY to enable)"}
+    if not hmac.compare_digest(str(headers.get("api_key", "")).encode(), key.encode()):
         return 401, {"status": "failure", "detail": "invalid or missing api_key"}
     if coordinator is None:
         return 503, {"status": "failure", "detail": "Model is not ready to receive predictions."}
@@ -164,7 +219,12 @@ def handle_reload_request(coordinator: Optional[ReloadCoordinator], settings, he
         return 422, {"detail": [{"type": "dict_type", "loc": ["body"], "msg": "JSON object required", "input": None}]}
     seed = payload.get("seed")
     try:
-        out = coordinator.request(weights=payload.get("weights"), seed=None if seed is None else int(seed))
+        weights = payload.get("weights")
+        if weights is not None:
+            weights = resolve_weights(settings, weights)
+        out = coordinator.request(weights=weights, seed=None if seed is None else int(seed))
+    except ReloadBusy as e:
+        return 409, {"status": "failure", "detail": str(e)}
     except (ReloadError, ValueError, KeyError) as e:
         return 400, {"status": "failure", "detail": str(e)}
     except TimeoutError as e:

@@ -67,6 +67,11 @@ class ModelPlugin:
     task: str = "image"  # image | text | generate | echo
     form_field: str = "image_file"  # multipart field /predict reads (reference main.py:120)
 
+    def configure(self, settings) -> None:
+        """Derive request geometry (sample shapes, tokenizer, labels) from the settings alone --
+        cheap, no GPU.  Called before :meth:`native_spec` and again at the start of :meth:`init`,
+        so the front end's row layout and the engines always agree."""
+
     def init(self, ctx: PluginContext) -> None:
         """Load / build weights; may take long (runs on a background thread)."""
 

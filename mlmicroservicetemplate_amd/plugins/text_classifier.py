@@ -32,6 +32,18 @@ class BertPlugin(ModelPlugin):
         self.labels: List[str] = []
         self.tokenizer = None
         self.max_seq = 128
+        self.cfg = None
+
+    def configure(self, settings) -> None:
+        """Labels, ``max_seq`` and the tokenizer from MODEL_CONFIG -- everything the native front
+        end's packed-row geometry depends on, without touching the GPU."""
+        from ..models import bert
+
+        extra = settings.model_yaml() if hasattr(settings, "model_yaml") else {}
+        self.cfg = bert.BertConfig(num_labels=int(extra.get("num_labels", 2)))
+        self.labels = list(extra.get("labels", [f"label_{i}" for i in range(self.cfg.num_labels)]))
+        self.max_seq = int(extra.get("max_seq", 128))
+        self.tokenizer = bert.HashTokenizer(self.cfg.vocab, extra.get("vocab_file"))
 
     def init(self, ctx: PluginContext) -> None:
         import torch
@@ -41,11 +53,8 @@ class BertPlugin(ModelPlugin):
         from ..parallel import dist as mdist
 
         s = ctx.settings
-        extra = s.model_yaml() if hasattr(s, "model_yaml") else {}
-        cfg = bert.BertConfig(num_labels=int(extra.get("num_labels", 2)))
-        self.labels = list(extra.get("labels", [f"label_{i}" for i in range(cfg.num_labels)]))
-        self.max_seq = int(extra.get("max_seq", 128))
-        self.tokenizer = bert.HashTokenizer(cfg.vocab, extra.get("vocab_file"))
+        self.configure(s)
+        cfg = self.cfg
         devices = ctx.devices or (["cuda:0"] if torch.cuda.is_available() else [])
         if not devices:
             raise RuntimeError("bert plugin needs a GPU")
@@ -93,11 +102,10 @@ class BertPlugin(ModelPlugin):
     def native_spec(self) -> dict:
         # raw_samples False: a packed row is only ever built here, never taken from a client body
         spec = {"sample_bytes": (2 * self._native_seq() + 1) * 4, "result": "topk", "raw_samples": False}
-        if (os.environ.get("MLS_NATIVE_TOKENIZER", "0") == "1" and self.tokenizer is not None
-                and self.tokenizer._wp is None):
+        if self.tokenizer is None:
+            raise RuntimeError("BertPlugin.native_spec() before configure(settings)")
+        if os.environ.get("MLS_NATIVE_TOKENIZER", "0") == "1" and self.tokenizer._wp is None:
             # opt-in: ASCII texts hash-tokenised on the C++ I/O threads (no Python per request).
-            # Measured slower end to end than the Python decode threads (15.6k vs 21.0k req/s at
-            # 64 connections, profiles/r1_http_bert_native_frontend.jsonl), hence off by default.
             from ..models import bert
 
             spec["text_hash"] = [self.tokenizer.vocab_size, self.max_seq, self._native_seq(), bert.CLS_ID, bert.SEP_ID]

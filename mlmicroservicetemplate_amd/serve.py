@@ -97,7 +97,7 @@ def run_rank(args) -> int:
     if settings.FRONTEND == "native":
         from .frontend.native import NativeService, supports_native
 
-        if supports_native(plugin):
+        if supports_native(plugin, settings):
             svc = NativeService(settings, plugin, ctx, host=args.host,
                                 listen_fd=int(fd) if fd is not None else None)
             return svc.serve_forever()

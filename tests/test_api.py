@@ -255,3 +255,29 @@ def test_request_timeout_is_504():
         assert r.status_code == 504 and r.json()["detail"] == "Prediction timed out."
         release.set()
 
+
+
+def test_upload_limit_applies_to_every_body_type():
+    """MAX_UPLOAD_BYTES -> 413 for multipart, JSON and urlencoded /predict bodies and for
+    /generate and /admin/reload JSON, by Content-Length and by streamed (chunked) length."""
+    with TestClient(create_app(settings(MAX_UPLOAD_BYTES=1000, API_KEY="k"), IdentityPlugin())) as c:
+        assert wait_ready(c)
+        big = b"x" * 2000
+        too_large = {"status": "failure", "detail": "Upload too large."}
+        for kw in (upload(big),
+                   {"content": b'{"image_file": "' + big + b'"}', "headers": {"content-type": "application/json"}},
+                   {"content": b"image_file=" + big, "headers": {"content-type": "application/x-www-form-urlencoded"}}):
+            r = c.post("/predict", **kw)
+            assert r.status_code == 413 and r.json() == too_large
+        for path in ("/generate", "/admin/reload"):
+            r = c.post(path, content=b'{"prompt": "' + big + b'"}',
+                       headers={"content-type": "application/json", "api_key": "k"})
+            assert r.status_code == 413 and r.json() == too_large
+
+        def chunks():  # no Content-Length: the streamed length is checked
+            for _ in range(4):
+                yield b"x" * 400
+
+        r = c.post("/predict", content=chunks(), headers={"content-type": "application/json"})
+        assert r.status_code == 413
+        assert c.post("/predict", **upload(b"y" * 100)).status_code == 200

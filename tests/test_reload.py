@@ -59,7 +59,7 @@ def _ready(get, timeout=10):
 
 def test_reload_python_frontend_seed_auth_and_errors(tmp_path):
     a = img(1)
-    with TestClient(create_app(settings(API_KEY="sekret"), ToyClassifierPlugin())) as c:
+    with TestClient(create_app(settings(API_KEY="sekret", WEIGHTS_DIR=str(tmp_path)), ToyClassifierPlugin())) as c:
         assert _ready(c.get)
         body, h = upload(a)
         assert c.post("/predict", content=body, headers=h).json()["result"]["classes"] == expected_classes(0, a)
@@ -69,28 +69,57 @@ def test_reload_python_frontend_seed_auth_and_errors(tmp_path):
         assert r.status_code == 200 and r.json()["result"]["generation"] == 1
         assert c.post("/predict", content=body, headers=h).json()["result"]["classes"] == expected_classes(3, a)
         bad = c.post("/admin/reload", json={"weights": str(tmp_path / "missing.safetensors")}, headers={"api_key": "sekret"})
-        assert bad.status_code == 400 and "not found" in bad.json()["detail"]
+        assert bad.status_code == 400 and "under WEIGHTS_DIR" in bad.json()["detail"]
+        # a file that exists outside WEIGHTS_DIR gets the same answer (no path-existence oracle)
+        outside = c.post("/admin/reload", json={"weights": os.path.abspath(__file__)}, headers={"api_key": "sekret"})
+        assert outside.status_code == 400 and outside.json()["detail"] == bad.json()["detail"]
+        dotdot = c.post("/admin/reload", json={"weights": "../" + os.path.basename(str(tmp_path))}, headers={"api_key": "sekret"})
+        assert dotdot.status_code == 400 and dotdot.json()["detail"] == bad.json()["detail"]
         assert c.post("/admin/reload", json={}, headers={"api_key": "sekret"}).status_code == 400
         # safetensors source, validated against the plugin's spec
         from mlmicroservicetemplate_amd.utils.checkpoint import save_state
 
         path = str(tmp_path / "toy.safetensors")
         save_state(path, ToyClassifierPlugin().load_params(None, 11))
-        r = c.post("/admin/reload", json={"weights": path}, headers={"api_key": "sekret"})
+        r = c.post("/admin/reload", json={"weights": "toy.safetensors"}, headers={"api_key": "sekret"})
         assert r.status_code == 200 and r.json()["result"]["generation"] == 2
+        r = c.post("/admin/reload", json={"weights": path}, headers={"api_key": "sekret"})  # absolute, inside
+        assert r.status_code == 200 and r.json()["result"]["generation"] == 3
         assert c.post("/predict", content=body, headers=h).json()["result"]["classes"] == expected_classes(11, a)
+
+
+def test_reload_disabled_without_api_key(tmp_path):
+    """No API_KEY configured: /admin/reload is refused on both front ends (403) and the weights
+    are untouched."""
+    a = img(1)
+    with TestClient(create_app(settings(WEIGHTS_DIR=str(tmp_path)), ToyClassifierPlugin())) as c:
+        assert _ready(c.get)
+        body, h = upload(a)
+        r = c.post("/admin/reload", json={"seed": 3})
+        assert r.status_code == 403 and "API_KEY" in r.json()["detail"]
+        assert c.post("/admin/reload", json={"seed": 3}, headers={"api_key": ""}).status_code == 403
+        assert c.post("/predict", content=body, headers=h).json()["result"]["classes"] == expected_classes(0, a)
+    s = settings()
+    svc = NativeService(s, ToyClassifierPlugin(), PluginContext(settings=s), host="127.0.0.1", port=0).start()
+    try:
+        url = f"http://127.0.0.1:{svc.port}"
+        assert _ready(lambda p: requests.get(url + p))
+        assert requests.post(url + "/admin/reload", json={"seed": 5}).status_code == 403
+        assert requests.post(url + "/predict", data=body, headers=h).json()["result"]["classes"] == expected_classes(0, a)
+    finally:
+        svc.stop()
 
 
 def test_reload_native_frontend():
     a = img(2)
-    s = settings()
+    s = settings(API_KEY="k")
     svc = NativeService(s, ToyClassifierPlugin(), PluginContext(settings=s), host="127.0.0.1", port=0).start()
     try:
         url = f"http://127.0.0.1:{svc.port}"
         assert _ready(lambda p: requests.get(url + p))
         body, h = upload(a)
         assert requests.post(url + "/predict", data=body, headers=h).json()["result"]["classes"] == expected_classes(0, a)
-        r = requests.post(url + "/admin/reload", json={"seed": 5})
+        r = requests.post(url + "/admin/reload", json={"seed": 5}, headers={"api_key": "k"})
         assert r.status_code == 200 and r.json()["result"]["ranks"] == 1
         assert requests.post(url + "/predict", data=body, headers=h).json()["result"]["classes"] == expected_classes(5, a)
         assert requests.get(url + "/admin/reload").status_code == 405
@@ -108,7 +137,7 @@ def _free_port():
 @pytest.mark.parametrize("frontend", ["python", "native"])
 def test_reload_two_ranks_broadcasts_to_every_rank(frontend):
     port = _free_port()
-    env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", API_KEY="k")
     proc = subprocess.Popen([sys.executable, "-m", "mlmicroservicetemplate_amd", "serve", "--model", "toy_classifier",
                              "--frontend", frontend, "--gpus", "2", "--port", str(port), "--host", "127.0.0.1",
                              "--no-register", "--env-file", "/nonexistent"], cwd=ROOT, env=env, start_new_session=True)
@@ -122,7 +151,21 @@ def test_reload_two_ranks_broadcasts_to_every_rank(frontend):
             except requests.RequestException:
                 time.sleep(0.2)
         assert ready
-        r = requests.post(url + "/admin/reload", json={"seed": 9}, timeout=60)
+        key = {"api_key": "k"}
+        r = requests.post(url + "/admin/reload", json={"seed": 7}, headers=key, timeout=60)
+        assert r.status_code == 200, r.text
+        assert r.json()["result"]["ranks"] == 2
+        # two reloads racing (fresh connections may land on different ranks): the ranks must stay
+        # in step -- each request is applied by every rank or refused with 409, never skipped
+        from concurrent.futures import ThreadPoolExecutor
+
+        with ThreadPoolExecutor(4) as ex:
+            codes = [f.result().status_code for f in
+                     [ex.submit(requests.post, url + "/admin/reload", json={"seed": 8}, headers=key, timeout=60)
+                      for _ in range(4)]]
+        assert set(codes) <= {200, 409} and 200 in codes, codes
+        # back to back: the group is not wedged and both ranks apply the final generation
+        r = requests.post(url + "/admin/reload", json={"seed": 9}, headers=key, timeout=60)
         assert r.status_code == 200, r.text
         assert r.json()["result"]["ranks"] == 2
         a = img(4)
