@@ -324,6 +324,9 @@ class ResNet50Fused:
             self.dual_w[p0] = torch.cat([w3.reshape(w3.shape[0], -1), wd.reshape(wd.shape[0], -1)], 1).contiguous()
             self.dual_b[p0] = (self.b[p0 + ".conv3"] + self.b[p0 + ".down"]).contiguous()
         self.fuse_down = True
+        # conv3 -> next conv1 chaining at the layer1 / layer2 boundaries (csrc/conv_chain.hip);
+        # MLS_CHAIN=0 runs the two convs as separate kernels
+        self.chain = os.environ.get("MLS_CHAIN", "1") != "0"
         # normalise + stem + max pool as one kernel (csrc/stem_pool.hip); MLS_FUSED_STEM=0 -> 3 kernels
         self.fuse_stem = image_size == 224 and os.environ.get("MLS_FUSED_STEM", "1") != "0"
         self.fc_w = params["fc.w"].to(device=self.device, dtype=torch.bfloat16).contiguous()
@@ -395,6 +398,18 @@ class ResNet50Fused:
                                     pad=s.pad if pad is None else pad,
                                     residual=residual, act=act, workspace=self.workspace, cfg=cfg, splitk=sk)
 
+    # (K of the conv3 GEMM, N1, N2) shapes csrc/conv_chain.hip is built for
+    CHAIN_SHAPES = ((64, 256, 64), (128, 256, 64), (64, 256, 128), (128, 512, 128))
+
+    def _chained(self, p: str, nxt: str, dual: bool) -> bool:
+        """Run block ``p``'s conv3 together with block ``nxt``'s conv1 (ops.conv1x1_chain)?"""
+        if not self.chain:
+            return False
+        c3 = self.specs[p + ".conv3"]
+        k = c3.cin + (self.specs[p + ".down"].cin if dual else 0)
+        c1 = self.specs[nxt + ".conv1"]
+        return c1.k == 1 and c1.stride == 1 and (k, c3.cout, c1.cout) in self.CHAIN_SHAPES
+
     def forward(self, images_u8_nhwc: torch.Tensor) -> torch.Tensor:
         """uint8 ``[B,H,W,3]`` on device -> bf16 logits ``[B, num_classes]``."""
         ops = self.ops
@@ -407,18 +422,35 @@ class ResNet50Fused:
             x = ops.normalize_u8(images_u8_nhwc, self.mean, self.std, pad=3)  # zero border = stem padding
             x = self._conv(x, "stem", ops.ACT_RELU, pad=0)
             x = ops.maxpool2d_nhwc(x, 3, 2, 1)
-        for si, (nblocks, _m, _c, _s) in enumerate(STAGES):
-            for bi in range(nblocks):
-                p = f"layer{si + 1}.{bi}"
-                y = self._conv(x, p + ".conv1", ops.ACT_RELU)
-                y = self._conv(y, p + ".conv2", ops.ACT_RELU)
-                if bi == 0 and self.fuse_down:
-                    cfg, sk = self.tuning.get(p + ".dual", (0, 0))
-                    x = ops.conv1x1_dual(y, x, self.dual_w[p], self.dual_b[p], stride2=self.specs[p + ".down"].stride,
-                                         act=ops.ACT_RELU, workspace=self.workspace, cfg=cfg, splitk=sk)
+        blocks = [(si, bi) for si, (nblocks, _m, _c, _s) in enumerate(STAGES) for bi in range(nblocks)]
+        t1 = self._conv(x, "layer1.0.conv1", ops.ACT_RELU)
+        for idx, (si, bi) in enumerate(blocks):
+            p = f"layer{si + 1}.{bi}"
+            nxt = f"layer{blocks[idx + 1][0] + 1}.{blocks[idx + 1][1]}" if idx + 1 < len(blocks) else None
+            t2 = self._conv(t1, p + ".conv2", ops.ACT_RELU)
+            dual = bi == 0 and self.fuse_down
+            if nxt is not None and self._chained(p, nxt, dual):
+                # this block's conv3 (+ residual / downsample) and the next block's conv1 in one
+                # kernel: the block output goes to HBM once and is never read back
+                w1n, b1n = self.w[nxt + ".conv1"], self.b[nxt + ".conv1"]
+                w1n = w1n.reshape(w1n.shape[0], -1)
+                if dual:
+                    x, t1 = ops.conv1x1_chain(t2, self.dual_w[p], self.dual_b[p], w1n, b1n, a2=x,
+                                              stride2=self.specs[p + ".down"].stride)
                 else:
-                    identity = self._conv(x, p + ".down", ops.ACT_NONE) if bi == 0 else x
-                    x = self._conv(y, p + ".conv3", ops.ACT_RELU, residual=identity)
+                    w3 = self.w[p + ".conv3"]
+                    x, t1 = ops.conv1x1_chain(t2, w3.reshape(w3.shape[0], -1), self.b[p + ".conv3"], w1n, b1n,
+                                              residual=x)
+                continue
+            if dual:
+                cfg, sk = self.tuning.get(p + ".dual", (0, 0))
+                x = ops.conv1x1_dual(t2, x, self.dual_w[p], self.dual_b[p], stride2=self.specs[p + ".down"].stride,
+                                     act=ops.ACT_RELU, workspace=self.workspace, cfg=cfg, splitk=sk)
+            else:
+                identity = self._conv(x, p + ".down", ops.ACT_NONE) if bi == 0 else x
+                x = self._conv(t2, p + ".conv3", ops.ACT_RELU, residual=identity)
+            if nxt is not None:
+                t1 = self._conv(x, nxt + ".conv1", ops.ACT_RELU)
         pooled = ops.avgpool_global_nhwc(x)
         cfg, sk = self.tuning.get("fc", (0, 0))
         return ops.gemm(pooled, self.fc_w, self.fc_b, workspace=self.workspace, cfg=cfg, splitk=sk)

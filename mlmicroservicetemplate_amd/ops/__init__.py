@@ -192,6 +192,53 @@ def conv1x1_dual(y: torch.Tensor, x: torch.Tensor, w_cat: torch.Tensor, bias: Op
     return out
 
 
+def conv1x1_chain(a1: torch.Tensor, w3: torch.Tensor, b3: Optional[torch.Tensor], w1: torch.Tensor,
+                  b1: Optional[torch.Tensor], *, residual: Optional[torch.Tensor] = None,
+                  a2: Optional[torch.Tensor] = None, stride2: int = 1,
+                  y_out: Optional[torch.Tensor] = None, t1_out: Optional[torch.Tensor] = None):
+    """One bottleneck boundary in one kernel (csrc/conv_chain.hip):
+    ``y = relu(conv1x1([a1 | a2 at stride2], w3) + b3 (+ residual))`` and
+    ``t1 = relu(conv1x1(y, w1) + b1)``; y never makes an HBM round trip.  Returns ``(y, t1)``.
+    ``w3`` is ``[N1][Ka (+ Kb)]`` (the dual concatenation when ``a2`` is given; no residual then),
+    ``w1`` ``[N2][N1]``.  Supported (Ka + Kb, N1, N2): (64, 256, 64), (128, 256, 64),
+    (64, 256, 128), (128, 512, 128) -- ResNet-50 layer1 / layer2 boundaries."""
+    dev = a1.device
+    _need(a1, "a1", torch.bfloat16, dev)
+    _need(w3, "w3", torch.bfloat16, dev)
+    _need(w1, "w1", torch.bfloat16, dev)
+    B, Ho, Wo, Ka = a1.shape
+    N1, N2 = w3.shape[0], w1.shape[0]
+    if a2 is not None:
+        _need(a2, "a2", torch.bfloat16, dev)
+        if residual is not None:
+            raise ValueError("conv1x1_chain: the dual form has no residual")
+        B2, H2, W2, Kb = a2.shape
+        if B2 != B or conv_out_hw(H2, W2, 1, stride2, 0) != (Ho, Wo):
+            raise ValueError("conv1x1_chain: a2 does not match a1's grid at stride2")
+    else:
+        H2 = W2 = Kb = 0
+    if w3.reshape(N1, -1).shape[1] != Ka + Kb or w1.reshape(N2, -1).shape[1] != N1:
+        raise ValueError("conv1x1_chain: weight shapes do not chain")
+    if (Ka + Kb, N1, N2) not in ((64, 256, 64), (128, 256, 64), (64, 256, 128), (128, 512, 128)):
+        raise ValueError(f"conv1x1_chain: unsupported shape (K {Ka + Kb}, N1 {N1}, N2 {N2})")
+    for name, t, n in (("b3", b3, N1), ("b1", b1, N2)):
+        if t is not None:
+            _need(t, name, torch.float32, dev)
+            if t.numel() != n:
+                raise ValueError(f"{name} must have {n} elements")
+    if residual is not None:
+        _need(residual, "residual", torch.bfloat16, dev)
+        if tuple(residual.shape) != (B, Ho, Wo, N1):
+            raise ValueError("residual shape mismatch")
+    y = torch.empty(B, Ho, Wo, N1, device=dev, dtype=torch.bfloat16) if y_out is None else y_out
+    t1 = torch.empty(B, Ho, Wo, N2, device=dev, dtype=torch.bfloat16) if t1_out is None else t1_out
+    rc = lib().mls_conv_chain(a1.data_ptr(), _ptr(a2), w3.data_ptr(), _ptr(b3), _ptr(residual), y.data_ptr(),
+                              w1.data_ptr(), _ptr(b1), t1.data_ptr(), B, Ho, Wo, Ka, H2, W2, Kb, stride2, N1, N2,
+                              stream_ptr(dev))
+    check(rc, "mls_conv_chain")
+    return y, t1
+
+
 def gemm(
     a: torch.Tensor,
     w: torch.Tensor,

@@ -34,6 +34,7 @@ FP = _c.POINTER(_c.c_float)
 _SIGS = {
     "mls_conv2d": [P, P, P, P, P, P, P, SZ, I, I, I, I, I, I, I, I, I, I, I, I, P],
     "mls_conv2d_dual": [P, P, P, P, P, P, SZ, I, I, I, I, I, I, I, I, I, I, I, I, P],
+    "mls_conv_chain": [P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P],
     "mls_gemm": [P, P, P, P, P, P, P, SZ, I, I, I, I, I, I, P],
     "mls_gemm_heuristic": [I, I, I, _c.POINTER(I), _c.POINTER(I)],
     "mls_gemm_num_cfgs": [],

@@ -1,0 +1,31 @@
+"""Run the fused ResNet-50 forward (bs=32) serially ITERS times, eagerly (one kernel per op), for
+rocprofv3 counter collection over a whole forward:
+
+    rocprofv3 --pmc FETCH_SIZE --kernel-trace -- python3 tools/probe/forward_probe.py
+"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+
+from mlmicroservicetemplate_amd.models.resnet import ResNet50Fused, init_resnet50  # noqa: E402
+from mlmicroservicetemplate_amd.ops import autotune  # noqa: E402
+
+
+def main():
+    batch = int(os.environ.get("BATCH", 32))
+    iters = int(os.environ.get("ITERS", 3))
+    dev = torch.device("cuda:0")
+    model = ResNet50Fused(init_resnet50(0), dev, max_batch=batch, tuning=autotune.load_tuning("resnet50", batch))
+    x = torch.randint(0, 256, (batch, 224, 224, 3), dtype=torch.uint8, device=dev)
+    with torch.no_grad():
+        for _ in range(iters):
+            model.classify(x, 5)
+            torch.cuda.synchronize()
+    print("forwards", iters, flush=True)
+
+
+if __name__ == "__main__":
+    main()
