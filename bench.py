@@ -69,7 +69,7 @@ def main(argv=None) -> int:
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=32)
-    ap.add_argument("--inflight", type=int, default=5)
+    ap.add_argument("--inflight", type=int, default=int(os.environ.get("INFLIGHT", 5)))
     ap.add_argument("--backend", default="fused", choices=["fused", "eager"])
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--serial", action="store_true", help="one compute stream (no concurrent in-flight batches)")

@@ -327,6 +327,8 @@ class ResNet50Fused:
         # conv3 -> next conv1 chaining at the layer1 / layer2 boundaries (csrc/conv_chain.hip);
         # MLS_CHAIN=0 runs the two convs as separate kernels
         self.chain = os.environ.get("MLS_CHAIN", "1") != "0"
+        # block names whose conv3 is NOT chained (A/B: MLS_CHAIN_SKIP=layer1.2,layer2.1)
+        self.chain_skip: set = {b for b in os.environ.get("MLS_CHAIN_SKIP", "").split(",") if b}
         # normalise + stem + max pool as one kernel (csrc/stem_pool.hip); MLS_FUSED_STEM=0 -> 3 kernels
         self.fuse_stem = image_size == 224 and os.environ.get("MLS_FUSED_STEM", "1") != "0"
         self.fc_w = params["fc.w"].to(device=self.device, dtype=torch.bfloat16).contiguous()
@@ -403,7 +405,7 @@ class ResNet50Fused:
 
     def _chained(self, p: str, nxt: str, dual: bool) -> bool:
         """Run block ``p``'s conv3 together with block ``nxt``'s conv1 (ops.conv1x1_chain)?"""
-        if not self.chain:
+        if not self.chain or p in self.chain_skip:
             return False
         c3 = self.specs[p + ".conv3"]
         k = c3.cin + (self.specs[p + ".down"].cin if dual else 0)

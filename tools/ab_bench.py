@@ -43,9 +43,12 @@ def build(spec: str, params, dev, batch: int, inflight: int):
         model = ResNet50Fused(params, dev, max_batch=batch, tuning=autotune.load_tuning("resnet50", batch))
         for k, v in attrs.items():
             cur = getattr(model, k)
-            setattr(model, k, type(cur)(int(v)) if isinstance(cur, (bool, int)) else type(cur)(v))
+            if k == "chain_skip":  # '+'-separated block names whose boundary is NOT chained
+                setattr(model, k, set(v.split("+")))
+            else:
+                setattr(model, k, type(cur)(int(v)) if isinstance(cur, (bool, int)) else type(cur)(v))
         eng = GpuEngine(lambda x: model.classify(x, 5), dev, (224, 224, 3), torch.uint8, buckets=[batch],
-                        inflight=inflight, name=f"ab.{spec}")
+                        inflight=inflight, name=f"ab.{spec}", concurrent=True)
         eng.warmup(capture=True)
     finally:
         for k, v in env_saved.items():
