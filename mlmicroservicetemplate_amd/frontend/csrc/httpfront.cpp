@@ -624,6 +624,7 @@ class Server {
     s["rejected_overload"] = n_overload_;
     s["python_routed"] = n_python_;
     s["decode_routed"] = n_decode_;
+    s["text_hashed"] = n_text_hash_;
     s["connections_open"] = n_conns_;
     {
       std::lock_guard<std::mutex> g(qmu_);
@@ -661,7 +662,7 @@ class Server {
   std::atomic<uint64_t> next_id_{1};
   std::atomic<uint64_t> next_conn_{2};  // 0 = listen socket, 1 = eventfd
 
-  std::atomic<long long> n_requests_{0}, n_batches_{0}, n_samples_{0}, n_overload_{0}, n_python_{0}, n_decode_{0},
+  std::atomic<long long> n_requests_{0}, n_batches_{0}, n_samples_{0}, n_overload_{0}, n_python_{0}, n_decode_{0}, n_text_hash_{0},
       n_conns_{0};
   std::mutex cmu_;
   std::map<int, long long> code_counts_;
@@ -1143,6 +1144,7 @@ class Server {
         p.ref = std::move(ref);
         p.body.assign(reinterpret_cast<const char*>(row.data()), row.size() * sizeof(int32_t));
         c.waiting = true;
+        n_text_hash_++;
         enqueue_sample(std::move(p));
         return;
       }

@@ -98,6 +98,9 @@ def main() -> int:
                 nat = requests.get(url + "/health", timeout=5).json().get("native") or {}
                 if nat.get("batches"):
                     res["server_mean_batch"] = round(nat["samples"] / nat["batches"], 2)
+                # which path tokenised / decoded the uploads (cumulative over the levels so far)
+                res["server_decode_routed"] = nat.get("decode_routed")
+                res["server_text_hashed"] = nat.get("text_hashed")
             except (requests.RequestException, ValueError):
                 pass
             res.update({"model": args.model, "frontend": args.frontend, "workers_per_gpu": args.workers_per_gpu,
