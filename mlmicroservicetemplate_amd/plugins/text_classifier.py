@@ -104,8 +104,11 @@ class BertPlugin(ModelPlugin):
         spec = {"sample_bytes": (2 * self._native_seq() + 1) * 4, "result": "topk", "raw_samples": False}
         if self.tokenizer is None:
             raise RuntimeError("BertPlugin.native_spec() before configure(settings)")
-        if os.environ.get("MLS_NATIVE_TOKENIZER", "0") == "1" and self.tokenizer._wp is None:
-            # opt-in: ASCII texts hash-tokenised on the C++ I/O threads (no Python per request).
+        if os.environ.get("MLS_NATIVE_TOKENIZER", "1") == "1" and self.tokenizer._wp is None:
+            # ASCII texts hash-tokenised on the C++ I/O threads (no Python per request; others go to
+            # the Python decode threads): 25.0k / 29.2k req/s vs 17.2-19.6k / 20.0-20.7k with Python
+            # tokenisation at 64 / 256 connections (profiles/r2_http_bert_tokenizer_ab_fixed.jsonl).
+            # MLS_NATIVE_TOKENIZER=0 turns it off.
             from ..models import bert
 
             spec["text_hash"] = [self.tokenizer.vocab_size, self.max_seq, self._native_seq(), bert.CLS_ID, bert.SEP_ID]

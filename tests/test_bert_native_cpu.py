@@ -18,7 +18,8 @@ def _plugin(max_seq):  # geometry set by hand (configure() is tested below)
     return p
 
 
-def test_native_row_matches_pack_requests():
+def test_native_row_matches_pack_requests(monkeypatch):
+    monkeypatch.setenv("MLS_NATIVE_TOKENIZER", "0")
     p = _plugin(128)
     spec = p.native_spec()
     assert spec == {"sample_bytes": (2 * 128 + 1) * 4, "result": "topk", "raw_samples": False}
@@ -30,9 +31,11 @@ def test_native_row_matches_pack_requests():
         np.testing.assert_array_equal(row, want)
 
 
-def test_native_tokenizer_opt_in(monkeypatch):
-    monkeypatch.setenv("MLS_NATIVE_TOKENIZER", "1")
+def test_native_tokenizer_default_on_and_opt_out(monkeypatch):
+    monkeypatch.delenv("MLS_NATIVE_TOKENIZER", raising=False)
     assert _plugin(128).native_spec()["text_hash"] == [30522, 128, 128, bert.CLS_ID, bert.SEP_ID]
+    monkeypatch.setenv("MLS_NATIVE_TOKENIZER", "0")
+    assert "text_hash" not in _plugin(128).native_spec()
 
 
 def test_native_seq_is_largest_bucket_below_max_seq():
