@@ -101,6 +101,8 @@ def _workspace_args(ws: Optional[torch.Tensor]):
 # variant 0 / 1) instead of an implicit-GEMM tile config; tuning-table values like any other.
 CFG_HALO = 100
 CFG_HALO_N32 = 101
+CFG_HALO_XL = 102  # 512 output pixels x 64 channels per block, 4 x 4 MFMA tiles per wave
+HALO_CFGS = (CFG_HALO, CFG_HALO_N32, CFG_HALO_XL)
 
 
 def conv2d_nhwc(
@@ -135,7 +137,7 @@ def conv2d_nhwc(
     if cout % 8:
         raise ValueError("Cout must be a multiple of 8")
     ho, wo = conv_out_hw(H, W, kernel, stride, pad)
-    if cfg in (CFG_HALO, CFG_HALO_N32):
+    if cfg in HALO_CFGS:
         if kernel != 3 or stride != 1 or pad != 1 or scale is not None:
             raise ValueError("CFG_HALO: 3x3 / stride 1 / pad 1 convolutions without a scale only")
         return conv3x3_halo(x, w, bias, act=act, residual=residual, out=out, variant=cfg - CFG_HALO,
@@ -481,7 +483,8 @@ def conv3x3_halo(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] 
     """3x3 / stride 1 / pad 1 NHWC conv on the halo-tiled direct kernel (csrc/conv3x3_halo.hip):
     x ``[B,H,W,Cin]`` bf16, w packed ``[N,3,3,Cin]`` bf16, bias fp32 ``[N]`` -> ``[B,H,W,N]``
     ``act(conv + bias (+ residual))``.  Cin % 32 == 0; ``variant`` 0 = 64 output channels x 8
-    waves per block (N % 64 == 0), 1 = 32 x 4 (N % 32 == 0).  ``splitk`` > 1 splits the input
+    waves per block (N % 64 == 0), 1 = 32 x 4 (N % 32 == 0), 2 = the XL tile (512 output pixels
+    x 64 channels, 8 waves of 4 x 4 MFMA tiles).  ``splitk`` > 1 splits the input
     channels over that many blocks per tile, reduced in the same launch through fp32 slabs in
     ``workspace`` (>= splitk * B*H*W * N floats; otherwise, or on an uneven split, one slice)."""
     dev = x.device
@@ -489,7 +492,7 @@ def conv3x3_halo(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] 
     _need(w, "w", torch.bfloat16, dev)
     B, H, W, C = x.shape
     N = w.shape[0]
-    if tuple(w.shape) != (N, 3, 3, C) or C % 32 or N % (32 if variant == 1 else 64) or variant not in (0, 1):
+    if tuple(w.shape) != (N, 3, 3, C) or C % 32 or N % (32 if variant == 1 else 64) or variant not in (0, 1, 2):
         raise ValueError("conv3x3_halo: w must be [N,3,3,Cin], Cin % 32 == 0, N % 64 (variant 1: 32) == 0")
     if bias is not None:
         _need(bias, "bias", torch.float32, dev)
@@ -513,10 +516,10 @@ def conv3x3_halo(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] 
     return out
 
 
-def conv3x3_halo_geometry(B: int, H: int, W: int) -> Optional[Tuple[int, int]]:
+def conv3x3_halo_geometry(B: int, H: int, W: int, variant: int = 0) -> Optional[Tuple[int, int]]:
     """(output rows per tile, images per tile) the halo kernel uses for this shape, or None."""
     th, nb = ctypes.c_int(0), ctypes.c_int(0)
-    rc = lib().mls_conv3x3_halo_geometry(B, H, W, ctypes.byref(th), ctypes.byref(nb))
+    rc = lib().mls_conv3x3_halo_geometry_v(B, H, W, variant, ctypes.byref(th), ctypes.byref(nb))
     return (th.value, nb.value) if rc == 0 else None
 
 

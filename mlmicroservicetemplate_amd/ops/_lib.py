@@ -43,6 +43,7 @@ _SIGS = {
     "mls_stem_pool": [P, P, P, P, I, I, I, FP, FP, P],
     "mls_conv3x3_halo": [P, P, P, P, P, P, SZ, I, I, I, I, I, I, I, I, P],
     "mls_conv3x3_halo_geometry": [I, I, I, _c.POINTER(I), _c.POINTER(I)],
+    "mls_conv3x3_halo_geometry_v": [I, I, I, I, _c.POINTER(I), _c.POINTER(I)],
     "mls_avgpool_global": [P, P, I, I, I, P],
     "mls_bn_act": [P, P, P, P, L, I, I, P],
     "mls_silu_mul_interleaved": [P, P, L, I, P],

@@ -16,7 +16,8 @@ import torch
 import torch.nn.functional as F
 
 CACHE_DIR = os.environ.get("MLS_TUNE_DIR", os.path.join(os.path.dirname(os.path.abspath(__file__)), "_native", "tune"))
-CANDIDATES: List[Tuple[int, int]] = [(c, s) for c in range(1, 19) for s in (1, 2, 4, 8)] + [(20, 1), (21, 1), (22, 1)]
+GEMM_CFGS = list(range(1, 20)) + list(range(23, 29))  # conv_gemm.hip kCfgs (20..22: persistent kernel)
+CANDIDATES: List[Tuple[int, int]] = [(c, s) for c in GEMM_CFGS for s in (1, 2, 4, 8)] + [(20, 1), (21, 1), (22, 1)]
 
 
 def _time(fn, iters: int = 20, warmup: int = 3) -> float:
@@ -90,10 +91,13 @@ def _time_multi(fns, iters: int = 20, warmup: int = 3) -> float:
 
 
 def tune_resnet50(batch: int, device="cuda:0", iters: int = 20, compare_torch: bool = True,
-                  candidates: Optional[List[Tuple[int, int]]] = None, concurrency: int = 1) -> Dict[str, dict]:
+                  candidates: Optional[List[Tuple[int, int]]] = None, concurrency: int = 1,
+                  layers: Optional[List[str]] = None) -> Dict[str, dict]:
     """Per-layer (cfg, splitk) search.  ``concurrency`` > 1 scores each candidate by its
-    per-batch cost with that many batches co-running (the serving engine's concurrent slots)."""
-    from . import CFG_HALO, CFG_HALO_N32, conv2d_nhwc, gemm, pack_conv_weight
+    per-batch cost with that many batches co-running (the serving engine's concurrent slots).
+    ``layers`` restricts the search to those layer names (probes); the FC is tuned only when
+    ``layers`` is None or names it."""
+    from . import CFG_HALO, CFG_HALO_N32, CFG_HALO_XL, conv2d_nhwc, gemm, pack_conv_weight
     from ..models.resnet import conv_shapes
 
     dev = torch.device(device)
@@ -101,6 +105,8 @@ def tune_resnet50(batch: int, device="cuda:0", iters: int = 20, compare_torch: b
     results: Dict[str, dict] = {}
     cands = candidates or CANDIDATES
     for s, hin, ho in conv_shapes():
+        if layers is not None and s.name not in layers:
+            continue
         cin = 4 if s.name == "stem" else s.cin
         hp = hin + 2 * s.pad if s.name == "stem" else hin  # stem runs on the pre-padded image
         x = torch.randn(batch, hp, hp, cin, device=dev).to(torch.bfloat16)
@@ -117,7 +123,8 @@ def tune_resnet50(batch: int, device="cuda:0", iters: int = 20, compare_torch: b
         best = (1e9, 0, 0)
         tried = {}
         halo = s.k == 3 and s.stride == 1 and s.cin % 32 == 0 and s.cout % 64 == 0
-        halo_cands = [(CFG_HALO, 1), (CFG_HALO, 2), (CFG_HALO, 4), (CFG_HALO_N32, 1)] if halo else []
+        halo_cands = [(CFG_HALO, 1), (CFG_HALO, 2), (CFG_HALO, 4), (CFG_HALO_N32, 1), (CFG_HALO_XL, 1),
+                      (CFG_HALO_XL, 2), (CFG_HALO_XL, 4)] if halo else []
         for cfg, sk in [(0, 0)] + cands + halo_cands:
             if sk > 1 and k // sk < 128:
                 continue
@@ -138,6 +145,8 @@ def tune_resnet50(batch: int, device="cuda:0", iters: int = 20, compare_torch: b
         entry = {"M": batch * ho * ho, "N": s.cout, "K": k, "best_cfg": best[1], "best_splitk": best[2],
                  "best_us": round(best[0] * 1e3, 2), "heuristic_us": tried.get("0,0"),
                  "tflops": round(flops / (best[0] * 1e-3) / 1e12, 1)}
+        if os.environ.get("MLS_TUNE_VERBOSE"):
+            entry["tried_us"] = tried
         if compare_torch:
             xt = x[:, 3:-3, 3:-3, :3] if s.name == "stem" else x
             xt = xt.permute(0, 3, 1, 2)
@@ -157,6 +166,8 @@ def tune_resnet50(batch: int, device="cuda:0", iters: int = 20, compare_torch: b
     shapes = {s.name: (s, hin, ho) for s, hin, ho in conv_shapes()}
     for si in range(len(STAGES)):
         p0 = f"layer{si + 1}.0"
+        if layers is not None and p0 + ".dual" not in layers:
+            continue
         sd, hin_d, ho = shapes[p0 + ".down"]
         s3 = shapes[p0 + ".conv3"][0]
         y = torch.randn(batch, ho, ho, s3.cin, device=dev).to(torch.bfloat16)
@@ -168,7 +179,7 @@ def tune_resnet50(batch: int, device="cuda:0", iters: int = 20, compare_torch: b
         best = (1e9, 0, 0)
         tried = {}
         for cfg, sk in [(0, 0)] + cands:
-            if cfg >= 20:
+            if 20 <= cfg <= 22:  # persistent kernel: no dual mode
                 continue
 
             def mk(o, wsc, cfg=cfg, sk=sk):
@@ -186,6 +197,8 @@ def tune_resnet50(batch: int, device="cuda:0", iters: int = 20, compare_torch: b
         results[p0 + ".dual"] = {"M": batch * ho * ho, "N": sd.cout, "K": s3.cin + sd.cin, "best_cfg": best[1],
                                  "best_splitk": best[2], "best_us": round(best[0] * 1e3, 2),
                                  "heuristic_us": tried.get("0,0"), "tflops": round(flops / (best[0] * 1e-3) / 1e12, 1)}
+    if layers is not None and "fc" not in layers:
+        return results
     # FC
     a = torch.randn(batch, 2048, device=dev).to(torch.bfloat16)
     w = torch.randn(1000, 2048, device=dev).to(torch.bfloat16)
@@ -250,9 +263,15 @@ if __name__ == "__main__":
     ap.add_argument("--out", default="")
     ap.add_argument("--concurrency", type=int, default=1)
     ap.add_argument("--no-torch", action="store_true")
+    ap.add_argument("--layers", nargs="*", default=None, help="only these layers (probe)")
+    ap.add_argument("--cfgs", nargs="*", type=int, default=None, help="only these tile cfgs (with splitk 1/2/4/8)")
     args = ap.parse_args()
     t0 = time.time()
-    res = tune_resnet50(args.batch, compare_torch=not args.no_torch, concurrency=args.concurrency)
+    cands = None
+    if args.cfgs:
+        cands = [(c, s) for c in args.cfgs for s in (1, 2, 4, 8)]
+    res = tune_resnet50(args.batch, compare_torch=not args.no_torch, concurrency=args.concurrency,
+                        candidates=cands, layers=args.layers)
     tot_best = sum(v["best_us"] for v in res.values())
     tot_heur = sum(v.get("heuristic_us") or v["best_us"] for v in res.values())
     tot_torch = sum(v.get("torch_us", 0) for v in res.values())

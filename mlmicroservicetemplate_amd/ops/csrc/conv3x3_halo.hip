@@ -37,7 +37,11 @@ namespace {
 constexpr int CK = 32;                           // input channels per chunk = one MFMA k-slab
 constexpr int MAX_ROWS = 256;                    // output pixels per block (16 MFMA row blocks)
 constexpr int PATCH_MAX = 384;                   // input pixels per patch
-constexpr int PATCH_BYTES = PATCH_MAX * CK * 2;  // 24576
+// the XL tile (variant 2): 512 output pixels x 64 channels, each wave a 4 x 4 grid of MFMA tiles
+// (half the LDS fragment reads per MFMA of the 2 x 4 grid: at 2 x 4 the fragment reads alone need
+// ~190 of the CU's 256 LDS bytes / clk), weights amortised over twice the pixels
+constexpr int XL_ROWS = 512;
+constexpr int XL_PATCH = 648;                    // 8 images of 9 x 9, or 10 x 58 rows of a 56-wide map
 
 #define LDS3 __attribute__((address_space(3)))
 
@@ -65,25 +69,32 @@ MLS_DEV int wswz(int n) { return (0x78 >> (2 * ((n >> 2) & 3))) & 3; }
 // BN output channels per block, NW waves; wave w owns MFMA row blocks w, w + NW, ... (16 / NW of
 // them) x all BN / 16 column blocks.  <64, 8>: 60 KB of LDS (2 blocks per CU); <32, 4>: 42 KB
 // (3 per CU), half the MFMA work per staged patch.
-template <int BN, int NW>
+// ROWS / PMAX: output pixels / patch pixels per block.  CONTIG (the XL tile): wave w owns the row
+// blocks w*RBW .. w*RBW+RBW-1 and skips (wave-uniformly) the ones past the tile's last pixel;
+// otherwise row blocks w, w + NW, ... and padded blocks are computed and dropped.
+template <int BN, int NW, int ROWS = MAX_ROWS, int PMAX = PATCH_MAX>
 struct HaloCfg {
   static constexpr int NTHR = NW * 64;
+  static constexpr int PATCH_BYTES = (PMAX + 15) / 16 * 1024;  // whole 16-pixel DMA pieces (the last may be partial)
   static constexpr int W_BYTES = 9 * BN * CK * 2;
   static constexpr int W_PIECES = W_BYTES / 1024;
   static constexpr int STAGE = PATCH_BYTES + W_BYTES;
   static constexpr int EPI_LD = BN + 8;  // bf16 row stride of the epilogue tile
-  static constexpr int RBW = 16 / NW;    // row blocks per wave
-  static constexpr int CB = BN / 16;     // column blocks
-  static constexpr int PP_WAVE = (PATCH_MAX / 16 + NW - 1) / NW;
+  static constexpr int RBW = ROWS / 16 / NW;  // row blocks per wave
+  static constexpr int CB = BN / 16;          // column blocks
+  static constexpr bool CONTIG = ROWS > MAX_ROWS;
+  static constexpr int PP_WAVE = ((PMAX + 15) / 16 + NW - 1) / NW;  // patch DMA pieces per wave
   static constexpr int WP_WAVE = (W_PIECES + NW - 1) / NW;
-  static_assert(MAX_ROWS * EPI_LD * 2 <= STAGE, "epilogue tile fits the stage buffer");
-  static_assert(RBW * NW == 16 && CB * 16 == BN, "tile split");
+  static_assert(ROWS * EPI_LD * 2 <= STAGE, "epilogue tile fits the stage buffer");
+  static_assert(RBW * NW * 16 == ROWS && CB * 16 == BN, "tile split");
+  static_assert(STAGE <= 160 * 1024, "LDS");
 };
 
-template <int BN, int NW, bool RS>
+template <int BN, int NW, bool RS, int ROWS = MAX_ROWS, int PMAX = PATCH_MAX>
 __global__ __launch_bounds__(NW * 64) void conv3x3_halo_kernel(const HaloArgs a) {
-  using C = HaloCfg<BN, NW>;
+  using C = HaloCfg<BN, NW, ROWS, PMAX>;
   constexpr int RBW = C::RBW, CB = C::CB;
+  constexpr int PATCH_BYTES = C::PATCH_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[C::STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -103,12 +114,13 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_halo_kernel(const HaloArgs a)
   const int oh0 = a.nb > 1 ? 0 : (tile - (tile / tpi) * tpi) * a.th;
   const long m_base = (long)tile * R;  // the tile's output pixels are contiguous rows
 
+  auto rb_of = [&](int i) { return C::CONTIG ? wid * RBW + i : wid + NW * i; };
   // A fragments: patch pixel of tap (0, 0) for this lane's row in each of the wave's row blocks
   int pb[RBW];
   bool rb_on[RBW];
 #pragma unroll
   for (int i = 0; i < RBW; ++i) {
-    const int rb = wid + NW * i;
+    const int rb = rb_of(i);
     rb_on[i] = rb * 16 < R;
     const int r = min(rb * 16 + fr, R - 1);  // padded rows read a valid pixel, never stored
     const int img = r / (a.th * a.W);
@@ -221,10 +233,12 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_halo_kernel(const HaloArgs a)
       const int cur = tap & 1;
       if (tap + 1 < 9) load(tap + 1, cur ^ 1);
 #pragma unroll
-      for (int i = 0; i < RBW; ++i)
+      for (int i = 0; i < RBW; ++i) {
+        if (C::CONTIG && !rb_on[i]) continue;  // wave-uniform: this row block is all padding
 #pragma unroll
         for (int j = 0; j < CB; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[cur][i], bf[cur][j], acc[i][j], 0, 0, 0);
+      }
     }
   }
 
@@ -236,7 +250,7 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_halo_kernel(const HaloArgs a)
     const rsrc_t wsr = make_rsrc(a.ws, a.ws_bytes);
 #pragma unroll
     for (int i = 0; i < RBW; ++i) {
-      const int rb = wid + NW * i;
+      const int rb = rb_of(i);
 #pragma unroll
       for (int j = 0; j < CB; ++j)
 #pragma unroll
@@ -294,7 +308,7 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_halo_kernel(const HaloArgs a)
 #pragma unroll
   for (int i = 0; i < RBW; ++i) {
     if (!rb_on[i]) continue;
-    const int rb = wid + NW * i;
+    const int rb = rb_of(i);
 #pragma unroll
     for (int j = 0; j < CB; ++j)
 #pragma unroll
@@ -326,13 +340,13 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_halo_kernel(const HaloArgs a)
 // Tile geometry for an H x W image: the largest th dividing H with th * W <= 256 output pixels
 // and (th + 2) * (W + 2) <= PATCH_MAX patch pixels; whole images (th == H) are packed nb per
 // block (nb | B).  Returns false when no geometry fits.
-bool halo_geometry(int B, int H, int W, int* th, int* nb) {
+bool halo_geometry(int B, int H, int W, int* th, int* nb, int max_rows = MAX_ROWS, int patch_max = PATCH_MAX) {
   for (int t = H; t >= 1; --t) {
-    if (H % t || t * W > MAX_ROWS || (t + 2) * (W + 2) > PATCH_MAX) continue;
+    if (H % t || t * W > max_rows || (t + 2) * (W + 2) > patch_max) continue;
     int n = 1;
     if (t == H)
       for (int c = 8; c >= 1; --c)
-        if (B % c == 0 && c * H * W <= MAX_ROWS && c * (H + 2) * (W + 2) <= PATCH_MAX) {
+        if (B % c == 0 && c * H * W <= max_rows && c * (H + 2) * (W + 2) <= patch_max) {
           n = c;
           break;
         }
@@ -355,10 +369,11 @@ int mls_conv3x3_halo(const void* x, const void* w, const float* bias, const void
                      size_t ws_bytes, int B, int H, int W, int Cin, int N, int act, int variant, int splitk,
                      void* stream) {
   const int bn = variant == 1 ? 32 : 64;
-  if (B <= 0 || H <= 0 || W <= 0 || Cin % CK || Cin <= 0 || N % bn || N <= 0 || variant < 0 || variant > 1)
+  if (B <= 0 || H <= 0 || W <= 0 || Cin % CK || Cin <= 0 || N % bn || N <= 0 || variant < 0 || variant > 2)
     return MLS_BAD_ARG;
   int th = 0, nb = 0;
-  if (!halo_geometry(B, H, W, &th, &nb)) return MLS_UNSUPPORTED;
+  const bool xl = variant == 2;
+  if (!halo_geometry(B, H, W, &th, &nb, xl ? XL_ROWS : MAX_ROWS, xl ? XL_PATCH : PATCH_MAX)) return MLS_UNSUPPORTED;
   const long xb = (long)B * H * W * Cin * 2, wb = (long)N * 9 * Cin * 2;
   if (xb >= 0x7fffffffL || wb >= 0x7fffffffL || (long)B * H * W * N >= 0x7fffffffL) return MLS_UNSUPPORTED;
   HaloArgs a;
@@ -394,7 +409,10 @@ int mls_conv3x3_halo(const void* x, const void* w, const float* bias, const void
   }();
   // (a 64-channel x 4-wave variant -- 4 x 4 MFMA tiles per wave, half the LDS reads per MFMA --
   // measured 15-25 % slower than <64, 8>: profiles/r1_halo_w4_probe.jsonl)
-  if (variant == 1) {
+  if (variant == 2) {
+    hipLaunchKernelGGL((conv3x3_halo_kernel<64, 8, true, XL_ROWS, XL_PATCH>), grid, dim3(512), 0, (hipStream_t)stream,
+                       a);
+  } else if (variant == 1) {
     if (rs) hipLaunchKernelGGL((conv3x3_halo_kernel<32, 4, true>), grid, dim3(256), 0, (hipStream_t)stream, a);
     else hipLaunchKernelGGL((conv3x3_halo_kernel<32, 4, false>), grid, dim3(256), 0, (hipStream_t)stream, a);
   } else {
@@ -407,6 +425,12 @@ int mls_conv3x3_halo(const void* x, const void* w, const float* bias, const void
 // The geometry the kernel would use (for tests / the tuner): returns 0 and fills th, nb.
 int mls_conv3x3_halo_geometry(int B, int H, int W, int* th, int* nb) {
   return halo_geometry(B, H, W, th, nb) ? 0 : MLS_UNSUPPORTED;
+}
+
+// ... for a given variant (2 = the 512-pixel XL tile)
+int mls_conv3x3_halo_geometry_v(int B, int H, int W, int variant, int* th, int* nb) {
+  const bool xl = variant == 2;
+  return halo_geometry(B, H, W, th, nb, xl ? XL_ROWS : MAX_ROWS, xl ? XL_PATCH : PATCH_MAX) ? 0 : MLS_UNSUPPORTED;
 }
 
 }  // extern "C"

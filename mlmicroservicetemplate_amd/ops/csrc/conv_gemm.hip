@@ -75,6 +75,12 @@ MLS_DEV void glds16(rsrc_t r, char* lds, int voff, int soff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS3 void*)lds, 16, voff, soff, 0, 0);
 }
 
+template <int N>
+MLS_DEV void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt field");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 // LDS chunk swizzle of a tile row: BK = 64 (128-B rows, 8 chunks): chunk ^ (row & 7);
 // BK = 32 (64-B rows, 4 chunks): chunk ^ f(row & 15), f = (r0 | r2 << 1) -- conflict-free for the
 // gfx950 ds_read_b128 lane groups over the MFMA fragment rows (checked exhaustively, 96 such linear
@@ -333,13 +339,14 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_kernel(const ConvArgs 
   const int fr = lane & 15, fq = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
     const int issued = (kt + STAGES - 1 < nk) ? kt + STAGES - 1 : nk;
-    const int ahead = issued - (kt + 1);  // stages still allowed in flight
-    if (STAGES >= 4 && ahead >= 2)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LPS) : "memory");
-    else if (ahead >= 1)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPS) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int ahead = issued - (kt + 1);  // stages still allowed in flight (<= STAGES - 2)
+    switch (ahead) {  // counted wait: stage kt landed, the younger `ahead` stages stay in flight
+      case 4: if constexpr (STAGES >= 6) { wait_vmcnt<4 * LPS>(); break; } [[fallthrough]];
+      case 3: if constexpr (STAGES >= 5) { wait_vmcnt<3 * LPS>(); break; } [[fallthrough]];
+      case 2: if constexpr (STAGES >= 4) { wait_vmcnt<2 * LPS>(); break; } [[fallthrough]];
+      case 1: wait_vmcnt<LPS>(); break;
+      default: wait_vmcnt<0>(); break;
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (kt + STAGES - 1 < nk && !(a.dbg & 4)) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
@@ -744,10 +751,14 @@ constexpr TileCfg kCfgs[] = {{0, 0, 0},       {128, 128, 256}, {128, 64, 256}, {
                              {64, 64, 256},   {128, 128, 512}, {64, 64, 256},  {128, 64, 512},
                              {64, 128, 512},  {64, 128, 512},  {128, 64, 512}, {64, 64, 256},
                              {128, 128, 512}, {128, 128, 512}, {128, 128, 512}, {64, 64, 256},
-                             {128, 64, 256},  {64, 128, 256},  {128, 128, 256}};
-constexpr int kNumCfgs = 19;
-// cfgs 13..18 stage K in 32-deep steps (BK = 32): not for the stem layout or the SiLU-mul epilogue
-constexpr bool cfg_bk32(int c) { return c >= 13 && c <= 18; }
+                             {128, 64, 256},  {64, 128, 256},  {128, 128, 256},
+                             // 19, 23..28: deep rings (3-4 stages in flight); 20..22 = persistent kernel
+                             {128, 128, 512}, {64, 64, 256},  {128, 64, 512}, {64, 128, 512},
+                             {128, 128, 512}, {64, 128, 256}, {128, 64, 256}, {64, 64, 256},
+                             {128, 128, 512}, {64, 128, 512}};
+constexpr int kNumCfgs = 29;
+// cfgs 13..19 and 23..26 stage K in 32-deep steps (BK = 32): not for the stem layout or the SiLU-mul epilogue
+constexpr bool cfg_bk32(int c) { return (c >= 13 && c <= 19) || (c >= 23 && c <= 26); }
 
 template <int MODE>
 void launch_mode(int cfg, dim3 grid, hipStream_t st, const ConvArgs& a) {
@@ -771,6 +782,14 @@ void launch_mode(int cfg, dim3 grid, hipStream_t st, const ConvArgs& a) {
     case 16: hipLaunchKernelGGL((conv_gemm_kernel<128, 64, 2, 2, 3, MODE, 32, 1>), grid, dim3(256), 0, st, a); break;
     case 17: hipLaunchKernelGGL((conv_gemm_kernel<64, 128, 2, 2, 3, MODE, 32, 1>), grid, dim3(256), 0, st, a); break;
     case 18: hipLaunchKernelGGL((conv_gemm_kernel<128, 128, 2, 2, 3, MODE, 32, 2>), grid, dim3(256), 0, st, a); break;
+    // deep rings: more K-steps of operands in flight per block (the latency-bound small-M layers)
+    case 19: hipLaunchKernelGGL((conv_gemm_kernel<128, 128, 4, 2, 4, MODE, 32, 2>), grid, dim3(512), 0, st, a); break;
+    case 23: hipLaunchKernelGGL((conv_gemm_kernel<128, 128, 4, 2, 5, MODE, 32, 2>), grid, dim3(512), 0, st, a); break;
+    case 24: hipLaunchKernelGGL((conv_gemm_kernel<64, 128, 2, 2, 4, MODE, 32, 1>), grid, dim3(256), 0, st, a); break;
+    case 25: hipLaunchKernelGGL((conv_gemm_kernel<128, 64, 2, 2, 4, MODE, 32, 1>), grid, dim3(256), 0, st, a); break;
+    case 26: hipLaunchKernelGGL((conv_gemm_kernel<64, 64, 2, 2, 5, MODE, 32, 1>), grid, dim3(256), 0, st, a); break;
+    case 27: hipLaunchKernelGGL((conv_gemm_kernel<128, 128, 4, 2, 4, MODE>), grid, dim3(512), 0, st, a); break;
+    case 28: hipLaunchKernelGGL((conv_gemm_kernel<64, 128, 2, 4, 4, MODE>), grid, dim3(512), 0, st, a); break;
     default: hipLaunchKernelGGL((conv_gemm_kernel<64, 64, 2, 2, 3, MODE>), grid, dim3(256), 0, st, a); break;
   }
 }

@@ -70,7 +70,7 @@ def test_conv_resnet_shapes(shape):
     res = torch.randn(B, ho, ho, cout, device=DEV).to(torch.bfloat16)
     ref = _conv_ref(x, w, bias, s, p, 1, res)
     ws = torch.empty(64 << 20, device=DEV, dtype=torch.float32)
-    for cfg in list(range(0, 19)) + [20, 21, 22]:
+    for cfg in list(range(0, 29)):
         out = ops.conv2d_nhwc(x, ops.pack_conv_weight(w), bias, kernel=k, stride=s, pad=p, residual=res, act=1,
                               workspace=ws, cfg=cfg)
         torch.cuda.synchronize()
@@ -92,7 +92,7 @@ def test_conv_stem():
     w = (torch.randn(64, 3, 7, 7, device=DEV) / 12.0).to(torch.bfloat16)
     bias = torch.randn(64, device=DEV)
     ref = _conv_ref(x4.to(torch.bfloat16)[..., :3], w, bias, 2, 3, 1)
-    for cfg in list(range(0, 19)) + [20, 21, 22]:
+    for cfg in list(range(0, 29)):
         out = ops.conv2d_nhwc(x4p, ops.pack_conv_weight(w), bias, kernel=7, stride=2, pad=0, act=1, cfg=cfg)
         assert out.shape == (B, 112, 112, 64)
         assert rel_err(out, ref) < 2e-2, f"cfg {cfg}"
@@ -114,7 +114,8 @@ def test_gemm(mnk, act):
     ref = {0: y, 1: torch.relu(y), 2: F.gelu(y), 3: torch.tanh(y), 4: F.silu(y)}[act]
     ws = torch.empty(16 << 20, device=DEV, dtype=torch.float32)
     for cfg, sk in ((0, 0), (1, 1), (4, 2), (2, 3), (5, 1), (6, 2), (7, 1), (8, 3), (13, 1), (14, 2), (15, 1),
-                    (16, 3), (17, 1), (18, 2), (20, 1), (21, 1), (22, 1)):
+                    (16, 3), (17, 1), (18, 2), (19, 1), (20, 1), (21, 1), (22, 1), (23, 2), (24, 1), (25, 3),
+                    (26, 1), (27, 2), (28, 1)):
         out = ops.gemm(a, w, bias, scale=scale, residual=res, act=act, workspace=ws, cfg=cfg, splitk=sk)
         assert rel_err(out, ref) < 2e-2, f"cfg {cfg} sk {sk}"
 
@@ -284,9 +285,10 @@ def test_conv3x3_halo_matches_reference(B, H, W, cin, cout, resid):
     bias = (torch.randn(cout, generator=g) * 0.1).to(DEV)
     res = torch.randn(B, H, W, cout, generator=g).to(DEV).to(torch.bfloat16) if resid else None
     assert ops.conv3x3_halo_geometry(B, H, W) is not None
+    assert ops.conv3x3_halo_geometry(B, H, W, variant=2) is not None
     ref = _conv_ref(x, w, bias, 1, 1, 1, res)
     ws = torch.empty(4 * B * H * W * cout, device=DEV, dtype=torch.float32)
-    for variant, sk in ((1, 1), (0, 1), (0, 2), (0, 4)):
+    for variant, sk in ((1, 1), (0, 1), (0, 2), (0, 4), (2, 1), (2, 2), (2, 4)):
         if (cin // 32) % sk:
             continue
         for _ in range(2):  # the second launch checks the split-K counters were left at zero
