@@ -329,6 +329,8 @@ class ResNet50Fused:
         self.chain = os.environ.get("MLS_CHAIN", "1") != "0"
         # block names whose conv3 is NOT chained (A/B: MLS_CHAIN_SKIP=layer1.2,layer2.1)
         self.chain_skip: set = {b for b in os.environ.get("MLS_CHAIN_SKIP", "").split(",") if b}
+        if os.environ.get("MLS_CHAIN_L2_CW"):  # A/B: layer2 boundaries' chunk width (64 / 32)
+            ops.set_chain_l2_cw(int(os.environ["MLS_CHAIN_L2_CW"]))
         # normalise + stem + max pool as one kernel (csrc/stem_pool.hip); MLS_FUSED_STEM=0 -> 3 kernels
         self.fuse_stem = image_size == 224 and os.environ.get("MLS_FUSED_STEM", "1") != "0"
         self.fc_w = params["fc.w"].to(device=self.device, dtype=torch.bfloat16).contiguous()
@@ -400,8 +402,6 @@ class ResNet50Fused:
                                     pad=s.pad if pad is None else pad,
                                     residual=residual, act=act, workspace=self.workspace, cfg=cfg, splitk=sk)
 
-    # (K of the conv3 GEMM, N1, N2) shapes csrc/conv_chain.hip is built for
-    CHAIN_SHAPES = ((64, 256, 64), (128, 256, 64), (64, 256, 128), (128, 512, 128))
 
     def _chained(self, p: str, nxt: str, dual: bool) -> bool:
         """Run block ``p``'s conv3 together with block ``nxt``'s conv1 (ops.conv1x1_chain)?"""
@@ -410,7 +410,7 @@ class ResNet50Fused:
         c3 = self.specs[p + ".conv3"]
         k = c3.cin + (self.specs[p + ".down"].cin if dual else 0)
         c1 = self.specs[nxt + ".conv1"]
-        return c1.k == 1 and c1.stride == 1 and (k, c3.cout, c1.cout) in self.CHAIN_SHAPES
+        return c1.k == 1 and c1.stride == 1 and (k, c3.cout, c1.cout) in self.ops.CHAIN_SHAPES
 
     def forward(self, images_u8_nhwc: torch.Tensor) -> torch.Tensor:
         """uint8 ``[B,H,W,3]`` on device -> bf16 logits ``[B, num_classes]``."""

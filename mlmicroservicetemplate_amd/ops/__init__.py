@@ -194,6 +194,15 @@ def conv1x1_dual(y: torch.Tensor, x: torch.Tensor, w_cat: torch.Tensor, bias: Op
     return out
 
 
+# (K of the conv3 GEMM, N1, N2) csrc/conv_chain.hip is instantiated for
+CHAIN_SHAPES = ((64, 256, 64), (128, 256, 64), (64, 256, 128), (128, 512, 128), (128, 512, 256), (256, 1024, 256))
+
+
+def set_chain_l2_cw(cw: int) -> None:
+    """A/B: output-channel chunk width of the layer2 chain boundaries (64 default, or 32)."""
+    lib().mls_chain_set_l2_cw(int(cw))
+
+
 def conv1x1_chain(a1: torch.Tensor, w3: torch.Tensor, b3: Optional[torch.Tensor], w1: torch.Tensor,
                   b1: Optional[torch.Tensor], *, residual: Optional[torch.Tensor] = None,
                   a2: Optional[torch.Tensor] = None, stride2: int = 1,
@@ -202,8 +211,8 @@ def conv1x1_chain(a1: torch.Tensor, w3: torch.Tensor, b3: Optional[torch.Tensor]
     ``y = relu(conv1x1([a1 | a2 at stride2], w3) + b3 (+ residual))`` and
     ``t1 = relu(conv1x1(y, w1) + b1)``; y never makes an HBM round trip.  Returns ``(y, t1)``.
     ``w3`` is ``[N1][Ka (+ Kb)]`` (the dual concatenation when ``a2`` is given; no residual then),
-    ``w1`` ``[N2][N1]``.  Supported (Ka + Kb, N1, N2): (64, 256, 64), (128, 256, 64),
-    (64, 256, 128), (128, 512, 128) -- ResNet-50 layer1 / layer2 boundaries."""
+    ``w1`` ``[N2][N1]``.  Supported (Ka + Kb, N1, N2): CHAIN_SHAPES -- the ResNet-50 layer1,
+    layer2 and layer3 boundaries."""
     dev = a1.device
     _need(a1, "a1", torch.bfloat16, dev)
     _need(w3, "w3", torch.bfloat16, dev)
@@ -221,7 +230,7 @@ def conv1x1_chain(a1: torch.Tensor, w3: torch.Tensor, b3: Optional[torch.Tensor]
         H2 = W2 = Kb = 0
     if w3.reshape(N1, -1).shape[1] != Ka + Kb or w1.reshape(N2, -1).shape[1] != N1:
         raise ValueError("conv1x1_chain: weight shapes do not chain")
-    if (Ka + Kb, N1, N2) not in ((64, 256, 64), (128, 256, 64), (64, 256, 128), (128, 512, 128)):
+    if (Ka + Kb, N1, N2) not in CHAIN_SHAPES:
         raise ValueError(f"conv1x1_chain: unsupported shape (K {Ka + Kb}, N1 {N1}, N2 {N2})")
     for name, t, n in (("b3", b3, N1), ("b1", b1, N2)):
         if t is not None:

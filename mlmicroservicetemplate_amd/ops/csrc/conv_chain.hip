@@ -52,34 +52,49 @@ struct ChainArgs {
   uint32_t a1_bytes, a2_bytes, w3_bytes, res_bytes, y_bytes, w1_bytes, t1_bytes;
 };
 
-// KS = (Ka + Kb) / 64 A1 slabs; KSA = Ka / 64 of them from a1, the rest from a2 (dual).  N1 is a
-// template parameter so the chunk loop unrolls and every bias lives in registers, loaded before the
-// first LDS-DMA: a plain global load consumed beside in-flight DMA makes hipcc wait vmcnt(0) and
-// drain the ring (cdna_hip_programming.md §5, "Projection GEMM" item 4(b)).
-// OCC = waves per SIMD the register allocation must allow: 4 where the LDS footprint lets two
-// blocks share a CU (<= 80 KB), else 2.
-template <int BM, int KS, int N1, int N2, int OCC>
+// 16-B chunk swizzle of an LDS image row: 128-B rows (8 chunks): chunk ^ (r & 7); 64-B rows (4
+// chunks): chunk ^ f(r & 7), f = (r0 | r2 << 1) -- conflict-free for the 16x16x32 fragment reads
+// (conv_gemm.hip row_swz).  The LDS-DMA writes lane-linearly, so the swizzle goes on the SOURCE.
+template <int CPR>
+MLS_DEV int row_swz(int r) {
+  if constexpr (CPR == 8) return r & 7;
+  else return (r & 1) | ((r >> 1) & 2);
+}
+
+// KS = (Ka + Kb) / 64 A1 slabs; KSA = Ka / 64 of them from a1, the rest from a2 (dual).  CW = the
+// output-channel chunk of GEMM1 = the K slab of GEMM2 (64, or 32 where the weights of a 64-wide
+// stage would not fit the LDS next to the A tile: layer2 -> 3 and layer3).  N1 is a template
+// parameter so the chunk loop unrolls and every bias lives in registers, loaded before the first
+// LDS-DMA: a plain global load consumed beside in-flight DMA makes hipcc wait vmcnt(0) and drain
+// the ring (cdna_hip_programming.md §5, "Projection GEMM" item 4(b)).  OCC = waves per SIMD the
+// register allocation must allow: 4 where the LDS footprint lets two blocks share a CU (<= 80 KB).
+template <int BM, int KS, int N1, int N2, int CW, int OCC>
 __global__ __launch_bounds__(512, OCC) void conv_chain_kernel(const ChainArgs a) {
   constexpr int NW = 8, NT = 512, WM = 4, WN = 2;
   constexpr int WTM = BM / WM, TM = WTM / 16;  // GEMM1 / GEMM2 wave rows
-  constexpr int TN = 2;                        // GEMM1: 64-wide chunk / WN / 16
+  constexpr int TN = CW / WN / 16;             // GEMM1 column fragments per wave
   constexpr int TN2 = N2 / WN / 16;            // GEMM2 column fragments per wave
+  constexpr int CPR = CW / 8;                  // 16-B chunks per row of the W1 / residual / y images
+  constexpr int RPP = 64 / CPR;                // rows of those images per 1-KiB DMA piece
   constexpr int A1_BYTES = BM * KS * 128;
-  constexpr int W3_BYTES = 64 * KS * 128;
-  constexpr int W1_BYTES = N2 * 128;
-  constexpr int R_BYTES = BM * 128;
+  constexpr int W3_BYTES = CW * KS * 128;
+  constexpr int W1_BYTES = N2 * CW * 2;
+  constexpr int R_BYTES = BM * CW * 2;
   constexpr int STAGE = W3_BYTES + W1_BYTES + R_BYTES;
   constexpr int EPI_BYTES = BM * N2 * 2;
   constexpr int RING = A1_BYTES + 2 * STAGE;
   constexpr int LDS_BYTES = RING > EPI_BYTES ? RING : EPI_BYTES;
   constexpr int A1_PW = BM / 8 * KS / NW;  // 1-KiB DMA pieces per wave
-  constexpr int W3_PW = KS;                // 8 * KS pieces / 8 waves
-  constexpr int W1_PW = N2 / 64;
-  constexpr int R_PW = BM / 64;
-  constexpr int Y_ST = BM * 8 / NT;       // 16-B y stores per thread per chunk
+  constexpr int W3_PW = CW / 8 * KS / NW;
+  constexpr int W1_PW = N2 / RPP / NW;
+  constexpr int R_PW = BM / RPP / NW;
+  constexpr int Y_ST = BM * CPR / NT;     // 16-B y stores per thread per chunk
   constexpr int T_ST = BM * N2 / 8 / NT;  // 16-B t1 stores per thread
-  static_assert(TM >= 1 && TN2 >= 1 && A1_PW * NW * 8 == BM * KS && R_PW * NW * 8 == BM, "tile");
-  static_assert(Y_ST * NT == BM * 8 && T_ST * NT == BM * N2 / 8, "epilogue split");
+  constexpr int NJ = N1 / CW;
+  static_assert(TM >= 1 && TN >= 1 && TN2 >= 1 && (CW == 64 || CW == 32), "tile");
+  static_assert(A1_PW * NW * 8 == BM * KS && W3_PW * NW * 8 == CW * KS, "A1 / W3 DMA split");
+  static_assert(W1_PW * NW * RPP == N2 && R_PW * NW * RPP == BM, "W1 / residual DMA split");
+  static_assert(Y_ST * NT == BM * CPR && T_ST * NT == BM * N2 / 8, "epilogue split");
   static_assert(LDS_BYTES <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
 
@@ -89,7 +104,6 @@ __global__ __launch_bounds__(512, OCC) void conv_chain_kernel(const ChainArgs a)
   const int fr = lane & 15, fq = lane >> 4;
   const int m0 = xcd_remap(blockIdx.x, gridDim.x) * BM;
   const int K1 = a.Ka + a.Kb, KSA = a.Ka / 64;
-  constexpr int NJ = N1 / 64;
   const bool has_res = a.res != nullptr;
 
   // biases of every column this lane touches, before any DMA is in flight
@@ -97,13 +111,14 @@ __global__ __launch_bounds__(512, OCC) void conv_chain_kernel(const ChainArgs a)
 #pragma unroll
   for (int j = 0; j < NJ; ++j)
 #pragma unroll
-    for (int jn = 0; jn < TN; ++jn) b3v[j][jn] = a.b3 ? a.b3[j * 64 + wn * 32 + jn * 16 + fr] : 0.f;
+    for (int jn = 0; jn < TN; ++jn) b3v[j][jn] = a.b3 ? a.b3[j * CW + wn * (CW / 2) + jn * 16 + fr] : 0.f;
 #pragma unroll
   for (int jn = 0; jn < TN2; ++jn) b1v[jn] = a.b1 ? a.b1[wn * (N2 / 2) + jn * 16 + fr] : 0.f;
 
-  // DMA lane geometry: 8 rows x 8 chunks per 1-KiB piece; LDS chunk (lane & 7) of row r holds the
-  // logical chunk (lane & 7) ^ (r & 7)
+  // DMA lane geometry.  128-B rows (A1, W3): 8 rows x 8 chunks per piece; CW-wide rows (W1,
+  // residual): RPP rows x CPR chunks.  LDS chunk c of row r holds the logical chunk c ^ swz(r).
   const int r8 = lane >> 3, lc = (lane & 7) ^ r8;
+  const int rq = lane / CPR, lq = (lane % CPR) ^ row_swz<CPR>(rq);
 
   const rsrc_t a1r = make_rsrc(a.a1, a.a1_bytes);
   const rsrc_t a2r = make_rsrc(a.a2, a.a2_bytes);
@@ -142,22 +157,22 @@ __global__ __launch_bounds__(512, OCC) void conv_chain_kernel(const ChainArgs a)
     char* sW1 = sW3 + W3_BYTES;
     char* sR = sW1 + W1_BYTES;
 #pragma unroll
-    for (int i = 0; i < W3_PW; ++i) {  // W3 rows j*64 + rb*8 + r8, K slab s
+    for (int i = 0; i < W3_PW; ++i) {  // W3 rows j*CW + rb*8 + r8 of K slab s ([KS][CW][64] image)
       const int q = wid * W3_PW + i;
-      const int s = q >> 3, rb = q & 7;
-      glds16(w3r, sW3 + q * 1024, ((j * 64 + rb * 8 + r8) * K1 + s * 64 + lc * 8) * 2, 0);
+      const int s = q / (CW / 8), rb = q - s * (CW / 8);
+      glds16(w3r, sW3 + q * 1024, ((j * CW + rb * 8 + r8) * K1 + s * 64 + lc * 8) * 2, 0);
     }
 #pragma unroll
-    for (int i = 0; i < W1_PW; ++i) {  // W1 rows n2 = q*8 + r8, columns j*64..
+    for (int i = 0; i < W1_PW; ++i) {  // W1 rows n2 = q*RPP + rq, columns j*CW..
       const int q = wid * W1_PW + i;
-      glds16(w1r, sW1 + q * 1024, ((q * 8 + r8) * N1 + j * 64 + lc * 8) * 2, 0);
+      glds16(w1r, sW1 + q * 1024, ((q * RPP + rq) * N1 + j * CW + lq * 8) * 2, 0);
     }
     if (has_res) {
 #pragma unroll
       for (int i = 0; i < R_PW; ++i) {
         const int q = wid * R_PW + i;
-        const int m = m0 + q * 8 + r8;
-        glds16(rr, sR + q * 1024, m < a.M ? (m * N1 + j * 64 + lc * 8) * 2 : OOB, 0);
+        const int m = m0 + q * RPP + rq;
+        glds16(rr, sR + q * 1024, m < a.M ? (m * N1 + j * CW + lq * 8) * 2 : OOB, 0);
       }
     }
   };
@@ -191,7 +206,7 @@ __global__ __launch_bounds__(512, OCC) void conv_chain_kernel(const ChainArgs a)
     char* sW1 = sW3 + W3_BYTES;
     char* sR = sW1 + W1_BYTES;
 
-    // ---- GEMM1: acc1[BM x 64] = A1 . W3_j^T
+    // ---- GEMM1: acc1[BM x CW] = A1 . W3_j^T
     f32x4 acc1[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -210,8 +225,8 @@ __global__ __launch_bounds__(512, OCC) void conv_chain_kernel(const ChainArgs a)
       }
 #pragma unroll
       for (int jn = 0; jn < TN; ++jn) {
-        const int n = wn * 32 + jn * 16 + fr;
-        bfv[jn] = __builtin_bit_cast(bf16x8, W3s[s * 512 + n * 8 + (ch ^ (n & 7))]);
+        const int n = wn * (CW / 2) + jn * 16 + fr;
+        bfv[jn] = __builtin_bit_cast(bf16x8, W3s[s * CW * 8 + n * 8 + (ch ^ (n & 7))]);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -223,14 +238,15 @@ __global__ __launch_bounds__(512, OCC) void conv_chain_kernel(const ChainArgs a)
     // ---- pass 1: y = relu(acc1 + b3 (+ res)) -> bf16, in place over the residual chunk
 #pragma unroll
     for (int jn = 0; jn < TN; ++jn) {
-      const int col = wn * 32 + jn * 16 + fr;
+      const int col = wn * (CW / 2) + jn * 16 + fr;
       const float bb = b3v[j][jn];
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = wm * WTM + i * 16 + fq * 4 + r;
-          bf16* p = reinterpret_cast<bf16*>(sR + row * 128 + ((((col >> 3) ^ (row & 7))) << 4) + (col & 7) * 2);
+          bf16* p = reinterpret_cast<bf16*>(sR + row * (CW * 2) + (((col >> 3) ^ row_swz<CPR>(row)) << 4) +
+                                            (col & 7) * 2);
           const float e = acc1[i][jn][r];  // through a named float (ext-vector element bit-cast hazard)
           float v = e + bb;
           if (has_res) v += (float)*p;
@@ -244,29 +260,29 @@ __global__ __launch_bounds__(512, OCC) void conv_chain_kernel(const ChainArgs a)
 #pragma unroll
     for (int it = 0; it < Y_ST; ++it) {
       const int q = tid + it * NT;
-      const int row = q >> 3, c = q & 7;
-      const uint4 v = *reinterpret_cast<const uint4*>(sR + row * 128 + ((c ^ (row & 7)) << 4));
+      const int row = q / CPR, c = q % CPR;
+      const uint4 v = *reinterpret_cast<const uint4*>(sR + row * (CW * 2) + ((c ^ row_swz<CPR>(row)) << 4));
       const int m = m0 + row;
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), yr,
-                                             m < a.M ? (m * N1 + j * 64 + c * 8) * 2 : OOB, 0, 0);
+                                             m < a.M ? (m * N1 + j * CW + c * 8) * 2 : OOB, 0, 0);
     }
 
     // ---- GEMM2: acc2[BM x N2] += y_j . W1_j^T
     const uint4* Ys = reinterpret_cast<const uint4*>(sR);
     const uint4* W1s = reinterpret_cast<const uint4*>(sW1);
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int kk = 0; kk < CW / 32; ++kk) {
       const int ch = fq + 4 * kk;
       bf16x8 af[TM], bfv[TN2];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int r = wm * WTM + i * 16 + fr;
-        af[i] = __builtin_bit_cast(bf16x8, Ys[r * 8 + (ch ^ (r & 7))]);
+        af[i] = __builtin_bit_cast(bf16x8, Ys[r * CPR + (ch ^ row_swz<CPR>(r))]);
       }
 #pragma unroll
       for (int jn = 0; jn < TN2; ++jn) {
         const int n = wn * (N2 / 2) + jn * 16 + fr;
-        bfv[jn] = __builtin_bit_cast(bf16x8, W1s[n * 8 + (ch ^ (n & 7))]);
+        bfv[jn] = __builtin_bit_cast(bf16x8, W1s[n * CPR + (ch ^ row_swz<CPR>(n))]);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -279,7 +295,7 @@ __global__ __launch_bounds__(512, OCC) void conv_chain_kernel(const ChainArgs a)
   // ---- epilogue: t1 = relu(acc2 + b1) -> bf16 tile in LDS -> 16-B stores
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();  // every wave is done reading the ring
-  constexpr int CPR = N2 / 8;    // 16-B chunks per t1 row
+  constexpr int TPR = N2 / 8;    // 16-B chunks per t1 row
   bf16* to = reinterpret_cast<bf16*>(smem);
 #pragma unroll
   for (int jn = 0; jn < TN2; ++jn) {
@@ -291,7 +307,7 @@ __global__ __launch_bounds__(512, OCC) void conv_chain_kernel(const ChainArgs a)
       for (int r = 0; r < 4; ++r) {
         const int row = wm * WTM + i * 16 + fq * 4 + r;
         const float e = acc2[i][jn][r];
-        // chunk swizzle by row (CPR >= 8) keeps the 16-lane column groups on distinct banks
+        // chunk swizzle by row (TPR >= 8) keeps the 16-lane column groups on distinct banks
         to[row * N2 + ((((col >> 3) ^ (row & 7))) << 3) + (col & 7)] = (bf16)fmaxf(e + bb, 0.f);
       }
   }
@@ -300,7 +316,7 @@ __global__ __launch_bounds__(512, OCC) void conv_chain_kernel(const ChainArgs a)
 #pragma unroll
   for (int it = 0; it < T_ST; ++it) {
     const int q = tid + it * NT;
-    const int row = q / CPR, c = q - (q / CPR) * CPR;
+    const int row = q / TPR, c = q - (q / TPR) * TPR;
     const uint4 v = *reinterpret_cast<const uint4*>(to + row * N2 + ((c ^ (row & 7)) << 3));
     const int m = m0 + row;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), tr, m < a.M ? (m * a.N2 + c * 8) * 2 : OOB,
@@ -308,20 +324,24 @@ __global__ __launch_bounds__(512, OCC) void conv_chain_kernel(const ChainArgs a)
   }
 }
 
-// The ResNet-50 boundaries (BM = 128):  KS N1  N2
-//   layer1.0 (dual) -> layer1.1            2  256  64
-//   layer1.1 -> layer1.2                    1  256  64
-//   layer1.2 -> layer2.0                    1  256 128
-//   layer2.1 -> 2.2, 2.2 -> 2.3             2  512 128
-template <int KS, int N1, int N2>
+// The ResNet-50 boundaries (BM = 128):          KS   N1   N2  CW
+//   layer1.0 (dual) -> layer1.1                  2   256   64  64
+//   layer1.1 -> layer1.2                         1   256   64  64
+//   layer1.2 -> layer2.0                         1   256  128  64
+//   layer2.1 -> 2.2, 2.2 -> 2.3                  2   512  128  64 (or 32: 80 KB, two blocks per CU)
+//   layer2.3 -> layer3.0                         2   512  256  32
+//   layer3.1 -> 3.2 ... layer3.4 -> 3.5          4  1024  256  32
+template <int KS, int N1, int N2, int CW>
 int launch_chain(const ChainArgs& a, hipStream_t st) {
   constexpr int BM = 128;
-  constexpr int LDS = BM * KS * 128 + 2 * (64 * KS * 128 + N2 * 128 + BM * 128);
+  constexpr int LDS = BM * KS * 128 + 2 * (CW * KS * 128 + N2 * CW * 2 + BM * CW * 2);
   constexpr int OCC = LDS <= 80 * 1024 ? 4 : 2;
-  hipLaunchKernelGGL((conv_chain_kernel<BM, KS, N1, N2, OCC>), dim3((unsigned)((a.M + BM - 1) / BM)), dim3(512), 0,
-                     st, a);
+  hipLaunchKernelGGL((conv_chain_kernel<BM, KS, N1, N2, CW, OCC>), dim3((unsigned)((a.M + BM - 1) / BM)), dim3(512),
+                     0, st, a);
   return (int)hipGetLastError();
 }
+
+int g_chain_cw_l2 = 0;  // layer2 chunk width override (0 = default 64; mls_chain_set_l2_cw for A/B)
 
 }  // namespace
 
@@ -330,7 +350,8 @@ extern "C" {
 // y = relu(conv1x1([a1 | a2 strided]) + b3 (+ res)); t1 = relu(conv1x1(y, w1) + b1).
 // a1 [M][Ka] (M = B*Ho*Wo), a2 [B][H2][W2][Kb] sampled at stride2 (Kb = 0: none), w3 [N1][Ka+Kb],
 // res [M][N1] or null, w1 [N2][N1]; y [M][N1], t1 [M][N2].  (KS = (Ka + Kb) / 64, N1, N2) one of
-// (1, 256, 64), (2, 256, 64), (1, 256, 128), (2, 512, 128); anything else MLS_UNSUPPORTED.
+// (1, 256, 64), (2, 256, 64), (1, 256, 128), (2, 512, 128), (2, 512, 256), (4, 1024, 256);
+// anything else MLS_UNSUPPORTED.
 int mls_conv_chain(const void* a1, const void* a2, const void* w3, const float* b3, const void* res, void* y,
                    const void* w1, const float* b1, void* t1, int B, int Ho, int Wo, int Ka, int H2, int W2, int Kb,
                    int stride2, int N1, int N2, void* stream) {
@@ -367,12 +388,19 @@ int mls_conv_chain(const void* a1, const void* a2, const void* w3, const float* 
   a.t1_bytes = (uint32_t)sizes[6];
   const hipStream_t st = (hipStream_t)stream;
   const int ks = (Ka + Kb) / 64;
-  if (ks == 1 && N1 == 256 && N2 == 64) return launch_chain<1, 256, 64>(a, st);
-  if (ks == 2 && N1 == 256 && N2 == 64) return launch_chain<2, 256, 64>(a, st);
-  if (ks == 1 && N1 == 256 && N2 == 128) return launch_chain<1, 256, 128>(a, st);
-  if (ks == 2 && N1 == 512 && N2 == 128) return launch_chain<2, 512, 128>(a, st);
+  if (ks == 1 && N1 == 256 && N2 == 64) return launch_chain<1, 256, 64, 64>(a, st);
+  if (ks == 2 && N1 == 256 && N2 == 64) return launch_chain<2, 256, 64, 64>(a, st);
+  if (ks == 1 && N1 == 256 && N2 == 128) return launch_chain<1, 256, 128, 64>(a, st);
+  if (ks == 2 && N1 == 512 && N2 == 128)
+    return g_chain_cw_l2 == 32 ? launch_chain<2, 512, 128, 32>(a, st) : launch_chain<2, 512, 128, 64>(a, st);
+  if (ks == 2 && N1 == 512 && N2 == 256) return launch_chain<2, 512, 256, 32>(a, st);
+  if (ks == 4 && N1 == 1024 && N2 == 256) return launch_chain<4, 1024, 256, 32>(a, st);
   return MLS_UNSUPPORTED;
 }
+
+// A/B switch for the layer2 boundaries' chunk width (64 = 128 KB of LDS, one block per CU; 32 =
+// 80 KB, two per CU).
+void mls_chain_set_l2_cw(int cw) { g_chain_cw_l2 = (cw == 32 || cw == 64) ? cw : 0; }
 
 }  // extern "C"
 

@@ -27,7 +27,7 @@ def _rand(*shape, scale=1.0):
 
 # (B, H, K, N1, N2): layer1 / layer2 boundaries at small batch, plus M tails (M % 128 != 0)
 SHAPES = [(2, 56, 64, 256, 64), (2, 56, 64, 256, 128), (2, 28, 128, 512, 128), (3, 9, 64, 256, 64),
-          (1, 7, 128, 512, 128)]
+          (1, 7, 128, 512, 128), (2, 28, 128, 512, 256), (2, 14, 256, 1024, 256), (3, 7, 256, 1024, 256)]
 
 
 @pytest.mark.parametrize("shape", SHAPES, ids=lambda s: "x".join(map(str, s)))
@@ -77,12 +77,33 @@ def test_chain_dual_downsample(stride2, H2):
     assert rel_err(y, y2) < 1e-2
 
 
+@pytest.mark.parametrize("cw", [32, 64])
+def test_chain_layer2_chunk_widths(cw):
+    """Both instantiations of the layer2 boundary (64-wide stages, one block per CU; 32-wide,
+    two per CU) compute the same y / t1."""
+    from mlmicroservicetemplate_amd import ops
+
+    B, H, K, N1, N2 = 2, 28, 128, 512, 128
+    torch.manual_seed(cw)
+    t2, res = torch.relu(_rand(B, H, H, K)), _rand(B, H, H, N1)
+    w3, w1 = _rand(N1, K, scale=K**-0.5), _rand(N2, N1, scale=N1**-0.5)
+    b3, b1 = torch.randn(N1, device=DEV) * 0.1, torch.randn(N2, device=DEV) * 0.1
+    try:
+        ops.set_chain_l2_cw(cw)
+        y, t1 = ops.conv1x1_chain(t2, w3, b3, w1, b1, residual=res)
+    finally:
+        ops.set_chain_l2_cw(0)
+    y_ref = torch.relu(t2.float() @ w3.float().T + b3 + res.float())
+    t1_ref = torch.relu(y_ref.to(torch.bfloat16).float() @ w1.float().T + b1)
+    assert rel_err(y, y_ref) < 1e-2 and rel_err(t1, t1_ref) < 2e-2
+
+
 def test_chain_rejects_unsupported_shapes():
     from mlmicroservicetemplate_amd import ops
 
-    t2 = _rand(1, 7, 7, 256)
-    with pytest.raises(ValueError):
-        ops.conv1x1_chain(t2, _rand(1024, 256), None, _rand(256, 1024), None, residual=_rand(1, 7, 7, 1024))
+    t2 = _rand(1, 7, 7, 512)
+    with pytest.raises(ValueError):  # a layer4 boundary: not instantiated
+        ops.conv1x1_chain(t2, _rand(2048, 512), None, _rand(512, 2048), None, residual=_rand(1, 7, 7, 2048))
 
 
 def test_resnet50_chain_matches_unchained():
