@@ -152,7 +152,12 @@ def test_reload_two_ranks_broadcasts_to_every_rank(frontend):
                 time.sleep(0.2)
         assert ready
         key = {"api_key": "k"}
-        r = requests.post(url + "/admin/reload", json={"seed": 7}, headers=key, timeout=60)
+        # /status answered by one rank does not mean the other (sharing the port) is ready yet
+        for _ in range(150):
+            r = requests.post(url + "/admin/reload", json={"seed": 7}, headers=key, timeout=60)
+            if r.status_code != 503:
+                break
+            time.sleep(0.2)
         assert r.status_code == 200, r.text
         assert r.json()["result"]["ranks"] == 2
         # two reloads racing (fresh connections may land on different ranks): the ranks must stay
