@@ -329,6 +329,9 @@ class ResNet50Fused:
         self.chain = os.environ.get("MLS_CHAIN", "1") != "0"
         # block names whose conv3 is NOT chained (A/B: MLS_CHAIN_SKIP=layer1.2,layer2.1)
         self.chain_skip: set = {b for b in os.environ.get("MLS_CHAIN_SKIP", "").split(",") if b}
+        # layer3 boundaries (K 256, N1 1024, N2 256): instantiated and tested, off by default --
+        # interleaved A/B 51.3k vs 52.2k req/s with them (profiles/r2_chain_v2_ab.jsonl)
+        self.chain_l3 = os.environ.get("MLS_CHAIN_L3", "0") == "1"
         if os.environ.get("MLS_CHAIN_L2_CW"):  # A/B: layer2 boundaries' chunk width (64 / 32)
             ops.set_chain_l2_cw(int(os.environ["MLS_CHAIN_L2_CW"]))
         # normalise + stem + max pool as one kernel (csrc/stem_pool.hip); MLS_FUSED_STEM=0 -> 3 kernels
@@ -410,7 +413,10 @@ class ResNet50Fused:
         c3 = self.specs[p + ".conv3"]
         k = c3.cin + (self.specs[p + ".down"].cin if dual else 0)
         c1 = self.specs[nxt + ".conv1"]
-        return c1.k == 1 and c1.stride == 1 and (k, c3.cout, c1.cout) in self.ops.CHAIN_SHAPES
+        shape = (k, c3.cout, c1.cout)
+        if shape == (256, 1024, 256) and not self.chain_l3:
+            return False  # layer3: 49 tiles re-reading 1 MB of weights each -- measured slower (-3 %)
+        return c1.k == 1 and c1.stride == 1 and shape in self.ops.CHAIN_SHAPES
 
     def forward(self, images_u8_nhwc: torch.Tensor) -> torch.Tensor:
         """uint8 ``[B,H,W,3]`` on device -> bf16 logits ``[B, num_classes]``."""
