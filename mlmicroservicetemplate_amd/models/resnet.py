@@ -336,6 +336,9 @@ class ResNet50Fused:
             ops.set_chain_l2_cw(int(os.environ["MLS_CHAIN_L2_CW"]))
         # normalise + stem + max pool as one kernel (csrc/stem_pool.hip); MLS_FUSED_STEM=0 -> 3 kernels
         self.fuse_stem = image_size == 224 and os.environ.get("MLS_FUSED_STEM", "1") != "0"
+        # ... with layer1.0's 1x1 conv on the pooled tiles in the same kernel: tested, measured level
+        # (51.3k vs 51.5k req/s, profiles/r2_stem_conv1_ab.jsonl), so opt-in (MLS_STEM_CONV1=1)
+        self.fuse_stem_conv1 = os.environ.get("MLS_STEM_CONV1", "0") == "1"
         self.fc_w = params["fc.w"].to(device=self.device, dtype=torch.bfloat16).contiguous()
         self.fc_b = params["fc.b"].to(device=self.device, dtype=torch.float32).contiguous()
         self.num_classes = self.fc_w.shape[0]
@@ -424,14 +427,18 @@ class ResNet50Fused:
         B = images_u8_nhwc.shape[0]
         if B > self.max_batch:
             raise ValueError(f"batch {B} > max_batch {self.max_batch}")
-        if self.fuse_stem:
-            x = ops.stem_pool_u8(images_u8_nhwc, self.w["stem"], self.b["stem"], self.mean, self.std)
+        if self.fuse_stem and self.fuse_stem_conv1:  # + layer1.0.conv1 on each pooled tile
+            x, t1 = ops.stem_pool_u8(images_u8_nhwc, self.w["stem"], self.b["stem"], self.mean, self.std,
+                                     conv1_w=self.w["layer1.0.conv1"], conv1_b=self.b["layer1.0.conv1"])
         else:
-            x = ops.normalize_u8(images_u8_nhwc, self.mean, self.std, pad=3)  # zero border = stem padding
-            x = self._conv(x, "stem", ops.ACT_RELU, pad=0)
-            x = ops.maxpool2d_nhwc(x, 3, 2, 1)
+            if self.fuse_stem:
+                x = ops.stem_pool_u8(images_u8_nhwc, self.w["stem"], self.b["stem"], self.mean, self.std)
+            else:
+                x = ops.normalize_u8(images_u8_nhwc, self.mean, self.std, pad=3)  # zero border = stem padding
+                x = self._conv(x, "stem", ops.ACT_RELU, pad=0)
+                x = ops.maxpool2d_nhwc(x, 3, 2, 1)
+            t1 = self._conv(x, "layer1.0.conv1", ops.ACT_RELU)
         blocks = [(si, bi) for si, (nblocks, _m, _c, _s) in enumerate(STAGES) for bi in range(nblocks)]
-        t1 = self._conv(x, "layer1.0.conv1", ops.ACT_RELU)
         for idx, (si, bi) in enumerate(blocks):
             p = f"layer{si + 1}.{bi}"
             nxt = f"layer{blocks[idx + 1][0] + 1}.{blocks[idx + 1][1]}" if idx + 1 < len(blocks) else None

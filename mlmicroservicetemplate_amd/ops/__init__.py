@@ -461,10 +461,13 @@ def normalize_u8(images: torch.Tensor, mean, std, pad: int = 0, out: Optional[to
 
 
 def stem_pool_u8(images: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, mean, std,
-                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 out: Optional[torch.Tensor] = None, conv1_w: Optional[torch.Tensor] = None,
+                 conv1_b: Optional[torch.Tensor] = None):
     """ResNet input block in one kernel: uint8 ``[B,224,224,3]`` -> normalise -> 7x7/2 conv
     (packed ``[64,7,8,4]`` weights, BN folded) + bias -> ReLU -> 3x3/2 max pool -> bf16
-    ``[B,56,56,64]`` (csrc/stem_pool.hip)."""
+    ``[B,56,56,64]`` (csrc/stem_pool.hip).  With ``conv1_w`` (``[64, 64]`` or ``[64,1,1,64]``, BN
+    folded) / ``conv1_b`` the first bottleneck's 1x1 conv + ReLU runs on each pooled tile in the
+    same kernel and ``(pooled, t1)`` is returned."""
     dev = images.device
     _need(images, "images", torch.uint8, dev)
     _need(w, "w", torch.bfloat16, dev)
@@ -481,9 +484,22 @@ def stem_pool_u8(images: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, mean
             raise ValueError(f"out must be {shape}")
     m = (ctypes.c_float * 3)(*[float(v) for v in mean])
     s = (ctypes.c_float * 3)(*[float(v) for v in std])
-    check(lib().mls_stem_pool(images.data_ptr(), w.data_ptr(), bias.data_ptr(), out.data_ptr(), B, H, W, m, s,
-                              stream_ptr(dev)), "mls_stem_pool")
-    return out
+    if conv1_w is None:
+        check(lib().mls_stem_pool(images.data_ptr(), w.data_ptr(), bias.data_ptr(), out.data_ptr(), B, H, W, m, s,
+                                  stream_ptr(dev)), "mls_stem_pool")
+        return out
+    _need(conv1_w, "conv1_w", torch.bfloat16, dev)
+    if conv1_w.numel() != 64 * 64 or conv1_w.shape[0] != 64:
+        raise ValueError("stem_pool_u8: conv1_w must be [64, 64] (Cout x Cin)")
+    if conv1_b is not None:
+        _need(conv1_b, "conv1_b", torch.float32, dev)
+        if conv1_b.numel() != 64:
+            raise ValueError("conv1_b must have 64 elements")
+    t1 = torch.empty(shape, device=dev, dtype=torch.bfloat16)
+    check(lib().mls_stem_pool_conv1(images.data_ptr(), w.data_ptr(), bias.data_ptr(), out.data_ptr(), B, H, W, m, s,
+                                    conv1_w.data_ptr(), _ptr(conv1_b), t1.data_ptr(), stream_ptr(dev)),
+          "mls_stem_pool_conv1")
+    return out, t1
 
 
 def conv3x3_halo(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, act=ACT_NONE,

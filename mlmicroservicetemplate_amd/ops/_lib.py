@@ -41,6 +41,7 @@ _SIGS = {
     "mls_normalize_u8": [P, P, I, I, I, I, FP, FP, P],
     "mls_maxpool2d": [P, P, I, I, I, I, I, I, I, P],
     "mls_stem_pool": [P, P, P, P, I, I, I, FP, FP, P],
+    "mls_stem_pool_conv1": [P, P, P, P, I, I, I, FP, FP, P, P, P, P],
     "mls_conv3x3_halo": [P, P, P, P, P, P, SZ, I, I, I, I, I, I, I, I, P],
     "mls_conv3x3_halo_geometry": [I, I, I, _c.POINTER(I), _c.POINTER(I)],
     "mls_conv3x3_halo_geometry_v": [I, I, I, I, _c.POINTER(I), _c.POINTER(I)],

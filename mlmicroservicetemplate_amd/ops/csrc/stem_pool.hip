@@ -34,15 +34,23 @@ constexpr int PATCH_BYTES = PR * PC * 8;           // 7360
 constexpr int TSTR = COUT + 8;                      // stem tile row stride (bf16): 144 B spreads the
                                                     // epilogue's 4 row groups and the pool's rows over banks
 constexpr int TILE_BYTES = MROWS * TSTR * 2;       // 23040
+constexpr int NPOOL = TPH * TPW;                   // 32 pooled pixels per tile
+constexpr int POOL_BYTES = NPOOL * COUT * 2;       // 4096: the pooled tile as the 1x1 conv's A operand
 
-// TILES_PER_BLOCK = consecutive tiles of one pooled-row strip per block
-template <int TILES_PER_BLOCK>
+// TILES_PER_BLOCK = consecutive tiles of one pooled-row strip per block.  CONV1: also run the first
+// bottleneck's 1x1 conv (64 -> 64, BN folded, ReLU) on each pooled tile while it is in LDS and
+// store its output t1 -- the layer1.0.conv1 launch and its 12.8 MB re-read of the pooled map go
+// away (the pooled map itself is still stored: the block's downsample branch reads it).
+template <int TILES_PER_BLOCK, bool CONV1>
 __global__ __launch_bounds__(256, 3) void stem_pool_kernel(const uint8_t* __restrict__ img, const bf16* __restrict__ w,
                                                         const float* __restrict__ bias, bf16* __restrict__ out, int B,
                                                         int H, int W, int Po, float m0, float m1, float m2, float s0,
-                                                        float s1, float s2, int dbg) {
-  __shared__ __attribute__((aligned(16))) char smem[PATCH_BYTES + TILE_BYTES];
+                                                        float s1, float s2, int dbg, const bf16* __restrict__ w1,
+                                                        const float* __restrict__ b1, bf16* __restrict__ t1) {
+  __shared__ __attribute__((aligned(16))) char smem[PATCH_BYTES + TILE_BYTES + (CONV1 ? 2 * POOL_BYTES : 0)];
   bf16* tile = reinterpret_cast<bf16*>(smem + PATCH_BYTES);  // [MROWS][TSTR]
+  char* sPool = smem + PATCH_BYTES + TILE_BYTES;             // [32 px][8 x 16 B], chunk ^ (px & 7)
+  char* sT1 = sPool + POOL_BYTES;                            // [32 px][8 x 16 B], chunk ^ (px & 7)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int tw = Po / TPW, th = Po / TPH;
   const int nparts = (tw + TILES_PER_BLOCK - 1) / TILES_PER_BLOCK;
@@ -71,6 +79,16 @@ __global__ __launch_bounds__(256, 3) void stem_pool_kernel(const uint8_t* __rest
   float bj[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) bj[j] = bias[wn * 32 + j * 16 + fr];
+  // CONV1: wave w owns t1 columns w*16 .. w*16+15 of both 16-pixel row blocks; its B fragments
+  // (64 input channels = 2 k-steps) and bias in registers for the whole block
+  bf16x8 bw1[2];
+  float bb1 = 0.f;
+  if constexpr (CONV1) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      bw1[k] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(w1 + (wid * 16 + fr) * COUT + k * 32 + fq * 8));
+    bb1 = b1 ? b1[wid * 16 + fr] : 0.f;
+  }
   int abase[5];
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
@@ -181,7 +199,38 @@ __global__ __launch_bounds__(256, 3) void stem_pool_kernel(const uint8_t* __rest
       if (m[0] == 12345.f) st16(out, pack8(m));  // keep the work live; never true
       continue;
     }
-    st16(out + (((long)b * Po + ph0 + pr) * Po + pw0 + pc) * COUT + c8 * 8, pack8(m));
+    const uint4 pooled = pack8(m);
+    st16(out + (((long)b * Po + ph0 + pr) * Po + pw0 + pc) * COUT + c8 * 8, pooled);
+    if constexpr (CONV1) {
+      // t1 = relu(pooled . W1^T + b1): the pooled tile [32 px][64 ch] in LDS is the A operand
+      *reinterpret_cast<uint4*>(sPool + pp * 128 + ((c8 ^ (pp & 7)) << 4)) = pooled;
+      __syncthreads();
+      f32x4 acc1[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        acc1[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int r = i * 16 + fr;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int ch = fq + 4 * k;
+          const bf16x8 av = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sPool + r * 128 + ((ch ^ (r & 7)) << 4)));
+          acc1[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bw1[k], acc1[i], 0, 0, 0);
+        }
+      }
+      const int col = wid * 16 + fr;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = i * 16 + fq * 4 + r;
+          const float e = acc1[i][r];  // through a named float (ext-vector element bit-cast hazard)
+          *reinterpret_cast<bf16*>(sT1 + row * 128 + (((col >> 3) ^ (row & 7)) << 4) + (col & 7) * 2) =
+              (bf16)fmaxf(e + bb1, 0.f);
+        }
+      __syncthreads();
+      st16(t1 + (((long)b * Po + ph0 + pr) * Po + pw0 + pc) * COUT + c8 * 8,
+           *reinterpret_cast<const uint4*>(sT1 + pp * 128 + ((c8 ^ (pp & 7)) << 4)));
+    }
   }
 }
 
@@ -189,10 +238,22 @@ __global__ __launch_bounds__(256, 3) void stem_pool_kernel(const uint8_t* __rest
 
 extern "C" {
 
+int mls_stem_pool_conv1(const void* images, const void* w, const float* bias, void* out, int B, int H, int W,
+                        const float* mean3, const float* std3, const void* w1, const float* b1, void* t1,
+                        void* stream);
+
 // images uint8 [B][H][W][3]; w = the packed stem weights [64][7][8][4] bf16 (BN scale folded);
 // bias fp32 [64]; out bf16 [B][Po][Po][64] with Po = H / 4.  224 x 224 (ResNet) only.
 int mls_stem_pool(const void* images, const void* w, const float* bias, void* out, int B, int H, int W,
                   const float* mean3, const float* std3, void* stream) {
+  return mls_stem_pool_conv1(images, w, bias, out, B, H, W, mean3, std3, nullptr, nullptr, nullptr, stream);
+}
+
+// ... and, with w1 [64][64] (BN folded) / b1 [64] / t1 [B][Po][Po][64] given, the first bottleneck's
+// 1x1 conv + ReLU on the pooled map in the same kernel.
+int mls_stem_pool_conv1(const void* images, const void* w, const float* bias, void* out, int B, int H, int W,
+                        const float* mean3, const float* std3, const void* w1, const float* b1, void* t1,
+                        void* stream) {
   if (B <= 0 || H != 224 || W != 224) return MLS_UNSUPPORTED;
   const int Po = H / 4;  // stem 112 -> pool 56
   if (Po % TPH || Po % TPW) return MLS_UNSUPPORTED;
@@ -210,11 +271,14 @@ int mls_stem_pool(const void* images, const void* w, const float* bias, void* ou
   }();
   const long blocks = (long)B * (Po / TPH) * ((Po / TPW + tpb - 1) / tpb);
   if (blocks > 0x7fffffffL) return MLS_BAD_ARG;
-  auto kernel = tpb == 1 ? stem_pool_kernel<1> : tpb == 2 ? stem_pool_kernel<2> : tpb == 7 ? stem_pool_kernel<7>
-                                                                                            : stem_pool_kernel<4>;
+  const bool c1 = w1 != nullptr && t1 != nullptr;
+  auto kernel = c1 ? (tpb == 1 ? stem_pool_kernel<1, true> : tpb == 2 ? stem_pool_kernel<2, true>
+                                         : tpb == 7 ? stem_pool_kernel<7, true> : stem_pool_kernel<4, true>)
+                   : (tpb == 1 ? stem_pool_kernel<1, false> : tpb == 2 ? stem_pool_kernel<2, false>
+                                         : tpb == 7 ? stem_pool_kernel<7, false> : stem_pool_kernel<4, false>);
   hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)images,
                      (const bf16*)w, bias, (bf16*)out, B, H, W, Po, mean3[0], mean3[1], mean3[2], 1.f / std3[0],
-                     1.f / std3[1], 1.f / std3[2], dbg);
+                     1.f / std3[1], 1.f / std3[2], dbg, (const bf16*)w1, b1, (bf16*)t1);
   return (int)hipGetLastError();
 }
 

@@ -267,6 +267,28 @@ def test_stem_pool_fused_matches_three_kernels(B):
     assert err < 2e-2, err
 
 
+@pytest.mark.parametrize("B", [1, 3])
+def test_stem_pool_conv1_fused(B):
+    """The stem kernel with layer1.0's 1x1 conv on its pooled tiles: pooled map unchanged, t1 equal
+    to the separate conv kernel on that map (and to fp32 within bf16 rounding)."""
+    from mlmicroservicetemplate_amd import ops
+    from mlmicroservicetemplate_amd.models.resnet import IMAGENET_MEAN, IMAGENET_STD
+
+    g = torch.Generator(device="cpu").manual_seed(10 + B)
+    imgs = torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8, generator=g).to(DEV)
+    wp = ops.pack_conv_weight((torch.randn(64, 3, 7, 7, generator=g) * 0.05).to(torch.bfloat16).to(DEV))
+    bias = (torch.randn(64, generator=g) * 0.5).to(DEV)
+    w1 = (torch.randn(64, 64, generator=g) / 8).to(torch.bfloat16).to(DEV)
+    b1 = (torch.randn(64, generator=g) * 0.1).to(DEV)
+    pooled = ops.stem_pool_u8(imgs, wp, bias, IMAGENET_MEAN, IMAGENET_STD)
+    x, t1 = ops.stem_pool_u8(imgs, wp, bias, IMAGENET_MEAN, IMAGENET_STD, conv1_w=w1, conv1_b=b1)
+    assert torch.equal(x, pooled)
+    sep = ops.conv2d_nhwc(x, w1.view(64, 1, 1, 64), b1, kernel=1, act=ops.ACT_RELU)
+    assert rel_err(t1, sep) < 1e-2
+    ref = torch.relu(x.float() @ w1.float().T + b1)
+    assert rel_err(t1, ref) < 1e-2
+
+
 @pytest.mark.parametrize("B,H,W,cin,cout,resid", [
     (2, 56, 56, 64, 64, False),   # layer1 conv2: 4 rows x 56 per tile
     (2, 28, 28, 128, 128, False),  # layer2: 7 x 28
