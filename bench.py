@@ -124,16 +124,26 @@ def main(argv=None) -> int:
             t.wait()
             lat.append(time.perf_counter() - t.t_submit)
 
+    phases = os.environ.get("MLS_BENCH_PHASES")  # diagnostics: wall-clock stamps of the phases
+
+    def stamp(what):
+        if phases and info.rank == 0:
+            with open(phases, "a") as f:
+                f.write(f"{what} {time.time():.3f}\n")
+
+    stamp("warmup")
     run_steps(args.warmup, [])
     host_s[0] = 0.0
     lat: list = []
     mdist.barrier()
     torch.cuda.synchronize(device)
+    stamp("timed")
     t_start = time.perf_counter()
     run_steps(args.steps, lat)
     torch.cuda.synchronize(device)
     mdist.barrier()
     elapsed = time.perf_counter() - t_start
+    stamp("done")
     elapsed_max = mdist.max_over_ranks(elapsed)
     p50 = float(np.percentile(lat, 50)) * 1e3
     p99 = float(np.percentile(lat, 99)) * 1e3
