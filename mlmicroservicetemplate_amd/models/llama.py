@@ -359,6 +359,24 @@ class LlamaTP:
                 self.p[f"l{i}.gate_up"] = ops.fold_norm(gu, mlp_g)
                 self.p[f"l{i}.qkv"] = ops.fold_norm(self.p[f"l{i}.qkv"], self.p.pop(f"l{i}.attn_norm"))
             self.p["lm_head"] = ops.fold_norm(self.p["lm_head"], self.p.pop("final_norm"))
+            # Decode (<= 16 tokens per step) streams a second, granule-packed copy of every projection
+            # (ops.pack_skinny: each wave reads contiguous 1 KiB granules, non-temporal): 3.4-4.5 ->
+            # 4.6-6.2 TB/s on the Llama-3-8B shapes (profiles/r2_decode_packed_weight_probe.jsonl).
+            # Costs one more copy of the weights in HBM (16 GB at 8B / TP = 1 of 288 GB);
+            # MLS_PACKED_DECODE=0 turns it off, "auto" packs while the copy stays under 1/4 of the card.
+            self.packed: Dict[str, torch.Tensor] = {}
+            self.pk_variant = int(os.environ.get("MLS_PACKED_VARIANT", "9"))
+            self.pk_fold = os.environ.get("MLS_PACKED_FOLD", "1") == "1"
+            mode = os.environ.get("MLS_PACKED_DECODE", "auto")
+            if self.device.type == "cuda" and mode != "0":
+                names = [f"l{i}.{n}" for i in range(cfg.layers) for n in ("qkv", "o", "gate_up", "down")]
+                names.append("lm_head")
+                names = [n for n in names if self.p[n].shape[0] % 16 == 0 and self.p[n].shape[1] % 32 == 0
+                         and self.p[n].numel() * 2 < (1 << 31)]
+                total = sum(self.p[n].numel() * 2 for n in names)
+                cap = torch.cuda.get_device_properties(self.device).total_memory
+                if mode == "1" or total <= cap // 4:
+                    self.packed = {n: ops.pack_skinny(self.p[n]) for n in names}
             self.ones = torch.ones(cfg.hidden, device=self.device, dtype=torch.bfloat16)
             self.workspace = torch.empty(32 << 20, device=self.device, dtype=torch.float32)
             self.dec_chunk = int(os.environ.get("MLS_DEC_CHUNK", "0"))  # 0: auto (see _fused_forward)
@@ -394,8 +412,8 @@ class LlamaTP:
         return self.comm.all_reduce_(x)
 
     def _local_topk(self, logits: torch.Tensor, k: int):
-        if self.backend == "fused":
-            vals, idx = self.ops.topk_large(logits, k)
+        if self.backend == "fused":  # shard offset + padded-tail mask inside the merge launch
+            return self.ops.topk_large(logits, k, lo=self.sd.vocab_lo, valid=self.cfg.vocab - self.sd.vocab_lo)
         else:
             vals, idx = torch.topk(logits.float(), k, dim=-1)
             idx = idx.to(torch.int32)
@@ -492,7 +510,26 @@ class LlamaTP:
         r = self._embed(ids.reshape(-1))  # residual stream (bf16)
         delta = None
 
-        def pre_norm(x, w, d, act=ops.ACT_NONE):
+        T = B * S
+        packed = self.packed if T <= 16 else {}
+
+        # TP = 1: the residual add rides in the o / down epilogues (h = r + a Wo^T, r' = h + g Wd^T), so
+        # the next pre-norm GEMM reads one activation stream instead of two (r + delta) and writes no
+        # residual copy.  With TP > 1 the add has to wait for the all-reduce.
+        fold = self.tp == 1 and bool(packed) and self.pk_fold
+
+        def linear(x, name, residual=None):
+            if name in packed:
+                return ops.skinny_packed(x, packed[name], p[name].shape[0], residual=residual, variant=self.pk_variant)
+            return ops.linear(x, p[name], workspace=ws)
+
+        def pre_norm(x, name, d, act=ops.ACT_NONE):
+            w = p[name]
+            if name in packed:
+                r_new = None if d is None else torch.empty_like(x)
+                y = ops.skinny_packed(x, packed[name], w.shape[0], delta=d, resid_out=r_new, norm=True, act=act,
+                                      eps=eps, variant=self.pk_variant)
+                return y, (x if d is None else r_new)
             if fuse:
                 r_new = None if d is None else torch.empty_like(x)
                 y = ops.gemm_rmsnorm(x, w, d, r_new, act=act, eps=eps, workspace=ws)
@@ -502,7 +539,7 @@ class LlamaTP:
             return ops.linear(xn, w, act=act, workspace=ws), x
 
         for i in range(cfg.layers):
-            qkv, r = pre_norm(r, p[f"l{i}.qkv"], delta)
+            qkv, r = pre_norm(r, f"l{i}.qkv", delta)
             if decode:  # RoPE + KV append ride inside the decode-attention launch
                 a = ops.decode_attention(qkv, self.k_cache[i][:B], self.v_cache[i][:B], lens, sd.hq, sd.hkv, D,
                                          workspace=self.dec_ws, counters=self.dec_cnt, positions=pos, cos=self.cos,
@@ -511,13 +548,22 @@ class LlamaTP:
                 ops.rope_kv_(qkv, pos, self.cos, self.sin, sd.hq, sd.hkv, D, explicit_slots, self.k_cache[i],
                              self.v_cache[i], lens=lens, seq=S, max_seq=self.max_seq)
                 a = ops.flash_attention(qkv, B, S, sd.hq, sd.hkv, D, kv_lens=lens, causal=True)
-            o = self.comm.all_reduce_(ops.linear(a, p[f"l{i}.o"], workspace=ws))
-            gu, r = pre_norm(r, p[f"l{i}.gate_up"], o, act=ops.ACT_SILU_MUL)
-            delta = self.comm.all_reduce_(ops.linear(gu, p[f"l{i}.down"], workspace=ws))
+            if fold:
+                h = linear(a, f"l{i}.o", residual=r)
+                gu, _ = pre_norm(h, f"l{i}.gate_up", None, act=ops.ACT_SILU_MUL)
+                r = linear(gu, f"l{i}.down", residual=h)
+                continue
+            o = self.comm.all_reduce_(linear(a, f"l{i}.o"))
+            gu, r = pre_norm(r, f"l{i}.gate_up", o, act=ops.ACT_SILU_MUL)
+            delta = self.comm.all_reduce_(linear(gu, f"l{i}.down"))
         if not decode:
             last = (torch.arange(B, device=r.device, dtype=torch.int64) * S + lens.long() - 1)
-            r, delta = r.index_select(0, last), delta.index_select(0, last)
-        if B <= 16:
+            r = r.index_select(0, last)
+            delta = None if delta is None else delta.index_select(0, last)
+        if B <= 16 and "lm_head" in self.packed:
+            logits = ops.skinny_packed(r, self.packed["lm_head"], p["lm_head"].shape[0], delta=delta, norm=True,
+                                       eps=eps, variant=self.pk_variant)
+        elif B <= 16:
             logits = ops.gemm_rmsnorm(r, p["lm_head"], delta, eps=eps, workspace=ws)
         else:
             xn = ops.rmsnorm(delta, self.ones, residual=r, eps=eps)

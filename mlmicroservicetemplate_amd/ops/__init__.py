@@ -356,6 +356,63 @@ def gemm_rmsnorm(x: torch.Tensor, w_folded: torch.Tensor, delta: Optional[torch.
     return out
 
 
+def pack_skinny(w: torch.Tensor) -> torch.Tensor:
+    """``w [N, K]`` -> the packed 1 KiB-granule layout of :func:`skinny_packed` (same bytes, flat)."""
+    _need(w, "w", torch.bfloat16, w.device)
+    N, K = w.shape
+    if N % 16 or K % 32:
+        raise ValueError("pack_skinny: N % 16 == 0 and K % 32 == 0")
+    wp = torch.empty(N * K, device=w.device, dtype=torch.bfloat16)
+    check(lib().mls_skinny_pack(w.data_ptr(), wp.data_ptr(), N, K, stream_ptr(w.device)), "mls_skinny_pack")
+    return wp
+
+
+def pack_skinny_reference(w: torch.Tensor) -> torch.Tensor:
+    """PyTorch form of the packed layout: ``[N/16][K/32][4][16][8]`` flattened."""
+    N, K = w.shape
+    return w.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).reshape(-1).contiguous()
+
+
+def skinny_packed(x: torch.Tensor, wp: torch.Tensor, N: int, *, delta: Optional[torch.Tensor] = None,
+                  resid_out: Optional[torch.Tensor] = None, norm: bool = False, act=ACT_NONE,
+                  bias: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
+                  eps: float = 1e-5, variant: int = 9, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Decode product (M <= 16) against a :func:`pack_skinny` weight: ``act([RMSNorm](x [+ delta]) @ W^T + b
+    [+ residual])``; with ``norm`` the RMSNorm gain must be folded into W (:func:`fold_norm`)."""
+    dev = x.device
+    _need(x, "x", torch.bfloat16, dev)
+    _need(wp, "wp", torch.bfloat16, dev)
+    M, K = x.shape
+    if M > 16 or N % 16 or K % 32 or wp.numel() != N * K:
+        raise ValueError("skinny_packed: M <= 16, N % 16 == 0, K % 32 == 0, wp of N*K elements")
+    if resid_out is not None and delta is None:
+        raise ValueError("resid_out needs delta")
+    if (delta is not None) and not norm:
+        raise ValueError("delta exists only with norm")
+    for name, t in (("delta", delta), ("resid_out", resid_out)):
+        if t is not None:
+            _need(t, name, torch.bfloat16, dev)
+            if tuple(t.shape) != (M, K):
+                raise ValueError(f"{name} must be [M, K]")
+    if bias is not None:
+        _need(bias, "bias", torch.float32, dev)
+    if residual is not None:
+        _need(residual, "residual", torch.bfloat16, dev)
+        if tuple(residual.shape) != (M, N):
+            raise ValueError("residual must be [M, N]")
+    code = _act(act)
+    n_out = N // 2 if code == ACT_SILU_MUL else N
+    if out is None:
+        out = torch.empty(M, n_out, device=dev, dtype=torch.bfloat16)
+    elif tuple(out.shape) != (M, n_out) or out.dtype != torch.bfloat16 or not out.is_contiguous():
+        raise ValueError(f"out must be contiguous bf16 [M, {n_out}]")
+    rc = lib().mls_skinny_packed(x.data_ptr(), _ptr(delta), _ptr(resid_out), wp.data_ptr(), _ptr(bias),
+                                 _ptr(residual), out.data_ptr(), M, N, K, code, int(norm), float(eps), int(variant),
+                                 stream_ptr(dev))
+    check(rc, "mls_skinny_packed")
+    return out
+
+
 def fold_norm(w: torch.Tensor, gain: torch.Tensor) -> torch.Tensor:
     """``W[:, k] * gain[k]`` in fp32, rounded once to bf16: RMSNorm(x) @ W^T == rstd * (x @ fold^T)."""
     return (w.float() * gain.float().view(1, -1)).to(w.dtype)
@@ -784,19 +841,42 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
     return out
 
 
-def topk_large(x: torch.Tensor, k: int, max_chunk: int = 16384) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Raw-logit top-k of rows longer than one LDS-resident row: split each row into equal
-    chunks (per-chunk top-k in the kernel), then merge the ``chunks * k`` candidates."""
+def topk_large(x: torch.Tensor, k: int, max_chunk: int = 16384, *, lo: int = 0,
+               valid: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Raw-logit top-k of rows longer than one LDS-resident row (LM heads): split each row into
+    equal chunks (per-chunk top-k in the kernel), then merge the ``chunks * k`` candidates.
+    Returned indices are ``+ lo`` (a vocab shard's offset); columns at or past ``valid`` (a shard's
+    zero-padded tail) never win.  bf16 rows whose length splits into <= 2048-wide chunks of a
+    multiple of 8 take two native launches (wave-per-chunk register top-k, then
+    ``mls_topk_merge``): ~10 us at vocab 128256 where the torch merge chain cost ~80 us."""
     rows, N = x.shape
+    valid = N if valid is None else int(valid)
+    if x.dtype == torch.bfloat16 and x.is_contiguous() and k <= 64 and N > 2048:
+        c = next((c for c in range(-(-N // 2048), N // 8 + 1) if N % c == 0 and (N // c) % 8 == 0), 0)
+        if c and c * k * 8 <= 65536:
+            L = N // c
+            cv = torch.empty(rows, c * k, device=x.device, dtype=torch.float32)
+            ci = torch.empty(rows, c * k, device=x.device, dtype=torch.int32)
+            check(lib().mls_topk_chunks(x.data_ptr(), cv.data_ptr(), ci.data_ptr(), rows, c, L, k, valid,
+                                        stream_ptr(x.device)), "mls_topk_chunks")
+            vals = torch.empty(rows, k, device=x.device, dtype=torch.float32)
+            idx = torch.empty(rows, k, device=x.device, dtype=torch.int32)
+            check(lib().mls_topk_merge(cv.data_ptr(), ci.data_ptr(), vals.data_ptr(), idx.data_ptr(), rows, c, k, L,
+                                       int(lo), valid, stream_ptr(x.device)), "mls_topk_merge")
+            return vals, idx
     if N <= max_chunk:
-        return softmax_topk(x, k, softmax=False)
-    c = -(-N // max_chunk)
-    while N % c:
-        c += 1
-    L = N // c
-    vals, idx = softmax_topk(x.reshape(rows * c, L), k, softmax=False)
-    vals = vals.view(rows, c * k)
-    off = (torch.arange(c, device=x.device, dtype=torch.int32) * L).repeat_interleave(k)
-    idx = idx.view(rows, c * k) + off
-    tv, tp = torch.topk(vals, k, dim=-1)
-    return tv, idx.gather(1, tp)
+        vals, idx = softmax_topk(x, k, softmax=False)
+    else:
+        c = -(-N // max_chunk)
+        while N % c:
+            c += 1
+        L = N // c
+        vals, idx = softmax_topk(x.reshape(rows * c, L), k, softmax=False)
+        vals = vals.view(rows, c * k)
+        off = (torch.arange(c, device=x.device, dtype=torch.int32) * L).repeat_interleave(k)
+        idx = idx.view(rows, c * k) + off
+        tv, tp = torch.topk(vals, k, dim=-1)
+        vals, idx = tv, idx.gather(1, tp)
+    if valid < N:  # (approximate: the padded tail can displace candidates of its own chunk)
+        vals = torch.where(idx < valid, vals, torch.full_like(vals, float("-inf")))
+    return vals, idx + lo if lo else idx

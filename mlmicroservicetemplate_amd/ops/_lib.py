@@ -50,6 +50,8 @@ _SIGS = {
     "mls_silu_mul_interleaved": [P, P, L, I, P],
     "mls_softmax_topk": [P, I, P, P, I, I, I, I, F, P],
     "mls_softmax_rows": [P, P, P, I, I, I, F, P],
+    "mls_topk_merge": [P, P, P, P, I, I, I, I, I, I, P],
+    "mls_topk_chunks": [P, P, P, I, I, I, I, I, P],
     "mls_layernorm": [P, P, P, P, P, P, L, I, F, I, P],
     "mls_embed_ln": [P, P, P, P, P, P, P, P, L, I, I, I, F, P],
     "mls_embedding": [P, P, P, L, I, I, I, P],
@@ -66,6 +68,8 @@ _SIGS = {
     "mls_flash_attention": [P, P, P, P, I, I, I, I, I, I, I, I, I, P, I, F, P],
     "mls_skinny_gemm": [P, P, P, P, P, P, SZ, I, I, I, I, I, P],
     "mls_skinny_gemm_norm": [P, P, P, P, P, P, P, P, SZ, I, I, I, I, I, I, F, P],
+    "mls_skinny_pack": [P, P, I, I, P],
+    "mls_skinny_packed": [P, P, P, P, P, P, P, I, I, I, I, I, F, I, P],
     "mls_decode_attention": [P, P, P, P, P, P, P, I, I, L, P, P, P, P, I, I, I, I, I, I, I, F, P],
 }
 _OPTIONAL_SIGS: dict = {"mls_set_debug_flags": [I], "mls_chain_set_l2_cw": [I], "mls_skinny_set_variant": [I], "mls_skinny_set_max_split": [I]}

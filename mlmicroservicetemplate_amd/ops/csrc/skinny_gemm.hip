@@ -314,6 +314,226 @@ __global__ __launch_bounds__(NWV * 64) void skinny_lds_kernel(const SkArgs s) {
   }
 }
 
+// Packed-weight variant of skinny_lds_kernel (M <= 4).  W is re-laid out once at load time
+// (pack_skinny_weight) so the 64 lanes' MFMA B fragments of one (16-row tile, 32-wide k-step) are
+// one contiguous 1 KiB granule: [tile][kstep][g][nr][8].  Each wave then streams a CONTIGUOUS
+// range of granules (its 1/NWV of the tile's k-steps), so every load instruction reads 1 KiB of
+// consecutive bytes and consecutive instructions continue the same run -- instead of 16 rows x
+// 64 B scattered K*2 bytes apart per instruction in the row-major layout.  NTL: non-temporal
+// cache policy on the weight stream (read exactly once per call).
+template <int NTL>
+MLS_DEV uint4 bload16_pol(rsrc_t r, int byte_off) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, NTL ? 2 : 0));
+}
+
+template <int UNROLL, int NWV, int FUSE, int NTL>
+__global__ __launch_bounds__(NWV * 64) void skinny_packed_kernel(const SkArgs s) {
+  extern __shared__ __attribute__((aligned(16))) uint4 a_lds[];  // [M][K/8]
+  __shared__ float red[NWV][16][17];
+  __shared__ float ssq_s[4];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nr = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.x * 16;
+  const int ksteps = s.K >> 5;
+  const int kch = s.K >> 3;
+  const int kpw = (ksteps + NWV - 1) / NWV;
+  const int kb = wid * kpw, ke = min(ksteps, kb + kpw);
+  const rsrc_t wr = make_rsrc(s.w, s.w_bytes);
+  const int wbase = blockIdx.x * ksteps * 1024 + lane * 16;
+
+  auto load_trip = [&](int ks0, uint4 (&wv)[UNROLL]) {
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) wv[u] = bload16_pol<NTL>(wr, ks0 + u < ke ? wbase + (ks0 + u) * 1024 : OOB);
+  };
+  uint4 wnext[UNROLL];
+  load_trip(kb, wnext);  // in flight during the prologue
+
+  if (tid < 4) ssq_s[tid] = 0.f;
+  __syncthreads();
+  float part[4] = {0.f, 0.f, 0.f, 0.f};
+  const bool wr_res = FUSE == FUSE_ADD_NORM && s.a_out && blockIdx.x == 0;
+  for (int q = tid; q < s.M * kch; q += NWV * 64) {
+    const int m = q / kch, c = q - m * kch;
+    uint4 v = ld16(s.a + (size_t)m * s.lda + c * 8);
+    if constexpr (FUSE == FUSE_ADD_NORM) {
+      v = add_round(v, ld16(s.a2 + (size_t)m * s.lda + c * 8));
+      if (wr_res) st16(s.a_out + (size_t)m * s.lda + c * 8, v);
+    }
+    a_lds[q] = v;
+    if constexpr (FUSE != FUSE_NONE) {
+      const float sq = sumsq8(v);
+#pragma unroll
+      for (int mm = 0; mm < 4; ++mm) part[mm] += mm == m ? sq : 0.f;
+    }
+  }
+  if constexpr (FUSE != FUSE_NONE) {
+#pragma unroll
+    for (int mm = 0; mm < 4; ++mm) {
+      const float t = wave_sum(part[mm]);
+      if (lane == 0 && mm < s.M) atomicAdd(&ssq_s[mm], t);
+    }
+  }
+  __syncthreads();
+
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool arow = nr < s.M;
+  for (int ks = kb; ks < ke; ks += UNROLL) {
+    uint4 wv[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) wv[u] = wnext[u];
+    if (ks + UNROLL < ke) load_trip(ks + UNROLL, wnext);
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int k = ks + u;
+      const uint4 av = (arow && k < ke) ? a_lds[nr * kch + k * 4 + g] : make_uint4(0, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, av), __builtin_bit_cast(bf16x8, wv[u]),
+                                                    acc, 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) red[wid][4 * g + i][nr] = acc[i];
+  __syncthreads();
+  const bool glu = s.act == ACT_SILU_MUL;
+  for (int q = tid; q < s.M * 16; q += NWV * 64) {
+    const int m = q >> 4, c = q & 15;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) v += red[w][m][c];
+    const float rs = FUSE != FUSE_NONE ? rsqrtf(ssq_s[m] / (float)s.K + s.eps) : 1.f;
+    const int n = n0 + c;
+    v *= rs;
+    if (glu) {
+      if (c < 8) {
+        float up = 0.f;
+#pragma unroll
+        for (int w = 0; w < NWV; ++w) up += red[w][m][c + 8];
+        up *= rs;
+        s.out[(size_t)m * s.ldo + (n >> 4) * 8 + (n & 7)] = (bf16)(silu(epi(v, n, s)) * epi(up, n + 8, s));
+      }
+      continue;
+    }
+    float o = epi(v, n, s);
+    if (s.res) o += (float)s.res[(size_t)m * s.N + n];
+    s.out[(size_t)m * s.ldo + n] = (bf16)apply_act(o, s.act);
+  }
+}
+
+// Packed weights, M <= 16 (or A too large for LDS): the A fragments (+ A2) ride beside the weight
+// granules in registers, read per k-step from L2 (every block re-reads A; at M = 16 that is half
+// the weight bytes, all L2 / MALL hits), register double-buffered like the weight stream.  Each
+// wave folds its own k range of the RMSNorm square sums; the block reduces them through LDS.
+template <int UNROLL, int NWV, int FUSE, int NTL, int NT>
+__global__ __launch_bounds__(NWV * 64) void skinny_packed_reg_kernel(const SkArgs s) {
+  __shared__ float red[NWV][16][NT * 16 + 1];
+  __shared__ float ssq_red[NWV][16];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nr = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.x * 16 * NT;
+  const int ksteps = s.K >> 5;
+  const int kpw = (ksteps + NWV - 1) / NWV;
+  const int kb = wid * kpw, ke = min(ksteps, kb + kpw);
+  const rsrc_t wr = make_rsrc(s.w, s.w_bytes);
+  const rsrc_t ar = make_rsrc(s.a, s.a_bytes);
+  const rsrc_t a2r = make_rsrc(s.a2, FUSE == FUSE_ADD_NORM ? s.a_bytes : 0);
+  const int wbase = blockIdx.x * NT * ksteps * 1024 + lane * 16;  // tile j: + j * ksteps * 1024
+  const int abase = nr < s.M ? (nr * s.lda + 8 * g) * 2 : OOB;
+  const bool wr_res = FUSE == FUSE_ADD_NORM && s.a_out && blockIdx.x == 0 && nr < s.M;
+
+  struct Trip {
+    uint4 w[UNROLL][NT], a[UNROLL], a2[UNROLL];
+  };
+  auto load_trip = [&](int ks0, Trip& t) {
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const bool in = ks0 + u < ke;
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        t.w[u][j] = bload16_pol<NTL>(wr, in ? wbase + (j * ksteps + ks0 + u) * 1024 : OOB);
+      const int ao = (in && abase != OOB) ? abase + (ks0 + u) * 64 : OOB;
+      t.a[u] = bload16(ar, ao);
+      if constexpr (FUSE == FUSE_ADD_NORM) t.a2[u] = bload16(a2r, ao);
+    }
+  };
+  Trip nxt;
+  load_trip(kb, nxt);
+  f32x4 acc[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float ssq = 0.f;
+  for (int ks = kb; ks < ke; ks += UNROLL) {
+    Trip cur = nxt;
+    if (ks + UNROLL < ke) load_trip(ks + UNROLL, nxt);
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      uint4 av = cur.a[u];
+      if constexpr (FUSE == FUSE_ADD_NORM) {
+        av = add_round(av, cur.a2[u]);
+        if (wr_res && ks + u < ke) st16(s.a_out + nr * s.lda + (ks + u) * 32 + 8 * g, av);
+      }
+      if constexpr (FUSE != FUSE_NONE) ssq += sumsq8(av);
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, av),
+                                                         __builtin_bit_cast(bf16x8, cur.w[u][j]), acc[j], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[wid][4 * g + i][16 * j + nr] = acc[j][i];
+  if constexpr (FUSE != FUSE_NONE) {
+    float v = ssq;  // lanes nr, nr+16, nr+32, nr+48 hold row nr's k slices
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    if (g == 0) ssq_red[wid][nr] = v;
+  }
+  __syncthreads();
+  const bool glu = s.act == ACT_SILU_MUL;
+  constexpr int COLS = NT * 16;
+  for (int q = tid; q < s.M * COLS; q += NWV * 64) {
+    const int m = q / COLS, c = q % COLS;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) v += red[w][m][c];
+    float rs = 1.f;
+    if constexpr (FUSE != FUSE_NONE) {
+      float t2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < NWV; ++w) t2 += ssq_red[w][m];
+      rs = rsqrtf(t2 / (float)s.K + s.eps);
+    }
+    const int n = n0 + c;
+    v *= rs;
+    if (glu) {
+      if ((c & 15) < 8) {
+        float up = 0.f;
+#pragma unroll
+        for (int w = 0; w < NWV; ++w) up += red[w][m][c + 8];
+        up *= rs;
+        s.out[(size_t)m * s.ldo + (n >> 4) * 8 + (n & 7)] = (bf16)(silu(epi(v, n, s)) * epi(up, n + 8, s));
+      }
+      continue;
+    }
+    float o = epi(v, n, s);
+    if (s.res) o += (float)s.res[(size_t)m * s.N + n];
+    s.out[(size_t)m * s.ldo + n] = (bf16)apply_act(o, s.act);
+  }
+}
+
+// [N][K] row-major -> [N/16][K/32][4][16][8] (the packed granule layout above)
+__global__ __launch_bounds__(256) void pack_skinny_kernel(const bf16* __restrict__ w, bf16* __restrict__ wp, int N,
+                                                          int K) {
+  const int ksteps = K >> 5;
+  const long total = (long)N * (K >> 3);  // 16-B chunks
+  for (long q = blockIdx.x * 256L + threadIdx.x; q < total; q += (long)gridDim.x * 256) {
+    const int lane = (int)(q & 63);
+    const long gr = q >> 6;  // granule = tile * ksteps + ks
+    const int ks = (int)(gr % ksteps), tile = (int)(gr / ksteps);
+    const int n = tile * 16 + (lane & 15), k = ks * 32 + 8 * (lane >> 4);
+    st16(wp + q * 8, ld16(w + (size_t)n * K + k));
+  }
+}
+
 __global__ __launch_bounds__(256) void skinny_finish_kernel(const SkArgs s) {
   const bool glu = s.act == ACT_SILU_MUL;
   const int ncols = glu ? s.N / 2 : s.N;
@@ -462,6 +682,110 @@ int mls_skinny_gemm_norm(const void* A, const void* A2, void* A_out, const void*
     blocks = blocks > 2048 ? 2048 : blocks;
     hipLaunchKernelGGL(skinny_finish_kernel, dim3(blocks), dim3(256), 0, st, s);
   }
+  return (int)hipGetLastError();
+}
+
+// W [N][K] -> packed granules (N % 16 == 0, K % 32 == 0); Wp must not alias W.
+int mls_skinny_pack(const void* W, void* Wp, int N, int K, void* stream) {
+  if (N <= 0 || K <= 0 || N % 16 || K % 32 || W == Wp) return MLS_BAD_ARG;
+  const long chunks = (long)N * (K / 8);
+  int blocks = (int)((chunks + 255) / 256);
+  blocks = blocks > 4096 ? 4096 : blocks;
+  hipLaunchKernelGGL(pack_skinny_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16*)W, (bf16*)Wp,
+                     N, K);
+  return (int)hipGetLastError();
+}
+
+// Packed-weight skinny GEMM (+ optional fused add + RMSNorm prologue), M <= 16.  M <= 4 with A
+// within 64 KiB stages A in LDS (skinny_packed_kernel), otherwise A rides in registers
+// (skinny_packed_reg_kernel; variant | 16 forces it).  variant = probe knob, (granules per trip,
+// waves, non-temporal): 0 (8,8,no) 1 (8,8,nt) 2 (8,4,no) 3 (8,4,nt) 4 (16,8,no) 5 (16,8,nt)
+// 6 (16,4,no) 7 (16,4,nt) 8 (8,16,nt) 9 (4,16,nt; the measured default) 10 (4,8,nt); register
+// path only: 11 / 12 = (4,8) over 2 / 4 column tiles per block, 13 = (4,16) over 2.
+int mls_skinny_packed(const void* A, const void* A2, void* A_out, const void* Wp, const float* bias, const void* res,
+                      void* out, int M, int N, int K, int act, int norm, float eps, int variant, void* stream) {
+  if (M <= 0 || M > 16 || N % 16 || K % 32 || K <= 0) return MLS_BAD_ARG;
+  if (A_out && (A_out == A || A_out == A2)) return MLS_BAD_ARG;
+  if ((A2 || A_out) && !norm) return MLS_UNSUPPORTED;
+  const size_t ab = (size_t)M * K * 2, wb = (size_t)N * K * 2;
+  if (wb >= 0x7FFFFFFFull) return MLS_UNSUPPORTED;
+  SkArgs s{};
+  s.a = (const bf16*)A;
+  s.a2 = (const bf16*)A2;
+  s.a_out = (bf16*)A_out;
+  s.norm = norm;
+  s.eps = eps;
+  s.w = (const bf16*)Wp;
+  s.bias = bias;
+  s.res = (const bf16*)res;
+  s.out = (bf16*)out;
+  s.M = M; s.N = N; s.K = K; s.lda = K;
+  s.act = act;
+  s.ldo = act == ACT_SILU_MUL ? N / 2 : N;
+  s.a_bytes = (uint32_t)ab;
+  s.w_bytes = (uint32_t)wb;
+  s.nsplit = 1;
+  const int mode = A2 ? FUSE_ADD_NORM : norm ? FUSE_NORM : FUSE_NONE;
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid(N / 16);
+  if (M > 4 || ab > 65536 || (variant & 16)) {  // A fragments from L2 in registers (16: forced)
+#define MLS_SKR(UN, NW, NT_)                                                                                    \
+  switch (mode) {                                                                                                 \
+    case FUSE_NONE:                                                                                               \
+      hipLaunchKernelGGL((skinny_packed_reg_kernel<UN, NW, FUSE_NONE, 1, NT_>), dim3(N / (16 * NT_)), dim3(NW * 64), \
+                         0, st, s);                                                                               \
+      break;                                                                                                      \
+    case FUSE_NORM:                                                                                               \
+      hipLaunchKernelGGL((skinny_packed_reg_kernel<UN, NW, FUSE_NORM, 1, NT_>), dim3(N / (16 * NT_)), dim3(NW * 64), \
+                         0, st, s);                                                                               \
+      break;                                                                                                      \
+    default:                                                                                                      \
+      hipLaunchKernelGGL((skinny_packed_reg_kernel<UN, NW, FUSE_ADD_NORM, 1, NT_>), dim3(N / (16 * NT_)),          \
+                         dim3(NW * 64), 0, st, s);                                                                \
+      break;                                                                                                      \
+  }
+    int v = variant & 15;
+    // default: two column tiles per block once there are >= 384 tiles (A fragments amortised over
+    // two weight granules; M = 8: QKV 14.3 -> 12.1 us, gate_up 47.0 -> 43.4), else one tile, 16 waves
+    // (profiles/r2_decode_packed_weight_probe.jsonl)
+    if (v == 9 && N / 16 >= 384) v = 11;
+    if ((v == 11 || v == 13) && N % 32) v = 9;
+    if (v == 12 && N % 64) v = 9;
+    switch (v) {
+      case 1: MLS_SKR(8, 8, 1) break;
+      case 10: MLS_SKR(4, 8, 1) break;
+      case 11: MLS_SKR(4, 8, 2) break;
+      case 12: MLS_SKR(4, 8, 4) break;
+      case 13: MLS_SKR(4, 16, 2) break;
+      default: MLS_SKR(4, 16, 1) break;
+    }
+#undef MLS_SKR
+    return (int)hipGetLastError();
+  }
+#define MLS_SKP(UN, NW, NTL_)                                                                                 \
+  switch (mode) {                                                                                               \
+    case FUSE_NONE:                                                                                             \
+      hipLaunchKernelGGL((skinny_packed_kernel<UN, NW, FUSE_NONE, NTL_>), grid, dim3(NW * 64), ab, st, s); break; \
+    case FUSE_NORM:                                                                                             \
+      hipLaunchKernelGGL((skinny_packed_kernel<UN, NW, FUSE_NORM, NTL_>), grid, dim3(NW * 64), ab, st, s); break; \
+    default:                                                                                                    \
+      hipLaunchKernelGGL((skinny_packed_kernel<UN, NW, FUSE_ADD_NORM, NTL_>), grid, dim3(NW * 64), ab, st, s);    \
+      break;                                                                                                    \
+  }
+  switch (variant) {
+    case 0: MLS_SKP(8, 8, 0) break;
+    case 2: MLS_SKP(8, 4, 0) break;
+    case 3: MLS_SKP(8, 4, 1) break;
+    case 4: MLS_SKP(16, 8, 0) break;
+    case 5: MLS_SKP(16, 8, 1) break;
+    case 6: MLS_SKP(16, 4, 0) break;
+    case 7: MLS_SKP(16, 4, 1) break;
+    case 8: MLS_SKP(8, 16, 1) break;
+    case 9: MLS_SKP(4, 16, 1) break;
+    case 10: MLS_SKP(4, 8, 1) break;
+    default: MLS_SKP(8, 8, 1) break;  // 1: the measured default
+  }
+#undef MLS_SKP
   return (int)hipGetLastError();
 }
 

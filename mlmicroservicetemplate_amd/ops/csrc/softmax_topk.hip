@@ -133,11 +133,15 @@ __global__ __launch_bounds__(256) void softmax_topk_wave_kernel(const Tin* __res
 template <int CPL>
 __global__ __launch_bounds__(256) void softmax_topk_reg_kernel(const bf16* __restrict__ x, float* __restrict__ vals,
                                                                int* __restrict__ idx, int rows, int N, int k,
-                                                               int apply_softmax, float temperature) {
+                                                               int apply_softmax, float temperature, int chunks,
+                                                               int valid) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const long r = (long)blockIdx.x * 4 + wid;
   if (r >= rows) return;
   const int nch = N >> 3;
+  // rows may be `chunks` equal pieces of one longer row: columns at or past `valid` of that row
+  // (a vocab shard's padded tail) are excluded before the selection
+  const int limit = valid - (int)(r % chunks) * N;
   const bf16* src = x + r * (long)N;
   const float invt = 1.f / temperature;
   float v[CPL][8];
@@ -154,7 +158,7 @@ __global__ __launch_bounds__(256) void softmax_topk_reg_kernel(const bf16* __res
     unpack8(raw[c], v[c]);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      v[c][e] = ok ? v[c][e] * invt : -INFINITY;
+      v[c][e] = ok && (lane + 64 * c) * 8 + e < limit ? v[c][e] * invt : -INFINITY;
       mx = fmaxf(mx, v[c][e]);
     }
   }
@@ -222,6 +226,41 @@ __global__ __launch_bounds__(256) void softmax_rows_kernel(const bf16* __restric
   for (int i = threadIdx.x; i < N; i += blockDim.x) y[r * (long)N + i] = f2bf(row[i] * inv);
 }
 
+// Second stage of the large-vocabulary top-k (LM heads): row r holds C chunks' k candidates each
+// (value, chunk-local index); the winners get their shard-global index chunk * L + local + lo, and
+// candidates at or past `valid` (the zero-padded vocabulary tail of a TP shard) are dropped BEFORE
+// the selection.  One block per row, candidates staged once in LDS, k block-argmax rounds.
+__global__ __launch_bounds__(256) void topk_merge_kernel(const float* __restrict__ cv, const int* __restrict__ ci,
+                                                         float* __restrict__ vals, int* __restrict__ idx, int C, int k,
+                                                         int L, int lo, int valid) {
+  extern __shared__ __attribute__((aligned(16))) float cand[];  // [n] values, then [n] global indices
+  __shared__ float rv[16];
+  __shared__ int ri[16];
+  const long r = blockIdx.x;
+  const int n = C * k;
+  int* gidx = reinterpret_cast<int*>(cand + n);
+  for (int j = threadIdx.x; j < n; j += blockDim.x) {
+    const int local = ci[r * n + j];
+    const int g = (j / k) * L + local;
+    const bool ok = local >= 0 && g < valid;
+    cand[j] = ok ? cv[r * n + j] : -INFINITY;
+    gidx[j] = ok ? g : -1;
+  }
+  __syncthreads();
+  for (int j = 0; j < k; ++j) {
+    KV best{-INFINITY, -1};
+    for (int i = threadIdx.x; i < n; i += blockDim.x)
+      if (gidx[i] >= 0) best = better(best, KV{cand[i], i});
+    best = block_argmax(best, rv, ri);
+    if (threadIdx.x == 0) {
+      vals[r * k + j] = best.i >= 0 ? best.v : -INFINITY;
+      idx[r * k + j] = best.i >= 0 ? gidx[best.i] + lo : lo;
+      if (best.i >= 0) gidx[best.i] = -1;
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -234,13 +273,13 @@ int mls_softmax_topk(const void* x, int dtype, float* vals, int* idx, int rows, 
     dim3 g((rows + 3) / 4);
     if (N <= 512)
       hipLaunchKernelGGL(softmax_topk_reg_kernel<1>, g, dim3(256), 0, (hipStream_t)stream, (const bf16*)x, vals, idx,
-                         rows, N, k, apply_softmax, temperature);
+                         rows, N, k, apply_softmax, temperature, 1, N);
     else if (N <= 1024)
       hipLaunchKernelGGL(softmax_topk_reg_kernel<2>, g, dim3(256), 0, (hipStream_t)stream, (const bf16*)x, vals, idx,
-                         rows, N, k, apply_softmax, temperature);
+                         rows, N, k, apply_softmax, temperature, 1, N);
     else
       hipLaunchKernelGGL(softmax_topk_reg_kernel<4>, g, dim3(256), 0, (hipStream_t)stream, (const bf16*)x, vals, idx,
-                         rows, N, k, apply_softmax, temperature);
+                         rows, N, k, apply_softmax, temperature, 1, N);
     return (int)hipGetLastError();
   }
   if (N <= 4096) {
@@ -269,6 +308,33 @@ int mls_softmax_rows(const void* x, void* y, const float* mask, int rows, int N,
   if (rows <= 0 || N <= 0 || N > 32768 || (mask && rows_per_mask <= 0)) return MLS_BAD_ARG;
   hipLaunchKernelGGL(softmax_rows_kernel, dim3(rows), dim3(256), (size_t)N * sizeof(float), (hipStream_t)stream,
                      (const bf16*)x, (bf16*)y, mask, N, rows_per_mask > 0 ? rows_per_mask : 1, scale);
+  return (int)hipGetLastError();
+}
+
+// Large-vocabulary raw-logit top-k, stage 1: x [rows][C * L] bf16 viewed as rows * C chunks of L
+// (L % 8 == 0, L <= 2048), columns >= valid excluded; cv / ci [rows][C * k] chunk-local winners.
+int mls_topk_chunks(const void* x, float* cv, int* ci, int rows, int C, int L, int k, int valid, void* stream) {
+  if (rows <= 0 || C <= 0 || L <= 0 || L % 8 || L > 2048 || k <= 0 || k > 64 || k > L) return MLS_BAD_ARG;
+  const int R = rows * C;
+  dim3 g((R + 3) / 4);
+  if (L <= 512)
+    hipLaunchKernelGGL(softmax_topk_reg_kernel<1>, g, dim3(256), 0, (hipStream_t)stream, (const bf16*)x, cv, ci, R, L,
+                       k, 0, 1.f, C, valid);
+  else if (L <= 1024)
+    hipLaunchKernelGGL(softmax_topk_reg_kernel<2>, g, dim3(256), 0, (hipStream_t)stream, (const bf16*)x, cv, ci, R, L,
+                       k, 0, 1.f, C, valid);
+  else
+    hipLaunchKernelGGL(softmax_topk_reg_kernel<4>, g, dim3(256), 0, (hipStream_t)stream, (const bf16*)x, cv, ci, R, L,
+                       k, 0, 1.f, C, valid);
+  return (int)hipGetLastError();
+}
+
+// cv / ci: [rows][C * k] per-chunk candidates (chunk-local indices) -> vals / idx [rows][k]
+int mls_topk_merge(const float* cv, const int* ci, float* vals, int* idx, int rows, int C, int k, int L, int lo,
+                   int valid, void* stream) {
+  if (rows <= 0 || C <= 0 || k <= 0 || L <= 0 || (size_t)C * k * 8 > 65536) return MLS_BAD_ARG;
+  hipLaunchKernelGGL(topk_merge_kernel, dim3(rows), dim3(256), (size_t)C * k * 8, (hipStream_t)stream, cv, ci, vals,
+                     idx, C, k, L, lo, valid);
   return (int)hipGetLastError();
 }
 

@@ -141,6 +141,27 @@ def test_topk_large():
     assert torch.allclose(v, rv) and torch.allclose(x.float().gather(1, i.long()), rv)
 
 
+@pytest.mark.parametrize("N,k,lo,valid", [(128256, 1, 0, 128256), (128256, 50, 0, 128256), (16032, 5, 112224, 16032),
+                                          (16032, 4, 120240, 8016), (16032, 3, 128256, 0), (30000, 2, 7, 29990)])
+def test_topk_large_shard_offset_and_tail(N, k, lo, valid):
+    """Native two-launch path: shard offset added and the padded tail never wins (vs torch.topk
+    over the valid columns)."""
+    from mlmicroservicetemplate_amd import ops
+
+    torch.manual_seed(k)
+    x = torch.randn(2, N, device=DEV).to(torch.bfloat16)
+    x[:, valid:] = 100.0  # the padded tail would win if it were not masked
+    v, i = ops.topk_large(x, k, lo=lo, valid=valid)
+    if valid == 0:
+        assert torch.isinf(v).all() and (v < 0).all()
+        return
+    rv, _ = torch.topk(x[:, :valid].float(), k, dim=-1)
+    assert torch.allclose(v, rv)
+    local = i.long() - lo
+    assert (local >= 0).all() and (local < valid).all()
+    assert torch.allclose(x.float().gather(1, local), rv)
+
+
 # 256 tokens: native GEMMs; 1024: hipBLASLt + LN-fused residual; 4096 (the benchmark shape):
 # + the TunableOp-chosen hipBLASLt FFN-up solution (ops/tuned/tunableop_gfx950.csv)
 @pytest.mark.parametrize("B,S", [(4, 64), (16, 64), (32, 128)])

@@ -42,14 +42,27 @@ def main():
                 lib.mls_skinny_set_variant(0)
             return run
 
-        if hasattr(lib, "mls_skinny_set_variant"):
+        if hasattr(lib, "mls_skinny_set_variant") and os.environ.get("REG", "0") == "1":
             for k in [k for k in impls if "skinny" in k]:
                 impls[k + "_reg"] = variant(impls[k], 1)
+        if M <= 16:  # packed 1 KiB-granule weights (ops.pack_skinny), variants of mls_skinny_packed
+            wp_list = [ops.pack_skinny(w) for w in ws_list]
+            norm_fused = K == 4096 and name != "o"
+            for v in [int(t) for t in os.environ.get("PACKED_VARIANTS", "0,1,2,3,4,5").split(",")]:
+                impls[f"packed_v{v}"] = (lambda v=v: [ops.skinny_packed(x, wp, N, act=act, variant=v) for wp in wp_list])
+                if norm_fused:
+                    impls[f"norm_packed_v{v}"] = (
+                        lambda v=v: [ops.skinny_packed(x, wp, N, norm=True, act=act, variant=v) for wp in wp_list])
+                    impls[f"fused_norm_packed_v{v}"] = (
+                        lambda v=v: [ops.skinny_packed(x, wp, N, delta=d, resid_out=r_out, norm=True, act=act, variant=v)
+                                     for wp in wp_list])
         for impl, fn in impls.items():
             t = _time(fn, iters=3) * 1e-3 / 32
             print(json.dumps({"shape": name, "M": M, "impl": impl, "us_per_call": round(t * 1e6, 2),
                               "hbm_tb_s": round(N * K * 2 / t / 1e12, 2)}), flush=True)
         del ws_list
+        impls.clear()
+        wp_list = None
         torch.cuda.empty_cache()
 
 
