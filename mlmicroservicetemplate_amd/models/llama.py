@@ -359,7 +359,7 @@ class LlamaTP:
                 self.p[f"l{i}.gate_up"] = ops.fold_norm(gu, mlp_g)
                 self.p[f"l{i}.qkv"] = ops.fold_norm(self.p[f"l{i}.qkv"], self.p.pop(f"l{i}.attn_norm"))
             self.p["lm_head"] = ops.fold_norm(self.p["lm_head"], self.p.pop("final_norm"))
-            # Decode (<= 16 tokens per step) streams a second, granule-packed copy of every projection
+            # Decode (<= 24 tokens per step) streams a second, granule-packed copy of every projection
             # (ops.pack_skinny: each wave reads contiguous 1 KiB granules, non-temporal): 3.4-4.5 ->
             # 4.6-6.2 TB/s on the Llama-3-8B shapes (profiles/r2_decode_packed_weight_probe.jsonl).
             # Costs one more copy of the weights in HBM (16 GB at 8B / TP = 1 of 288 GB);
@@ -511,7 +511,10 @@ class LlamaTP:
         delta = None
 
         T = B * S
-        packed = self.packed if T <= 16 else {}
+        # packed decode GEMMs up to 24 rows: at 25-32 (two 16-row A fragments per weight granule)
+        # every column-tile block re-reads A, and the row-major split-K kernel is ahead (batch 24:
+        # 4.99 vs 5.36 ms/step, batch 32: 5.75 vs 5.64; profiles/r2_llama8b_decode_packed_ab.jsonl)
+        packed = self.packed if T <= 24 else {}
 
         # TP = 1: the residual add rides in the o / down epilogues (h = r + a Wo^T, r' = h + g Wd^T), so
         # the next pre-norm GEMM reads one activation stream instead of two (r + delta) and writes no
@@ -560,7 +563,7 @@ class LlamaTP:
             last = (torch.arange(B, device=r.device, dtype=torch.int64) * S + lens.long() - 1)
             r = r.index_select(0, last)
             delta = None if delta is None else delta.index_select(0, last)
-        if B <= 16 and "lm_head" in self.packed:
+        if B <= 24 and "lm_head" in self.packed:
             logits = ops.skinny_packed(r, self.packed["lm_head"], p["lm_head"].shape[0], delta=delta, norm=True,
                                        eps=eps, variant=self.pk_variant)
         elif B <= 16:

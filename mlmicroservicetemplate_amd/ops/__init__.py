@@ -377,14 +377,14 @@ def skinny_packed(x: torch.Tensor, wp: torch.Tensor, N: int, *, delta: Optional[
                   resid_out: Optional[torch.Tensor] = None, norm: bool = False, act=ACT_NONE,
                   bias: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
                   eps: float = 1e-5, variant: int = 9, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Decode product (M <= 16) against a :func:`pack_skinny` weight: ``act([RMSNorm](x [+ delta]) @ W^T + b
+    """Decode product (M <= 32) against a :func:`pack_skinny` weight: ``act([RMSNorm](x [+ delta]) @ W^T + b
     [+ residual])``; with ``norm`` the RMSNorm gain must be folded into W (:func:`fold_norm`)."""
     dev = x.device
     _need(x, "x", torch.bfloat16, dev)
     _need(wp, "wp", torch.bfloat16, dev)
     M, K = x.shape
-    if M > 16 or N % 16 or K % 32 or wp.numel() != N * K:
-        raise ValueError("skinny_packed: M <= 16, N % 16 == 0, K % 32 == 0, wp of N*K elements")
+    if M > 32 or N % 16 or K % 32 or wp.numel() != N * K:
+        raise ValueError("skinny_packed: M <= 32, N % 16 == 0, K % 32 == 0, wp of N*K elements")
     if resid_out is not None and delta is None:
         raise ValueError("resid_out needs delta")
     if (delta is not None) and not norm:

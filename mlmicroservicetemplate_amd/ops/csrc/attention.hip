@@ -251,7 +251,9 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(const DecodeArgs a) {
   __shared__ __attribute__((aligned(16))) float sm_o[4][G][D];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int grp = lane / LPR, gl = lane % LPR, glp = gl ^ (LPR / 2);
-  const int b = blockIdx.z, hk = blockIdx.y, sp = blockIdx.x;
+  // grid (Hkv, splits, B): the Hkv blocks of one (split, sequence) dispatch back to back, so the
+  // 256-B head slices of each 2 KiB cache row are read together (one DRAM row open, not Hkv)
+  const int b = blockIdx.z, hk = blockIdx.x, sp = blockIdx.y;
   const int L0 = a.lens[b];
   // keys past the split grid are never visited: a host context bound below lens is a caller bug
   MLS_CHECK(sp != 0 || L0 <= a.nsplit * CHUNK, 201);
@@ -279,31 +281,62 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(const DecodeArgs a) {
     kraw[i] = ld ? ld16(a.kc + cbase + r * rstride) : make_uint4(0, 0, 0, 0);
     vraw[i] = ld ? ld16(a.vc + cbase + r * rstride) : make_uint4(0, 0, 0, 0);
   }
-  float qv[G][8];
+  // every small operand (the G query heads, their RoPE partners, the position's cos / sin, the new
+  // token's K / V) is loaded in the same batch as the cache rows, before any of it is used: one
+  // memory round trip per block instead of a dependent q -> rope chain per head
+  uint4 qraw[G], qpraw[G], knew = make_uint4(0, 0, 0, 0), kpnew = knew, vnew = knew;
+  float4 cs[4] = {};
 #pragma unroll
   for (int hh = 0; hh < G; ++hh) {
     const bf16* qh = qrow + (long)(hk * G + hh) * D;
-    unpack8(ld16(qh + gl * 8), qv[hh]);
+    qraw[hh] = ld16(qh + gl * 8);
+    qpraw[hh] = rope ? ld16(qh + glp * 8) : make_uint4(0, 0, 0, 0);
+  }
+  const bool has_new = rope && L - 1 >= start && L - 1 < end;
+  if (rope) {
+    const int i0 = (gl % (D / 16)) * 8;
+    const float* cp = a.cos_t + (long)pos * (D / 2) + i0;
+    const float* sp_ = a.sin_t + (long)pos * (D / 2) + i0;
+    cs[0] = *reinterpret_cast<const float4*>(cp);
+    cs[1] = *reinterpret_cast<const float4*>(cp + 4);
+    cs[2] = *reinterpret_cast<const float4*>(sp_);
+    cs[3] = *reinterpret_cast<const float4*>(sp_ + 4);
+    // (every block of the sequence loads the new row, so the loads batch with the rest unbranched)
+    const bf16* kh = qrow + (long)(a.Hq + hk) * D;
+    knew = ld16(kh + gl * 8);
+    kpnew = ld16(kh + glp * 8);
+    vnew = ld16(qrow + (long)(a.Hq + a.Hkv + hk) * D + gl * 8);
+  }
+  auto rope_regs = [&](float (&x)[8], const float (&xp)[8]) {
+    const float c[8] = {cs[0].x, cs[0].y, cs[0].z, cs[0].w, cs[1].x, cs[1].y, cs[1].z, cs[1].w};
+    const float sn[8] = {cs[2].x, cs[2].y, cs[2].z, cs[2].w, cs[3].x, cs[3].y, cs[3].z, cs[3].w};
+    const float sgn = gl < D / 16 ? -1.f : 1.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] = x[e] * c[e] + sgn * xp[e] * sn[e];
+  };
+  float qv[G][8];
+#pragma unroll
+  for (int hh = 0; hh < G; ++hh) {
+    unpack8(qraw[hh], qv[hh]);
     if (rope) {
       float xp[8];
-      unpack8(ld16(qh + glp * 8), xp);
-      rope8<D>(qv[hh], xp, a.cos_t, a.sin_t, pos, gl);
+      unpack8(qpraw[hh], xp);
+      rope_regs(qv[hh], xp);
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e) qv[hh][e] = (float)(bf16)qv[hh][e] * a.scale_log2;  // bf16 q, as the cache path
   }
-  if (rope && L - 1 >= start && L - 1 < end) {  // the new token's row, appended to the cache
+  if (has_new) {  // the new token's row, appended to the cache
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
       const int r = start + i * ROWS + wid * RPW + grp;
       if (r == L - 1) {
-        const bf16* kh = qrow + (long)(a.Hq + hk) * D;
         float kx[8], kp[8];
-        unpack8(ld16(kh + gl * 8), kx);
-        unpack8(ld16(kh + glp * 8), kp);
-        rope8<D>(kx, kp, a.cos_t, a.sin_t, pos, gl);
+        unpack8(knew, kx);
+        unpack8(kpnew, kp);
+        rope_regs(kx, kp);
         kraw[i] = pack8(kx);
-        vraw[i] = ld16(qrow + (long)(a.Hq + a.Hkv + hk) * D + gl * 8);
+        vraw[i] = vnew;
         st16(a.kc + cbase + r * rstride, kraw[i]);
         st16(a.vc + cbase + r * rstride, vraw[i]);
       }
@@ -519,7 +552,7 @@ int mls_decode_attention(const void* q, void* k_cache, void* v_cache, void* o, f
   const int nit = chunk / rows;
   if (chunk % rows || (nit != 1 && nit != 2 && nit != 4 && nit != 8 && nit != 16)) return MLS_BAD_ARG;
   if (a.nsplit > 1024) return MLS_UNSUPPORTED;  // combine keeps one weight per split in LDS
-  dim3 grid(a.nsplit, Hkv, B);
+  dim3 grid(Hkv, a.nsplit, B);
   hipStream_t st = (hipStream_t)stream;
 #define DEC(DD, GG)                                                                                        \
   switch (nit) {                                                                                           \

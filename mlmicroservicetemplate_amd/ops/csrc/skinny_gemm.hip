@@ -422,10 +422,10 @@ __global__ __launch_bounds__(NWV * 64) void skinny_packed_kernel(const SkArgs s)
 // granules in registers, read per k-step from L2 (every block re-reads A; at M = 16 that is half
 // the weight bytes, all L2 / MALL hits), register double-buffered like the weight stream.  Each
 // wave folds its own k range of the RMSNorm square sums; the block reduces them through LDS.
-template <int UNROLL, int NWV, int FUSE, int NTL, int NT>
+template <int UNROLL, int NWV, int FUSE, int NTL, int NT, int TMS>
 __global__ __launch_bounds__(NWV * 64) void skinny_packed_reg_kernel(const SkArgs s) {
-  __shared__ float red[NWV][16][NT * 16 + 1];
-  __shared__ float ssq_red[NWV][16];
+  __shared__ float red[NWV][16 * TMS][NT * 16 + 1];
+  __shared__ float ssq_red[NWV][16 * TMS];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int nr = lane & 15, g = lane >> 4;
   const int n0 = blockIdx.x * 16 * NT;
@@ -436,56 +436,73 @@ __global__ __launch_bounds__(NWV * 64) void skinny_packed_reg_kernel(const SkArg
   const rsrc_t ar = make_rsrc(s.a, s.a_bytes);
   const rsrc_t a2r = make_rsrc(s.a2, FUSE == FUSE_ADD_NORM ? s.a_bytes : 0);
   const int wbase = blockIdx.x * NT * ksteps * 1024 + lane * 16;  // tile j: + j * ksteps * 1024
-  const int abase = nr < s.M ? (nr * s.lda + 8 * g) * 2 : OOB;
-  const bool wr_res = FUSE == FUSE_ADD_NORM && s.a_out && blockIdx.x == 0 && nr < s.M;
+  int abase[TMS];
+#pragma unroll
+  for (int t = 0; t < TMS; ++t) abase[t] = 16 * t + nr < s.M ? ((16 * t + nr) * s.lda + 8 * g) * 2 : OOB;
+  const bool wr_res = FUSE == FUSE_ADD_NORM && s.a_out && blockIdx.x == 0;
 
   struct Trip {
-    uint4 w[UNROLL][NT], a[UNROLL], a2[UNROLL];
+    uint4 w[UNROLL][NT], a[UNROLL][TMS], a2[UNROLL][TMS];
   };
-  auto load_trip = [&](int ks0, Trip& t) {
+  auto load_trip = [&](int ks0, Trip& tr) {
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       const bool in = ks0 + u < ke;
 #pragma unroll
       for (int j = 0; j < NT; ++j)
-        t.w[u][j] = bload16_pol<NTL>(wr, in ? wbase + (j * ksteps + ks0 + u) * 1024 : OOB);
-      const int ao = (in && abase != OOB) ? abase + (ks0 + u) * 64 : OOB;
-      t.a[u] = bload16(ar, ao);
-      if constexpr (FUSE == FUSE_ADD_NORM) t.a2[u] = bload16(a2r, ao);
+        tr.w[u][j] = bload16_pol<NTL>(wr, in ? wbase + (j * ksteps + ks0 + u) * 1024 : OOB);
+#pragma unroll
+      for (int t = 0; t < TMS; ++t) {
+        const int ao = (in && abase[t] != OOB) ? abase[t] + (ks0 + u) * 64 : OOB;
+        tr.a[u][t] = bload16(ar, ao);
+        if constexpr (FUSE == FUSE_ADD_NORM) tr.a2[u][t] = bload16(a2r, ao);
+      }
     }
   };
   Trip nxt;
   load_trip(kb, nxt);
-  f32x4 acc[NT];
+  f32x4 acc[TMS][NT];
+  float ssq[TMS];
 #pragma unroll
-  for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float ssq = 0.f;
+  for (int t = 0; t < TMS; ++t) {
+    ssq[t] = 0.f;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   for (int ks = kb; ks < ke; ks += UNROLL) {
     Trip cur = nxt;
     if (ks + UNROLL < ke) load_trip(ks + UNROLL, nxt);
 #pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
-      uint4 av = cur.a[u];
-      if constexpr (FUSE == FUSE_ADD_NORM) {
-        av = add_round(av, cur.a2[u]);
-        if (wr_res && ks + u < ke) st16(s.a_out + nr * s.lda + (ks + u) * 32 + 8 * g, av);
-      }
-      if constexpr (FUSE != FUSE_NONE) ssq += sumsq8(av);
+    for (int u = 0; u < UNROLL; ++u)
 #pragma unroll
-      for (int j = 0; j < NT; ++j)
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, av),
-                                                         __builtin_bit_cast(bf16x8, cur.w[u][j]), acc[j], 0, 0, 0);
-    }
+      for (int t = 0; t < TMS; ++t) {
+        uint4 av = cur.a[u][t];
+        if constexpr (FUSE == FUSE_ADD_NORM) {
+          av = add_round(av, cur.a2[u][t]);
+          if (wr_res && abase[t] != OOB && ks + u < ke)
+            st16(s.a_out + (16 * t + nr) * s.lda + (ks + u) * 32 + 8 * g, av);
+        }
+        if constexpr (FUSE != FUSE_NONE) ssq[t] += sumsq8(av);
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[t][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, av),
+                                                              __builtin_bit_cast(bf16x8, cur.w[u][j]), acc[t][j], 0, 0, 0);
+      }
   }
 #pragma unroll
-  for (int j = 0; j < NT; ++j)
+  for (int t = 0; t < TMS; ++t)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) red[wid][4 * g + i][16 * j + nr] = acc[j][i];
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[wid][16 * t + 4 * g + i][16 * j + nr] = acc[t][j][i];
   if constexpr (FUSE != FUSE_NONE) {
-    float v = ssq;  // lanes nr, nr+16, nr+32, nr+48 hold row nr's k slices
-    v += __shfl_xor(v, 16);
-    v += __shfl_xor(v, 32);
-    if (g == 0) ssq_red[wid][nr] = v;
+#pragma unroll
+    for (int t = 0; t < TMS; ++t) {
+      float v = ssq[t];  // lanes nr, nr+16, nr+32, nr+48 hold row 16t+nr's k slices
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      if (g == 0) ssq_red[wid][16 * t + nr] = v;
+    }
   }
   __syncthreads();
   const bool glu = s.act == ACT_SILU_MUL;
@@ -696,7 +713,7 @@ int mls_skinny_pack(const void* W, void* Wp, int N, int K, void* stream) {
   return (int)hipGetLastError();
 }
 
-// Packed-weight skinny GEMM (+ optional fused add + RMSNorm prologue), M <= 16.  M <= 4 with A
+// Packed-weight skinny GEMM (+ optional fused add + RMSNorm prologue), M <= 32.  M <= 4 with A
 // within 64 KiB stages A in LDS (skinny_packed_kernel), otherwise A rides in registers
 // (skinny_packed_reg_kernel; variant | 16 forces it).  variant = probe knob, (granules per trip,
 // waves, non-temporal): 0 (8,8,no) 1 (8,8,nt) 2 (8,4,no) 3 (8,4,nt) 4 (16,8,no) 5 (16,8,nt)
@@ -704,7 +721,7 @@ int mls_skinny_pack(const void* W, void* Wp, int N, int K, void* stream) {
 // path only: 11 / 12 = (4,8) over 2 / 4 column tiles per block, 13 = (4,16) over 2.
 int mls_skinny_packed(const void* A, const void* A2, void* A_out, const void* Wp, const float* bias, const void* res,
                       void* out, int M, int N, int K, int act, int norm, float eps, int variant, void* stream) {
-  if (M <= 0 || M > 16 || N % 16 || K % 32 || K <= 0) return MLS_BAD_ARG;
+  if (M <= 0 || M > 32 || N % 16 || K % 32 || K <= 0) return MLS_BAD_ARG;
   if (A_out && (A_out == A || A_out == A2)) return MLS_BAD_ARG;
   if ((A2 || A_out) && !norm) return MLS_UNSUPPORTED;
   const size_t ab = (size_t)M * K * 2, wb = (size_t)N * K * 2;
@@ -729,22 +746,33 @@ int mls_skinny_packed(const void* A, const void* A2, void* A_out, const void* Wp
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid(N / 16);
   if (M > 4 || ab > 65536 || (variant & 16)) {  // A fragments from L2 in registers (16: forced)
-#define MLS_SKR(UN, NW, NT_)                                                                                    \
+#define MLS_SKR3(UN, NW, NT_, TM)                                                                               \
   switch (mode) {                                                                                                 \
     case FUSE_NONE:                                                                                               \
-      hipLaunchKernelGGL((skinny_packed_reg_kernel<UN, NW, FUSE_NONE, 1, NT_>), dim3(N / (16 * NT_)), dim3(NW * 64), \
-                         0, st, s);                                                                               \
+      hipLaunchKernelGGL((skinny_packed_reg_kernel<UN, NW, FUSE_NONE, 1, NT_, TM>), dim3(N / (16 * NT_)),          \
+                         dim3(NW * 64), 0, st, s);                                                                \
       break;                                                                                                      \
     case FUSE_NORM:                                                                                               \
-      hipLaunchKernelGGL((skinny_packed_reg_kernel<UN, NW, FUSE_NORM, 1, NT_>), dim3(N / (16 * NT_)), dim3(NW * 64), \
-                         0, st, s);                                                                               \
+      hipLaunchKernelGGL((skinny_packed_reg_kernel<UN, NW, FUSE_NORM, 1, NT_, TM>), dim3(N / (16 * NT_)),          \
+                         dim3(NW * 64), 0, st, s);                                                                \
       break;                                                                                                      \
     default:                                                                                                      \
-      hipLaunchKernelGGL((skinny_packed_reg_kernel<UN, NW, FUSE_ADD_NORM, 1, NT_>), dim3(N / (16 * NT_)),          \
+      hipLaunchKernelGGL((skinny_packed_reg_kernel<UN, NW, FUSE_ADD_NORM, 1, NT_, TM>), dim3(N / (16 * NT_)),      \
                          dim3(NW * 64), 0, st, s);                                                                \
       break;                                                                                                      \
   }
+#define MLS_SKR(UN, NW, NT_) MLS_SKR3(UN, NW, NT_, 1)
     int v = variant & 15;
+    if (M > 16) {  // two 16-row A fragments per granule
+      if (N / 16 >= 384 && N % 32 == 0 && v != 10) {
+        MLS_SKR3(4, 8, 2, 2)  // 8 waves: the double-buffered 2-tile trip needs > 128 VGPRs
+      } else if (v == 10) {
+        MLS_SKR3(4, 8, 1, 2)
+      } else {
+        MLS_SKR3(4, 16, 1, 2)
+      }
+      return (int)hipGetLastError();
+    }
     // default: two column tiles per block once there are >= 384 tiles (A fragments amortised over
     // two weight granules; M = 8: QKV 14.3 -> 12.1 us, gate_up 47.0 -> 43.4), else one tile, 16 waves
     // (profiles/r2_decode_packed_weight_probe.jsonl)
@@ -760,6 +788,7 @@ int mls_skinny_packed(const void* A, const void* A2, void* A_out, const void* Wp
       default: MLS_SKR(4, 16, 1) break;
     }
 #undef MLS_SKR
+#undef MLS_SKR3
     return (int)hipGetLastError();
   }
 #define MLS_SKP(UN, NW, NTL_)                                                                                 \

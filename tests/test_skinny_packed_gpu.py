@@ -25,7 +25,7 @@ def test_pack_matches_reference_layout():
 
 @pytest.mark.parametrize("variant", list(range(14)) + [17, 25, 26, 27, 28, 29])
 @pytest.mark.parametrize("M,N,K", [(1, 256, 4096), (3, 128, 1024), (2, 64, 14336), (4, 64, 8192), (2, 48, 96),
-                                   (8, 128, 4096), (16, 64, 1024), (5, 32, 14336)])
+                                   (8, 128, 4096), (16, 64, 1024), (5, 32, 14336), (24, 96, 2048), (32, 6144, 256)])
 def test_packed_plain(variant, M, N, K):
     from mlmicroservicetemplate_amd import ops
 
@@ -38,7 +38,7 @@ def test_packed_plain(variant, M, N, K):
 
 
 @pytest.mark.parametrize("variant", [0, 3, 5, 6, 9, 25, 17, 11, 12, 13])
-@pytest.mark.parametrize("M", [1, 4, 8, 16])
+@pytest.mark.parametrize("M", [1, 4, 8, 16, 17, 32])
 def test_packed_add_norm_silu_mul(variant, M):
     """The decode gate_up form: RMSNorm(x + delta) with the gain folded into W, SiLU-mul epilogue,
     x + delta written back to the residual stream."""
@@ -80,7 +80,7 @@ def test_packed_rejects_bad_shapes():
     w = _rand(64, 256)
     wp = ops.pack_skinny(w)
     with pytest.raises(ValueError):
-        ops.skinny_packed(_rand(17, 256), wp, 64)  # M > 16
+        ops.skinny_packed(_rand(33, 256), wp, 64)  # M > 32
     with pytest.raises(ValueError):
         ops.skinny_packed(_rand(1, 256), wp, 48)  # wp size mismatch
     with pytest.raises(ValueError):
