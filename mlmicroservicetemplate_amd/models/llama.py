@@ -333,11 +333,14 @@ class GenParams:
 
 
 class LlamaTP:
-    """One rank of a tensor-parallel Llama with a KV cache ``[layers][max_batch, max_seq, hkv, D]``."""
+    """One rank of a tensor-parallel Llama with a KV cache ``[layers][max_batch, max_seq, hkv, D]``
+    (or, paged, ``[layers][pages, 64, hkv, D]`` pools addressed through a page table)."""
 
     def __init__(self, params: Dict[str, torch.Tensor], cfg: LlamaConfig, tp: int = 1, rank: int = 0,
                  comm: Optional[TPComm] = None, backend: str = "reference", device="cpu", max_batch: int = 8,
-                 max_seq: int = 1024, top_k_max: int = 50):
+                 max_seq: int = 1024, top_k_max: int = 50, kv_pages: int = 0):
+        """``kv_pages > 0``: paged KV cache -- per layer a pool of ``kv_pages`` pages of 64 rows
+        shared by all sequences (:class:`~.kv_pages.PageTable`), instead of ``max_batch x max_seq``."""
         self.cfg = cfg
         self.sd = shard_dims(cfg, tp, rank)
         self.tp, self.rank = tp, rank
@@ -384,8 +387,16 @@ class LlamaTP:
                                       device=self.device, dtype=torch.float32)
             self.dec_cnt = torch.zeros(max_batch * self.sd.hkv, device=self.device, dtype=torch.int32)
         cdt = torch.bfloat16 if backend == "fused" else torch.float32
-        self.k_cache = [torch.zeros(max_batch, max_seq, self.sd.hkv, D, device=self.device, dtype=cdt)
-                        for _ in range(cfg.layers)]
+        self.pages = None
+        if kv_pages > 0:
+            from .kv_pages import PageTable
+
+            self.page_rows = 64  # = the decode split: one page per split block
+            self.pages = PageTable(kv_pages, self.page_rows, max_batch, -(-max_seq // self.page_rows), self.device)
+            shape = (kv_pages, self.page_rows, self.sd.hkv, D)
+        else:
+            shape = (max_batch, max_seq, self.sd.hkv, D)
+        self.k_cache = [torch.zeros(shape, device=self.device, dtype=cdt) for _ in range(cfg.layers)]
         self.v_cache = [torch.zeros_like(self.k_cache[0]) for _ in range(cfg.layers)]
         self.cos, self.sin = R.rope_tables(max_seq, D, cfg.rope_theta, self.device)
         # hipGraph capture of the decode step (P4): removes ~300 host launches per token.  With
@@ -457,11 +468,21 @@ class LlamaTP:
             valid = valid & (positions < lens.long()[b_of])
         rows = b_of if slots_b is None else slots_b.long()[b_of]  # batch row -> cache row
         bi, pi = rows[valid], positions[valid].long()
-        self.k_cache[i][bi, pi] = k[valid].to(self.k_cache[i].dtype)
-        self.v_cache[i][bi, pi] = v[valid].to(self.v_cache[i].dtype)
+        if self.pages is not None:  # paged: flat pool rows through the page table
+            flat = self.pages.rows(bi, pi)
+            self.k_cache[i].view(-1, sd.hkv, D)[flat] = k[valid].to(self.k_cache[i].dtype)
+            self.v_cache[i].view(-1, sd.hkv, D)[flat] = v[valid].to(self.v_cache[i].dtype)
+        else:
+            self.k_cache[i][bi, pi] = k[valid].to(self.k_cache[i].dtype)
+            self.v_cache[i][bi, pi] = v[valid].to(self.v_cache[i].dtype)
         if decode:
             qrow = q.reshape(B, sd.hq * D)
-            a = R.decode_attention(qrow, self.k_cache[i][:B], self.v_cache[i][:B], lens, sd.hq, sd.hkv, D)
+            if self.pages is not None:  # gather each sequence's pages back into [B, rows, hkv, D]
+                table = self.pages.device_table()[:B].long()
+                kv = [c[table].reshape(B, -1, sd.hkv, D) for c in (self.k_cache[i], self.v_cache[i])]
+                a = R.decode_attention(qrow, kv[0], kv[1], lens, sd.hq, sd.hkv, D)
+            else:
+                a = R.decode_attention(qrow, self.k_cache[i][:B], self.v_cache[i][:B], lens, sd.hq, sd.hkv, D)
         else:
             qkv_r = torch.cat([q.reshape(T, -1), k.reshape(T, -1), v.reshape(T, -1)], dim=1)
             a = R.attention(qkv_r, B, S, sd.hq, sd.hkv, D, kv_lens=lens, causal=True)
@@ -497,11 +518,17 @@ class LlamaTP:
         fuse = B * S <= 16
         pos = positions.reshape(-1)
         explicit_slots = None
-        if slot_ids is not None and not decode:  # prefill into arbitrary cache rows (continuous batching)
+        if (slot_ids is not None or self.pages is not None) and not decode:
+            # prefill into arbitrary cache rows (continuous batching) / through the page table
             b = torch.arange(B, device=ids.device, dtype=torch.int64).repeat_interleave(S)
             pl = pos.long()
-            explicit_slots = torch.where(pl < lens.long()[b], slot_ids.long()[b] * self.max_seq + pl,
-                                         torch.full_like(pl, -1)).to(torch.int32)
+            slot = slot_ids.long()[b] if slot_ids is not None else b
+            valid = pl < lens.long()[b]
+            if self.pages is not None:
+                row = self.pages.rows(slot, torch.where(valid, pl, torch.zeros_like(pl)))
+            else:
+                row = slot * self.max_seq + pl
+            explicit_slots = torch.where(valid, row, torch.full_like(pl, -1)).to(torch.int32)
         # decode split size: 64 rows measured best from batch 1 to 32, at TP = 1 and on an emulated
         # TP = 8 rank (one KV head).  A single 256-row split per KV head (no combine launch) was
         # 1.6 % slower at batch 1, and one 8-wave block walking a whole <= 1024 context in passes
@@ -544,9 +571,15 @@ class LlamaTP:
         for i in range(cfg.layers):
             qkv, r = pre_norm(r, f"l{i}.qkv", delta)
             if decode:  # RoPE + KV append ride inside the decode-attention launch
-                a = ops.decode_attention(qkv, self.k_cache[i][:B], self.v_cache[i][:B], lens, sd.hq, sd.hkv, D,
-                                         workspace=self.dec_ws, counters=self.dec_cnt, positions=pos, cos=self.cos,
-                                         sin=self.sin, max_len=self._dec_ctx, chunk=dec_chunk)
+                if self.pages is not None:
+                    a = ops.decode_attention(qkv, self.k_cache[i], self.v_cache[i], lens, sd.hq, sd.hkv, D,
+                                             workspace=self.dec_ws, counters=self.dec_cnt, positions=pos,
+                                             cos=self.cos, sin=self.sin, max_len=self._dec_ctx, chunk=self.page_rows,
+                                             page_table=self.pages.dev[:B])
+                else:
+                    a = ops.decode_attention(qkv, self.k_cache[i][:B], self.v_cache[i][:B], lens, sd.hq, sd.hkv,
+                                             D, workspace=self.dec_ws, counters=self.dec_cnt, positions=pos,
+                                             cos=self.cos, sin=self.sin, max_len=self._dec_ctx, chunk=dec_chunk)
             else:
                 ops.rope_kv_(qkv, pos, self.cos, self.sin, sd.hq, sd.hkv, D, explicit_slots, self.k_cache[i],
                              self.v_cache[i], lens=lens, seq=S, max_seq=self.max_seq)
@@ -581,6 +614,8 @@ class LlamaTP:
         batch row itself) -- how continuous batching prefills new requests into free slots."""
         B, S = ids.shape
         ids, positions, lens = ids.contiguous(), positions.contiguous(), lens.contiguous()
+        if self.pages is not None and not (self.device.type == "cuda" and torch.cuda.is_current_stream_capturing()):
+            self.pages.device_table()
         if slot_ids is not None:
             slot_ids = slot_ids.to(self.device).contiguous()
         if self.backend == "fused":
@@ -650,6 +685,8 @@ class LlamaTP:
         ctx = self.ctx_bucket(max_ctx)
         if self.use_graphs:
             g, t_s, p_s, l_s, v_s, i_s = self._decode_graph(B, k, ctx)
+            if self.pages is not None:
+                self.pages.device_table()  # the graph reads the table buffer in place
             t_s.copy_(tok.view(B, 1))
             p_s.copy_(cur.view(B, 1))
             l_s.copy_(cur.view(B) + 1)
@@ -674,19 +711,27 @@ class LlamaTP:
         ids = ids.to(dev)
         lens = lens.to(dev).to(torch.int32)
         k = max(1, min(gp.top_k, self.top_k_max))
-        pos = torch.arange(S, device=dev, dtype=torch.int32).unsqueeze(0).expand(B, S).contiguous()
-        vals, idx = self.step(ids, pos, lens, decode=False, k=k)
-        out = []
-        tok = self._sample_rows(vals, idx, gp, 0)
-        out.append(tok)
-        cur = lens.clone()
-        for t in range(1, gp.max_new_tokens):
-            # the new token sits at position cur; attention covers cur + 1 keys
-            vals, idx = self.decode_step(tok.to(dev), cur, k, max_ctx=S + t)
-            tok = self._sample_rows(vals, idx, gp, t)
+        if self.pages is not None:  # batch row b = slot b, pages for the prompt + the generation budget
+            for b in range(B):
+                self.pages.assign(b, S + gp.max_new_tokens)
+        try:
+            pos = torch.arange(S, device=dev, dtype=torch.int32).unsqueeze(0).expand(B, S).contiguous()
+            vals, idx = self.step(ids, pos, lens, decode=False, k=k)
+            out = []
+            tok = self._sample_rows(vals, idx, gp, 0)
             out.append(tok)
-            cur = cur + 1
-        return torch.stack(out, dim=1)
+            cur = lens.clone()
+            for t in range(1, gp.max_new_tokens):
+                # the new token sits at position cur; attention covers cur + 1 keys
+                vals, idx = self.decode_step(tok.to(dev), cur, k, max_ctx=S + t)
+                tok = self._sample_rows(vals, idx, gp, t)
+                out.append(tok)
+                cur = cur + 1
+            return torch.stack(out, dim=1)
+        finally:
+            if self.pages is not None:
+                for b in range(B):
+                    self.pages.release(b)
 
     def _sample_rows(self, vals, idx, gp: GenParams, step: int) -> torch.Tensor:
         cv, ci = self.gather_candidates(vals, idx)

@@ -11,6 +11,10 @@ one scheduler thread owns the model's ``max_batch`` KV-cache slots and runs iter
 3. retire sequences that hit ``max_new_tokens`` or an end-of-sequence id; their slots are free
    for the next iteration's admissions.
 
+With a paged KV cache (``LlamaTP(kv_pages=...)``) a request is admitted only while the page pool
+holds its prompt + ``max_new_tokens`` rows (FIFO: the head of the queue waits for pages rather
+than being overtaken), and its pages return to the pool when it retires.
+
 Each sequence samples with its own parameters and the same seeded rule as a batch-of-one
 ``LlamaTP.generate`` (``pick_token``), so results do not depend on what else is in flight.
 
@@ -85,6 +89,9 @@ class ContinuousLlama:
             raise ValueError("empty prompt")
         if len(ids) + gp.max_new_tokens > self.m.max_seq:
             raise ValueError(f"prompt + max_new_tokens exceeds the {self.m.max_seq}-token KV cache")
+        pages = self.m.pages
+        if pages is not None and pages.pages_for(len(ids) + gp.max_new_tokens) > pages.num_pages - 1:
+            raise ValueError("prompt + max_new_tokens exceeds the whole KV page pool")
         fut: cf.Future = cf.Future()
         with self._wake:
             if self._stop:
@@ -96,8 +103,12 @@ class ContinuousLlama:
         return fut
 
     def stats(self) -> dict:
-        return {"active": sum(s is not None for s in self.slots), "queued": len(self._pending),
-                "iterations": self.iterations, "tokens": self.tokens, "slots": self.B}
+        d = {"active": sum(s is not None for s in self.slots), "queued": len(self._pending),
+             "iterations": self.iterations, "tokens": self.tokens, "slots": self.B}
+        if self.m.pages is not None:
+            d["kv_pages_free"] = self.m.pages.free_pages
+            d["kv_pages"] = self.m.pages.num_pages
+        return d
 
     # ---------------------------------------------------------------- scheduler (rank 0)
     def _take_admissions(self) -> Optional[List[_Seq]]:
@@ -108,10 +119,19 @@ class ContinuousLlama:
                 return None
             free = [i for i, s in enumerate(self.slots) if s is None]
             admit = []
+            pages = self.m.pages
+            budget = pages.free_pages if pages is not None else 0
             while self._pending and free:
-                seq = self._pending.popleft()
+                seq = self._pending[0]
                 if seq.future is not None and seq.future.cancelled():
+                    self._pending.popleft()
                     continue
+                if pages is not None:  # paged KV: admit while the pool holds prompt + budget (FIFO)
+                    need = pages.pages_for(len(seq.ids) + seq.gp.max_new_tokens)
+                    if need > budget:
+                        break
+                    budget -= need
+                self._pending.popleft()
                 seq.slot = free.pop(0)
                 admit.append(seq)
             return admit
@@ -132,6 +152,8 @@ class ContinuousLlama:
                         if s.future is not None and not s.future.done():
                             s.future.set_exception(e)
                         self.slots[i] = None
+                        if self.m.pages is not None:
+                            self.m.pages.release(i)
 
     # ---------------------------------------------------------------- one iteration (all ranks)
     @torch.no_grad()
@@ -140,6 +162,8 @@ class ContinuousLlama:
         if admit:
             for seq in admit:
                 self.slots[seq.slot] = seq
+                if m.pages is not None:  # every rank assigns the same pages (same calls, same order)
+                    m.pages.assign(seq.slot, len(seq.ids) + seq.gp.max_new_tokens)
             S = max(len(s.ids) for s in admit)
             ids = torch.zeros(len(admit), S, dtype=torch.int32)
             for j, s in enumerate(admit):
@@ -179,5 +203,7 @@ class ContinuousLlama:
                 continue
             if len(s.out) >= s.gp.max_new_tokens or (s.out and s.out[-1] in self.eos):
                 self.slots[i] = None
+                if self.m.pages is not None:
+                    self.m.pages.release(i)
                 if s.future is not None and not s.future.done():
                     s.future.set_result(list(s.out))

@@ -809,17 +809,27 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
                      scale: Optional[float] = None, workspace: Optional[torch.Tensor] = None,
                      counters: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
                      positions: Optional[torch.Tensor] = None, cos: Optional[torch.Tensor] = None,
-                     sin: Optional[torch.Tensor] = None, max_len: Optional[int] = None) -> torch.Tensor:
+                     sin: Optional[torch.Tensor] = None, max_len: Optional[int] = None,
+                     page_table: Optional[torch.Tensor] = None) -> torch.Tensor:
     """One query token per sequence vs the cache ``[B, max_len, Hkv, D]``; q rows ``[B, >= Hq*D]``
     (head h at column h*D, e.g. the fused QKV row).  Split-KV, combined in the same launch.
     With ``positions``/``cos``/``sin`` (rope mode) q is the raw fused QKV row: RoPE is applied to q
     and to the new K (row ``lens - 1 == positions``), and the new K/V are appended to the cache.
     ``max_len``: a host-side bound on ``lens`` (default: the cache length) -- it sizes the split grid,
     so a tight bound keeps idle split blocks out of short-context launches; keys beyond it are not
-    visited, so it must be >= every ``lens[b]``."""
+    visited, so it must be >= every ``lens[b]``.
+    Paged KV (``page_table [B, pages_per_seq]`` int32): the caches are page pools ``[pages, chunk,
+    Hkv, D]`` and row ``r`` of sequence ``b`` is row ``r % chunk`` of page ``page_table[b, r // chunk]``."""
     dev = q.device
     B = lens.numel()
-    max_len = k_cache.shape[1] if max_len is None else min(int(max_len), k_cache.shape[1])
+    if page_table is not None:
+        _need(page_table, "page_table", torch.int32, dev)
+        if page_table.dim() != 2 or page_table.shape[0] < B or k_cache.shape[1] != chunk:
+            raise ValueError("paged decode: page_table [>= B, pages_per_seq], caches [pages, chunk, Hkv, D]")
+        cap = page_table.shape[1] * chunk
+        max_len = cap if max_len is None else min(int(max_len), cap)
+    else:
+        max_len = k_cache.shape[1] if max_len is None else min(int(max_len), k_cache.shape[1])
     nsplit = (max_len + chunk - 1) // chunk
     need = B * n_q_heads * nsplit * (head_dim + 2)
     if workspace is None or workspace.numel() < need:
@@ -836,7 +846,8 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
                                     ws.data_ptr(), ws_ml.data_ptr(), counters.data_ptr(), q.stride(0), out.stride(0),
                                     k_cache.stride(0), lens.data_ptr(), _ptr(positions), _ptr(cos), _ptr(sin),
                                     cos.shape[0] if cos is not None else 0, B, n_q_heads, n_kv_heads, head_dim, max_len,
-                                    chunk, float(scale), stream_ptr(dev))
+                                    chunk, float(scale), _ptr(page_table),
+                                    page_table.shape[1] if page_table is not None else 0, stream_ptr(dev))
     check(rc, "mls_decode_attention")
     return out
 

@@ -208,6 +208,8 @@ struct DecodeArgs {
   int q_stride, o_stride;
   long seq_stride;  // elements per sequence in the cache (max_len * Hkv * D)
   const int* lens;
+  const int* page_table;  // paged cache: [B][pages_per_seq] page ids, a page = one split's CHUNK rows
+  int pages_per_seq;
   const int* positions;  // rope mode: query position per sequence (== lens[b] - 1)
   const float* cos_t;    // [max_pos][D/2]
   const float* sin_t;
@@ -270,7 +272,11 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(const DecodeArgs a) {
   MLS_CHECK(!rope || (pos >= 0 && pos < a.max_pos && pos == L0 - 1), 202);
   const bf16* qrow = a.q + (long)b * a.q_stride;
   const long rstride = (long)a.Hkv * D;
-  const long cbase = (long)b * a.seq_stride + (long)hk * D + gl * 8;
+  // row r of this split lives at sbase + r * rstride: contiguous per sequence, or (paged) in the page
+  // the table maps this split to -- a page holds exactly one split's CHUNK rows
+  const long sbase = a.page_table ? ((long)a.page_table[b * a.pages_per_seq + sp] * CHUNK - start) * rstride
+                                  : (long)b * a.seq_stride;
+  const long cbase = sbase + (long)hk * D + gl * 8;
 
   // issue every K/V row load of this block first
   uint4 kraw[NIT], vraw[NIT];
@@ -518,13 +524,16 @@ int mls_flash_attention(const void* q, const void* k, const void* v, void* o, in
 }
 
 // workspace: ws >= B*Hq*nsplit*D floats, ws_ml >= B*Hq*nsplit*2 floats, nsplit = ceil(max_len/chunk);
+// page_table (optional): [B][pages_per_seq] ids of chunk-row pages of the caches (paged KV).
 // counters: B*Hkv zero-initialised ints.  chunk: rows per split (D=128: 16..256; D=64: 32..512).
 // positions/cos/sin non-null: rope mode (q = the fused QKV rows, positions[b] == lens[b] - 1).
 int mls_decode_attention(const void* q, void* k_cache, void* v_cache, void* o, float* ws, float* ws_ml, int* counters,
                          int q_stride, int o_stride, long seq_stride, const int* lens, const int* positions,
                          const float* cos_t, const float* sin_t, int max_pos, int B, int Hq, int Hkv, int D,
-                         int max_len, int chunk, float scale, void* stream) {
+                         int max_len, int chunk, float scale, const int* page_table, int pages_per_seq,
+                         void* stream) {
   if (B <= 0 || Hq % Hkv || chunk <= 0 || max_len <= 0) return MLS_BAD_ARG;
+  if (page_table && (long)pages_per_seq * chunk < max_len) return MLS_BAD_ARG;
   (void)counters;  // reserved (in-launch merge variants); the combine runs as its own launch
   if (positions && (!cos_t || !sin_t)) return MLS_BAD_ARG;
   DecodeArgs a{};
@@ -539,6 +548,8 @@ int mls_decode_attention(const void* q, void* k_cache, void* v_cache, void* o, f
   a.o_stride = o_stride;
   a.seq_stride = seq_stride;
   a.lens = lens;
+  a.page_table = page_table;
+  a.pages_per_seq = pages_per_seq;
   a.positions = positions;
   a.cos_t = cos_t;
   a.sin_t = sin_t;

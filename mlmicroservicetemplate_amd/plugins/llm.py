@@ -57,8 +57,10 @@ class LlamaPlugin(ModelPlugin):
         # every TP rank reads just its own slices from the checkpoint (no weight broadcast needed)
         source = llama.CheckpointSource(s.WEIGHTS, device=dev) if s.WEIGHTS else None
         params = llama.init_llama_shard(cfg, tp, ctx.rank, int(s.SEED), device=dev, source=source)
+        max_batch, max_seq = int(s.MAX_BATCH) or 32, int(extra.get("max_seq", 2048))
+        kv_pages = self._kv_pages(extra.get("kv_pages", 0), cfg, tp, max_batch, max_seq, dev)
         self.model = llama.LlamaTP(params, cfg, tp=tp, rank=ctx.rank, comm=llama.TPComm(None, tp, device=dev), backend=backend,
-                                   device=dev, max_batch=int(s.MAX_BATCH) or 32, max_seq=int(extra.get("max_seq", 2048)))
+                                   device=dev, max_batch=max_batch, max_seq=max_seq, kv_pages=kv_pages)
         self.tok = llama.LlamaTokenizer(cfg, extra.get("tokenizer_file"))
         self.cfg = cfg
         self.engine = None
@@ -70,6 +72,26 @@ class LlamaPlugin(ModelPlugin):
             if ctx.rank == 0:
                 self.engine.start()
         logger.info("llama ready: tp=%d rank=%d backend=%s device=%s", tp, ctx.rank, backend, dev)
+
+    @staticmethod
+    def _kv_pages(spec, cfg, tp, max_batch, max_seq, dev) -> int:
+        """MODEL_CONFIG ``kv_pages``: 0 = per-slot caches (``max_batch x max_seq`` rows), N = a
+        shared pool of N 64-row pages, ``auto`` = as many pages as half the free HBM holds, capped
+        at what ``max_batch`` full-length sequences could use (+ the scratch page).  TP ranks must
+        agree (the scheduler's admissions assume identical pools): ``auto`` is sized from rank
+        0's free memory only when every rank sees the same, so prefer an explicit N under TP."""
+        if spec in (0, "0", None, ""):
+            return 0
+        full = max_batch * -(-max_seq // 64) + 1
+        if str(spec) != "auto":
+            return int(spec)
+        from ..models.llama import shard_dims
+
+        page_bytes = cfg.layers * 2 * 64 * shard_dims(cfg, tp, 0).hkv * cfg.head_dim * 2
+        if torch.device(dev).type != "cuda":
+            return full
+        free, _total = torch.cuda.mem_get_info(torch.device(dev))
+        return max(2, min(full, int(free * 0.5) // page_bytes))
 
     # ------------------------------------------------------------------ request path
     def prepare_generate(self, req: dict) -> Tuple[List[int], Any]:

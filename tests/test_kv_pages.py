@@ -1,0 +1,112 @@
+"""Paged KV cache (models/kv_pages.py) on CPU: the page allocator's accounting, paged generate()
+reproducing the contiguous cache exactly (reference backend), and continuous batching admitting
+requests by free pages -- a pool far smaller than ``max_batch x max_seq`` serves them all."""
+import time
+
+import pytest
+import torch
+
+from mlmicroservicetemplate_amd.models.kv_pages import OutOfPages, PageTable
+from mlmicroservicetemplate_amd.models.llama import GenParams, LlamaTP, init_llama_shard, tiny_config
+from mlmicroservicetemplate_amd.models.llama_serving import ContinuousLlama
+
+CFG = dict(vocab=2048, hidden=256, layers=2, heads=8, kv_heads=4, head_dim=32, intermediate=512)
+
+
+@pytest.fixture(scope="module")
+def params():
+    torch.set_num_threads(1)
+    cfg = tiny_config(**CFG)
+    return cfg, init_llama_shard(cfg, 1, 0, seed=4)
+
+
+def test_page_table_accounting():
+    pt = PageTable(num_pages=6, page_rows=64, max_batch=3, pages_per_seq=4)
+    assert pt.free_pages == 5  # page 0 is the scratch page
+    pt.assign(0, 100)  # 2 pages
+    pt.assign(1, 64)  # 1 page
+    assert pt.free_pages == 2 and len(pt.pages_of(0)) == 2 and 0 not in pt.pages_of(0) + pt.pages_of(1)
+    pt.assign(0, 120)  # still 2 pages: no change
+    assert pt.free_pages == 2
+    assert not pt.can_fit(64 * 3) and pt.can_fit(64 * 4, slot=0)
+    with pytest.raises(OutOfPages):
+        pt.assign(2, 64 * 3)
+    assert pt.free_pages == 2 and pt.pages_of(2) == []  # a failed assign changes nothing
+    with pytest.raises(ValueError):
+        pt.assign(2, 64 * 5)  # beyond pages_per_seq
+    pt.release(0)
+    assert pt.free_pages == 4 and pt.host[0].tolist() == [0, 0, 0, 0]
+    pt.assign(2, 256)
+    assert sorted(pt.pages_of(2) + pt.pages_of(1)) == [1, 2, 3, 4, 5]
+
+
+def test_page_rows_mapping():
+    pt = PageTable(num_pages=8, page_rows=4, max_batch=2, pages_per_seq=3)
+    pt.assign(1, 10)
+    pages = pt.pages_of(1)
+    pos = torch.arange(10)
+    rows = pt.rows(torch.ones(10, dtype=torch.long), pos)
+    want = [pages[p // 4] * 4 + p % 4 for p in range(10)]
+    assert rows.tolist() == want
+    # unassigned slot -> the scratch page
+    assert pt.rows(torch.zeros(3, dtype=torch.long), torch.arange(3)).tolist() == [0, 1, 2]
+
+
+def test_paged_generate_matches_contiguous(params):
+    cfg, p = params
+    g = torch.Generator().manual_seed(3)
+    ids = torch.randint(3, 2000, (3, 70), generator=g)
+    lens = torch.tensor([70, 41, 5])
+    for gp in (GenParams(max_new_tokens=9), GenParams(9, top_k=8, temperature=0.7, seed=2)):
+        want = LlamaTP(p, cfg, max_batch=3, max_seq=192).generate(ids, lens, gp)
+        paged = LlamaTP(p, cfg, max_batch=3, max_seq=192, kv_pages=7)
+        got = paged.generate(ids, lens, gp)
+        assert torch.equal(got, want)
+        assert paged.pages.free_pages == 6  # released afterwards
+
+
+def test_continuous_batching_admits_by_pages(params):
+    """6 slots but pages for only ~2 requests at a time: everything queues behind the pool and
+    still matches a batch-of-one generate()."""
+    cfg, p = params
+    m = LlamaTP(p, cfg, max_batch=6, max_seq=256, kv_pages=5)  # 4 data pages of 64 rows
+    eng = ContinuousLlama(m).start()
+    g = torch.Generator().manual_seed(1)
+    reqs = []
+    for i in range(6):
+        n = int(torch.randint(65, 110, (1,), generator=g))  # + <= 7 new: 2 pages each
+        ids = torch.randint(3, 2000, (n,), generator=g).tolist()
+        reqs.append((ids, GenParams(max_new_tokens=int(torch.randint(2, 8, (1,), generator=g)), seed=i)))
+    futs = [eng.submit(ids, gp) for ids, gp in reqs]
+    peak = 0
+    while not all(f.done() for f in futs):
+        peak = max(peak, eng.stats()["active"])
+        time.sleep(0.002)
+    outs = [f.result(timeout=60) for f in futs]
+    eng.stop()
+    assert peak <= 2  # each request needs 2 pages of the 4
+    eos = set(cfg.eos_ids)
+    for (ids, gp), got in zip(reqs, outs):
+        single = LlamaTP(p, cfg, max_batch=1, max_seq=256)
+        want = single.generate(torch.tensor([ids]), torch.tensor([len(ids)]), gp)[0].tolist()
+        cut = next((i + 1 for i, t in enumerate(want) if t in eos), len(want))
+        assert got == want[:cut]
+    st = eng.stats()
+    assert st["kv_pages_free"] == 4 and st["active"] == 0
+
+
+def test_paged_submit_rejects_requests_larger_than_the_pool(params):
+    cfg, p = params
+    m = LlamaTP(p, cfg, max_batch=2, max_seq=512, kv_pages=3)
+    eng = ContinuousLlama(m)
+    with pytest.raises(ValueError):
+        eng.submit(list(range(3, 200)), GenParams(8))  # 205 rows = 4 pages > 2 data pages
+
+
+def test_plugin_kv_pages_setting():
+    from mlmicroservicetemplate_amd.plugins.llm import LlamaPlugin
+
+    cfg = tiny_config(**CFG)
+    assert LlamaPlugin._kv_pages(0, cfg, 1, 8, 1024, "cpu") == 0
+    assert LlamaPlugin._kv_pages("12", cfg, 1, 8, 1024, "cpu") == 12
+    assert LlamaPlugin._kv_pages("auto", cfg, 1, 8, 1000, "cpu") == 8 * 16 + 1  # full coverage + scratch

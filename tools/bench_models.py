@@ -73,12 +73,20 @@ def bench_llama(args):
     p = init_llama_shard(LLAMA3_8B, tp, 0, seed=0, device=dev)
     comm = ShardEmulationComm(tp) if tp > 1 else None
     m = LlamaTP(p, LLAMA3_8B, tp=tp, rank=0, comm=comm, backend="fused", device=dev, max_batch=max(args.batches),
-                max_seq=2048)
+                max_seq=2048, kv_pages=args.kv_pages)
+    if m.pages is not None and args.shuffle_pages:  # pages scattered as in a long-running server
+        import random
+
+        random.Random(0).shuffle(m.pages._free)
     print(json.dumps({"bench": "llama3-8b", "tp": tp, "collectives": "stubbed" if tp > 1 else "none",
-                      "skinny_max_split": args.skinny_max_split,
+                      "skinny_max_split": args.skinny_max_split, "kv_pages": args.kv_pages,
                       "init_s": round(time.time() - t0, 1)}), flush=True)
     for B in args.batches:
         S = args.prompt
+        if m.pages is not None:
+            m.pages.reset()
+            for b in range(B):
+                m.pages.assign(b, S + 1)
         ids = torch.randint(1000, 100000, (B, S), device=dev, dtype=torch.int32)
         lens = torch.full((B,), S, device=dev, dtype=torch.int32)
         pos = torch.arange(S, device=dev, dtype=torch.int32).unsqueeze(0).expand(B, S).contiguous()
@@ -101,7 +109,7 @@ def bench_llama(args):
             m.decode_step(tok, cur, 1, max_ctx=S + 1)
         torch.cuda.synchronize()
         dec = (time.perf_counter() - t2) / n
-        print(json.dumps({"bench": "llama3-8b", "tp": tp, "batch": B, "prompt": S,
+        print(json.dumps({"bench": "llama3-8b", "tp": tp, "batch": B, "prompt": S, "kv_pages": args.kv_pages,
                           "prefill_ms": round(pre * 1e3, 2), "prefill_tok_s": round(B * S / pre, 1),
                           "decode_ms_per_step": round(dec * 1e3, 3), "decode_tok_s": round(B / dec, 1)}), flush=True)
 
@@ -115,7 +123,7 @@ def bench_llama_serve(args):
     dev = torch.device("cuda:0")
     B = args.batches[0]
     p = init_llama_shard(LLAMA3_8B, 1, 0, seed=0, device=dev)
-    m = LlamaTP(p, LLAMA3_8B, backend="fused", device=dev, max_batch=B, max_seq=2048)
+    m = LlamaTP(p, LLAMA3_8B, backend="fused", device=dev, max_batch=B, max_seq=2048, kv_pages=args.kv_pages)
     eng = ContinuousLlama(m).start()
     rng = np.random.default_rng(0)
     warm = [eng.submit(rng.integers(1000, 100000, args.prompt).tolist(), GenParams(4)) for _ in range(B)]
@@ -130,7 +138,7 @@ def bench_llama_serve(args):
     dt = time.perf_counter() - t0
     toks = sum(len(f.result()) for f in futs)
     eng.stop()
-    print(json.dumps({"bench": "llama3-8b-continuous", "max_batch": B, "requests": args.requests,
+    print(json.dumps({"bench": "llama3-8b-continuous", "max_batch": B, "kv_pages": args.kv_pages, "requests": args.requests,
                       "prompt": args.prompt, "new_tokens": args.new, "tokens_per_s": round(toks / dt, 1),
                       "requests_per_s": round(args.requests / dt, 2), "p50_latency_s": round(float(np.median(lat)), 3),
                       "iterations": eng.iterations}), flush=True)
@@ -149,6 +157,8 @@ def main():
     ap.add_argument("--backends", nargs="+", default=["fused", "eager"], help="bert: which implementations")
     ap.add_argument("--emulate-tp", type=int, default=1)
     ap.add_argument("--skinny-max-split", type=int, default=0)
+    ap.add_argument("--kv-pages", type=int, default=0, help="llama: paged KV pool of N 64-row pages (0: per-slot)")
+    ap.add_argument("--shuffle-pages", action="store_true", help="llama: hand out pages in random order")
     args = ap.parse_args()
     if args.skinny_max_split:
         from mlmicroservicetemplate_amd.ops import _lib
