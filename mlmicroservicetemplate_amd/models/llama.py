@@ -370,6 +370,7 @@ class LlamaTP:
             self.packed: Dict[str, torch.Tensor] = {}
             self.pk_variant = int(os.environ.get("MLS_PACKED_VARIANT", "9"))
             self.pk_fold = os.environ.get("MLS_PACKED_FOLD", "1") == "1"
+            self.fuse_combine = os.environ.get("MLS_FUSE_COMBINE", "1") == "1"
             mode = os.environ.get("MLS_PACKED_DECODE", "auto")
             if self.device.type == "cuda" and mode != "0":
                 names = [f"l{i}.{n}" for i in range(cfg.layers) for n in ("qkv", "o", "gate_up", "down")]
@@ -547,6 +548,12 @@ class LlamaTP:
         # the next pre-norm GEMM reads one activation stream instead of two (r + delta) and writes no
         # residual copy.  With TP > 1 the add has to wait for the all-reduce.
         fold = self.tp == 1 and bool(packed) and self.pk_fold
+        # decode: the o-projection merges the split-KV partials in its prologue (one launch instead of
+        # two) while every block's share of partials is small -- B x local q heads <= 32: one emulated
+        # TP = 8 rank 1.166 -> 1.125 ms/token at batch 1, 1.294 -> 1.254 at 4; TP = 1 batch 1 level,
+        # batch 4 (128 head rows per block) 3.17 -> 3.37, so off there (profiles/r2_llama8b_fused_combine_ab.jsonl)
+        fuse_combine = (decode and self.fuse_combine and "l0.o" in packed and B <= 4
+                        and B * sd.hq <= 32 and B * sd.hq * D * 2 <= 65536)
 
         def linear(x, name, residual=None):
             if name in packed:
@@ -570,20 +577,34 @@ class LlamaTP:
 
         for i in range(cfg.layers):
             qkv, r = pre_norm(r, f"l{i}.qkv", delta)
+            parts = None
             if decode:  # RoPE + KV append ride inside the decode-attention launch
+                kw = dict(workspace=self.dec_ws, counters=self.dec_cnt, positions=pos, cos=self.cos, sin=self.sin,
+                          max_len=self._dec_ctx, combine=not fuse_combine)
                 if self.pages is not None:
                     a = ops.decode_attention(qkv, self.k_cache[i], self.v_cache[i], lens, sd.hq, sd.hkv, D,
-                                             workspace=self.dec_ws, counters=self.dec_cnt, positions=pos,
-                                             cos=self.cos, sin=self.sin, max_len=self._dec_ctx, chunk=self.page_rows,
-                                             page_table=self.pages.dev[:B])
+                                             chunk=self.page_rows, page_table=self.pages.dev[:B], **kw)
                 else:
                     a = ops.decode_attention(qkv, self.k_cache[i][:B], self.v_cache[i][:B], lens, sd.hq, sd.hkv,
-                                             D, workspace=self.dec_ws, counters=self.dec_cnt, positions=pos,
-                                             cos=self.cos, sin=self.sin, max_len=self._dec_ctx, chunk=dec_chunk)
+                                             D, chunk=dec_chunk, **kw)
+                if fuse_combine:
+                    a, parts = a
             else:
                 ops.rope_kv_(qkv, pos, self.cos, self.sin, sd.hq, sd.hkv, D, explicit_slots, self.k_cache[i],
                              self.v_cache[i], lens=lens, seq=S, max_seq=self.max_seq)
                 a = ops.flash_attention(qkv, B, S, sd.hq, sd.hkv, D, kv_lens=lens, causal=True)
+            if parts is not None:  # split-KV combine in the o-projection's prologue (one launch, not two)
+                o_w = p[f"l{i}.o"]
+                o = ops.skinny_packed_combine(a, parts, packed[f"l{i}.o"], o_w.shape[0], residual=r if fold else None,
+                                              variant=self.pk_variant)
+                if fold:
+                    gu, _ = pre_norm(o, f"l{i}.gate_up", None, act=ops.ACT_SILU_MUL)
+                    r = linear(gu, f"l{i}.down", residual=o)
+                    continue
+                o = self.comm.all_reduce_(o)
+                gu, r = pre_norm(r, f"l{i}.gate_up", o, act=ops.ACT_SILU_MUL)
+                delta = self.comm.all_reduce_(linear(gu, f"l{i}.down"))
+                continue
             if fold:
                 h = linear(a, f"l{i}.o", residual=r)
                 gu, _ = pre_norm(h, f"l{i}.gate_up", None, act=ops.ACT_SILU_MUL)

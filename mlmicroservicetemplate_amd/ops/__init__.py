@@ -810,7 +810,7 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
                      counters: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
                      positions: Optional[torch.Tensor] = None, cos: Optional[torch.Tensor] = None,
                      sin: Optional[torch.Tensor] = None, max_len: Optional[int] = None,
-                     page_table: Optional[torch.Tensor] = None) -> torch.Tensor:
+                     page_table: Optional[torch.Tensor] = None, combine: bool = True):
     """One query token per sequence vs the cache ``[B, max_len, Hkv, D]``; q rows ``[B, >= Hq*D]``
     (head h at column h*D, e.g. the fused QKV row).  Split-KV, combined in the same launch.
     With ``positions``/``cos``/``sin`` (rope mode) q is the raw fused QKV row: RoPE is applied to q
@@ -819,7 +819,9 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
     so a tight bound keeps idle split blocks out of short-context launches; keys beyond it are not
     visited, so it must be >= every ``lens[b]``.
     Paged KV (``page_table [B, pages_per_seq]`` int32): the caches are page pools ``[pages, chunk,
-    Hkv, D]`` and row ``r`` of sequence ``b`` is row ``r % chunk`` of page ``page_table[b, r // chunk]``."""
+    Hkv, D]`` and row ``r`` of sequence ``b`` is row ``r % chunk`` of page ``page_table[b, r // chunk]``.
+    ``combine=False``: multi-split rows are left as fp32 partials for the consumer GEMM to merge
+    (:func:`skinny_packed_combine`); returns ``(out, DecodePartials)``."""
     dev = q.device
     B = lens.numel()
     if page_table is not None:
@@ -847,8 +849,45 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
                                     k_cache.stride(0), lens.data_ptr(), _ptr(positions), _ptr(cos), _ptr(sin),
                                     cos.shape[0] if cos is not None else 0, B, n_q_heads, n_kv_heads, head_dim, max_len,
                                     chunk, float(scale), _ptr(page_table),
-                                    page_table.shape[1] if page_table is not None else 0, stream_ptr(dev))
+                                    page_table.shape[1] if page_table is not None else 0, int(not combine),
+                                    stream_ptr(dev))
     check(rc, "mls_decode_attention")
+    if not combine:
+        return out, DecodePartials(ws, ws_ml, nsplit, chunk, lens, n_q_heads, head_dim)
+    return out
+
+
+class DecodePartials:
+    """Split-KV decode attention partials left for a consumer to merge (see ``combine=False``)."""
+
+    def __init__(self, ws, ws_ml, nsplit, chunk, lens, n_q_heads, head_dim):
+        self.ws, self.ws_ml, self.nsplit, self.chunk = ws, ws_ml, int(nsplit), int(chunk)
+        self.lens, self.n_q_heads, self.head_dim = lens, int(n_q_heads), int(head_dim)
+
+
+def skinny_packed_combine(attn_out: torch.Tensor, parts: DecodePartials, wp: torch.Tensor, N: int, *,
+                          bias: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
+                          variant: int = 9) -> torch.Tensor:
+    """``merge(attention partials) @ W^T (+ bias) (+ residual)`` with W packed (:func:`pack_skinny`):
+    the o-projection of a decode step that also does the split-KV combine in its prologue (one
+    launch instead of two).  ``attn_out``: the attention's direct-written rows ``[M, Hq*D]``."""
+    dev = attn_out.device
+    _need(attn_out, "attn_out", torch.bfloat16, dev)
+    M, K = attn_out.shape
+    if M > 4 or K != parts.n_q_heads * parts.head_dim or wp.numel() != N * K or M * K * 2 > 65536:
+        raise ValueError("skinny_packed_combine: M <= 4, K == Hq * D, M * K * 2 <= 64 KiB, wp of N*K elements")
+    if residual is not None:
+        _need(residual, "residual", torch.bfloat16, dev)
+        if tuple(residual.shape) != (M, N):
+            raise ValueError("residual must be [M, N]")
+    if bias is not None:
+        _need(bias, "bias", torch.float32, dev)
+    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    rc = lib().mls_skinny_packed_combine(attn_out.data_ptr(), parts.ws.data_ptr(), parts.ws_ml.data_ptr(),
+                                         parts.lens.data_ptr(), parts.nsplit, parts.chunk, parts.n_q_heads,
+                                         parts.head_dim, wp.data_ptr(), _ptr(bias), _ptr(residual), out.data_ptr(),
+                                         M, N, K, ACT_NONE, int(variant), stream_ptr(dev))
+    check(rc, "mls_skinny_packed_combine")
     return out
 
 

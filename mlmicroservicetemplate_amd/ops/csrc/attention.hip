@@ -525,13 +525,15 @@ int mls_flash_attention(const void* q, const void* k, const void* v, void* o, in
 
 // workspace: ws >= B*Hq*nsplit*D floats, ws_ml >= B*Hq*nsplit*2 floats, nsplit = ceil(max_len/chunk);
 // page_table (optional): [B][pages_per_seq] ids of chunk-row pages of the caches (paged KV).
+// skip_combine: leave multi-split rows as partials in ws / ws_ml (a consumer merges them, e.g.
+// mls_skinny_packed_combine); rows that fit one split are still written to `o`.
 // counters: B*Hkv zero-initialised ints.  chunk: rows per split (D=128: 16..256; D=64: 32..512).
 // positions/cos/sin non-null: rope mode (q = the fused QKV rows, positions[b] == lens[b] - 1).
 int mls_decode_attention(const void* q, void* k_cache, void* v_cache, void* o, float* ws, float* ws_ml, int* counters,
                          int q_stride, int o_stride, long seq_stride, const int* lens, const int* positions,
                          const float* cos_t, const float* sin_t, int max_pos, int B, int Hq, int Hkv, int D,
                          int max_len, int chunk, float scale, const int* page_table, int pages_per_seq,
-                         void* stream) {
+                         int skip_combine, void* stream) {
   if (B <= 0 || Hq % Hkv || chunk <= 0 || max_len <= 0) return MLS_BAD_ARG;
   if (page_table && (long)pages_per_seq * chunk < max_len) return MLS_BAD_ARG;
   (void)counters;  // reserved (in-launch merge variants); the combine runs as its own launch
@@ -579,12 +581,14 @@ int mls_decode_attention(const void* q, void* k_cache, void* v_cache, void* o, f
     else if (G == 4) { DEC(128, 4) }
     else if (G == 8) { DEC(128, 8) }
     else return MLS_UNSUPPORTED;
-    if (a.nsplit > 1) hipLaunchKernelGGL(decode_combine_kernel<128>, dim3(B * Hq), dim3(128), 0, st, a, chunk);
+    if (a.nsplit > 1 && !skip_combine)
+      hipLaunchKernelGGL(decode_combine_kernel<128>, dim3(B * Hq), dim3(128), 0, st, a, chunk);
   } else if (D == 64) {
     if (G == 1) { DEC(64, 1) }
     else if (G == 4) { DEC(64, 4) }
     else return MLS_UNSUPPORTED;
-    if (a.nsplit > 1) hipLaunchKernelGGL(decode_combine_kernel<64>, dim3(B * Hq), dim3(64), 0, st, a, chunk);
+    if (a.nsplit > 1 && !skip_combine)
+      hipLaunchKernelGGL(decode_combine_kernel<64>, dim3(B * Hq), dim3(64), 0, st, a, chunk);
   } else {
     return MLS_UNSUPPORTED;
   }

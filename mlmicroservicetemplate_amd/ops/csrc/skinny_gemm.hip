@@ -33,11 +33,18 @@ struct SkArgs {
   int M, N, K, lda, ldo, act, nsplit, ksteps_per_split, norm;
   float eps;
   uint32_t a_bytes, w_bytes;
+  // FUSE_COMBINE (packed LDS kernel): A = the split-KV decode attention's merged output, combined
+  // here from its fp32 partials (o [M][Hq][nsplit][D], (m, l) [M][Hq][nsplit][2]); rows whose
+  // sequence fit one split were written to `a` directly by the attention kernel
+  const float* cws;
+  const float* cml;
+  const int* lens;
+  int c_nsplit, c_chunk, c_hq, c_hd;
 };
 
 // fusion modes of the A prologue (template parameter, so the unrolled k loop has no runtime
 // branches -- a branch there makes hipcc drain vmcnt(0) per k-step, cdna_hip_programming.md item 4c)
-enum { FUSE_NONE = 0, FUSE_NORM = 1, FUSE_ADD_NORM = 2 };
+enum { FUSE_NONE = 0, FUSE_NORM = 1, FUSE_ADD_NORM = 2, FUSE_COMBINE = 3 };
 
 MLS_DEV uint4 add_round(uint4 a, uint4 b) {  // bf16 + bf16 -> bf16 (the residual stream's precision)
   float x[8], y[8];
@@ -234,25 +241,81 @@ __global__ __launch_bounds__(NWV * 64) void skinny_lds_kernel(const SkArgs s) {
   load_trip(ks, wnext);  // in flight during the prologue
 
   // prologue: A (+ A2) -> LDS, residual write-back (column-tile-0 blocks), square sums
+  constexpr bool NORM = FUSE == FUSE_NORM || FUSE == FUSE_ADD_NORM;
   if (tid < 4) ssq_s[tid] = 0.f;
   __syncthreads();
   float part[4] = {0.f, 0.f, 0.f, 0.f};
   const bool wr_res = FUSE == FUSE_ADD_NORM && s.a_out && blockIdx.x == 0;
+  int lens4[4] = {0, 0, 0, 0};
+  if constexpr (FUSE == FUSE_COMBINE) {
+    // block-uniform reads (scalar loads): they do not queue behind the weight loads in flight
+#pragma unroll
+    for (int mm = 0; mm < 4; ++mm) lens4[mm] = mm < s.M ? __builtin_nontemporal_load(s.lens + mm) : 0;
+  }
   for (int q = tid; q < s.M * kch; q += NWV * 64) {
     const int m = q / kch, c = q - m * kch;
-    uint4 v = ld16(s.a + (size_t)m * s.lda + c * 8);
+    uint4 v;
+    if constexpr (FUSE == FUSE_COMBINE) {
+      // the decode_combine_kernel arithmetic for this row's 8 dims of one head
+      const int h = (c * 8) / s.c_hd, d0 = (c * 8) % s.c_hd;
+      const int L = m == 0 ? lens4[0] : m == 1 ? lens4[1] : m == 2 ? lens4[2] : lens4[3];
+      const int ns = min(s.c_nsplit, (L + s.c_chunk - 1) / s.c_chunk);
+      if (ns <= 1) {
+        v = ld16(s.a + (size_t)m * s.lda + c * 8);
+      } else {
+        const long rec = ((long)m * s.c_hq + h) * s.c_nsplit;
+        // online merge in groups of 4 splits: each group's (m, l, o) loads are issued together
+        // (one memory round trip per group, not two per split)
+        float mx = -INFINITY, l = 0.f, o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int s0 = 0; s0 < ns; s0 += 4) {
+          float2 ml[4];
+          float4 x0[4], x1[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const bool in = s0 + j < ns;
+            const long r = rec + (in ? s0 + j : 0);
+            ml[j] = in ? *reinterpret_cast<const float2*>(s.cml + r * 2) : make_float2(-INFINITY, 0.f);
+            x0[j] = in ? *reinterpret_cast<const float4*>(s.cws + r * s.c_hd + d0) : make_float4(0.f, 0.f, 0.f, 0.f);
+            x1[j] = in ? *reinterpret_cast<const float4*>(s.cws + r * s.c_hd + d0 + 4)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+          float gm = mx;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) gm = fmaxf(gm, ml[j].x);
+          if (gm == -INFINITY) continue;
+          const float al = __builtin_amdgcn_exp2f(mx - gm);
+          l *= al;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] *= al;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float w = __builtin_amdgcn_exp2f(ml[j].x - gm);
+            l += ml[j].y * w;
+            o[0] += x0[j].x * w; o[1] += x0[j].y * w; o[2] += x0[j].z * w; o[3] += x0[j].w * w;
+            o[4] += x1[j].x * w; o[5] += x1[j].y * w; o[6] += x1[j].z * w; o[7] += x1[j].w * w;
+          }
+          mx = gm;
+        }
+        const float inv = l > 0.f ? 1.f / l : 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] *= inv;
+        v = pack8(o);
+      }
+    } else {
+      v = ld16(s.a + (size_t)m * s.lda + c * 8);
+    }
     if constexpr (FUSE == FUSE_ADD_NORM) {
       v = add_round(v, ld16(s.a2 + (size_t)m * s.lda + c * 8));
       if (wr_res) st16(s.a_out + (size_t)m * s.lda + c * 8, v);
     }
     a_lds[q] = v;
-    if constexpr (FUSE != FUSE_NONE) {
+    if constexpr (NORM) {
       const float sq = sumsq8(v);
 #pragma unroll
       for (int mm = 0; mm < 4; ++mm) part[mm] += mm == m ? sq : 0.f;
     }
   }
-  if constexpr (FUSE != FUSE_NONE) {
+  if constexpr (NORM) {
 #pragma unroll
     for (int mm = 0; mm < 4; ++mm) {
       const float t = wave_sum(part[mm]);
@@ -331,49 +394,127 @@ __global__ __launch_bounds__(NWV * 64) void skinny_packed_kernel(const SkArgs s)
   extern __shared__ __attribute__((aligned(16))) uint4 a_lds[];  // [M][K/8]
   __shared__ float red[NWV][16][17];
   __shared__ float ssq_s[4];
+  constexpr int T = NWV * 64;
+  constexpr bool NORM = FUSE == FUSE_NORM || FUSE == FUSE_ADD_NORM;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int nr = lane & 15, g = lane >> 4;
   const int n0 = blockIdx.x * 16;
   const int ksteps = s.K >> 5;
   const int kch = s.K >> 3;
+  const int nq = s.M * kch;
   const int kpw = (ksteps + NWV - 1) / NWV;
   const int kb = wid * kpw, ke = min(ksteps, kb + kpw);
   const rsrc_t wr = make_rsrc(s.w, s.w_bytes);
+  const rsrc_t ar = make_rsrc(s.a, s.a_bytes);
+  const rsrc_t a2r = make_rsrc(s.a2, FUSE == FUSE_ADD_NORM ? s.a_bytes : 0);
   const int wbase = blockIdx.x * ksteps * 1024 + lane * 16;
 
   auto load_trip = [&](int ks0, uint4 (&wv)[UNROLL]) {
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) wv[u] = bload16_pol<NTL>(wr, ks0 + u < ke ? wbase + (ks0 + u) * 1024 : OOB);
   };
+  // The first QPT A (+ A2) chunks per thread -- all of A up to 2048 chunks, e.g. 4 rows at K = 4096
+  // -- are loaded BEFORE the first weight trip: the vector memory counter retires in order, so
+  // consuming them then does not wait for the weights, and the barriers below are LDS-only (a
+  // __syncthreads would drain the weight loads too).  Larger A goes through the loop after.
+  constexpr int QPT = 2048 / T;
+  uint4 a0[QPT], a20[QPT];
+#pragma unroll
+  for (int j = 0; j < QPT; ++j) {
+    const int q = tid + j * T;
+    const int m = q / kch, c = q - m * kch;
+    const int off = q < nq ? (m * s.lda + c * 8) * 2 : OOB;
+    a0[j] = bload16(ar, off);
+    if constexpr (FUSE == FUSE_ADD_NORM) a20[j] = bload16(a2r, off);
+  }
   uint4 wnext[UNROLL];
   load_trip(kb, wnext);  // in flight during the prologue
 
   if (tid < 4) ssq_s[tid] = 0.f;
-  __syncthreads();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
   float part[4] = {0.f, 0.f, 0.f, 0.f};
   const bool wr_res = FUSE == FUSE_ADD_NORM && s.a_out && blockIdx.x == 0;
-  for (int q = tid; q < s.M * kch; q += NWV * 64) {
+  int lens4[4] = {0, 0, 0, 0};
+  if constexpr (FUSE == FUSE_COMBINE) {
+    // block-uniform reads (scalar loads): they do not queue behind the weight loads in flight
+#pragma unroll
+    for (int mm = 0; mm < 4; ++mm) lens4[mm] = mm < s.M ? __builtin_nontemporal_load(s.lens + mm) : 0;
+  }
+  auto stage = [&](int q, uint4 v, uint4 v2) {
     const int m = q / kch, c = q - m * kch;
-    uint4 v = ld16(s.a + (size_t)m * s.lda + c * 8);
+    if constexpr (FUSE == FUSE_COMBINE) {
+      // the decode_combine_kernel arithmetic for this row's 8 dims of one head
+      const int h = (c * 8) / s.c_hd, d0 = (c * 8) % s.c_hd;
+      const int L = m == 0 ? lens4[0] : m == 1 ? lens4[1] : m == 2 ? lens4[2] : lens4[3];
+      const int ns = min(s.c_nsplit, (L + s.c_chunk - 1) / s.c_chunk);
+      if (ns > 1) {
+        const long rec = ((long)m * s.c_hq + h) * s.c_nsplit;
+        // online merge in groups of 4 splits: each group's (m, l, o) loads are issued together
+        float mx = -INFINITY, l = 0.f, o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int s0 = 0; s0 < ns; s0 += 4) {
+          float2 ml[4];
+          float4 x0[4], x1[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const bool in = s0 + j < ns;
+            const long r = rec + (in ? s0 + j : 0);
+            ml[j] = in ? *reinterpret_cast<const float2*>(s.cml + r * 2) : make_float2(-INFINITY, 0.f);
+            x0[j] = in ? *reinterpret_cast<const float4*>(s.cws + r * s.c_hd + d0) : make_float4(0.f, 0.f, 0.f, 0.f);
+            x1[j] = in ? *reinterpret_cast<const float4*>(s.cws + r * s.c_hd + d0 + 4)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+          float gm = mx;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) gm = fmaxf(gm, ml[j].x);
+          if (gm == -INFINITY) continue;
+          const float al = __builtin_amdgcn_exp2f(mx - gm);
+          l *= al;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] *= al;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float w = __builtin_amdgcn_exp2f(ml[j].x - gm);
+            l += ml[j].y * w;
+            o[0] += x0[j].x * w; o[1] += x0[j].y * w; o[2] += x0[j].z * w; o[3] += x0[j].w * w;
+            o[4] += x1[j].x * w; o[5] += x1[j].y * w; o[6] += x1[j].z * w; o[7] += x1[j].w * w;
+          }
+          mx = gm;
+        }
+        const float inv = l > 0.f ? 1.f / l : 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] *= inv;
+        v = pack8(o);
+      }
+    }
     if constexpr (FUSE == FUSE_ADD_NORM) {
-      v = add_round(v, ld16(s.a2 + (size_t)m * s.lda + c * 8));
+      v = add_round(v, v2);
       if (wr_res) st16(s.a_out + (size_t)m * s.lda + c * 8, v);
     }
     a_lds[q] = v;
-    if constexpr (FUSE != FUSE_NONE) {
+    if constexpr (NORM) {
       const float sq = sumsq8(v);
 #pragma unroll
       for (int mm = 0; mm < 4; ++mm) part[mm] += mm == m ? sq : 0.f;
     }
+  };
+#pragma unroll
+  for (int j = 0; j < QPT; ++j)
+    if (tid + j * T < nq) stage(tid + j * T, a0[j], a20[j]);
+  for (int q = tid + QPT * T; q < nq; q += T) {
+    const int m = q / kch, c = q - m * kch;
+    stage(q, ld16(s.a + (size_t)m * s.lda + c * 8),
+          FUSE == FUSE_ADD_NORM ? ld16(s.a2 + (size_t)m * s.lda + c * 8) : make_uint4(0, 0, 0, 0));
   }
-  if constexpr (FUSE != FUSE_NONE) {
+  if constexpr (NORM) {
 #pragma unroll
     for (int mm = 0; mm < 4; ++mm) {
       const float t = wave_sum(part[mm]);
       if (lane == 0 && mm < s.M) atomicAdd(&ssq_s[mm], t);
     }
   }
-  __syncthreads();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
 
   f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
   const bool arow = nr < s.M;
@@ -399,7 +540,7 @@ __global__ __launch_bounds__(NWV * 64) void skinny_packed_kernel(const SkArgs s)
     float v = 0.f;
 #pragma unroll
     for (int w = 0; w < NWV; ++w) v += red[w][m][c];
-    const float rs = FUSE != FUSE_NONE ? rsqrtf(ssq_s[m] / (float)s.K + s.eps) : 1.f;
+    const float rs = NORM ? rsqrtf(ssq_s[m] / (float)s.K + s.eps) : 1.f;
     const int n = n0 + c;
     v *= rs;
     if (glu) {
@@ -815,6 +956,42 @@ int mls_skinny_packed(const void* A, const void* A2, void* A_out, const void* Wp
     default: MLS_SKP(8, 8, 1) break;  // 1: the measured default
   }
 #undef MLS_SKP
+  return (int)hipGetLastError();
+}
+
+// Packed-weight decode GEMM whose A operand is the split-KV decode attention's output, merged
+// from its partials in the prologue (FUSE_COMBINE; the attention launch then skips its combine
+// kernel).  M <= 4, M * K * 2 <= 64 KiB, K == Hq * D, D % 8 == 0.
+int mls_skinny_packed_combine(const void* A, const float* cws, const float* cml, const int* lens, int nsplit,
+                              int chunk, int Hq, int D, const void* Wp, const float* bias, const void* res, void* out,
+                              int M, int N, int K, int act, int variant, void* stream) {
+  if (M <= 0 || M > 4 || N % 16 || K % 32 || K != Hq * D || D % 8 || nsplit <= 0 || chunk <= 0) return MLS_BAD_ARG;
+  const size_t ab = (size_t)M * K * 2, wb = (size_t)N * K * 2;
+  if (wb >= 0x7FFFFFFFull || ab > 65536) return MLS_UNSUPPORTED;
+  SkArgs s{};
+  s.a = (const bf16*)A;
+  s.w = (const bf16*)Wp;
+  s.bias = bias;
+  s.res = (const bf16*)res;
+  s.out = (bf16*)out;
+  s.M = M; s.N = N; s.K = K; s.lda = K;
+  s.act = act;
+  s.ldo = act == ACT_SILU_MUL ? N / 2 : N;
+  s.a_bytes = (uint32_t)ab;
+  s.w_bytes = (uint32_t)wb;
+  s.nsplit = 1;
+  s.cws = cws;
+  s.cml = cml;
+  s.lens = lens;
+  s.c_nsplit = nsplit;
+  s.c_chunk = chunk;
+  s.c_hq = Hq;
+  s.c_hd = D;
+  hipStream_t st = (hipStream_t)stream;
+  if (variant == 1)
+    hipLaunchKernelGGL((skinny_packed_kernel<8, 8, FUSE_COMBINE, 1>), dim3(N / 16), dim3(512), ab, st, s);
+  else
+    hipLaunchKernelGGL((skinny_packed_kernel<4, 16, FUSE_COMBINE, 1>), dim3(N / 16), dim3(1024), ab, st, s);
   return (int)hipGetLastError();
 }
 

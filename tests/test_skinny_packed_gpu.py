@@ -85,3 +85,26 @@ def test_packed_rejects_bad_shapes():
         ops.skinny_packed(_rand(1, 256), wp, 48)  # wp size mismatch
     with pytest.raises(ValueError):
         ops.pack_skinny(_rand(64, 200))  # K % 32
+
+
+@pytest.mark.parametrize("lens_list", [[300], [1, 64, 65, 700], [129, 20]])
+def test_packed_combine_matches_attention_then_gemm(lens_list):
+    """o-projection with the split-KV combine in its prologue == decode attention (own combine
+    launch) followed by the packed GEMM; rows that fit one split come from the direct-written A."""
+    from mlmicroservicetemplate_amd import ops
+
+    torch.manual_seed(len(lens_list))
+    B, Hq, Hkv, D, L = len(lens_list), 32, 8, 128, 1024
+    kc = torch.randn(B, L, Hkv, D, device=DEV).to(torch.bfloat16)
+    vc = torch.randn_like(kc)
+    q = torch.randn(B, (Hq + 2 * Hkv) * D, device=DEV).to(torch.bfloat16)
+    lens = torch.tensor(lens_list, device=DEV, dtype=torch.int32)
+    N = 4096
+    w = _rand(N, Hq * D, scale=(Hq * D) ** -0.5)
+    wp = ops.pack_skinny(w)
+    res = _rand(B, N)
+    a_ref = ops.decode_attention(q, kc, vc, lens, Hq, Hkv, D, max_len=L)
+    want = ops.skinny_packed(a_ref, wp, N, residual=res)
+    a, parts = ops.decode_attention(q, kc, vc, lens, Hq, Hkv, D, max_len=L, combine=False)
+    got = ops.skinny_packed_combine(a, parts, wp, N, residual=res)
+    assert rel_err(got, want) < 1e-2
