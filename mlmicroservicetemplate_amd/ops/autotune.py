@@ -16,7 +16,7 @@ import torch
 import torch.nn.functional as F
 
 CACHE_DIR = os.environ.get("MLS_TUNE_DIR", os.path.join(os.path.dirname(os.path.abspath(__file__)), "_native", "tune"))
-GEMM_CFGS = list(range(1, 20)) + list(range(23, 29))  # conv_gemm.hip kCfgs (20..22: persistent kernel)
+GEMM_CFGS = list(range(1, 20)) + list(range(23, 32))  # conv_gemm.hip kCfgs (20..22: persistent kernel)
 CANDIDATES: List[Tuple[int, int]] = [(c, s) for c in GEMM_CFGS for s in (1, 2, 4, 8)] + [(20, 1), (21, 1), (22, 1)]
 
 

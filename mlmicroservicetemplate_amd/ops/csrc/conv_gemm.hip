@@ -755,8 +755,10 @@ constexpr TileCfg kCfgs[] = {{0, 0, 0},       {128, 128, 256}, {128, 64, 256}, {
                              // 19, 23..28: deep rings (3-4 stages in flight); 20..22 = persistent kernel
                              {128, 128, 512}, {64, 64, 256},  {128, 64, 512}, {64, 128, 512},
                              {128, 128, 512}, {64, 128, 256}, {128, 64, 256}, {64, 64, 256},
-                             {128, 128, 512}, {64, 128, 512}};
-constexpr int kNumCfgs = 29;
+                             {128, 128, 512}, {64, 128, 512},
+                             // 29..31: 256-wide tiles for the large plain GEMMs (BERT projections, prefill)
+                             {256, 128, 512}, {256, 128, 512}, {128, 256, 512}};
+constexpr int kNumCfgs = 32;
 // cfgs 13..19 and 23..26 stage K in 32-deep steps (BK = 32): not for the stem layout or the SiLU-mul epilogue
 constexpr bool cfg_bk32(int c) { return (c >= 13 && c <= 19) || (c >= 23 && c <= 26); }
 
@@ -790,6 +792,9 @@ void launch_mode(int cfg, dim3 grid, hipStream_t st, const ConvArgs& a) {
     case 26: hipLaunchKernelGGL((conv_gemm_kernel<64, 64, 2, 2, 5, MODE, 32, 1>), grid, dim3(256), 0, st, a); break;
     case 27: hipLaunchKernelGGL((conv_gemm_kernel<128, 128, 4, 2, 4, MODE>), grid, dim3(512), 0, st, a); break;
     case 28: hipLaunchKernelGGL((conv_gemm_kernel<64, 128, 2, 4, 4, MODE>), grid, dim3(512), 0, st, a); break;
+    case 29: hipLaunchKernelGGL((conv_gemm_kernel<256, 128, 4, 2, 2, MODE, 64, 2>), grid, dim3(512), 0, st, a); break;
+    case 30: hipLaunchKernelGGL((conv_gemm_kernel<256, 128, 4, 2, 3, MODE, 64, 2>), grid, dim3(512), 0, st, a); break;
+    case 31: hipLaunchKernelGGL((conv_gemm_kernel<128, 256, 2, 4, 2, MODE, 64, 2>), grid, dim3(512), 0, st, a); break;
     default: hipLaunchKernelGGL((conv_gemm_kernel<64, 64, 2, 2, 3, MODE>), grid, dim3(256), 0, st, a); break;
   }
 }

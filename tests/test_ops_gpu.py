@@ -70,7 +70,7 @@ def test_conv_resnet_shapes(shape):
     res = torch.randn(B, ho, ho, cout, device=DEV).to(torch.bfloat16)
     ref = _conv_ref(x, w, bias, s, p, 1, res)
     ws = torch.empty(64 << 20, device=DEV, dtype=torch.float32)
-    for cfg in list(range(0, 29)):
+    for cfg in list(range(0, 32)):
         out = ops.conv2d_nhwc(x, ops.pack_conv_weight(w), bias, kernel=k, stride=s, pad=p, residual=res, act=1,
                               workspace=ws, cfg=cfg)
         torch.cuda.synchronize()
@@ -92,7 +92,7 @@ def test_conv_stem():
     w = (torch.randn(64, 3, 7, 7, device=DEV) / 12.0).to(torch.bfloat16)
     bias = torch.randn(64, device=DEV)
     ref = _conv_ref(x4.to(torch.bfloat16)[..., :3], w, bias, 2, 3, 1)
-    for cfg in list(range(0, 29)):
+    for cfg in list(range(0, 32)):
         out = ops.conv2d_nhwc(x4p, ops.pack_conv_weight(w), bias, kernel=7, stride=2, pad=0, act=1, cfg=cfg)
         assert out.shape == (B, 112, 112, 64)
         assert rel_err(out, ref) < 2e-2, f"cfg {cfg}"
@@ -115,7 +115,7 @@ def test_gemm(mnk, act):
     ws = torch.empty(16 << 20, device=DEV, dtype=torch.float32)
     for cfg, sk in ((0, 0), (1, 1), (4, 2), (2, 3), (5, 1), (6, 2), (7, 1), (8, 3), (13, 1), (14, 2), (15, 1),
                     (16, 3), (17, 1), (18, 2), (19, 1), (20, 1), (21, 1), (22, 1), (23, 2), (24, 1), (25, 3),
-                    (26, 1), (27, 2), (28, 1)):
+                    (26, 1), (27, 2), (28, 1), (29, 1), (30, 1), (31, 2)):
         out = ops.gemm(a, w, bias, scale=scale, residual=res, act=act, workspace=ws, cfg=cfg, splitk=sk)
         assert rel_err(out, ref) < 2e-2, f"cfg {cfg} sk {sk}"
 
