@@ -44,7 +44,7 @@ def test_tp1_consistency():
     assert torch.equal(a, b2)
 
 
-def _tp_worker(rank, world, port, cfg_kw, q):
+def _tp_worker(rank, world, port, cfg_kw, q, kv_pages=0):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
 
@@ -55,7 +55,8 @@ def _tp_worker(rank, world, port, cfg_kw, q):
     try:
         cfg = tiny_config(**cfg_kw)
         p = init_llama_shard(cfg, world, rank, seed=1)
-        m = LlamaTP(p, cfg, tp=world, rank=rank, comm=TPComm(None, world), max_batch=4, max_seq=64)
+        m = LlamaTP(p, cfg, tp=world, rank=rank, comm=TPComm(None, world), max_batch=4, max_seq=64,
+                    kv_pages=kv_pages)
         ids, lens = _prompts()
         greedy = m.generate(ids, lens, GenParams(max_new_tokens=6))
         sampled = m.generate(ids, lens, GenParams(6, top_k=20, temperature=0.8, seed=3))
@@ -66,9 +67,10 @@ def _tp_worker(rank, world, port, cfg_kw, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,kv", [(2, 4), (4, 2)])
+@pytest.mark.parametrize("world,kv,kv_pages", [(2, 4, 0), (4, 2, 0), (2, 4, 5)])
 @pytest.mark.timeout(240)
-def test_tp_matches_tp1(world, kv):
+def test_tp_matches_tp1(world, kv, kv_pages):
+    """(kv_pages > 0: every rank's cache is a paged pool -- same tokens as contiguous TP = 1.)"""
     cfg_kw = dict(CFG, kv_heads=kv)
     torch.set_num_threads(1)
     cfg = tiny_config(**cfg_kw)
@@ -80,7 +82,7 @@ def test_tp_matches_tp1(world, kv):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_tp_worker, args=(r, world, port, cfg_kw, q)) for r in range(world)]
+    procs = [ctx.Process(target=_tp_worker, args=(r, world, port, cfg_kw, q, kv_pages)) for r in range(world)]
     for pr in procs:
         pr.start()
     res = [q.get(timeout=200) for _ in range(world)]

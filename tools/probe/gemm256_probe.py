@@ -10,7 +10,10 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 SHAPES = {"bert_qkv": (4096, 2304, 768), "bert_o": (4096, 768, 768), "bert_ffn1": (4096, 3072, 768),
-          "bert_ffn2": (4096, 768, 3072), "llama_qkv_p512": (512, 6144, 4096), "llama_gu_p4096": (4096, 28672, 4096)}
+          "bert_ffn2": (4096, 768, 3072), "llama_qkv_p512": (512, 6144, 4096), "llama_gu_p4096": (4096, 28672, 4096),
+          "llama_o_p512": (512, 4096, 4096), "llama_gu_p512": (512, 28672, 4096), "llama_down_p512": (512, 4096, 14336)}
+if os.environ.get("SHAPES"):
+    SHAPES = {k: v for k, v in SHAPES.items() if k in os.environ["SHAPES"].split(",")}
 
 
 def timed(fn, conc, iters=20):
@@ -54,7 +57,7 @@ def main():
             out = ops.gemm(a, w, workspace=ws, cfg=c, splitk=1)
             err = ((out.float() - ref).abs().max() / ref.abs().max()).item()
             assert err < 2e-2, (name, c, err)
-        for conc in (1, 4):
+        for conc in [int(c) for c in os.environ.get("CONC", "1,4").split(",")]:
             for impl, fn in impls.items():
                 us = timed(fn, conc)
                 print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "conc": conc, "impl": impl,
