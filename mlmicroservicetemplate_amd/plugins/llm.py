@@ -59,6 +59,10 @@ class LlamaPlugin(ModelPlugin):
         params = llama.init_llama_shard(cfg, tp, ctx.rank, int(s.SEED), device=dev, source=source)
         max_batch, max_seq = int(s.MAX_BATCH) or 32, int(extra.get("max_seq", 2048))
         kv_pages = self._kv_pages(extra.get("kv_pages", 0), cfg, tp, max_batch, max_seq, dev)
+        if tp > 1 and kv_pages:  # the scheduler replays rank 0's admissions: every pool must be equal
+            from ..parallel import dist as mdist
+
+            kv_pages = int(-mdist.max_over_ranks(-float(kv_pages)))
         self.model = llama.LlamaTP(params, cfg, tp=tp, rank=ctx.rank, comm=llama.TPComm(None, tp, device=dev), backend=backend,
                                    device=dev, max_batch=max_batch, max_seq=max_seq, kv_pages=kv_pages)
         self.tok = llama.LlamaTokenizer(cfg, extra.get("tokenizer_file"))
@@ -77,9 +81,8 @@ class LlamaPlugin(ModelPlugin):
     def _kv_pages(spec, cfg, tp, max_batch, max_seq, dev) -> int:
         """MODEL_CONFIG ``kv_pages``: 0 = per-slot caches (``max_batch x max_seq`` rows), N = a
         shared pool of N 64-row pages, ``auto`` = as many pages as half the free HBM holds, capped
-        at what ``max_batch`` full-length sequences could use (+ the scratch page).  TP ranks must
-        agree (the scheduler's admissions assume identical pools): ``auto`` is sized from rank
-        0's free memory only when every rank sees the same, so prefer an explicit N under TP."""
+        at what ``max_batch`` full-length sequences could use (+ the scratch page).  Under TP the
+        ranks then agree on the minimum (rank 0's admissions are replayed on every rank)."""
         if spec in (0, "0", None, ""):
             return 0
         full = max_batch * -(-max_seq // 64) + 1
