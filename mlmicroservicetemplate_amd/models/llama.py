@@ -381,6 +381,20 @@ class LlamaTP:
                 cap = torch.cuda.get_device_properties(self.device).total_memory
                 if mode == "1" or total <= cap // 4:
                     self.packed = {n: ops.pack_skinny(self.p[n]) for n in names}
+            # Opt-in FP8 decode (MLS_DECODE_FP8=1): W8A8 e4m3 copies of the projections, per-channel
+            # weight scales and per-row activation scales (ops.skinny_fp8), for <= 4 tokens per step --
+            # half the weight stream (profiles/r2_decode_fp8_weight_probe.jsonl).  Changes numerics
+            # (e4m3 has a 3-bit mantissa), so bf16 stays the default.
+            self.fp8: Dict[str, Tuple[torch.Tensor, torch.Tensor]] = {}
+            if self.device.type == "cuda" and os.environ.get("MLS_DECODE_FP8", "0") == "1":
+                names = [f"l{i}.{n}" for i in range(cfg.layers) for n in ("qkv", "o", "gate_up", "down")]
+                names.append("lm_head")
+                # only matrices of >= 16M weights: below that a decode GEMM is latency-bound and the
+                # fp8 prologue (row |max| reduction + requantisation) costs more than the bytes saved
+                # -- one emulated TP = 8 rank was 1.13 -> 1.18 ms/token with every projection in fp8
+                self.fp8 = {n: ops.pack_skinny_fp8(self.p[n]) for n in names
+                            if self.p[n].shape[0] % 16 == 0 and self.p[n].shape[1] % 64 == 0
+                            and (1 << 24) <= self.p[n].numel() < (1 << 31)}
             self.ones = torch.ones(cfg.hidden, device=self.device, dtype=torch.bfloat16)
             self.workspace = torch.empty(32 << 20, device=self.device, dtype=torch.float32)
             self.dec_chunk = int(os.environ.get("MLS_DEC_CHUNK", "0"))  # 0: auto (see _fused_forward)
@@ -552,16 +566,29 @@ class LlamaTP:
         # two) while every block's share of partials is small -- B x local q heads <= 32: one emulated
         # TP = 8 rank 1.166 -> 1.125 ms/token at batch 1, 1.294 -> 1.254 at 4; TP = 1 batch 1 level,
         # batch 4 (128 head rows per block) 3.17 -> 3.37, so off there (profiles/r2_llama8b_fused_combine_ab.jsonl)
-        fuse_combine = (decode and self.fuse_combine and "l0.o" in packed and B <= 4
+        fuse_combine = (decode and self.fuse_combine and "l0.o" in packed and "l0.o" not in self.fp8 and B <= 4
                         and B * sd.hq <= 32 and B * sd.hq * D * 2 <= 65536)
 
+        fp8 = self.fp8 if T <= 4 else {}
+
+        def use_fp8(name, K):
+            return name in fp8 and T * K * 2 <= 65536
+
         def linear(x, name, residual=None):
+            if use_fp8(name, x.shape[1]):
+                q, sc = fp8[name]
+                return ops.skinny_fp8(x, q, sc, p[name].shape[0], residual=residual)
             if name in packed:
                 return ops.skinny_packed(x, packed[name], p[name].shape[0], residual=residual, variant=self.pk_variant)
             return ops.linear(x, p[name], workspace=ws)
 
         def pre_norm(x, name, d, act=ops.ACT_NONE):
             w = p[name]
+            if use_fp8(name, x.shape[1]):
+                q, sc = fp8[name]
+                r_new = None if d is None else torch.empty_like(x)
+                y = ops.skinny_fp8(x, q, sc, w.shape[0], delta=d, resid_out=r_new, norm=True, act=act, eps=eps)
+                return y, (x if d is None else r_new)
             if name in packed:
                 r_new = None if d is None else torch.empty_like(x)
                 y = ops.skinny_packed(x, packed[name], w.shape[0], delta=d, resid_out=r_new, norm=True, act=act,
@@ -617,7 +644,10 @@ class LlamaTP:
             last = (torch.arange(B, device=r.device, dtype=torch.int64) * S + lens.long() - 1)
             r = r.index_select(0, last)
             delta = None if delta is None else delta.index_select(0, last)
-        if B <= 24 and "lm_head" in self.packed:
+        if B <= 4 and "lm_head" in self.fp8 and B * r.shape[1] * 2 <= 65536:
+            q, sc = self.fp8["lm_head"]
+            logits = ops.skinny_fp8(r, q, sc, p["lm_head"].shape[0], delta=delta, norm=True, eps=eps)
+        elif B <= 24 and "lm_head" in self.packed:
             logits = ops.skinny_packed(r, self.packed["lm_head"], p["lm_head"].shape[0], delta=delta, norm=True,
                                        eps=eps, variant=self.pk_variant)
         elif B <= 16:

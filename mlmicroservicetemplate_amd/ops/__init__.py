@@ -413,6 +413,69 @@ def skinny_packed(x: torch.Tensor, wp: torch.Tensor, N: int, *, delta: Optional[
     return out
 
 
+FP8_MAX = 448.0  # OCP e4m3fn
+
+
+def pack_skinny_fp8(w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """``w [N, K]`` -> (fp8 e4m3 weights in the 1 KiB granule layout of :func:`skinny_fp8`
+    (``[N/16][K/64][4][16][2][8]`` bytes, flat uint8), per-row fp32 scales ``max|w[n]| / 448``)."""
+    N, K = w.shape
+    if N % 16 or K % 64:
+        raise ValueError("pack_skinny_fp8: N % 16 == 0 and K % 64 == 0")
+    wf = w.float()
+    scale = (wf.abs().amax(1) / FP8_MAX).clamp_min(1e-12)
+    q = (wf / scale[:, None]).to(torch.float8_e4m3fn)
+    q = q.view(N // 16, 16, K // 64, 2, 4, 8).permute(0, 2, 4, 1, 3, 5).contiguous()
+    return q.view(torch.uint8).reshape(-1), scale.contiguous()
+
+
+def fp8_reference(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """fp32 emulation of :func:`skinny_fp8`'s W8A8 product (per-row x scale, per-row w scale)."""
+    xf, wf = x.float(), w.float()
+    sx = (xf.abs().amax(1, keepdim=True) / FP8_MAX).clamp_min(1e-30)
+    sw = (wf.abs().amax(1, keepdim=True) / FP8_MAX).clamp_min(1e-12)
+    xq = (xf / sx).to(torch.float8_e4m3fn).float() * sx
+    wq = (wf / sw).to(torch.float8_e4m3fn).float() * sw
+    return xq @ wq.T
+
+
+def skinny_fp8(x: torch.Tensor, wq: torch.Tensor, wscale: torch.Tensor, N: int, *,
+               delta: Optional[torch.Tensor] = None, resid_out: Optional[torch.Tensor] = None, norm: bool = False,
+               act=ACT_NONE, bias: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
+               eps: float = 1e-5, variant: int = 1) -> torch.Tensor:
+    """FP8 (W8A8, e4m3) decode product, M <= 4: ``act([RMSNorm](x [+ delta]) @ W^T + b [+ residual])``
+    with W from :func:`pack_skinny_fp8` (the RMSNorm gain folded into W before packing) and the
+    activation rows quantised per row inside the kernel.  Half the weight bytes of :func:`skinny_packed`."""
+    dev = x.device
+    _need(x, "x", torch.bfloat16, dev)
+    M, K = x.shape
+    if M > 4 or N % 16 or K % 64 or wq.numel() != N * K or M * K * 2 > 65536:
+        raise ValueError("skinny_fp8: M <= 4, N % 16 == 0, K % 64 == 0, M * K * 2 <= 64 KiB, wq of N*K bytes")
+    _need(wscale, "wscale", torch.float32, dev)
+    if resid_out is not None and delta is None:
+        raise ValueError("resid_out needs delta")
+    if delta is not None and not norm:
+        raise ValueError("delta exists only with norm")
+    for name, t in (("delta", delta), ("resid_out", resid_out)):
+        if t is not None:
+            _need(t, name, torch.bfloat16, dev)
+            if tuple(t.shape) != (M, K):
+                raise ValueError(f"{name} must be [M, K]")
+    if bias is not None:
+        _need(bias, "bias", torch.float32, dev)
+    if residual is not None:
+        _need(residual, "residual", torch.bfloat16, dev)
+        if tuple(residual.shape) != (M, N):
+            raise ValueError("residual must be [M, N]")
+    code = _act(act)
+    out = torch.empty(M, N // 2 if code == ACT_SILU_MUL else N, device=dev, dtype=torch.bfloat16)
+    rc = lib().mls_skinny_fp8(x.data_ptr(), _ptr(delta), _ptr(resid_out), wq.data_ptr(), wscale.data_ptr(),
+                              _ptr(bias), _ptr(residual), out.data_ptr(), M, N, K, code, int(norm), float(eps),
+                              int(variant), stream_ptr(dev))
+    check(rc, "mls_skinny_fp8")
+    return out
+
+
 def fold_norm(w: torch.Tensor, gain: torch.Tensor) -> torch.Tensor:
     """``W[:, k] * gain[k]`` in fp32, rounded once to bf16: RMSNorm(x) @ W^T == rstd * (x @ fold^T)."""
     return (w.float() * gain.float().view(1, -1)).to(w.dtype)

@@ -40,6 +40,7 @@ struct SkArgs {
   const float* cml;
   const int* lens;
   int c_nsplit, c_chunk, c_hq, c_hd;
+  const float* wscale;  // fp8 weights: per-output-channel dequantisation scale [N]
 };
 
 // fusion modes of the A prologue (template parameter, so the unrolled k loop has no runtime
@@ -678,6 +679,183 @@ __global__ __launch_bounds__(NWV * 64) void skinny_packed_reg_kernel(const SkArg
   }
 }
 
+
+// FP8 (OCP e4m3) weight-and-activation decode GEMM, M <= 4: W8A8 with a per-output-channel weight
+// scale and a per-row dynamic activation scale, on v_mfma_f32_16x16x32_fp8_fp8.  Half the weight
+// bytes of the bf16 stream (decode is weight-bandwidth bound).  W is packed in 1 KiB granules of
+// 16 rows x 64 k ([N/16][K/64][g][nr][2 k-steps][8]), so one 16-B load per lane feeds two MFMAs.
+// Prologue: A (+ A2) staged in LDS as bf16 with the row square sums and |max|, then requantised
+// in place to fp8 with scale |max| / 448; epilogue: acc * s_a[m] * s_w[n] (* rstd[m]).
+template <int UNROLL, int NWV, int FUSE>
+__global__ __launch_bounds__(NWV * 64) void skinny_fp8_kernel(const SkArgs s) {
+  extern __shared__ __attribute__((aligned(16))) uint4 a_lds[];  // bf16 [M][K], then fp8 [M][K]
+  __shared__ float red[NWV][16][17];
+  __shared__ float ssq_s[4];
+  __shared__ int amax_s[4];
+  constexpr int T = NWV * 64;
+  constexpr bool NORM = FUSE == FUSE_NORM || FUSE == FUSE_ADD_NORM;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nr = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.x * 16;
+  const int kgs = s.K >> 6;  // 64-wide granules per row
+  const int kch = s.K >> 3;
+  const int nq = s.M * kch;
+  const int kpw = (kgs + NWV - 1) / NWV;
+  const int kb = wid * kpw, ke = min(kgs, kb + kpw);
+  const rsrc_t wr = make_rsrc(s.w, s.w_bytes);
+  const rsrc_t ar = make_rsrc(s.a, s.a_bytes);
+  const rsrc_t a2r = make_rsrc(s.a2, FUSE == FUSE_ADD_NORM ? s.a_bytes : 0);
+  const int wbase = blockIdx.x * kgs * 1024 + lane * 16;
+
+  auto load_trip = [&](int kg0, uint4 (&wv)[UNROLL]) {
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) wv[u] = bload16_pol<1>(wr, kg0 + u < ke ? wbase + (kg0 + u) * 1024 : OOB);
+  };
+  constexpr int QPT = 2048 / T;
+  uint4 a0[QPT], a20[QPT];
+#pragma unroll
+  for (int j = 0; j < QPT; ++j) {
+    const int q = tid + j * T;
+    const int m = q / kch, c = q - m * kch;
+    const int off = q < nq ? (m * s.lda + c * 8) * 2 : OOB;
+    a0[j] = bload16(ar, off);
+    if constexpr (FUSE == FUSE_ADD_NORM) a20[j] = bload16(a2r, off);
+  }
+  uint4 wnext[UNROLL];
+  load_trip(kb, wnext);
+
+  if (tid < 4) {
+    ssq_s[tid] = 0.f;
+    amax_s[tid] = 0;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  float part[4] = {0.f, 0.f, 0.f, 0.f}, amx[4] = {0.f, 0.f, 0.f, 0.f};
+  const bool wr_res = FUSE == FUSE_ADD_NORM && s.a_out && blockIdx.x == 0;
+  auto stage = [&](int q, uint4 v, uint4 v2) {
+    const int m = q / kch, c = q - m * kch;
+    if constexpr (FUSE == FUSE_ADD_NORM) {
+      v = add_round(v, v2);
+      if (wr_res) st16(s.a_out + (size_t)m * s.lda + c * 8, v);
+    }
+    a_lds[q] = v;
+    float x[8];
+    unpack8(v, x);
+    float sq = 0.f, mx = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      sq += x[e] * x[e];
+      mx = fmaxf(mx, fabsf(x[e]));
+    }
+#pragma unroll
+    for (int mm = 0; mm < 4; ++mm) {
+      part[mm] += mm == m ? sq : 0.f;
+      amx[mm] = mm == m ? fmaxf(amx[mm], mx) : amx[mm];
+    }
+  };
+#pragma unroll
+  for (int j = 0; j < QPT; ++j)
+    if (tid + j * T < nq) stage(tid + j * T, a0[j], a20[j]);
+  for (int q = tid + QPT * T; q < nq; q += T) {
+    const int m = q / kch, c = q - m * kch;
+    stage(q, ld16(s.a + (size_t)m * s.lda + c * 8),
+          FUSE == FUSE_ADD_NORM ? ld16(s.a2 + (size_t)m * s.lda + c * 8) : make_uint4(0, 0, 0, 0));
+  }
+#pragma unroll
+  for (int mm = 0; mm < 4; ++mm) {
+    const float t = wave_sum(part[mm]);
+    const float mxw = wave_max(amx[mm]);
+    if (lane == 0 && mm < s.M) {
+      if constexpr (NORM) atomicAdd(&ssq_s[mm], t);
+      atomicMax(&amax_s[mm], __float_as_int(mxw));  // non-negative floats order as their bits
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  // requantise A to fp8 in place: every thread first reads its chunks, then (after a barrier) writes
+  float inv[4];
+#pragma unroll
+  for (int mm = 0; mm < 4; ++mm) {
+    const float amax = __int_as_float(amax_s[mm]);
+    inv[mm] = amax > 0.f ? 448.f / amax : 0.f;
+  }
+  constexpr int QMAX = 4096 / T;  // M * K / 8 <= 4096 chunks (host: M * K * 2 <= 64 KiB)
+  uint4 hold[QMAX];
+#pragma unroll
+  for (int j = 0; j < QMAX; ++j) {
+    const int q = tid + j * T;
+    hold[j] = q < nq ? a_lds[q] : make_uint4(0, 0, 0, 0);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  uint2* a8 = reinterpret_cast<uint2*>(a_lds);  // fp8 [M][K]: chunk q -> 8 bytes at q * 8
+#pragma unroll
+  for (int j = 0; j < QMAX; ++j) {
+    const int q = tid + j * T;
+    if (q < nq) {
+      const int m = q / kch;
+      const float sc = m == 0 ? inv[0] : m == 1 ? inv[1] : m == 2 ? inv[2] : inv[3];
+      float x[8];
+      unpack8(hold[j], x);
+      int lo = __builtin_amdgcn_cvt_pk_fp8_f32(x[0] * sc, x[1] * sc, 0, false);
+      lo = __builtin_amdgcn_cvt_pk_fp8_f32(x[2] * sc, x[3] * sc, lo, true);
+      int hi = __builtin_amdgcn_cvt_pk_fp8_f32(x[4] * sc, x[5] * sc, 0, false);
+      hi = __builtin_amdgcn_cvt_pk_fp8_f32(x[6] * sc, x[7] * sc, hi, true);
+      a8[q] = make_uint2((uint32_t)lo, (uint32_t)hi);
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool arow = nr < s.M;
+  const char* a8b = reinterpret_cast<const char*>(a_lds) + nr * s.K + 8 * g;
+  for (int kg = kb; kg < ke; kg += UNROLL) {
+    uint4 wv[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) wv[u] = wnext[u];
+    if (kg + UNROLL < ke) load_trip(kg + UNROLL, wnext);
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int k = kg + u;
+      const bool ok = arow && k < ke;
+      const long x0 = ok ? *reinterpret_cast<const long*>(a8b + k * 64) : 0;
+      const long x1 = ok ? *reinterpret_cast<const long*>(a8b + k * 64 + 32) : 0;
+      const long w0 = (long)(((unsigned long)wv[u].y << 32) | wv[u].x);
+      const long w1 = (long)(((unsigned long)wv[u].w << 32) | wv[u].z);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(x0, w0, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(x1, w1, acc, 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) red[wid][4 * g + i][nr] = acc[i];
+  __syncthreads();
+  const bool glu = s.act == ACT_SILU_MUL;
+  for (int q = tid; q < s.M * 16; q += T) {
+    const int m = q >> 4, c = q & 15;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) v += red[w][m][c];
+    const float sa = __int_as_float(amax_s[m]) * (1.f / 448.f);
+    const float rs = (NORM ? rsqrtf(ssq_s[m] / (float)s.K + s.eps) : 1.f) * sa;
+    const int n = n0 + c;
+    v *= rs * s.wscale[n];
+    if (glu) {
+      if (c < 8) {
+        float up = 0.f;
+#pragma unroll
+        for (int w = 0; w < NWV; ++w) up += red[w][m][c + 8];
+        up *= rs * s.wscale[n + 8];
+        s.out[(size_t)m * s.ldo + (n >> 4) * 8 + (n & 7)] = (bf16)(silu(epi(v, n, s)) * epi(up, n + 8, s));
+      }
+      continue;
+    }
+    float o = epi(v, n, s);
+    if (s.res) o += (float)s.res[(size_t)m * s.N + n];
+    s.out[(size_t)m * s.ldo + n] = (bf16)apply_act(o, s.act);
+  }
+}
+
 // [N][K] row-major -> [N/16][K/32][4][16][8] (the packed granule layout above)
 __global__ __launch_bounds__(256) void pack_skinny_kernel(const bf16* __restrict__ w, bf16* __restrict__ wp, int N,
                                                           int K) {
@@ -992,6 +1170,55 @@ int mls_skinny_packed_combine(const void* A, const float* cws, const float* cml,
     hipLaunchKernelGGL((skinny_packed_kernel<8, 8, FUSE_COMBINE, 1>), dim3(N / 16), dim3(512), ab, st, s);
   else
     hipLaunchKernelGGL((skinny_packed_kernel<4, 16, FUSE_COMBINE, 1>), dim3(N / 16), dim3(1024), ab, st, s);
+  return (int)hipGetLastError();
+}
+
+// FP8 (e4m3) decode GEMM (W8A8, see skinny_fp8_kernel): M <= 4, K % 64 == 0, M * K * 2 <= 64 KiB.
+// Wq: packed fp8 granules; wscale [N] fp32.  Same fusion options as mls_skinny_packed.
+int mls_skinny_fp8(const void* A, const void* A2, void* A_out, const void* Wq, const float* wscale, const float* bias,
+                   const void* res, void* out, int M, int N, int K, int act, int norm, float eps, int variant,
+                   void* stream) {
+  if (M <= 0 || M > 4 || N % 16 || K % 64 || K <= 0 || !wscale) return MLS_BAD_ARG;
+  if (A_out && (A_out == A || A_out == A2)) return MLS_BAD_ARG;
+  if ((A2 || A_out) && !norm) return MLS_UNSUPPORTED;
+  const size_t ab = (size_t)M * K * 2, wb = (size_t)N * K;
+  if (wb >= 0x7FFFFFFFull || ab > 65536) return MLS_UNSUPPORTED;
+  SkArgs s{};
+  s.a = (const bf16*)A;
+  s.a2 = (const bf16*)A2;
+  s.a_out = (bf16*)A_out;
+  s.norm = norm;
+  s.eps = eps;
+  s.w = (const bf16*)Wq;
+  s.wscale = wscale;
+  s.bias = bias;
+  s.res = (const bf16*)res;
+  s.out = (bf16*)out;
+  s.M = M; s.N = N; s.K = K; s.lda = K;
+  s.act = act;
+  s.ldo = act == ACT_SILU_MUL ? N / 2 : N;
+  s.a_bytes = (uint32_t)ab;
+  s.w_bytes = (uint32_t)wb;
+  s.nsplit = 1;
+  const int mode = A2 ? FUSE_ADD_NORM : norm ? FUSE_NORM : FUSE_NONE;
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid(N / 16);
+#define MLS_SK8(UN, NW)                                                                                     \
+  switch (mode) {                                                                                           \
+    case FUSE_NONE: hipLaunchKernelGGL((skinny_fp8_kernel<UN, NW, FUSE_NONE>), grid, dim3(NW * 64), ab, st, s); break; \
+    case FUSE_NORM: hipLaunchKernelGGL((skinny_fp8_kernel<UN, NW, FUSE_NORM>), grid, dim3(NW * 64), ab, st, s); break; \
+    default: hipLaunchKernelGGL((skinny_fp8_kernel<UN, NW, FUSE_ADD_NORM>), grid, dim3(NW * 64), ab, st, s); break;    \
+  }
+  // variant: 1 (default) 4 granules per trip x 8 waves; 0: 4 x 16; 2: 2 x 16
+  // (profiles/r2_decode_fp8_weight_probe.jsonl: 1 is fastest on every Llama-3-8B shape)
+  if (variant == 0) {
+    MLS_SK8(4, 16)
+  } else if (variant == 2) {
+    MLS_SK8(2, 16)
+  } else {
+    MLS_SK8(4, 8)
+  }
+#undef MLS_SK8
   return (int)hipGetLastError();
 }
 

@@ -100,3 +100,38 @@ def test_fused_llama_paged_matches_contiguous():
         cut = next((i + 1 for i, t in enumerate(w) if t in eos), len(w))
         assert outs[b] == w[:cut]
     assert paged.pages.free_pages == 8
+
+
+def test_fused_llama_fp8_decode_close_to_bf16(monkeypatch):
+    """MLS_DECODE_FP8=1: decode steps run the W8A8 kernel (counted) and their top logits stay within
+    fp8 error of the bf16 model's."""
+    from mlmicroservicetemplate_amd import ops
+    from mlmicroservicetemplate_amd.models.llama import LlamaTP, init_llama_shard, tiny_config
+
+    cfg = tiny_config(layers=2, hidden=512, heads=8, kv_heads=2, head_dim=128, intermediate=1024)
+    p = init_llama_shard(cfg, 1, 0, seed=6, device=DEV)
+    ref = LlamaTP(p, cfg, backend="fused", device=DEV, max_batch=2, max_seq=128)
+    monkeypatch.setenv("MLS_DECODE_FP8", "1")
+    q8 = LlamaTP(p, cfg, backend="fused", device=DEV, max_batch=2, max_seq=128)
+    assert q8.fp8
+    calls = {"n": 0}
+    real = ops.skinny_fp8
+
+    def counting(*a, **k):
+        calls["n"] += 1
+        return real(*a, **k)
+
+    monkeypatch.setattr(ops, "skinny_fp8", counting)
+    g = torch.Generator().manual_seed(2)
+    ids = torch.randint(3, 2000, (2, 20), generator=g).to(DEV).to(torch.int32)
+    lens = torch.tensor([20, 11], device=DEV, dtype=torch.int32)
+    pos = torch.arange(20, device=DEV, dtype=torch.int32).unsqueeze(0).expand(2, 20).contiguous()
+    for m in (ref, q8):
+        m.use_graphs = False  # eager decode so the counter sees the calls
+        m.step(ids, pos, lens, decode=False, k=5)
+    tok = torch.tensor([[7], [9]], device=DEV, dtype=torch.int32)
+    cur = lens.view(2, 1).clone()
+    v_ref, i_ref = ref.decode_step(tok, cur, 5, max_ctx=21)
+    v_q8, i_q8 = q8.decode_step(tok, cur, 5, max_ctx=21)
+    assert calls["n"] >= 2 * cfg.layers
+    assert ((v_q8 - v_ref).abs().max() / v_ref.abs().max()).item() < 0.1

@@ -108,3 +108,57 @@ def test_packed_combine_matches_attention_then_gemm(lens_list):
     a, parts = ops.decode_attention(q, kc, vc, lens, Hq, Hkv, D, max_len=L, combine=False)
     got = ops.skinny_packed_combine(a, parts, wp, N, residual=res)
     assert rel_err(got, want) < 1e-2
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("M,N,K", [(1, 256, 4096), (3, 128, 1024), (2, 64, 14336), (4, 48, 128)])
+def test_fp8_plain_matches_emulation(variant, M, N, K):
+    """W8A8 e4m3 kernel == an fp32 emulation of the same quantisation (and within fp8 error of
+    the bf16 product)."""
+    from mlmicroservicetemplate_amd import ops
+
+    torch.manual_seed(variant * 7 + M)
+    x, w = _rand(M, K), _rand(N, K, scale=K**-0.5)
+    b, res = torch.randn(N, device=DEV) * 0.1, _rand(M, N)
+    wq, sw = ops.pack_skinny_fp8(w)
+    out = ops.skinny_fp8(x, wq, sw, N, bias=b, residual=res, variant=variant)
+    emu = ops.fp8_reference(x, w) + b + res.float()
+    assert rel_err(out, emu) < 1e-2
+    exact = x.float() @ w.float().T + b + res.float()
+    assert rel_err(out, exact) < 6e-2
+
+
+def test_fp8_identity_asymmetric():
+    """A = I rows against an asymmetric W catches a transposed operand map."""
+    from mlmicroservicetemplate_amd import ops
+
+    K, N = 64, 16
+    w = (torch.arange(N * K, device=DEV, dtype=torch.float32).view(N, K).remainder(13) - 6).to(torch.bfloat16)
+    for r in range(4):
+        x = torch.zeros(1, K, device=DEV, dtype=torch.bfloat16)
+        x[0, 5 + 9 * r] = 1.0
+        wq, sw = ops.pack_skinny_fp8(w)
+        out = ops.skinny_fp8(x, wq, sw, N)
+        assert torch.allclose(out.float()[0], w.float()[:, 5 + 9 * r], atol=0.05 * 6), r
+
+
+@pytest.mark.parametrize("M", [1, 4])
+def test_fp8_add_norm_silu_mul(M):
+    from mlmicroservicetemplate_amd import ops
+
+    K, N = 1024, 256
+    torch.manual_seed(M)
+    x, d = _rand(M, K), _rand(M, K)
+    gain = torch.rand(K, device=DEV) + 0.5
+    w = ops.interleave_gate_up(_rand(N // 2, K, scale=K**-0.5), _rand(N // 2, K, scale=K**-0.5))
+    wf = ops.fold_norm(w, gain)
+    wq, sw = ops.pack_skinny_fp8(wf)
+    r_out = torch.empty_like(x)
+    out = ops.skinny_fp8(x, wq, sw, N, delta=d, resid_out=r_out, norm=True, act="silu_mul")
+    h = (x.float() + d.float()).to(torch.bfloat16)
+    assert torch.equal(r_out, h)
+    rstd = torch.rsqrt(h.float().pow(2).mean(-1, keepdim=True) + 1e-5)
+    y = ops.fp8_reference(h, wf) * rstd
+    g_, u_ = y.view(M, N // 16, 2, 8)[:, :, 0].reshape(M, -1), y.view(M, N // 16, 2, 8)[:, :, 1].reshape(M, -1)
+    ref = torch.nn.functional.silu(g_) * u_
+    assert rel_err(out, ref) < 2e-2

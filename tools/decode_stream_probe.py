@@ -45,6 +45,15 @@ def main():
         if hasattr(lib, "mls_skinny_set_variant") and os.environ.get("REG", "0") == "1":
             for k in [k for k in impls if "skinny" in k]:
                 impls[k + "_reg"] = variant(impls[k], 1)
+        if M <= 4 and os.environ.get("FP8_VARIANTS"):  # W8A8 e4m3 (ops.pack_skinny_fp8): half the bytes
+            q_list = [ops.pack_skinny_fp8(w) for w in ws_list]
+            for v in [int(t) for t in os.environ["FP8_VARIANTS"].split(",")]:
+                if M * K * 2 <= 65536:
+                    impls[f"fp8_v{v}"] = (lambda v=v: [ops.skinny_fp8(x, q, sc, N, act=act, variant=v) for q, sc in q_list])
+                    if K == 4096 and name != "o":
+                        impls[f"fused_norm_fp8_v{v}"] = (
+                            lambda v=v: [ops.skinny_fp8(x, q, sc, N, delta=d, resid_out=r_out, norm=True, act=act,
+                                                        variant=v) for q, sc in q_list])
         if M <= 16:  # packed 1 KiB-granule weights (ops.pack_skinny), variants of mls_skinny_packed
             wp_list = [ops.pack_skinny(w) for w in ws_list]
             norm_fused = K == 4096 and name != "o"
