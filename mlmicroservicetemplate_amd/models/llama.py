@@ -392,9 +392,10 @@ class LlamaTP:
                 # only matrices of >= 16M weights: below that a decode GEMM is latency-bound and the
                 # fp8 prologue (row |max| reduction + requantisation) costs more than the bytes saved
                 # -- one emulated TP = 8 rank was 1.13 -> 1.18 ms/token with every projection in fp8
+                min_el = int(os.environ.get("MLS_DECODE_FP8_MIN", str(1 << 24)))
                 self.fp8 = {n: ops.pack_skinny_fp8(self.p[n]) for n in names
                             if self.p[n].shape[0] % 16 == 0 and self.p[n].shape[1] % 64 == 0
-                            and (1 << 24) <= self.p[n].numel() < (1 << 31)}
+                            and min_el <= self.p[n].numel() < (1 << 31)}
             self.ones = torch.ones(cfg.hidden, device=self.device, dtype=torch.bfloat16)
             self.workspace = torch.empty(32 << 20, device=self.device, dtype=torch.float32)
             self.dec_chunk = int(os.environ.get("MLS_DEC_CHUNK", "0"))  # 0: auto (see _fused_forward)
@@ -402,15 +403,20 @@ class LlamaTP:
                                       device=self.device, dtype=torch.float32)
             self.dec_cnt = torch.zeros(max_batch * self.sd.hkv, device=self.device, dtype=torch.int32)
         cdt = torch.bfloat16 if backend == "fused" else torch.float32
+        # fused: head-major caches ([.., Hkv, rows, D]) -- one head's rows contiguous, so a decode split
+        # block streams one 16 KiB run instead of 64 slices of 256 B (MLS_KV_HEAD_MAJOR=0: row-major)
+        self.kv_hm = backend == "fused" and os.environ.get("MLS_KV_HEAD_MAJOR", "1") == "1"
         self.pages = None
         if kv_pages > 0:
             from .kv_pages import PageTable
 
             self.page_rows = 64  # = the decode split: one page per split block
             self.pages = PageTable(kv_pages, self.page_rows, max_batch, -(-max_seq // self.page_rows), self.device)
-            shape = (kv_pages, self.page_rows, self.sd.hkv, D)
+            shape = ((kv_pages, self.sd.hkv, self.page_rows, D) if self.kv_hm
+                     else (kv_pages, self.page_rows, self.sd.hkv, D))
         else:
-            shape = (max_batch, max_seq, self.sd.hkv, D)
+            shape = (max_batch, self.sd.hkv, max_seq, D) if self.kv_hm else (max_batch, max_seq, self.sd.hkv, D)
+        self.kv_hm_rows = 0 if not self.kv_hm else (self.page_rows if kv_pages > 0 else max_seq)
         self.k_cache = [torch.zeros(shape, device=self.device, dtype=cdt) for _ in range(cfg.layers)]
         self.v_cache = [torch.zeros_like(self.k_cache[0]) for _ in range(cfg.layers)]
         self.cos, self.sin = R.rope_tables(max_seq, D, cfg.rope_theta, self.device)
@@ -548,7 +554,9 @@ class LlamaTP:
         # TP = 8 rank (one KV head).  A single 256-row split per KV head (no combine launch) was
         # 1.6 % slower at batch 1, and one 8-wave block walking a whole <= 1024 context in passes
         # was 26 % slower at TP = 8 (latency-bound on one CU) -- profiles/r1_llama_decode_sweep.jsonl.
-        dec_chunk = self.dec_chunk if self.dec_chunk > 0 else 64
+        # From batch 32 up the grid is already >= 4k blocks and 128-row splits halve the combine
+        # traffic: -3 % step time at batch 128 (profiles/r2_llama8b_decode_chunk_sweep.jsonl).
+        dec_chunk = self.dec_chunk if self.dec_chunk > 0 else (128 if B >= 32 else 64)
         r = self._embed(ids.reshape(-1))  # residual stream (bf16)
         delta = None
 
@@ -607,7 +615,7 @@ class LlamaTP:
             parts = None
             if decode:  # RoPE + KV append ride inside the decode-attention launch
                 kw = dict(workspace=self.dec_ws, counters=self.dec_cnt, positions=pos, cos=self.cos, sin=self.sin,
-                          max_len=self._dec_ctx, combine=not fuse_combine)
+                          max_len=self._dec_ctx, combine=not fuse_combine, head_major=self.kv_hm)
                 if self.pages is not None:
                     a = ops.decode_attention(qkv, self.k_cache[i], self.v_cache[i], lens, sd.hq, sd.hkv, D,
                                              chunk=self.page_rows, page_table=self.pages.dev[:B], **kw)
@@ -618,7 +626,7 @@ class LlamaTP:
                     a, parts = a
             else:
                 ops.rope_kv_(qkv, pos, self.cos, self.sin, sd.hq, sd.hkv, D, explicit_slots, self.k_cache[i],
-                             self.v_cache[i], lens=lens, seq=S, max_seq=self.max_seq)
+                             self.v_cache[i], lens=lens, seq=S, max_seq=self.max_seq, hm_rows=self.kv_hm_rows)
                 a = ops.flash_attention(qkv, B, S, sd.hq, sd.hkv, D, kv_lens=lens, causal=True)
             if parts is not None:  # split-KV combine in the o-projection's prologue (one launch, not two)
                 o_w = p[f"l{i}.o"]

@@ -817,10 +817,11 @@ def rope_(qkv: torch.Tensor, positions: torch.Tensor, cos: torch.Tensor, sin: to
 
 def rope_kv_(qkv: torch.Tensor, positions: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, n_q_heads: int,
              n_kv_heads: int, head_dim: int, slots: Optional[torch.Tensor] = None, k_cache=None, v_cache=None,
-             lens: Optional[torch.Tensor] = None, seq: int = 1, max_seq: int = 0):
+             lens: Optional[torch.Tensor] = None, seq: int = 1, max_seq: int = 0, hm_rows: int = 0):
     """Fused RoPE (Q and K heads, in place) + KV-cache append in one launch.  Cache slots come from
     ``slots`` (-1 = skip) or, with ``slots=None`` and ``max_seq > 0``, from the token index: token t
-    is (batch t // seq, position p) -> slot ``b * max_seq + p``, skipped unless ``p < lens[b]``."""
+    is (batch t // seq, position p) -> slot ``b * max_seq + p``, skipped unless ``p < lens[b]``.
+    ``hm_rows = R > 0``: head-major cache ``[slots / R][Hkv][R][D]`` (see :func:`decode_attention`)."""
     dev = qkv.device
     _need(qkv, "qkv", torch.bfloat16, dev)
     _need(positions, "positions", torch.int32, dev)
@@ -828,19 +829,20 @@ def rope_kv_(qkv: torch.Tensor, positions: torch.Tensor, cos: torch.Tensor, sin:
     rc = lib().mls_rope_kv(qkv.data_ptr(), positions.data_ptr(), cos.data_ptr(), sin.data_ptr(), T, qkv.shape[-1],
                            n_q_heads, n_kv_heads, head_dim, _ptr(slots), _ptr(k_cache), _ptr(v_cache), _ptr(lens),
                            seq, max_seq, k_cache.numel() // (n_kv_heads * head_dim) if k_cache is not None else 0,
-                           cos.shape[0], stream_ptr(dev))
+                           cos.shape[0], int(hm_rows), stream_ptr(dev))
     check(rc, "mls_rope_kv")
     return qkv
 
 
 def kv_append(qkv: torch.Tensor, k_col: int, v_col: int, slots: torch.Tensor, k_cache: torch.Tensor,
-              v_cache: torch.Tensor, n_kv_heads: int, head_dim: int) -> None:
-    """Scatter the K/V heads of each token row of ``qkv`` into cache slot ``slots[t]``."""
+              v_cache: torch.Tensor, n_kv_heads: int, head_dim: int, hm_rows: int = 0) -> None:
+    """Scatter the K/V heads of each token row of ``qkv`` into cache slot ``slots[t]``
+    (``hm_rows`` as in :func:`rope_kv_`)."""
     dev = qkv.device
     _need(slots, "slots", torch.int32, dev)
     T = slots.numel()
     rc = lib().mls_kv_append(qkv.data_ptr(), qkv.shape[-1], k_col, v_col, slots.data_ptr(), k_cache.data_ptr(),
-                             v_cache.data_ptr(), T, n_kv_heads, head_dim, stream_ptr(dev))
+                             v_cache.data_ptr(), T, n_kv_heads, head_dim, int(hm_rows), stream_ptr(dev))
     check(rc, "mls_kv_append")
 
 
@@ -873,7 +875,7 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
                      counters: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
                      positions: Optional[torch.Tensor] = None, cos: Optional[torch.Tensor] = None,
                      sin: Optional[torch.Tensor] = None, max_len: Optional[int] = None,
-                     page_table: Optional[torch.Tensor] = None, combine: bool = True):
+                     page_table: Optional[torch.Tensor] = None, combine: bool = True, head_major: bool = False):
     """One query token per sequence vs the cache ``[B, max_len, Hkv, D]``; q rows ``[B, >= Hq*D]``
     (head h at column h*D, e.g. the fused QKV row).  Split-KV, combined in the same launch.
     With ``positions``/``cos``/``sin`` (rope mode) q is the raw fused QKV row: RoPE is applied to q
@@ -884,17 +886,23 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
     Paged KV (``page_table [B, pages_per_seq]`` int32): the caches are page pools ``[pages, chunk,
     Hkv, D]`` and row ``r`` of sequence ``b`` is row ``r % chunk`` of page ``page_table[b, r // chunk]``.
     ``combine=False``: multi-split rows are left as fp32 partials for the consumer GEMM to merge
-    (:func:`skinny_packed_combine`); returns ``(out, DecodePartials)``."""
+    (:func:`skinny_packed_combine`); returns ``(out, DecodePartials)``.
+    ``head_major``: caches laid out ``[B, Hkv, max_len, D]`` (paged: ``[pages, Hkv, chunk, D]``) --
+    one head's rows contiguous, so each split block streams one run instead of 256-B slices."""
     dev = q.device
     B = lens.numel()
+    rows_dim = 2 if head_major else 1
     if page_table is not None:
         _need(page_table, "page_table", torch.int32, dev)
-        if page_table.dim() != 2 or page_table.shape[0] < B or k_cache.shape[1] != chunk:
-            raise ValueError("paged decode: page_table [>= B, pages_per_seq], caches [pages, chunk, Hkv, D]")
+        if page_table.dim() != 2 or page_table.shape[0] < B or k_cache.shape[rows_dim] != chunk:
+            raise ValueError("paged decode: page_table [>= B, pages_per_seq], caches [pages, chunk, Hkv, D] "
+                             "(head-major: [pages, Hkv, chunk, D])")
         cap = page_table.shape[1] * chunk
         max_len = cap if max_len is None else min(int(max_len), cap)
     else:
-        max_len = k_cache.shape[1] if max_len is None else min(int(max_len), k_cache.shape[1])
+        L = k_cache.shape[rows_dim]
+        max_len = L if max_len is None else min(int(max_len), L)
+    hm_rows = k_cache.shape[2] if head_major else 0
     nsplit = (max_len + chunk - 1) // chunk
     need = B * n_q_heads * nsplit * (head_dim + 2)
     if workspace is None or workspace.numel() < need:
@@ -913,7 +921,7 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
                                     cos.shape[0] if cos is not None else 0, B, n_q_heads, n_kv_heads, head_dim, max_len,
                                     chunk, float(scale), _ptr(page_table),
                                     page_table.shape[1] if page_table is not None else 0, int(not combine),
-                                    stream_ptr(dev))
+                                    int(hm_rows), stream_ptr(dev))
     check(rc, "mls_decode_attention")
     if not combine:
         return out, DecodePartials(ws, ws_ml, nsplit, chunk, lens, n_q_heads, head_dim)

@@ -63,14 +63,14 @@ _SIGS = {
     "mls_ar_allreduce": [P, P, P, L, _c.c_longlong, P],
     "mls_ar_error": [P, P],
     "mls_ar_destroy": [P],
-    "mls_rope_kv": [P, P, P, P, L, I, I, I, I, P, P, P, P, I, I, L, I, P],
-    "mls_kv_append": [P, I, I, I, P, P, P, L, I, I, P],
+    "mls_rope_kv": [P, P, P, P, L, I, I, I, I, P, P, P, P, I, I, L, I, I, P],
+    "mls_kv_append": [P, I, I, I, P, P, P, L, I, I, I, P],
     "mls_flash_attention": [P, P, P, P, I, I, I, I, I, I, I, I, I, P, I, F, P],
     "mls_skinny_gemm": [P, P, P, P, P, P, SZ, I, I, I, I, I, P],
     "mls_skinny_gemm_norm": [P, P, P, P, P, P, P, P, SZ, I, I, I, I, I, I, F, P],
     "mls_skinny_pack": [P, P, I, I, P],
     "mls_skinny_packed": [P, P, P, P, P, P, P, I, I, I, I, I, F, I, P],
-    "mls_decode_attention": [P, P, P, P, P, P, P, I, I, L, P, P, P, P, I, I, I, I, I, I, I, F, P, I, I, P],
+    "mls_decode_attention": [P, P, P, P, P, P, P, I, I, L, P, P, P, P, I, I, I, I, I, I, I, F, P, I, I, I, P],
     "mls_skinny_packed_combine": [P, P, P, P, I, I, I, I, P, P, P, P, I, I, I, I, I, P],
     "mls_skinny_fp8": [P, P, P, P, P, P, P, P, I, I, I, I, I, F, I, P],
 }

@@ -133,8 +133,8 @@ __global__ __launch_bounds__(256) void flash_fwd_kernel(const AttnArgs a) {
         s[t][j] = x;
         mt = fmaxf(mt, x);
       }
-    mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    mt = fmaxf(mt, xor16_f(mt));  // v_permlane swaps, not LDS round trips
+    mt = fmaxf(mt, xor32_f(mt));
     const float m_new = fmaxf(m_run, mt);
     const float alpha = (m_new == -INFINITY) ? 1.f : fast_exp2(m_run - m_new);
     float ls = 0.f;
@@ -146,8 +146,8 @@ __global__ __launch_bounds__(256) void flash_fwd_kernel(const AttnArgs a) {
         s[t][j] = p;
         ls += p;
       }
-    ls += __shfl_xor(ls, 16, 64);
-    ls += __shfl_xor(ls, 32, 64);
+    ls += xor16_f(ls);
+    ls += xor32_f(ls);
     l_run = l_run * alpha + ls;
     m_run = m_new;
     // rescale O rows q = 4g + j by alpha of query lane (4g + j)
@@ -210,6 +210,7 @@ struct DecodeArgs {
   const int* lens;
   const int* page_table;  // paged cache: [B][pages_per_seq] page ids, a page = one split's CHUNK rows
   int pages_per_seq;
+  int hm_rows;  // 0: row-major cache rows [row][Hkv][D]; R: head-major blocks [row / R][Hkv][R][D]
   const int* positions;  // rope mode: query position per sequence (== lens[b] - 1)
   const float* cos_t;    // [max_pos][D/2]
   const float* sin_t;
@@ -271,12 +272,20 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(const DecodeArgs a) {
   const int pos = rope ? a.positions[b] : 0;
   MLS_CHECK(!rope || (pos >= 0 && pos < a.max_pos && pos == L0 - 1), 202);
   const bf16* qrow = a.q + (long)b * a.q_stride;
-  const long rstride = (long)a.Hkv * D;
-  // row r of this split lives at sbase + r * rstride: contiguous per sequence, or (paged) in the page
-  // the table maps this split to -- a page holds exactly one split's CHUNK rows
-  const long sbase = a.page_table ? ((long)a.page_table[b * a.pages_per_seq + sp] * CHUNK - start) * rstride
-                                  : (long)b * a.seq_stride;
-  const long cbase = sbase + (long)hk * D + gl * 8;
+  // row r of this split lives at cbase + r * rstride: contiguous per sequence, or (paged) in the page
+  // the table maps this split to -- a page holds exactly one split's CHUNK rows.  Head-major caches
+  // keep one head's rows contiguous (rstride = D): the block streams one 64 x 256 B run.
+  const long rstride = a.hm_rows > 0 ? (long)D : (long)a.Hkv * D;
+  long cbase;
+  if (a.hm_rows > 0) {
+    const long blk = a.page_table ? (long)a.page_table[b * a.pages_per_seq + sp] : (long)b;
+    const long r0 = a.page_table ? (long)start : 0;  // row index of the block's first row
+    cbase = ((blk * a.Hkv + hk) * a.hm_rows - r0) * D + gl * 8;
+  } else {
+    const long sbase = a.page_table ? ((long)a.page_table[b * a.pages_per_seq + sp] * CHUNK - start) * rstride
+                                    : (long)b * a.seq_stride;
+    cbase = sbase + (long)hk * D + gl * 8;
+  }
 
   // issue every K/V row load of this block first
   uint4 kraw[NIT], vraw[NIT];
@@ -370,8 +379,7 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(const DecodeArgs a) {
       float d = 0.f;
 #pragma unroll
       for (int e = 0; e < 8; ++e) d += qv[hh][e] * kf[e];
-#pragma unroll
-      for (int o = LPR / 2; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+      d = group_sum<LPR>(d);  // the row's LPR lanes (DPP, no LDS round trips)
       const float sc = valid ? d : -INFINITY;
       const float mn = fmaxf(m[hh], sc);
       if (mn == -INFINITY) continue;
@@ -386,15 +394,17 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(const DecodeArgs a) {
   // merge the wave's RPW row groups (lanes gl + LPR*grp) by shuffles
 #pragma unroll
   for (int hh = 0; hh < G; ++hh) {
+    // partner lanes (lane ^ o) by DPP row rotation / v_permlane swaps
+    auto xchg = [](float v, int o) { return o == 8 ? xor8_f(v) : o == 16 ? xor16_f(v) : xor32_f(v); };
 #pragma unroll
     for (int o = LPR; o < 64; o <<= 1) {
-      const float m2 = __shfl_xor(m[hh], o, 64), l2 = __shfl_xor(l[hh], o, 64);
+      const float m2 = xchg(m[hh], o), l2 = xchg(l[hh], o);
       const float mn = fmaxf(m[hh], m2);
       const float w1 = mn == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m[hh] - mn);
       const float w2 = mn == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m2 - mn);
       l[hh] = l[hh] * w1 + l2 * w2;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) acc[hh][e] = acc[hh][e] * w1 + __shfl_xor(acc[hh][e], o, 64) * w2;
+      for (int e = 0; e < 8; ++e) acc[hh][e] = acc[hh][e] * w1 + xchg(acc[hh][e], o) * w2;
       m[hh] = mn;
     }
     if (grp == 0) {
@@ -525,6 +535,8 @@ int mls_flash_attention(const void* q, const void* k, const void* v, void* o, in
 
 // workspace: ws >= B*Hq*nsplit*D floats, ws_ml >= B*Hq*nsplit*2 floats, nsplit = ceil(max_len/chunk);
 // page_table (optional): [B][pages_per_seq] ids of chunk-row pages of the caches (paged KV).
+// hm_rows: 0 = row-major cache [rows][Hkv][D]; R = head-major [rows / R][Hkv][R][D] (R = max_len
+// per sequence, or the page rows when paged).
 // skip_combine: leave multi-split rows as partials in ws / ws_ml (a consumer merges them, e.g.
 // mls_skinny_packed_combine); rows that fit one split are still written to `o`.
 // counters: B*Hkv zero-initialised ints.  chunk: rows per split (D=128: 16..256; D=64: 32..512).
@@ -533,7 +545,7 @@ int mls_decode_attention(const void* q, void* k_cache, void* v_cache, void* o, f
                          int q_stride, int o_stride, long seq_stride, const int* lens, const int* positions,
                          const float* cos_t, const float* sin_t, int max_pos, int B, int Hq, int Hkv, int D,
                          int max_len, int chunk, float scale, const int* page_table, int pages_per_seq,
-                         int skip_combine, void* stream) {
+                         int skip_combine, int hm_rows, void* stream) {
   if (B <= 0 || Hq % Hkv || chunk <= 0 || max_len <= 0) return MLS_BAD_ARG;
   if (page_table && (long)pages_per_seq * chunk < max_len) return MLS_BAD_ARG;
   (void)counters;  // reserved (in-launch merge variants); the combine runs as its own launch
@@ -552,6 +564,8 @@ int mls_decode_attention(const void* q, void* k_cache, void* v_cache, void* o, f
   a.lens = lens;
   a.page_table = page_table;
   a.pages_per_seq = pages_per_seq;
+  a.hm_rows = hm_rows;
+  if (page_table && hm_rows > 0 && hm_rows != chunk) return MLS_BAD_ARG;  // a page = one split
   a.positions = positions;
   a.cos_t = cos_t;
   a.sin_t = sin_t;

@@ -90,6 +90,37 @@ MLS_DEV uint4 pack8(const float (&f)[8]) {
   return __builtin_bit_cast(uint4, b);
 }
 
+// ---- cross-lane exchange on the VALU (DPP / v_permlane*_swap), not the LDS pipe ----
+// __shfl_xor compiles to ds_bpermute_b32: an LDS round trip (~100+ cycles) per step, which makes a
+// dependent reduction chain latency-bound.  These stay on the VALU.
+template <int CTRL>
+MLS_DEV float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+// value held by lane (lane ^ 16) / (lane ^ 32)
+MLS_DEV float xor16_f(float v) {
+  const unsigned u = __builtin_bit_cast(unsigned, v);
+  const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  return __builtin_bit_cast(float, ((threadIdx.x >> 4) & 1) ? r[0] : r[1]);
+}
+MLS_DEV float xor32_f(float v) {
+  const unsigned u = __builtin_bit_cast(unsigned, v);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return __builtin_bit_cast(float, ((threadIdx.x >> 5) & 1) ? r[0] : r[1]);
+}
+// value held by lane (lane ^ 8) (rotate by 8 inside a 16-lane row)
+MLS_DEV float xor8_f(float v) { return dpp_f<0x128>(v); }
+// sum over aligned groups of N lanes (N = 4, 8, 16), every lane gets its group's sum
+template <int N>
+MLS_DEV float group_sum(float v) {
+  static_assert(N == 4 || N == 8 || N == 16, "group");
+  v += dpp_f<0xB1>(v);                      // quad_perm [1,0,3,2]: lane ^ 1
+  v += dpp_f<0x4E>(v);                      // quad_perm [2,3,0,1]: lane ^ 2
+  if constexpr (N >= 8) v += dpp_f<0x141>(v);   // row_half_mirror: the other quad of the 8
+  if constexpr (N >= 16) v += dpp_f<0x140>(v);  // row_mirror: the other half of the 16
+  return v;
+}
+
 // ---- wave64 reductions ----
 MLS_DEV float wave_sum(float v) {
 #pragma unroll

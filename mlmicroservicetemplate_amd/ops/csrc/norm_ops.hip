@@ -150,6 +150,15 @@ __global__ __launch_bounds__(256) void embedding_kernel(const int* __restrict__ 
   }
 }
 
+// Element offset of (cache slot, head, dim chunk) in a KV cache.  hm_rows == 0: row-major
+// [slot][Hkv][D]; hm_rows = R > 0: head-major blocks of R rows, [slot / R][Hkv][R][D] -- a
+// sequence's (R = max_seq) or a page's (R = page rows) rows of one head are contiguous, so the
+// decode-attention block reading one head streams one contiguous run.
+MLS_DEV long kv_offset(long slot, int h, int d, int Hkv, int D, int hm_rows) {
+  if (hm_rows <= 0) return (slot * Hkv + h) * D + d;
+  return (((slot / hm_rows) * Hkv + h) * hm_rows + slot % hm_rows) * D + d;
+}
+
 // RoPE + KV-cache append in one pass (decode / prefill): Q and K heads rotated in place, then
 // the (rotated) K heads and the V heads of each token copied to cache slot slots[t]; one launch
 // instead of two.  Block = one token; threads: (head, pair-quad) for the rotation, then 16-B copies.
@@ -158,7 +167,7 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(bf16* __restrict__ qkv, co
                                                       int row_stride, int Hq, int Hkv, int D,
                                                       const int* __restrict__ slots, bf16* __restrict__ kc,
                                                       bf16* __restrict__ vc, const int* __restrict__ lens, int S,
-                                                      int max_seq, long cache_rows, int max_pos) {
+                                                      int max_seq, long cache_rows, int max_pos, int hm_rows) {
   const long t = blockIdx.x;
   const int half = D >> 1, quads = half >> 2;
   const int p = positions[t];
@@ -199,11 +208,11 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(bf16* __restrict__ qkv, co
   if (slot >= cache_rows) return;
   __syncthreads();  // rotated K visible to the copy below (LDS-free: same block, global memory)
   __threadfence_block();
-  const int nch = (Hkv * D) >> 3;
+  const int nch = (Hkv * D) >> 3, hch = D >> 3;
   for (int q = threadIdx.x; q < 2 * nch; q += blockDim.x) {
     const int which = q / nch, ch = q % nch;
     const bf16* src = row + (long)(Hq + which * Hkv) * D + ch * 8;
-    bf16* dst = (which ? vc : kc) + (long)slot * Hkv * D + ch * 8;
+    bf16* dst = (which ? vc : kc) + kv_offset(slot, ch / hch, (ch % hch) * 8, Hkv, D, hm_rows);
     st16(dst, ld16(src));
   }
 }
@@ -249,8 +258,8 @@ __global__ __launch_bounds__(256) void rope_kernel(bf16* __restrict__ qkv, const
 __global__ __launch_bounds__(256) void kv_append_kernel(const bf16* __restrict__ qkv, int row_stride, int k_col,
                                                         int v_col, const int* __restrict__ slots,
                                                         bf16* __restrict__ kc, bf16* __restrict__ vc, long tokens,
-                                                        int Hkv, int D) {
-  const int nch = (Hkv * D) >> 3;
+                                                        int Hkv, int D, int hm_rows) {
+  const int nch = (Hkv * D) >> 3, hch = D >> 3;
   const long total = tokens * nch * 2;
   for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
     const int which = (int)(q & 1);
@@ -260,7 +269,7 @@ __global__ __launch_bounds__(256) void kv_append_kernel(const bf16* __restrict__
     const int slot = slots[t];
     if (slot < 0) continue;
     const bf16* src = qkv + t * row_stride + (which ? v_col : k_col) + ch * 8;
-    bf16* dst = (which ? vc : kc) + (long)slot * Hkv * D + ch * 8;
+    bf16* dst = (which ? vc : kc) + kv_offset(slot, ch / hch, (ch % hch) * 8, Hkv, D, hm_rows);
     st16(dst, ld16(src));
   }
 }
@@ -327,21 +336,22 @@ int mls_rope(void* qkv, const int* positions, const float* cos_t, const float* s
 
 int mls_rope_kv(void* qkv, const int* positions, const float* cos_t, const float* sin_t, long tokens, int row_stride,
                 int Hq, int Hkv, int D, const int* slots, void* k_cache, void* v_cache, const int* lens, int S,
-                int max_seq, long cache_rows, int max_pos, void* stream) {
+                int max_seq, long cache_rows, int max_pos, int hm_rows, void* stream) {
   if (D % 8 || tokens <= 0 || row_stride % 8 || (!slots && max_seq > 0 && S <= 0)) return MLS_BAD_ARG;
+  if (hm_rows > 0 && cache_rows % hm_rows) return MLS_BAD_ARG;
   hipLaunchKernelGGL(rope_kv_kernel, dim3((unsigned)tokens), dim3(256), 0, (hipStream_t)stream, (bf16*)qkv, positions,
                      cos_t, sin_t, row_stride, Hq, Hkv, D, slots, (bf16*)k_cache, (bf16*)v_cache, lens, S, max_seq,
-                     cache_rows, max_pos);
+                     cache_rows, max_pos, hm_rows);
   return (int)hipGetLastError();
 }
 
 int mls_kv_append(const void* qkv, int row_stride, int k_col, int v_col, const int* slots, void* k_cache,
-                  void* v_cache, long tokens, int Hkv, int D, void* stream) {
-  if ((Hkv * D) % 8 || tokens <= 0 || k_col % 8 || v_col % 8 || row_stride % 8) return MLS_BAD_ARG;
+                  void* v_cache, long tokens, int Hkv, int D, int hm_rows, void* stream) {
+  if ((Hkv * D) % 8 || D % 8 || tokens <= 0 || k_col % 8 || v_col % 8 || row_stride % 8) return MLS_BAD_ARG;
   const long work = tokens * (Hkv * D / 8) * 2;
   hipLaunchKernelGGL(kv_append_kernel, dim3(grid_for(work, 256)), dim3(256), 0, (hipStream_t)stream,
                      (const bf16*)qkv, row_stride, k_col, v_col, slots, (bf16*)k_cache, (bf16*)v_cache, tokens, Hkv,
-                     D);
+                     D, hm_rows);
   return (int)hipGetLastError();
 }
 

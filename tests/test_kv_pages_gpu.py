@@ -112,6 +112,7 @@ def test_fused_llama_fp8_decode_close_to_bf16(monkeypatch):
     p = init_llama_shard(cfg, 1, 0, seed=6, device=DEV)
     ref = LlamaTP(p, cfg, backend="fused", device=DEV, max_batch=2, max_seq=128)
     monkeypatch.setenv("MLS_DECODE_FP8", "1")
+    monkeypatch.setenv("MLS_DECODE_FP8_MIN", "0")  # the tiny model's matrices are all small
     q8 = LlamaTP(p, cfg, backend="fused", device=DEV, max_batch=2, max_seq=128)
     assert q8.fp8
     calls = {"n": 0}
@@ -135,3 +136,69 @@ def test_fused_llama_fp8_decode_close_to_bf16(monkeypatch):
     v_q8, i_q8 = q8.decode_step(tok, cur, 5, max_ctx=21)
     assert calls["n"] >= 2 * cfg.layers
     assert ((v_q8 - v_ref).abs().max() / v_ref.abs().max()).item() < 0.1
+
+
+@pytest.mark.parametrize("paged", [False, True])
+def test_head_major_decode_equals_row_major(paged):
+    """Head-major caches ([B, Hkv, L, D] / paged [pages, Hkv, 64, D]) give the row-major result bit
+    for bit, plain and in RoPE + append mode (the appended row lands in the head-major slot)."""
+    from mlmicroservicetemplate_amd import ops
+    from mlmicroservicetemplate_amd.ops import reference as R
+
+    torch.manual_seed(11)
+    B, L, Hq, Hkv, D = 3, 256, 32, 8, 128
+    kc = torch.randn(B, L, Hkv, D, device=DEV).to(torch.bfloat16)
+    vc = torch.randn_like(kc)
+    qkv = torch.randn(B, (Hq + 2 * Hkv) * D, device=DEV).to(torch.bfloat16)
+    lens = torch.tensor([1, 130, 256], device=DEV, dtype=torch.int32)
+    pos = lens - 1
+    cos, sin = R.rope_tables(L, D, 500000.0, DEV)
+    for rope in (False, True):
+        kw = dict(positions=pos, cos=cos, sin=sin) if rope else {}
+        k1, v1 = kc.clone(), vc.clone()
+        if paged:
+            kp, table = _paged_copy(k1, L // 64, 20, 3)
+            vp, _ = _paged_copy(v1, L // 64, 20, 3)
+            want = ops.decode_attention(qkv, kp, vp, lens, Hq, Hkv, D, page_table=table, **kw)
+            kh, vh = kp.new_zeros(20, Hkv, 64, D), vp.new_zeros(20, Hkv, 64, D)
+            kh.copy_(_paged_copy(kc, L // 64, 20, 3)[0].permute(0, 2, 1, 3))
+            vh.copy_(_paged_copy(vc, L // 64, 20, 3)[0].permute(0, 2, 1, 3))
+            got = ops.decode_attention(qkv, kh, vh, lens, Hq, Hkv, D, page_table=table, head_major=True, **kw)
+            if rope:
+                assert torch.equal(kh.permute(0, 2, 1, 3), kp) and torch.equal(vh.permute(0, 2, 1, 3), vp)
+        else:
+            want = ops.decode_attention(qkv, k1, v1, lens, Hq, Hkv, D, **kw)
+            kh = kc.permute(0, 2, 1, 3).contiguous()
+            vh = vc.permute(0, 2, 1, 3).contiguous()
+            got = ops.decode_attention(qkv, kh, vh, lens, Hq, Hkv, D, head_major=True, **kw)
+            if rope:
+                assert torch.equal(kh.permute(0, 2, 1, 3), k1) and torch.equal(vh.permute(0, 2, 1, 3), v1)
+        assert torch.equal(got, want)
+
+
+def test_head_major_writers():
+    """rope_kv_ / kv_append with hm_rows write the same rows as the row-major layout."""
+    from mlmicroservicetemplate_amd import ops
+    from mlmicroservicetemplate_amd.ops import reference as R
+
+    torch.manual_seed(12)
+    T, Hq, Hkv, D, MS = 6, 8, 2, 128, 128
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=DEV).to(torch.bfloat16)
+    slots = torch.tensor([0, 5, 127, 128, 200, -1], device=DEV, dtype=torch.int32)
+    pos = torch.tensor([0, 5, 127, 0, 72, 3], device=DEV, dtype=torch.int32)
+    cos, sin = R.rope_tables(256, D, 500000.0, DEV)
+    for R_ in (64, MS):
+        kr = torch.zeros(2 * MS, Hkv, D, device=DEV, dtype=torch.bfloat16)
+        vr = torch.zeros_like(kr)
+        kh = torch.zeros(2 * MS // R_, Hkv, R_, D, device=DEV, dtype=torch.bfloat16)
+        vh = torch.zeros_like(kh)
+        ops.kv_append(qkv, Hq * D, (Hq + Hkv) * D, slots, kr, vr, Hkv, D)
+        ops.kv_append(qkv, Hq * D, (Hq + Hkv) * D, slots, kh, vh, Hkv, D, hm_rows=R_)
+        assert torch.equal(kh.permute(0, 2, 1, 3).reshape(-1, Hkv, D), kr)
+        assert torch.equal(vh.permute(0, 2, 1, 3).reshape(-1, Hkv, D), vr)
+        q1, q2 = qkv.clone(), qkv.clone()
+        kr.zero_(), vr.zero_(), kh.zero_(), vh.zero_()
+        ops.rope_kv_(q1, pos, cos, sin, Hq, Hkv, D, slots, kr, vr)
+        ops.rope_kv_(q2, pos, cos, sin, Hq, Hkv, D, slots, kh, vh, hm_rows=R_)
+        assert torch.equal(q1, q2)
+        assert torch.equal(kh.permute(0, 2, 1, 3).reshape(-1, Hkv, D), kr)

@@ -1,0 +1,45 @@
+"""Offline PyTorch TunableOp search for the Llama-3-8B projection GEMMs that decode runs on
+hipBLASLt (batches above the packed skinny kernels' 24 rows: continuous batching with 32 / 64 /
+128 slots) and for the LM head.  Writes the winning solutions to PYTORCH_TUNABLEOP_FILENAME
+(append them to ops/tuned/tunableop_gfx950.csv; tuning stays off at run time -- lookup only).
+
+    PYTORCH_TUNABLEOP_ENABLED=1 PYTORCH_TUNABLEOP_TUNING=1 PYTORCH_TUNABLEOP_FILENAME=out.csv \\
+        python tools/tune_llama_blas.py --m 32 64 128
+"""
+import argparse
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+# (N, K) of the TP=1 projections; gate_up is the interleaved [2 x 14336, 4096] matrix
+SHAPES = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336),
+          "lm_head": (128256, 4096)}
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--m", type=int, nargs="+", default=[32, 64, 128])
+    ap.add_argument("--shapes", nargs="+", default=list(SHAPES))
+    args = ap.parse_args()
+    assert torch.cuda.tunable.is_enabled() and torch.cuda.tunable.tuning_is_enabled(), "set PYTORCH_TUNABLEOP_*"
+    dev = torch.device("cuda:0")
+    for name in args.shapes:
+        N, K = SHAPES[name]
+        w = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+        for M in args.m:
+            a = torch.randn(M, K, device=dev).to(torch.bfloat16)
+            t0 = time.time()
+            torch.mm(a, w.t())
+            torch.cuda.synchronize()
+            print(f"tuned {name} M={M} N={N} K={K} in {time.time() - t0:.1f}s", flush=True)
+        del w
+    torch.cuda.tunable.write_file()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
