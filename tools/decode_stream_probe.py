@@ -20,6 +20,8 @@ def main():
     dev = torch.device("cuda:0")
     ws = torch.empty(64 << 20, device=dev)
     M = int(os.environ.get("M", "1"))
+    if os.environ.get("BLAS_TUNING") == "1":  # hipBLASLt on the shipped TunableOp table
+        ops.load_blas_tuning()
     for name, (N, K) in SHAPES.items():
         ws_list = [(torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16) for _ in range(32)]
         x = torch.randn(M, K, device=dev).to(torch.bfloat16)

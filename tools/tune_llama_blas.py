@@ -7,6 +7,7 @@ hipBLASLt (batches above the packed skinny kernels' 24 rows: continuous batching
         python tools/tune_llama_blas.py --m 32 64 128
 """
 import argparse
+import json
 import os
 import sys
 import time
@@ -26,6 +27,9 @@ def main() -> int:
     ap.add_argument("--shapes", nargs="+", default=list(SHAPES))
     args = ap.parse_args()
     assert torch.cuda.tunable.is_enabled() and torch.cuda.tunable.tuning_is_enabled(), "set PYTORCH_TUNABLEOP_*"
+    from mlmicroservicetemplate_amd import ops
+    from mlmicroservicetemplate_amd.ops.autotune import _time
+
     dev = torch.device("cuda:0")
     for name in args.shapes:
         N, K = SHAPES[name]
@@ -36,6 +40,13 @@ def main() -> int:
             torch.mm(a, w.t())
             torch.cuda.synchronize()
             print(f"tuned {name} M={M} N={N} K={K} in {time.time() - t0:.1f}s", flush=True)
+            if name == "lm_head":  # 1 GB of weights: cold in the 256 MB Infinity Cache on every call
+                ws = torch.empty(64 << 20, device=dev)
+                for impl, fn in (("hipblaslt_tuned", lambda: torch.mm(a, w.t())),
+                                 ("ops.gemm", lambda: ops.gemm(a, w, workspace=ws))):
+                    us = _time(fn, iters=10) * 1e3
+                    print(json.dumps({"shape": name, "M": M, "impl": impl, "us": round(us, 1),
+                                      "hbm_tb_s": round(N * K * 2 / us / 1e6, 2)}), flush=True)
         del w
     torch.cuda.tunable.write_file()
     return 0
