@@ -10,8 +10,10 @@ Layouts: activations NHWC / row-major ``[rows][features]`` bf16; conv weights
 from __future__ import annotations
 
 import ctypes
+import functools
+import json
 import os
-from typing import Optional, Tuple
+from typing import Dict, Optional, Tuple
 
 import torch
 
@@ -511,6 +513,18 @@ def silu_mul_interleaved(x: torch.Tensor, out: Optional[torch.Tensor] = None) ->
     return out
 
 
+@functools.lru_cache(maxsize=None)
+def gemm_plan() -> Dict[Tuple[int, int, int], Tuple[int, int]]:
+    """Measured per-shape choices for :func:`linear` (``tuned/gemm_plan_gfx950.json``): exact
+    ``(M, N, K)`` -> ``(cfg, splitk)`` of the native kernel, cfg 0 = hipBLASLt.  ``MLS_GEMM_PLAN=0``
+    disables it."""
+    if os.environ.get("MLS_GEMM_PLAN", "1") == "0":
+        return {}
+    with open(os.path.join(_TUNED_DIR, "gemm_plan_gfx950.json")) as f:
+        doc = json.load(f)
+    return {(e["M"], e["N"], e["K"]): (int(e["plan"][0]), int(e["plan"][1])) for e in doc["entries"]}
+
+
 def linear(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, act=ACT_NONE,
            residual: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
            impl: str = "auto") -> torch.Tensor:
@@ -520,6 +534,11 @@ def linear(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     code = _act(act)
     M = a.shape[0]
     blas = impl == "blas" or (impl == "auto" and M >= BLAS_MIN_M)
+    plan = gemm_plan().get((M, w.shape[0], w.shape[1])) if impl == "auto" else None
+    if plan is not None:
+        if plan[0] > 0 and not (code == ACT_SILU_MUL and residual is not None):
+            return gemm(a, w, bias, act=code, residual=residual, workspace=workspace, cfg=plan[0], splitk=plan[1])
+        blas = plan[0] == 0
     if not blas or code not in (ACT_NONE, ACT_GELU, ACT_SILU_MUL) or a.device.type != "cuda":
         return gemm(a, w, bias, act=code, residual=residual, workspace=workspace)
     b16 = _bias_bf16(bias) if bias is not None else None

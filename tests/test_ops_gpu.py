@@ -322,3 +322,25 @@ def test_conv3x3_halo_matches_reference(B, H, W, cin, cout, resid):
     gemm = ops.conv2d_nhwc(x, ops.pack_conv_weight(w), bias, kernel=3, stride=1, pad=1, act=ops.ACT_RELU,
                            residual=res, workspace=torch.empty(8 << 20, device=DEV, dtype=torch.float32))
     assert rel_err(out, gemm) < 2e-2
+
+
+@pytest.mark.parametrize("M,N,K,act", [(64, 4096, 14336, "none"), (64, 28672, 4096, "silu_mul"),
+                                       (128, 4096, 4096, "none"), (128, 4096, 14336, "none")])
+def test_linear_gemm_plan_shapes(M, N, K, act):
+    """ops.linear on the shapes tuned/gemm_plan_gfx950.json routes to a fixed native cfg / split-K."""
+    from mlmicroservicetemplate_amd import ops
+
+    assert (M, N, K) in ops.gemm_plan()
+    g = torch.Generator(device="cpu").manual_seed(M + N)
+    a = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) / K**0.5).to(DEV, torch.bfloat16)
+    res = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16) if act == "none" else None
+    ws = torch.empty(32 << 20, device=DEV)
+    y = ops.linear(a, w, act=act, residual=res, workspace=ws)
+    ref = a.float() @ w.float().t()
+    if act == "silu_mul":
+        r = ref.view(M, N // 16, 2, 8)
+        ref = (F.silu(r[:, :, 0]) * r[:, :, 1]).reshape(M, N // 2)
+    else:
+        ref = ref + res.float()
+    assert rel_err(y, ref) < 2e-2

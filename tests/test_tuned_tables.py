@@ -23,3 +23,10 @@ def test_resnet_table_loads():
 
     t = autotune.load_tuning("resnet50", 32)
     assert "stem" in t and all(len(v) == 2 for v in t.values())
+
+
+def test_gemm_plan_table():
+    plan = ops.gemm_plan()
+    assert plan and all(len(k) == 3 and len(v) == 2 and v[0] >= 0 and v[1] >= 0 for k, v in plan.items())
+    for (M, N, K), (cfg, sk) in plan.items():
+        assert cfg < 32 and N % 16 == 0 and K % 8 == 0

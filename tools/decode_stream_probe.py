@@ -32,9 +32,14 @@ def main():
             "skinny": lambda: [ops.gemm(x, w, act=act, workspace=ws) for w in ws_list],
             "hipblaslt": lambda: [torch.mm(x, w.t()) for w in ws_list],
         }
-        if K == 4096 and name != "o":
+        if K == 4096 and name != "o" and M <= 32:
             impls["fused_norm_skinny"] = lambda: [ops.gemm_rmsnorm(x, w, d, r_out, act=act, workspace=ws)
                                                   for w in ws_list]
+        if os.environ.get("GEMM_CFGS"):  # native tile configs x split-K factors (ops.gemm cfg / splitk)
+            for c in [int(t) for t in os.environ["GEMM_CFGS"].split(",")]:
+                for sk in [int(t) for t in os.environ.get("GEMM_SPLITS", "1,2,4,8").split(",")]:
+                    impls[f"gemm_c{c}_s{sk}"] = (lambda c=c, sk=sk: [ops.gemm(x, w, act=act, workspace=ws, cfg=c, splitk=sk)
+                                                               for w in ws_list])
         lib = ops.lib()
 
         def variant(fn, no_lds):
