@@ -894,7 +894,8 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
                      counters: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
                      positions: Optional[torch.Tensor] = None, cos: Optional[torch.Tensor] = None,
                      sin: Optional[torch.Tensor] = None, max_len: Optional[int] = None,
-                     page_table: Optional[torch.Tensor] = None, combine: bool = True, head_major: bool = False):
+                     page_table: Optional[torch.Tensor] = None, combine: bool = True, head_major: bool = False,
+                     impl: Optional[str] = None):
     """One query token per sequence vs the cache ``[B, max_len, Hkv, D]``; q rows ``[B, >= Hq*D]``
     (head h at column h*D, e.g. the fused QKV row).  Split-KV, combined in the same launch.
     With ``positions``/``cos``/``sin`` (rope mode) q is the raw fused QKV row: RoPE is applied to q
@@ -907,7 +908,11 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
     ``combine=False``: multi-split rows are left as fp32 partials for the consumer GEMM to merge
     (:func:`skinny_packed_combine`); returns ``(out, DecodePartials)``.
     ``head_major``: caches laid out ``[B, Hkv, max_len, D]`` (paged: ``[pages, Hkv, chunk, D]``) --
-    one head's rows contiguous, so each split block streams one run instead of 256-B slices."""
+    one head's rows contiguous, so each split block streams one run instead of 256-B slices.
+    ``impl``: "mfma" (matrix-core kernel: D = 128, chunk 64 / 128, G <= 8), "valu", or "auto"
+    (default, env ``MLS_DECODE_ATTN``): the matrix-core kernel wherever it applies."""
+    impl = impl or os.environ.get("MLS_DECODE_ATTN", "auto")
+    impl_code = {"auto": 0, "valu": 1, "mfma": 2}[impl]
     dev = q.device
     B = lens.numel()
     rows_dim = 2 if head_major else 1
@@ -940,7 +945,7 @@ def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tens
                                     cos.shape[0] if cos is not None else 0, B, n_q_heads, n_kv_heads, head_dim, max_len,
                                     chunk, float(scale), _ptr(page_table),
                                     page_table.shape[1] if page_table is not None else 0, int(not combine),
-                                    int(hm_rows), stream_ptr(dev))
+                                    int(hm_rows), impl_code, stream_ptr(dev))
     check(rc, "mls_decode_attention")
     if not combine:
         return out, DecodePartials(ws, ws_ml, nsplit, chunk, lens, n_q_heads, head_dim)

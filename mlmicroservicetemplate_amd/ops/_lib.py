@@ -70,7 +70,7 @@ _SIGS = {
     "mls_skinny_gemm_norm": [P, P, P, P, P, P, P, P, SZ, I, I, I, I, I, I, F, P],
     "mls_skinny_pack": [P, P, I, I, P],
     "mls_skinny_packed": [P, P, P, P, P, P, P, I, I, I, I, I, F, I, P],
-    "mls_decode_attention": [P, P, P, P, P, P, P, I, I, L, P, P, P, P, I, I, I, I, I, I, I, F, P, I, I, I, P],
+    "mls_decode_attention": [P, P, P, P, P, P, P, I, I, L, P, P, P, P, I, I, I, I, I, I, I, F, P, I, I, I, I, P],
     "mls_skinny_packed_combine": [P, P, P, P, I, I, I, I, P, P, P, P, I, I, I, I, I, P],
     "mls_skinny_fp8": [P, P, P, P, P, P, P, P, I, I, I, I, I, F, I, P],
 }

@@ -445,6 +445,242 @@ __global__ __launch_bounds__(256) void decode_attn_kernel(const DecodeArgs a) {
   }
 }
 
+// Decode attention on the matrix cores (D = 128, chunk = 32 keys per wave).  The VALU kernel
+// above spends ~850 VALU instructions per wave on a 64-key split (per key and head: the 8-lane
+// dot, its DPP reduction, the online-softmax rescale of 8 accumulators), which is what bounds it
+// at large batch (batch 128: 55M VALU instructions per layer, ~2.3 TB/s of KV).  Here, per wave:
+//   S^T = K . Q^T  (A = 32 key rows straight from the cache, 16-B loads; B = the G roped query
+//                  heads from LDS, head on the lane column, padded to 16 with zeros): 8 MFMAs
+//   O   = P . V    (A = P packed from the S^T accumulators, B = V through a per-wave row-major
+//                  LDS image read with ds_read_b64_tr_b16, keys in the same permuted order):
+//                  8 MFMAs, one softmax pass (all 32 keys are in registers, no rescale)
+// RoPE of q / the new key and the KV append run once per block in an LDS prologue.  Partials
+// (m, l, O) are merged over the block's waves and written exactly as the VALU kernel does, so
+// decode_combine_kernel and the fused combine of mls_skinny_packed_combine are shared.
+template <int G, int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void decode_attn_mfma_kernel(const DecodeArgs a) {
+  constexpr int D = 128, KK = D / 32, DT = D / 16;
+  constexpr int NT = WAVES * 64, CHUNK = WAVES * 32;
+  constexpr int VST = D * 2 + 32;          // padded V row (bytes): conflict-free transposed reads
+  constexpr int NPRO = (G + 1) * 16;       // prologue tasks: G query heads + the new key row, 16-B chunks
+  constexpr int PIT = (NPRO + NT - 1) / NT;
+  __shared__ __attribute__((aligned(16))) char vs[WAVES][32 * VST];
+  __shared__ __attribute__((aligned(16))) bf16 qimg[G + 2][D];  // roped q heads, roped new K, new V
+  __shared__ float sm_m[WAVES][G], sm_l[WAVES][G];
+  __shared__ __attribute__((aligned(16))) float sm_o[WAVES][G][D];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int g = lane >> 4, fr = lane & 15;
+  const int b = blockIdx.z, hk = blockIdx.x, sp = blockIdx.y;
+  const int L0 = a.lens[b];
+  MLS_CHECK(sp != 0 || L0 <= a.nsplit * CHUNK, 201);
+  const int L = min(L0, a.nsplit * CHUNK);
+  const int start = sp * CHUNK;
+  if (start >= L) {
+    if (L <= 0 && sp == 0)
+      for (int idx = tid; idx < G * D; idx += NT) a.o[(long)b * a.o_stride + (long)hk * G * D + idx] = (bf16)0.f;
+    return;
+  }
+  const int end = min(L, start + CHUNK);
+  const bool rope = a.positions != nullptr;
+  const int pos = rope ? a.positions[b] : 0;
+  MLS_CHECK(!rope || (pos >= 0 && pos < a.max_pos && pos == L0 - 1), 202);
+  const bf16* qrow = a.q + (long)b * a.q_stride;
+  const long rstride = a.hm_rows > 0 ? (long)D : (long)a.Hkv * D;
+  long cbase;
+  if (a.hm_rows > 0) {
+    const long blk = a.page_table ? (long)a.page_table[b * a.pages_per_seq + sp] : (long)b;
+    const long r0 = a.page_table ? (long)start : 0;
+    cbase = ((blk * a.Hkv + hk) * a.hm_rows - r0) * D;
+  } else {
+    cbase = a.page_table ? ((long)a.page_table[b * a.pages_per_seq + sp] * CHUNK - start) * rstride
+                         : (long)b * a.seq_stride;
+    cbase += (long)hk * D;
+  }
+  const bool has_new = rope && L - 1 >= start && L - 1 < end;
+  const int w0 = start + wid * 32;  // this wave's first key
+
+  // small operands first (so their vmcnt waits leave the cache rows in flight), then the rows
+  uint4 px[PIT], pxp[PIT], pv[PIT];
+  float4 pcs[PIT][4];
+#pragma unroll
+  for (int it = 0; it < PIT; ++it) {
+    const int t = tid + it * NT, r = t >> 4, c = t & 15;
+    px[it] = pxp[it] = pv[it] = make_uint4(0, 0, 0, 0);
+    pcs[it][0] = pcs[it][1] = pcs[it][2] = pcs[it][3] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (t < NPRO && (r < G || rope)) {
+      const bf16* src = qrow + (long)(r < G ? hk * G + r : a.Hq + hk) * D;
+      px[it] = ld16(src + c * 8);
+      if (rope) {
+        pxp[it] = ld16(src + ((c + 8) & 15) * 8);
+        const float* cp = a.cos_t + (long)pos * (D / 2) + (c & 7) * 8;
+        const float* sq = a.sin_t + (long)pos * (D / 2) + (c & 7) * 8;
+        pcs[it][0] = *reinterpret_cast<const float4*>(cp);
+        pcs[it][1] = *reinterpret_cast<const float4*>(cp + 4);
+        pcs[it][2] = *reinterpret_cast<const float4*>(sq);
+        pcs[it][3] = *reinterpret_cast<const float4*>(sq + 4);
+        if (r == G) pv[it] = ld16(qrow + (long)(a.Hq + a.Hkv + hk) * D + c * 8);
+      }
+    }
+  }
+  uint4 kraw[2][KK], vraw[8];
+#pragma unroll
+  for (int t2 = 0; t2 < 2; ++t2) {
+    const int key = w0 + 16 * t2 + fr;
+    const bool ok = key < end && !(rope && key == L - 1);
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk)
+      kraw[t2][kk] = ok ? ld16(a.kc + cbase + key * rstride + 32 * kk + 8 * g) : make_uint4(0, 0, 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int key = w0 + 4 * i + g;
+    const bool ok = key < end && !(rope && key == L - 1);
+    vraw[i] = ok ? ld16(a.vc + cbase + key * rstride + fr * 8) : make_uint4(0, 0, 0, 0);
+  }
+
+  // prologue: RoPE'd q heads (bf16, as the cache path rounds them) and the new key row -> LDS;
+  // the block holding row L-1 appends the new K / V to the cache
+#pragma unroll
+  for (int it = 0; it < PIT; ++it) {
+    const int t = tid + it * NT, r = t >> 4, c = t & 15;
+    if (t < NPRO && (r < G || rope)) {
+      float x[8];
+      unpack8(px[it], x);
+      if (rope) {
+        float xp[8];
+        unpack8(pxp[it], xp);
+        const float cc[8] = {pcs[it][0].x, pcs[it][0].y, pcs[it][0].z, pcs[it][0].w,
+                             pcs[it][1].x, pcs[it][1].y, pcs[it][1].z, pcs[it][1].w};
+        const float sn[8] = {pcs[it][2].x, pcs[it][2].y, pcs[it][2].z, pcs[it][2].w,
+                             pcs[it][3].x, pcs[it][3].y, pcs[it][3].z, pcs[it][3].w};
+        const float sgn = c < 8 ? -1.f : 1.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = x[e] * cc[e] + sgn * xp[e] * sn[e];
+      }
+      const uint4 xb = pack8(x);
+      *reinterpret_cast<uint4*>(&qimg[r][c * 8]) = xb;
+      if (r == G) {
+        *reinterpret_cast<uint4*>(&qimg[G + 1][c * 8]) = pv[it];
+        if (has_new) {
+          st16(a.kc + cbase + (long)(L - 1) * rstride + c * 8, xb);
+          st16(a.vc + cbase + (long)(L - 1) * rstride + c * 8, pv[it]);
+        }
+      }
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  bf16x8 qf[KK];
+#pragma unroll
+  for (int kk = 0; kk < KK; ++kk)
+    qf[kk] = fr < G ? __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(&qimg[fr < G ? fr : 0][32 * kk + 8 * g]))
+                    : __builtin_bit_cast(bf16x8, make_uint4(0, 0, 0, 0));
+  f32x4 s[2];
+#pragma unroll
+  for (int t2 = 0; t2 < 2; ++t2) {
+    if (rope && w0 + 16 * t2 + fr == L - 1) {
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) kraw[t2][kk] = *reinterpret_cast<const uint4*>(&qimg[G][32 * kk + 8 * g]);
+    }
+    s[t2] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk)
+      s[t2] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kraw[t2][kk]), qf[kk], s[t2], 0, 0, 0);
+  }
+  // softmax over the wave's 32 keys (key = w0 + 16 t2 + 4g + j on accumulator row, head fr on the lane)
+  float mt = -INFINITY;
+#pragma unroll
+  for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float x = w0 + 16 * t2 + 4 * g + j < end ? s[t2][j] * a.scale_log2 : -INFINITY;
+      s[t2][j] = x;
+      mt = fmaxf(mt, x);
+    }
+  mt = fmaxf(mt, xor16_f(mt));
+  mt = fmaxf(mt, xor32_f(mt));
+  float ls = 0.f;
+#pragma unroll
+  for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float p = mt == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(s[t2][j] - mt);
+      s[t2][j] = p;
+      ls += p;
+    }
+  ls += xor16_f(ls);
+  ls += xor32_f(ls);
+
+  // V rows -> this wave's LDS image (row-major, padded); the new row from the prologue image
+  char* V = vs[wid];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    uint4 v = vraw[i];
+    if (rope && w0 + 4 * i + g == L - 1) v = *reinterpret_cast<const uint4*>(&qimg[G + 1][fr * 8]);
+    *reinterpret_cast<uint4*>(V + (4 * i + g) * VST + fr * 16) = v;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's image, read back by the same wave
+  bf16x8 pf;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    pf[j] = (bf16)s[0][j];
+    pf[4 + j] = (bf16)s[1][j];
+  }
+  const int row0 = 4 * g + (fr >> 2), row1 = row0 + 16;
+  f32x4 o[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+    const int colb = (16 * dt + 4 * (fr & 3)) * 2;
+    const short4v r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS short4v*)(V + row0 * VST + colb));
+    const short4v r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS short4v*)(V + row1 * VST + colb));
+    typedef short short8v __attribute__((ext_vector_type(8)));
+    const short8v vv = {r0[0], r0[1], r0[2], r0[3], r1[0], r1[1], r1[2], r1[3]};
+    o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, __builtin_bit_cast(bf16x8, vv), f32x4{0.f, 0.f, 0.f, 0.f},
+                                                    0, 0, 0);
+  }
+  // O rows = heads 4g + j, columns d = 16 dt + fr
+  if (g == 0 && fr < G) {
+    sm_m[wid][fr] = mt;
+    sm_l[wid][fr] = ls;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int h = 4 * g + j;
+    if (h < G) {
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) sm_o[wid][h < G ? h : 0][16 * dt + fr] = o[dt][j];
+    }
+  }
+  __syncthreads();
+  const bool direct = L <= CHUNK;
+  for (int idx = tid; idx < G * D; idx += NT) {
+    const int hh = idx / D, d = idx % D;
+    float M = -INFINITY;
+#pragma unroll
+    for (int p = 0; p < WAVES; ++p) M = fmaxf(M, sm_m[p][hh]);
+    float Ls = 0.f, O = 0.f;
+    if (M != -INFINITY) {
+#pragma unroll
+      for (int p = 0; p < WAVES; ++p) {
+        const float w = __builtin_amdgcn_exp2f(sm_m[p][hh] - M);
+        Ls += sm_l[p][hh] * w;
+        O += sm_o[p][hh][d] * w;
+      }
+    }
+    if (direct) {
+      a.o[(long)b * a.o_stride + (long)(hk * G + hh) * D + d] = (bf16)(Ls > 0.f ? O / Ls : 0.f);
+    } else {
+      const long base = ((long)b * a.Hq + hk * G + hh) * a.nsplit + sp;
+      a.ws[base * D + d] = O;
+      if (d == 0) {
+        a.ws_ml[base * 2] = M;
+        a.ws_ml[base * 2 + 1] = Ls;
+      }
+    }
+  }
+}
+
 // merge the splits of one (b, q-head): block of D threads; the (m, l) of every split are read
 // once into LDS (one round trip), then each thread's O loads are issued 8 at a time
 template <int D>
@@ -545,7 +781,7 @@ int mls_decode_attention(const void* q, void* k_cache, void* v_cache, void* o, f
                          int q_stride, int o_stride, long seq_stride, const int* lens, const int* positions,
                          const float* cos_t, const float* sin_t, int max_pos, int B, int Hq, int Hkv, int D,
                          int max_len, int chunk, float scale, const int* page_table, int pages_per_seq,
-                         int skip_combine, int hm_rows, void* stream) {
+                         int skip_combine, int hm_rows, int impl, void* stream) {
   if (B <= 0 || Hq % Hkv || chunk <= 0 || max_len <= 0) return MLS_BAD_ARG;
   if (page_table && (long)pages_per_seq * chunk < max_len) return MLS_BAD_ARG;
   (void)counters;  // reserved (in-launch merge variants); the combine runs as its own launch
@@ -581,6 +817,22 @@ int mls_decode_attention(const void* q, void* k_cache, void* v_cache, void* o, f
   if (a.nsplit > 1024) return MLS_UNSUPPORTED;  // combine keeps one weight per split in LDS
   dim3 grid(Hkv, a.nsplit, B);
   hipStream_t st = (hipStream_t)stream;
+  // impl: 0 auto, 1 VALU kernel, 2 matrix-core kernel (D = 128, 64- or 128-key splits, G <= 8)
+  const bool mfma_ok = D == 128 && (chunk == 64 || chunk == 128) && (G == 1 || G == 2 || G == 4 || G == 8);
+  if (impl == 2 && !mfma_ok) return MLS_UNSUPPORTED;
+  if (impl != 1 && mfma_ok) {
+#define DECM(GG)                                                                                            \
+  if (chunk == 64) hipLaunchKernelGGL((decode_attn_mfma_kernel<GG, 2>), grid, dim3(128), 0, st, a);        \
+  else hipLaunchKernelGGL((decode_attn_mfma_kernel<GG, 4>), grid, dim3(256), 0, st, a);
+    if (G == 1) { DECM(1) }
+    else if (G == 2) { DECM(2) }
+    else if (G == 4) { DECM(4) }
+    else { DECM(8) }
+#undef DECM
+    if (a.nsplit > 1 && !skip_combine)
+      hipLaunchKernelGGL(decode_combine_kernel<128>, dim3(B * Hq), dim3(128), 0, st, a, chunk);
+    return (int)hipGetLastError();
+  }
 #define DEC(DD, GG)                                                                                        \
   switch (nit) {                                                                                           \
     case 1: hipLaunchKernelGGL((decode_attn_kernel<DD, GG, 1>), grid, dim3(256), 0, st, a); break;        \

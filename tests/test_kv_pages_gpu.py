@@ -24,8 +24,11 @@ def _paged_copy(cache, pages_per_seq, num_pages, perm_seed=0):
 
 
 @pytest.mark.parametrize("Hq,Hkv", [(4, 1), (32, 8)])
-def test_paged_decode_attention_equals_contiguous(Hq, Hkv):
+@pytest.mark.parametrize("impl", ["valu", "mfma"])
+def test_paged_decode_attention_equals_contiguous(Hq, Hkv, impl, monkeypatch):
     from mlmicroservicetemplate_amd import ops
+
+    monkeypatch.setenv("MLS_DECODE_ATTN", impl)
 
     torch.manual_seed(9)
     B, L, D = 3, 512, 128
@@ -40,9 +43,12 @@ def test_paged_decode_attention_equals_contiguous(Hq, Hkv):
     assert torch.equal(got, want)
 
 
-def test_paged_decode_attention_rope_append():
+@pytest.mark.parametrize("impl", ["valu", "mfma"])
+def test_paged_decode_attention_rope_append(impl, monkeypatch):
     from mlmicroservicetemplate_amd import ops
     from mlmicroservicetemplate_amd.ops import reference as R
+
+    monkeypatch.setenv("MLS_DECODE_ATTN", impl)
 
     torch.manual_seed(10)
     B, L, Hq, Hkv, D = 3, 256, 32, 8, 128
@@ -139,12 +145,14 @@ def test_fused_llama_fp8_decode_close_to_bf16(monkeypatch):
 
 
 @pytest.mark.parametrize("paged", [False, True])
-def test_head_major_decode_equals_row_major(paged):
+@pytest.mark.parametrize("impl", ["valu", "mfma"])
+def test_head_major_decode_equals_row_major(paged, impl, monkeypatch):
     """Head-major caches ([B, Hkv, L, D] / paged [pages, Hkv, 64, D]) give the row-major result bit
     for bit, plain and in RoPE + append mode (the appended row lands in the head-major slot)."""
     from mlmicroservicetemplate_amd import ops
     from mlmicroservicetemplate_amd.ops import reference as R
 
+    monkeypatch.setenv("MLS_DECODE_ATTN", impl)
     torch.manual_seed(11)
     B, L, Hq, Hkv, D = 3, 256, 32, 8, 128
     kc = torch.randn(B, L, Hkv, D, device=DEV).to(torch.bfloat16)

@@ -133,9 +133,12 @@ def test_flash_attention_spike_rescale(ops):
     assert rel(out, ref) < 2e-2
 
 
-@pytest.mark.parametrize("Hq,Hkv,D", [(4, 1, 128), (32, 8, 128), (12, 12, 64)])
+@pytest.mark.parametrize("Hq,Hkv,D", [(4, 1, 128), (32, 8, 128), (64, 8, 128), (8, 4, 128), (12, 12, 64)])
 @pytest.mark.parametrize("chunk", [64, 128, 256])
-def test_decode_attention(ops, Hq, Hkv, D, chunk):
+@pytest.mark.parametrize("impl", ["valu", "mfma"])
+def test_decode_attention(ops, Hq, Hkv, D, chunk, impl):
+    if impl == "mfma" and (D != 128 or chunk == 256):
+        pytest.skip("matrix-core decode kernel: D = 128, 64- / 128-key splits")
     torch.manual_seed(5)
     B, max_len = 4, 1024
     kc = torch.randn(B, max_len, Hkv, D, device=DEV).to(torch.bfloat16)
@@ -146,26 +149,27 @@ def test_decode_attention(ops, Hq, Hkv, D, chunk):
     cnt = torch.zeros(B * Hkv, device=DEV, dtype=torch.int32)
     ref = R.decode_attention(q, kc, vc, lens, Hq, Hkv, D)
     for _ in range(3):  # the ticket counters must come back to zero between launches
-        out = ops.decode_attention(q, kc, vc, lens, Hq, Hkv, D, chunk=chunk, counters=cnt)
+        out = ops.decode_attention(q, kc, vc, lens, Hq, Hkv, D, chunk=chunk, counters=cnt, impl=impl)
         assert rel(out, ref) < 2e-2
     assert not cnt.any()
 
 
-@pytest.mark.parametrize("Hq,Hkv", [(4, 1), (32, 8)])
-def test_decode_attention_rope_append(ops, Hq, Hkv):
+@pytest.mark.parametrize("Hq,Hkv", [(4, 1), (32, 8), (64, 8)])
+@pytest.mark.parametrize("impl,chunk", [("valu", 64), ("mfma", 64), ("mfma", 128)])
+def test_decode_attention_rope_append(ops, Hq, Hkv, impl, chunk):
     """Rope mode == rope_kv_ (RoPE + append) followed by plain decode attention."""
     torch.manual_seed(6)
-    B, max_len, D = 3, 512, 128
+    B, max_len, D = 4, 512, 128
     kc = torch.randn(B, max_len, Hkv, D, device=DEV).to(torch.bfloat16)
     vc = torch.randn(B, max_len, Hkv, D, device=DEV).to(torch.bfloat16)
     qkv = torch.randn(B, (Hq + 2 * Hkv) * D, device=DEV).to(torch.bfloat16)
-    lens = torch.tensor([1, 77, 512], device=DEV, dtype=torch.int32)
+    lens = torch.tensor([1, 77, 512, 129], device=DEV, dtype=torch.int32)
     pos = lens - 1
     cos, sin = R.rope_tables(max_len, D, 500000.0, DEV)
     kc2, vc2, qkv2 = kc.clone(), vc.clone(), qkv.clone()
     ops.rope_kv_(qkv2, pos, cos, sin, Hq, Hkv, D, None, kc2, vc2, lens=lens, seq=1, max_seq=max_len)
-    ref = ops.decode_attention(qkv2, kc2, vc2, lens, Hq, Hkv, D)
-    out = ops.decode_attention(qkv, kc, vc, lens, Hq, Hkv, D, positions=pos, cos=cos, sin=sin)
+    ref = R.decode_attention(qkv2, kc2, vc2, lens, Hq, Hkv, D)
+    out = ops.decode_attention(qkv, kc, vc, lens, Hq, Hkv, D, positions=pos, cos=cos, sin=sin, chunk=chunk, impl=impl)
     assert rel(out, ref) < 1e-2
     for b in range(B):
         p_ = int(pos[b])
