@@ -21,7 +21,7 @@ def ops():
     return o
 
 
-@pytest.mark.parametrize("D", [64, 768, 1000, 4096])
+@pytest.mark.parametrize("D", [64, 768, 1000, 2056, 4096, 8192])
 @pytest.mark.parametrize("rms", [False, True])
 def test_layernorm(ops, D, rms):
     torch.manual_seed(0)
