@@ -324,7 +324,8 @@ def test_conv3x3_halo_matches_reference(B, H, W, cin, cout, resid):
     assert rel_err(out, gemm) < 2e-2
 
 
-@pytest.mark.parametrize("M,N,K,act", [(64, 4096, 14336, "none"), (64, 28672, 4096, "silu_mul"),
+@pytest.mark.parametrize("M,N,K,act", [(32, 28672, 4096, "silu_mul"), (32, 4096, 4096, "none"),
+                                       (64, 4096, 14336, "none"), (64, 28672, 4096, "silu_mul"),
                                        (128, 4096, 4096, "none"), (128, 4096, 14336, "none")])
 def test_linear_gemm_plan_shapes(M, N, K, act):
     """ops.linear on the shapes tuned/gemm_plan_gfx950.json routes to a fixed native cfg / split-K."""

@@ -61,7 +61,7 @@ def main():
                         impls[f"fused_norm_fp8_v{v}"] = (
                             lambda v=v: [ops.skinny_fp8(x, q, sc, N, delta=d, resid_out=r_out, norm=True, act=act,
                                                         variant=v) for q, sc in q_list])
-        if M <= 16:  # packed 1 KiB-granule weights (ops.pack_skinny), variants of mls_skinny_packed
+        if M <= int(os.environ.get("PACKED_MAX_M", "16")):  # packed 1 KiB-granule weights (ops.pack_skinny), variants of mls_skinny_packed
             wp_list = [ops.pack_skinny(w) for w in ws_list]
             norm_fused = K == 4096 and name != "o"
             for v in [int(t) for t in os.environ.get("PACKED_VARIANTS", "0,1,2,3,4,5").split(",")]:
