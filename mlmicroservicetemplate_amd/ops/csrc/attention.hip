@@ -817,13 +817,14 @@ int mls_decode_attention(const void* q, void* k_cache, void* v_cache, void* o, f
   if (a.nsplit > 1024) return MLS_UNSUPPORTED;  // combine keeps one weight per split in LDS
   dim3 grid(Hkv, a.nsplit, B);
   hipStream_t st = (hipStream_t)stream;
-  // impl: 0 auto, 1 VALU kernel, 2 matrix-core kernel (D = 128, 64- or 128-key splits, G <= 8)
-  const bool mfma_ok = D == 128 && (chunk == 64 || chunk == 128) && (G == 1 || G == 2 || G == 4 || G == 8);
+  // impl: 0 auto, 1 VALU kernel, 2 matrix-core kernel (D = 128, 64- / 128- / 256-key splits, G <= 8)
+  const bool mfma_ok = D == 128 && (chunk == 64 || chunk == 128 || chunk == 256) && (G == 1 || G == 2 || G == 4 || G == 8);
   if (impl == 2 && !mfma_ok) return MLS_UNSUPPORTED;
   if (impl != 1 && mfma_ok) {
 #define DECM(GG)                                                                                            \
   if (chunk == 64) hipLaunchKernelGGL((decode_attn_mfma_kernel<GG, 2>), grid, dim3(128), 0, st, a);        \
-  else hipLaunchKernelGGL((decode_attn_mfma_kernel<GG, 4>), grid, dim3(256), 0, st, a);
+  else if (chunk == 128) hipLaunchKernelGGL((decode_attn_mfma_kernel<GG, 4>), grid, dim3(256), 0, st, a);  \
+  else hipLaunchKernelGGL((decode_attn_mfma_kernel<GG, 8>), grid, dim3(512), 0, st, a);
     if (G == 1) { DECM(1) }
     else if (G == 2) { DECM(2) }
     else if (G == 4) { DECM(4) }
