@@ -1,0 +1,90 @@
+"""Host staging copies for :class:`~.worker.GpuEngine` (request arrays -> one pinned slot).
+
+Wraps the C++ pool in ``csrc/staging.cpp`` (built in-tree by ``frontend/build.py``): persistent
+copy threads, GIL released, the calling thread copies too, 256 KiB chunks from an atomic cursor.
+``MLS_STAGE_THREADS`` sets the number of pool threads (default 4, plus the caller);
+``MLS_NATIVE_STAGING=0`` selects the Python thread-pool path (kept for A/B and for hosts where
+the module has not been built).
+"""
+from __future__ import annotations
+
+import importlib.util
+import logging
+import os
+from concurrent.futures import ThreadPoolExecutor
+from typing import Optional, Sequence
+
+import numpy as np
+
+logger = logging.getLogger("mlsamd.engine")
+
+_mod = None
+_mod_err: Optional[str] = None
+
+
+def _load():
+    global _mod, _mod_err
+    if _mod is not None or _mod_err is not None:
+        return _mod
+    from ..frontend import build as fbuild
+
+    path = fbuild.staging_path()
+    try:
+        if not os.path.exists(path):
+            fbuild.build()  # host C++ only: seconds, no GPU toolchain involved
+        spec = importlib.util.spec_from_file_location("_staging", path)
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        _mod = mod
+    except Exception as e:  # noqa: BLE001 -- host-side fallback, logged
+        _mod_err = f"{type(e).__name__}: {e}"
+        logger.warning("native staging unavailable (%s); using the Python copy threads", _mod_err)
+    return _mod
+
+
+class HostStager:
+    """Copies ``n`` per-request arrays of ``sample_bytes`` each into a pinned buffer."""
+
+    def __init__(self, threads: Optional[int] = None, name: str = "engine", native: Optional[bool] = None):
+        if threads is None:
+            threads = int(os.environ.get("MLS_STAGE_THREADS", "4"))
+        if native is None:
+            native = os.environ.get("MLS_NATIVE_STAGING", "1") != "0"
+        self.threads = max(0, int(threads))
+        self._native = None
+        self._pool = None
+        if native:
+            mod = _load()
+            if mod is not None:
+                self._native = mod.Stager(self.threads)
+        if self._native is None and self.threads > 1:
+            self._pool = ThreadPoolExecutor(max_workers=self.threads, thread_name_prefix=f"{name}-stage")
+
+    @property
+    def native(self) -> bool:
+        return self._native is not None
+
+    def gather(self, dst: np.ndarray, samples: Sequence[np.ndarray]) -> None:
+        """``dst[i] = samples[i]`` for every request (``dst`` a pinned ``[max_b, ...]`` view)."""
+        n = len(samples)
+        if self._native is not None and n > 0:
+            each = dst[0].nbytes
+            srcs = [s if (isinstance(s, np.ndarray) and s.dtype == dst.dtype and s.flags.c_contiguous)
+                    else np.ascontiguousarray(s, dtype=dst.dtype) for s in samples]
+            for s in srcs:
+                if s.nbytes != each:
+                    raise ValueError(f"sample of shape {s.shape} does not fit the slot row {dst.shape[1:]}")
+            self._native.gather(dst.ctypes.data, srcs, each)
+            return
+        if self._pool is not None and n >= 8:
+            step = -(-n // self._pool._max_workers)
+
+            def _copy(lo):
+                for i in range(lo, min(n, lo + step)):
+                    dst[i] = samples[i]
+
+            for f in [self._pool.submit(_copy, lo) for lo in range(0, n, step)]:
+                f.result()
+            return
+        for i, s in enumerate(samples):
+            dst[i] = s

@@ -4,7 +4,9 @@
 
 * ``csrc/httpfront.cpp`` -> ``_native/_httpfront<EXT_SUFFIX>`` (pybind11 extension: epoll HTTP/1.1
   server + C++ dynamic batcher, see :mod:`.native`), and
-* ``csrc/loadgen.cpp``   -> ``_native/mls_loadgen`` (closed-loop keep-alive HTTP load generator).
+* ``csrc/loadgen.cpp``   -> ``_native/mls_loadgen`` (closed-loop keep-alive HTTP load generator),
+* ``../engine/csrc/staging.cpp`` -> ``engine/_native/_staging<EXT_SUFFIX>`` (the engine's host
+  staging copy pool, :mod:`mlmicroservicetemplate_amd.engine.staging`).
 
 In-tree like the kernel library (``ops/build.py``), so the artefacts travel with the repo
 snapshot; rebuilt only when a source or the flags change (hash stamp).
@@ -22,11 +24,17 @@ import sysconfig
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT_DIR = os.path.join(HERE, "_native")
+ENGINE_CSRC = os.path.join(os.path.dirname(HERE), "engine", "csrc")
+ENGINE_OUT = os.path.join(os.path.dirname(HERE), "engine", "_native")
 CXXFLAGS = ["-O2", "-std=c++17", "-Wall", "-Wno-unused-result", "-pthread"]
 
 
 def ext_path() -> str:
     return os.path.join(OUT_DIR, "_httpfront" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
+
+
+def staging_path() -> str:
+    return os.path.join(ENGINE_OUT, "_staging" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
 
 
 def loadgen_path() -> str:
@@ -54,7 +62,7 @@ def _build_one(src: str, out: str, flags, verbose: bool, force: bool) -> str:
         with open(sf) as f:
             if f.read().strip() == stamp:
                 return out
-    os.makedirs(OUT_DIR, exist_ok=True)
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     cmd = [_cxx(), *flags, src, "-o", out + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)
@@ -74,7 +82,8 @@ def build(force: bool = False, verbose: bool = False):
                             "-I", sysconfig.get_paths()["include"]]
     ext = _build_one(os.path.join(CSRC, "httpfront.cpp"), ext_path(), ext_flags, verbose, force)
     lg = _build_one(os.path.join(CSRC, "loadgen.cpp"), loadgen_path(), CXXFLAGS, verbose, force)
-    return ext, lg
+    stg = _build_one(os.path.join(ENGINE_CSRC, "staging.cpp"), staging_path(), ext_flags + ["-O3"], verbose, force)
+    return ext, lg, stg
 
 
 def main(argv=None) -> int:

@@ -281,9 +281,11 @@ def main(argv: Optional[List[str]] = None) -> int:
     ap = build_parser()
     args = ap.parse_args(argv)
     if args.cmd == "build":
+        from .frontend import build as fbuild
         from .ops import build
 
         print(build.build(force=args.force, verbose=True))
+        print(*fbuild.build(force=args.force, verbose=True))
         return 0
     if args.cmd == "plugins":
         from .plugins.base import available_plugins
