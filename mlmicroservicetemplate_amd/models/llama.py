@@ -256,7 +256,9 @@ class TPComm:
         self.tp = tp
         self.car = None
         if custom_ar is None:
-            custom_ar = os.environ.get("MLS_CUSTOM_AR", "0") == "1"
+            # on by default for TP > 1 on GPUs: a start-up self-test against the group's own
+            # all-reduce gates it, and it is what lets the TP decode step run as one hipGraph
+            custom_ar = os.environ.get("MLS_CUSTOM_AR", "1") == "1"
         if custom_ar and tp > 1 and device is not None and torch.device(device).type == "cuda":
             from ..parallel.custom_ar import CustomAllReduce
 
@@ -423,10 +425,14 @@ class LlamaTP:
         self.v_cache = [torch.zeros_like(self.k_cache[0]) for _ in range(cfg.layers)]
         self.cos, self.sin = R.rope_tables(max_seq, D, cfg.rope_theta, self.device)
         # hipGraph capture of the decode step (P4): removes ~300 host launches per token.  With
-        # tp > 1 the RCCL all-reduces are captured too (opt-in: MLS_TP_GRAPHS=1).
+        # tp > 1 the step's collectives are captured too: the one-shot IPC all-reduce is graph-safe
+        # (device-side epochs), so with it enabled every decode batch whose messages it takes is
+        # captured (see _graph_ok); RCCL collectives inside the graph are opt-in (MLS_TP_GRAPHS=1).
+        self._rccl_graphs = (os.environ.get("MLS_TP_GRAPHS", "0") == "1"
+                             and not getattr(self.comm, "host_staged", False))
         self.use_graphs = backend == "fused" and self.device.type == "cuda" and (
-            tp == 1 or getattr(self.comm, "graph_safe", False)
-            or (os.environ.get("MLS_TP_GRAPHS", "0") == "1" and not getattr(self.comm, "host_staged", False)))
+            tp == 1 or getattr(self.comm, "graph_safe", False) or self._rccl_graphs
+            or getattr(self.comm, "car", None) is not None)
         self._graphs: Dict[Tuple[int, int, int], tuple] = {}
         self._dec_ctx: Optional[int] = None  # host bound on decode context (sizes the split grid)
 
@@ -711,6 +717,16 @@ class LlamaTP:
             return self.max_seq
         return min(self.max_seq, max(256, 1 << (max(1, int(max_ctx)) - 1).bit_length()))
 
+    def _graph_ok(self, B: int) -> bool:
+        """May the decode step for batch B be captured?  Always at tp == 1 / under a graph-safe
+        comm; with the IPC all-reduce only while its B x hidden bf16 messages fit the one-shot
+        buffer (larger ones would fall back to an uncapturable collective) unless RCCL capture
+        is enabled."""
+        if self.tp == 1 or getattr(self.comm, "graph_safe", False) or self._rccl_graphs:
+            return True
+        car = getattr(self.comm, "car", None)
+        return car is not None and B * self.cfg.hidden * 2 <= car.cap
+
     def _decode_graph(self, B: int, k: int, ctx: int):
         """Captured decode step for batch B and context bound ctx (static token / position / length
         buffers).  The warm-up steps run at position ctx - 1: for a sequence being decoded under
@@ -745,7 +761,7 @@ class LlamaTP:
         host-side bound on cur + 1 (e.g. prompt length + step), used to pick a tight split grid."""
         B = tok.shape[0]
         ctx = self.ctx_bucket(max_ctx)
-        if self.use_graphs:
+        if self.use_graphs and self._graph_ok(B):
             g, t_s, p_s, l_s, v_s, i_s = self._decode_graph(B, k, ctx)
             if self.pages is not None:
                 self.pages.device_table()  # the graph reads the table buffer in place

@@ -8,7 +8,11 @@ a start-up self-test against the group's own all-reduce.  Anything unexpected (I
 unavailable, a timeout, a wrong sum) leaves :attr:`CustomAllReduce.enabled` False and callers
 keep RCCL; messages larger than ``cap`` always use RCCL (bandwidth-bound: the ring wins there).
 
-``TPComm`` uses it when ``MLS_CUSTOM_AR=1`` (opt-in until measured on an 8-GPU node).
+``TPComm`` uses it for TP > 1 on GPUs unless ``MLS_CUSTOM_AR=0``.  Being graph-safe, it is also
+what lets ``LlamaTP`` capture the TP decode step (RCCL inside graphs stays opt-in,
+``MLS_TP_GRAPHS=1``).  Exercised with 8 ranks on one GPU (``tests/test_llama_tp_gpu.py``, world 8:
+IPC handles, 8-peer one-shot kernel inside the captured decode graphs); the 8-GPU xGMI timing is
+not measured here.
 """
 from __future__ import annotations
 
@@ -30,7 +34,10 @@ class CustomAllReduce:
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
-        self.device = torch.device(device or torch.cuda.current_device())
+        dev = torch.device(device if device is not None else "cuda")
+        if dev.index is None:  # "cuda" -> "cuda:<current>": eligible() compares tensor devices exactly
+            dev = torch.device("cuda", torch.cuda.current_device())
+        self.device = dev
         self.cap = int(cap_bytes)
         self.timeout = int(timeout_iters)
         self.enabled = False

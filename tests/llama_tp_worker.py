@@ -1,5 +1,6 @@
 """Child process for test_llama_tp_gpu.py: one TP rank of the fused (native-kernel) Llama; all
 ranks share cuda:0 and talk over gloo (host-staged collectives)."""
+import json
 import os
 import sys
 
@@ -12,7 +13,7 @@ def main():
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from mlmicroservicetemplate_amd.models.llama import GenParams, LlamaTP, TPComm, init_llama_shard, tiny_config
 
-    cfg = tiny_config(layers=2, hidden=512, heads=8, kv_heads=2, head_dim=128, intermediate=1024)
+    cfg = tiny_config(**json.loads(os.environ["TP_CFG"]))
     p = init_llama_shard(cfg, world, rank, seed=3, device="cuda")
     m = LlamaTP(p, cfg, tp=world, rank=rank, comm=TPComm(None, world, device="cuda"), backend="fused",
                 device="cuda", max_batch=4, max_seq=256)
@@ -24,7 +25,11 @@ def main():
     allv = m.comm.all_gather(vals)
     alli = m.comm.all_gather(idx)
     out = m.generate(ids, lens, GenParams(max_new_tokens=8))
-    torch.save({"tokens": out.cpu(), "vals": allv.cpu(), "idx": alli.cpu()}, os.environ["OUT"] + f".{rank}.pt")
+    info = torch.tensor([int(m.use_graphs), int(m.comm.car is not None), len(m._graphs)])
+    if m.comm.car is not None:
+        info[1] += 10 * m.comm.car._errors()  # peer-wait timeouts would show here
+    torch.save({"tokens": out.cpu(), "vals": allv.cpu(), "idx": alli.cpu(), "info": info},
+               os.environ["OUT"] + f".{rank}.pt")
     dist.destroy_process_group()
 
 

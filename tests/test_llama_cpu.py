@@ -67,11 +67,13 @@ def _tp_worker(rank, world, port, cfg_kw, q, kv_pages=0):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,kv,kv_pages", [(2, 4, 0), (4, 2, 0), (2, 4, 5)])
+@pytest.mark.parametrize("world,kv,kv_pages,heads", [(2, 4, 0, 8), (4, 2, 0, 8), (2, 4, 5, 8), (8, 8, 0, 32)])
 @pytest.mark.timeout(240)
-def test_tp_matches_tp1(world, kv, kv_pages):
-    """(kv_pages > 0: every rank's cache is a paged pool -- same tokens as contiguous TP = 1.)"""
-    cfg_kw = dict(CFG, kv_heads=kv)
+def test_tp_matches_tp1(world, kv, kv_pages, heads):
+    """(kv_pages > 0: every rank's cache is a paged pool -- same tokens as contiguous TP = 1.
+    world 8 with 32 query / 8 KV heads is Llama-3-8B's TP = 8 split: 4 query heads and 1 KV head
+    per rank.)"""
+    cfg_kw = dict(CFG, kv_heads=kv, heads=heads)
     torch.set_num_threads(1)
     cfg = tiny_config(**cfg_kw)
     p = init_llama_shard(cfg, 1, 0, seed=1)

@@ -1,6 +1,11 @@
 """Fused-backend tensor parallelism on the GPU (column/row/vocab-parallel native kernels, the
-post-all-reduce residual, the top-k merge): TP=2 ranks sharing the test box's one GPU over gloo
-must generate the TP=1 tokens.  (8-way RCCL over xGMI runs the same code with another backend.)"""
+post-all-reduce residual, the top-k merge): TP ranks sharing the test box's one GPU over gloo
+must generate the TP=1 tokens.  (8-way RCCL over xGMI runs the same code with another backend.)
+
+world 8 is Llama-3-8B's TP = 8 head split (32 query / 8 KV heads -> 4 + 1 per rank, head_dim 128)
+with the one-shot IPC all-reduce (MLS_CUSTOM_AR=1) taking every decode all-reduce, so the decode
+steps run as captured hipGraphs with the 8-peer kernel inside (X2 + P4 together)."""
+import json
 import os
 import socket
 import subprocess
@@ -21,11 +26,20 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("world", [2])
+CASES = {
+    # world 2: the collectives go through the group itself (host-staged gloo here), decode uncaptured
+    2: (dict(layers=2, hidden=512, heads=8, kv_heads=2, head_dim=128, intermediate=1024), {"MLS_CUSTOM_AR": "0"}),
+    8: (dict(layers=2, hidden=512, heads=32, kv_heads=8, head_dim=128, intermediate=2048),
+        {"MLS_CUSTOM_AR": "1", "GPU_MAX_HW_QUEUES": "1"}),
+}
+
+
+@pytest.mark.parametrize("world", [2, 8])
 def test_fused_tp_matches_tp1(tmp_path, world):
     from mlmicroservicetemplate_amd.models.llama import GenParams, LlamaTP, init_llama_shard, tiny_config
 
-    cfg = tiny_config(layers=2, hidden=512, heads=8, kv_heads=2, head_dim=128, intermediate=1024)
+    cfg_kw, extra_env = CASES[world]
+    cfg = tiny_config(**cfg_kw)
     m = LlamaTP(init_llama_shard(cfg, 1, 0, seed=3, device="cuda"), cfg, backend="fused", device="cuda",
                 max_batch=4, max_seq=256)
     g = torch.Generator().manual_seed(7)
@@ -40,12 +54,18 @@ def test_fused_tp_matches_tp1(tmp_path, world):
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
-                   OUT=out, PYTHONPATH=os.pathsep.join([root, os.environ.get("PYTHONPATH", "")]))
+                   OUT=out, TP_CFG=json.dumps(cfg_kw), PYTHONPATH=os.pathsep.join([root, os.environ.get("PYTHONPATH", "")]),
+                   **extra_env)
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "llama_tp_worker.py")], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     logs = []
     for p in procs:
-        o, _ = p.communicate(timeout=300)
+        try:
+            o, _ = p.communicate(timeout=300)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
         logs.append((p.returncode, o[-2000:]))
     assert all(rc == 0 for rc, _ in logs), logs
     for r in range(world):
@@ -61,3 +81,7 @@ def test_fused_tp_matches_tp1(tmp_path, world):
         # the greedy continuations agree (a near-tie may flip late tokens)
         agree = (d["tokens"] == want).float().mean().item()
         assert agree >= 0.6, (r, d["tokens"], want)
+        if extra_env.get("MLS_CUSTOM_AR") == "1":
+            use_graphs, car, graphs = d["info"].tolist()
+            assert car == 1, f"rank {r}: IPC all-reduce disabled or a peer wait timed out ({car})"
+            assert use_graphs == 1 and graphs >= 1, f"rank {r}: decode steps were not captured ({d['info']})"
