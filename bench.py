@@ -110,6 +110,9 @@ def main(argv=None) -> int:
 
     host_s = [0.0]  # host time spent inside submit() (staging copy + enqueue): diagnostics
 
+    tickets_log = os.environ.get("MLS_BENCH_TICKETS")  # diagnostics: per-batch submit / done times
+    events: list = []
+
     def run_steps(n, lat):
         pending = []
         for i in range(n):
@@ -120,9 +123,11 @@ def main(argv=None) -> int:
                 t = pending.pop(0)
                 t.wait()
                 lat.append(time.perf_counter() - t.t_submit)
+                events.append((t.t_submit, time.perf_counter()))
         for t in pending:
             t.wait()
             lat.append(time.perf_counter() - t.t_submit)
+            events.append((t.t_submit, time.perf_counter()))
 
     phases = os.environ.get("MLS_BENCH_PHASES")  # diagnostics: wall-clock stamps of the phases
 
@@ -134,6 +139,7 @@ def main(argv=None) -> int:
     stamp("warmup")
     run_steps(args.warmup, [])
     host_s[0] = 0.0
+    events.clear()
     lat: list = []
     mdist.barrier()
     torch.cuda.synchronize(device)
@@ -144,6 +150,11 @@ def main(argv=None) -> int:
     mdist.barrier()
     elapsed = time.perf_counter() - t_start
     stamp("done")
+    if tickets_log and info.rank == 0:
+        with open(tickets_log, "a") as f:
+            f.write(json.dumps({"steps": args.steps, "elapsed_ms": elapsed * 1e3,
+                                "tickets_ms": [[round((a - t_start) * 1e3, 3), round((b - t_start) * 1e3, 3)]
+                                               for a, b in events]}) + "\n")
     elapsed_max = mdist.max_over_ranks(elapsed)
     p50 = float(np.percentile(lat, 50)) * 1e3
     p99 = float(np.percentile(lat, 99)) * 1e3
