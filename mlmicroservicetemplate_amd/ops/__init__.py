@@ -316,14 +316,15 @@ def load_blas_tuning(path: Optional[str] = None) -> bool:
     in ``tuned/tunableop_gfx950.csv`` (BERT FFN-up + GELU: 26.4 vs 30.1 us at 4-way concurrency,
     ``profiles/r1_bert_gemm_probe.jsonl``).  Lookup only -- tuning stays off, so nothing is timed or
     written at run time, and untuned shapes keep the library default.  ``MLS_BLAS_TUNING=0``
-    disables it.  Returns whether the table was loaded."""
+    disables it; ``MLS_BLAS_TUNING_FILE`` reads another table (A/B).  Returns whether it loaded."""
     if os.environ.get("MLS_BLAS_TUNING", "1") == "0" or not torch.cuda.is_available():
         return False
     from torch.cuda import tunable
 
     tunable.enable(True)
     tunable.tuning_enable(False)
-    ok = bool(tunable.read_file(path or os.path.join(_TUNED_DIR, "tunableop_gfx950.csv")))
+    path = path or os.environ.get("MLS_BLAS_TUNING_FILE") or os.path.join(_TUNED_DIR, "tunableop_gfx950.csv")
+    ok = bool(tunable.read_file(path))
     if not ok:
         tunable.enable(False)
     return ok
