@@ -122,6 +122,21 @@ class GpuEngine:
         self._stager = HostStager(stage_workers, name=name)
         self.name = name
         self._enqueue_lock = threading.Lock()
+        # Launch pacing.  Batches that become ready together (a closed loop, a burst, two slots
+        # freed by one clump of completions) otherwise enter the network in lock step: all in the
+        # bandwidth-bound early layers at once, then all in the latency-bound late ones, and keep
+        # completing in clumps.  Near saturation a launch waits until PACE x (batch latency EWMA /
+        # inflight) -- Little's law: the completion interval of a full pipeline -- has passed since
+        # the previous launch.  The estimate shrinks when pacing shortens the latency, so it cannot
+        # run away (an estimate from observed completion intervals does: pacing stretches them).
+        # MLS_LAUNCH_PACE=0 disables, MLS_LAUNCH_GAP_US=<us> fixes the gap instead.
+        import os as _os
+
+        self._pace = float(_os.environ.get("MLS_LAUNCH_PACE", "1.0"))
+        self._fixed_gap_s = float(_os.environ.get("MLS_LAUNCH_GAP_US", "0")) * 1e-6
+        self._last_launch = 0.0
+        self._lat_s = 0.0  # EWMA of launch -> done latency
+        self._pace_lock = threading.Lock()
         self._free: "queue.Queue[_Slot]" = queue.Queue()
         self.slots: List[_Slot] = []
         self.batches = 0
@@ -251,6 +266,7 @@ class GpuEngine:
         try:
             bucket = pick_bucket(n, self.buckets)
             with self._enqueue_lock, torch.cuda.device(self.device):
+                self._pace_launch()
                 with tracing.range(f"{self.name}.enqueue"):
                     s_h2d = slot.s_comp if self.copies_on_slot_stream else self.s_h2d
                     s_d2h = slot.s_comp if self.copies_on_slot_stream else self.s_d2h
@@ -280,11 +296,29 @@ class GpuEngine:
             raise
         return Ticket(self, slot, bucket, n)
 
+    def _pace_launch(self) -> None:
+        """Called under the enqueue lock, with this batch's slot already taken."""
+        gap = self._fixed_gap_s or (self._pace * self._lat_s / self.inflight if self.inflight > 1 else 0.0)
+        busy_others = self.inflight - self._free.qsize() - 1
+        # only near saturation: at light load a launch never waits
+        if gap > 0 and busy_others >= max(1, self.inflight - 2):
+            wait_until = self._last_launch + min(gap, 5e-3)
+            while time.perf_counter() < wait_until:
+                time.sleep(0)  # yield the GIL; sleeping for real overshoots by 0.1-1 ms
+        self._last_launch = time.perf_counter()
+
+    def _note_done(self, t: "Ticket") -> None:
+        with self._pace_lock:
+            lat = time.perf_counter() - t.t_submit
+            self._lat_s = lat if self._lat_s == 0.0 else 0.9 * self._lat_s + 0.1 * lat
+
     def _finish(self, t: Ticket) -> Tuple[np.ndarray, ...]:
         slot = t.slot
         try:
             try:
                 slot.ev_done.synchronize()
+                if self._pace > 0 and self.inflight > 1:
+                    self._note_done(t)
             except RuntimeError as e:  # device fault surfaced at the sync: this worker is dead
                 self.healthy = False
                 self.last_error = f"{type(e).__name__}: {e}"
@@ -309,5 +343,6 @@ class GpuEngine:
         return {"name": self.name, "device": str(self.device), "batches": self.batches, "samples": self.samples,
                 "inflight": self.inflight, "buckets": self.buckets, "graphs": self.use_graphs,
                 "concurrent": self.concurrent, "native_staging": self._stager.native,
+                "pace_gap_us": round(self._pace * self._lat_s / max(1, self.inflight) * 1e6, 1),
                 "healthy": self.healthy, "last_error": self.last_error,
                 "free_slots": self._free.qsize()}
