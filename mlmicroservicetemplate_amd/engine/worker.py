@@ -109,12 +109,15 @@ class GpuEngine:
         self.inflight = max(1, int(inflight))
         self.use_graphs = use_graphs
         self.concurrent = bool(concurrent) and self.inflight > 1
-        # concurrent slots: a slot's H2D and D2H may ride its own compute stream (fewer streams
-        # than hardware queues need sharing; MLS_SLOT_COPIES=1) instead of the shared copy streams
+        # concurrent slots: a slot's H2D and D2H ride its own compute stream instead of the shared
+        # copy streams (those share the 4 hardware queues with the slot streams).  With native
+        # staging + launch pacing this is +3-4 % req/s on ResNet-50 (20 steps 47.2-48.3k vs
+        # 45.9-46.3k, 300 steps 53.3k vs 51.3-51.7k; profiles/r2_hwq_slotcopies_with_pacing.jsonl);
+        # MLS_SLOT_COPIES=0 restores the copy streams
         if copies_on_slot_stream is None:
             import os
 
-            copies_on_slot_stream = os.environ.get("MLS_SLOT_COPIES", "0") == "1"
+            copies_on_slot_stream = os.environ.get("MLS_SLOT_COPIES", "1") == "1"
         self.copies_on_slot_stream = bool(copies_on_slot_stream) and self.concurrent
         # host staging (request arrays -> pinned slot): a persistent native copy pool (GIL released,
         # the submitting thread copies too); one thread's ~5-8 GB/s memcpy is not enough for a
