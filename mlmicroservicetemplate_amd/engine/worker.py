@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import contextlib
 import logging
+import os
 import queue
 import threading
 import time
@@ -115,8 +116,6 @@ class GpuEngine:
         # 45.9-46.3k, 300 steps 53.3k vs 51.3-51.7k; profiles/r2_hwq_slotcopies_with_pacing.jsonl);
         # MLS_SLOT_COPIES=0 restores the copy streams
         if copies_on_slot_stream is None:
-            import os
-
             copies_on_slot_stream = os.environ.get("MLS_SLOT_COPIES", "1") == "1"
         self.copies_on_slot_stream = bool(copies_on_slot_stream) and self.concurrent
         # host staging (request arrays -> pinned slot): a persistent native copy pool (GIL released,
@@ -133,10 +132,8 @@ class GpuEngine:
         # the previous launch.  The estimate shrinks when pacing shortens the latency, so it cannot
         # run away (an estimate from observed completion intervals does: pacing stretches them).
         # MLS_LAUNCH_PACE=0 disables, MLS_LAUNCH_GAP_US=<us> fixes the gap instead.
-        import os as _os
-
-        self._pace = float(_os.environ.get("MLS_LAUNCH_PACE", "1.0"))
-        self._fixed_gap_s = float(_os.environ.get("MLS_LAUNCH_GAP_US", "0")) * 1e-6
+        self._pace = float(os.environ.get("MLS_LAUNCH_PACE", "1.0"))
+        self._fixed_gap_s = float(os.environ.get("MLS_LAUNCH_GAP_US", "0")) * 1e-6
         self._last_launch = 0.0
         self._lat_s = 0.0  # EWMA of launch -> done latency
         self._pace_lock = threading.Lock()
