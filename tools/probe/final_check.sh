@@ -17,3 +17,5 @@ cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_seria
 cd $GRAFT_REPO_ROOT && python3 tools/kernel_summary.py $OUT/prof_serial --window 940 --per 20 --top 40 > $OUT/prof_serial_summary.txt 2>&1; head -12 $OUT/prof_serial_summary.txt
 timeout -k 10 300 python3 -u tools/http_bench.py --model resnet50 --frontend native --conns 128 256 --duration 6 --warmup 2 --ready-timeout 200 > $OUT/http_resnet.jsonl 2> $OUT/http.err || { tail -20 $OUT/http.err; exit 1; }
 cut -c1-330 $OUT/http_resnet.jsonl
+MLS_DIST_BACKEND=gloo timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 > $OUT/bench_2rank_gloo.json 2> $OUT/bench_2rank.err || { tail -20 $OUT/bench_2rank.err; exit 1; }
+cat $OUT/bench_2rank_gloo.json
