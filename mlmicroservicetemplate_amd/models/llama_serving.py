@@ -174,28 +174,46 @@ class ContinuousLlama:
             slot_ids = torch.tensor([s.slot for s in admit], dtype=torch.int32, device=m.device)
             vals, idx = m.step(ids.to(m.device), pos, lens, decode=False, k=k, slot_ids=slot_ids)
             cv, ci = m.gather_candidates(vals, idx)
-            for j, s in enumerate(admit):
-                s.out.append(m.pick_token(cv[j], ci[j], s.gp, 0))
+            for s, t in zip(admit, self._pick_rows(cv, ci, [(j, s.gp, 0) for j, s in enumerate(admit)])):
+                s.out.append(t)
                 s.cur = len(s.ids)
             self.tokens += len(admit)
             self._retire()
         active = [s for s in self.slots if s is not None]
         if active:
-            tok = torch.zeros(self.B, dtype=torch.int32)
-            cur = torch.zeros(self.B, dtype=torch.int32)
+            # host lists -> one tensor each (per-element tensor writes cost ~us apiece at 128 slots)
+            tok_l, cur_l = [0] * self.B, [0] * self.B
             for s in active:
-                tok[s.slot] = s.out[-1]
-                cur[s.slot] = s.cur
+                tok_l[s.slot] = s.out[-1]
+                cur_l[s.slot] = s.cur
+            tok = torch.tensor(tok_l, dtype=torch.int32)
+            cur = torch.tensor(cur_l, dtype=torch.int32)
             k = max(1, min(max(s.gp.top_k for s in active), m.top_k_max))
             max_ctx = max(s.cur for s in active) + 1
             vals, idx = m.decode_step(tok.to(m.device), cur.to(m.device), k, max_ctx=max_ctx)
             cv, ci = m.gather_candidates(vals, idx)
-            for s in active:
-                s.out.append(m.pick_token(cv[s.slot], ci[s.slot], s.gp, len(s.out)))
+            picks = self._pick_rows(cv, ci, [(s.slot, s.gp, len(s.out)) for s in active])
+            for s, t in zip(active, picks):
+                s.out.append(t)
                 s.cur += 1
             self.tokens += len(active)
             self._retire()
         self.iterations += 1
+
+    def _pick_rows(self, cv: torch.Tensor, ci: torch.Tensor, rows) -> List[int]:
+        """Next token of each ``(row, gen params, step)``: the greedy rows in one vectorised
+        argmax / gather (first maximum, as ``pick_token``), sampled rows one by one."""
+        out: List[Optional[int]] = [None] * len(rows)
+        greedy = [j for j, (_r, gp, _t) in enumerate(rows) if gp.top_k <= 1]
+        if greedy:
+            r = torch.tensor([rows[j][0] for j in greedy], dtype=torch.long)
+            best = ci[r].gather(1, cv[r].argmax(1, keepdim=True)).squeeze(1).tolist()
+            for j, t in zip(greedy, best):
+                out[j] = int(t)
+        for j, (r, gp, step) in enumerate(rows):
+            if out[j] is None:
+                out[j] = self.m.pick_token(cv[r], ci[r], gp, step)
+        return out  # type: ignore[return-value]
 
     def _retire(self) -> None:
         for i, s in enumerate(self.slots):
