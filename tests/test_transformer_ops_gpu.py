@@ -154,6 +154,33 @@ def test_decode_attention(ops, Hq, Hkv, D, chunk, impl):
     assert not cnt.any()
 
 
+@pytest.mark.parametrize("impl,chunk", [("valu", 64), ("mfma", 256)])
+def test_decode_attention_8k_context(ops, impl, chunk):
+    """SURVEY K8's long end: one TP = 8 rank of Llama-3-8B (4 query heads, 1 KV head, D = 128)
+    decoding against 8192-row caches (128 splits of 64 / 32 of 256)."""
+    torch.manual_seed(6)
+    B, max_len, Hq, Hkv, D = 2, 8192, 4, 1, 128
+    kc = torch.randn(B, max_len, Hkv, D, device=DEV).to(torch.bfloat16)
+    vc = torch.randn(B, max_len, Hkv, D, device=DEV).to(torch.bfloat16)
+    q = torch.randn(B, (Hq + 2 * Hkv) * D, device=DEV).to(torch.bfloat16)
+    lens = torch.tensor([8192, 5001], device=DEV, dtype=torch.int32)
+    cnt = torch.zeros(B * Hkv, device=DEV, dtype=torch.int32)
+    ref = R.decode_attention(q, kc, vc, lens, Hq, Hkv, D)
+    out = ops.decode_attention(q, kc, vc, lens, Hq, Hkv, D, chunk=chunk, counters=cnt, impl=impl)
+    assert rel(out, ref) < 2e-2
+    assert not cnt.any()
+
+
+def test_flash_attention_8k_causal(ops):
+    """Causal prefill of an 8192-token prompt with the TP = 8 rank's head split."""
+    torch.manual_seed(7)
+    B, S, Hq, Hkv, D = 1, 8192, 4, 1, 128
+    qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device=DEV).to(torch.bfloat16)
+    out = ops.flash_attention(qkv, B, S, Hq, Hkv, D, causal=True)
+    ref = R.attention(qkv, B, S, Hq, Hkv, D, causal=True)
+    assert rel(out, ref) < 2e-2
+
+
 @pytest.mark.parametrize("Hq,Hkv", [(4, 1), (32, 8), (64, 8)])
 @pytest.mark.parametrize("impl,chunk", [("valu", 64), ("mfma", 64), ("mfma", 128), ("mfma", 256)])
 def test_decode_attention_rope_append(ops, Hq, Hkv, impl, chunk):
