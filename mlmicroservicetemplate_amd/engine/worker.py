@@ -137,6 +137,8 @@ class GpuEngine:
         self._last_launch = 0.0
         self._lat_s = 0.0  # EWMA of launch -> done latency
         self._pace_lock = threading.Lock()
+        # pace only with at least this many other batches in flight (default: inflight - 2)
+        self._pace_min_busy = int(os.environ.get("MLS_PACE_MIN_BUSY", "0")) or max(1, int(inflight) - 2)
         self._free: "queue.Queue[_Slot]" = queue.Queue()
         self.slots: List[_Slot] = []
         self.batches = 0
@@ -301,7 +303,7 @@ class GpuEngine:
         gap = self._fixed_gap_s or (self._pace * self._lat_s / self.inflight if self.inflight > 1 else 0.0)
         busy_others = self.inflight - self._free.qsize() - 1
         # only near saturation: at light load a launch never waits
-        if gap > 0 and busy_others >= max(1, self.inflight - 2):
+        if gap > 0 and busy_others >= self._pace_min_busy:
             wait_until = self._last_launch + min(gap, 5e-3)
             while time.perf_counter() < wait_until:
                 time.sleep(0)  # yield the GIL; sleeping for real overshoots by 0.1-1 ms

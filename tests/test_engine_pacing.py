@@ -18,6 +18,7 @@ def _engine(inflight=5, pace=1.0, busy=4):
     e._pace, e._fixed_gap_s = pace, 0.0
     e._last_launch, e._lat_s = 0.0, 0.0
     e._pace_lock = threading.Lock()
+    e._pace_min_busy = max(1, inflight - 2)
     e._free = queue.Queue()
     for _ in range(inflight - busy - 1):  # this launch's slot is already taken
         e._free.put(object())
