@@ -75,3 +75,20 @@ def test_queue_bound_and_validation(params):
         eng.submit([1] * 30, GenParams(8))
     with pytest.raises(ValueError):
         eng.submit([], GenParams(1))
+
+
+def test_vectorised_picks_match_pick_token():
+    """ContinuousLlama._pick_rows == LlamaTP.pick_token row by row: greedy rows (ties resolve to
+    the first maximum) in one argmax / gather, sampled rows on the seeded per-row path."""
+    g = torch.Generator().manual_seed(0)
+    cv = torch.randn(6, 16, generator=g)
+    cv[2, 3] = cv[2, 9] = cv[2].max() + 1.0  # a tie
+    ci = torch.randint(0, 1000, (6, 16), generator=g)
+    rows = [(0, GenParams(top_k=1), 0), (2, GenParams(top_k=1), 3), (5, GenParams(8, top_k=5, seed=2), 4),
+            (4, GenParams(top_k=1), 1), (1, GenParams(8, top_k=3, temperature=0.5, seed=9), 0)]
+    eng = object.__new__(ContinuousLlama)
+    eng.m = LlamaTP  # pick_token is a staticmethod
+    got = eng._pick_rows(cv, ci, rows)
+    want = [LlamaTP.pick_token(cv[r], ci[r], gp, step) for r, gp, step in rows]
+    assert got == want
+    assert got[1] == int(ci[2, 3])
