@@ -48,15 +48,16 @@ def _cxx() -> str:
     raise RuntimeError("no C++ compiler found (g++ / clang++)")
 
 
-def _stamp(src: str, flags) -> str:
+def _stamp(src: str, flags, deps=()) -> str:
     h = hashlib.sha256(" ".join(flags).encode())
-    with open(src, "rb") as f:
-        h.update(f.read())
+    for path in (src, *deps):
+        with open(path, "rb") as f:
+            h.update(f.read())
     return h.hexdigest()[:16]
 
 
-def _build_one(src: str, out: str, flags, verbose: bool, force: bool) -> str:
-    stamp = _stamp(src, flags)
+def _build_one(src: str, out: str, flags, verbose: bool, force: bool, deps=()) -> str:
+    stamp = _stamp(src, flags, deps)
     sf = out + ".stamp"
     if not force and os.path.exists(out) and os.path.exists(sf):
         with open(sf) as f:
@@ -82,7 +83,8 @@ def build(force: bool = False, verbose: bool = False):
                             "-I", sysconfig.get_paths()["include"]]
     ext = _build_one(os.path.join(CSRC, "httpfront.cpp"), ext_path(), ext_flags, verbose, force)
     lg = _build_one(os.path.join(CSRC, "loadgen.cpp"), loadgen_path(), CXXFLAGS, verbose, force)
-    stg = _build_one(os.path.join(ENGINE_CSRC, "staging.cpp"), staging_path(), ext_flags + ["-O3"], verbose, force)
+    stg = _build_one(os.path.join(ENGINE_CSRC, "staging.cpp"), staging_path(), ext_flags + ["-O3"], verbose, force,
+                     deps=(os.path.join(ENGINE_CSRC, "staging_core.h"),))
     return ext, lg, stg
 
 
