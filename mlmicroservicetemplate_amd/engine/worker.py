@@ -136,6 +136,7 @@ class GpuEngine:
         self._fixed_gap_s = float(os.environ.get("MLS_LAUNCH_GAP_US", "0")) * 1e-6
         self._last_launch = 0.0
         self._lat_s = 0.0  # EWMA of launch -> done latency
+        self._lat_n = 0  # completions seen
         self._pace_lock = threading.Lock()
         # pace only with at least this many other batches in flight (default: inflight - 2)
         self._pace_min_busy = int(os.environ.get("MLS_PACE_MIN_BUSY", "0")) or max(1, int(inflight) - 2)
@@ -310,9 +311,19 @@ class GpuEngine:
         self._last_launch = time.perf_counter()
 
     def _note_done(self, t: "Ticket") -> None:
+        """Latency EWMA for pacing.  The first pipeline turn after start-up is skipped (first
+        launches of freshly captured graphs can take many times the steady latency), and a
+        sample counts at most twice the current estimate, so one slow batch cannot make the
+        gap throttle the next dozen launches."""
         with self._pace_lock:
             lat = time.perf_counter() - t.t_submit
-            self._lat_s = lat if self._lat_s == 0.0 else 0.9 * self._lat_s + 0.1 * lat
+            self._lat_n += 1
+            if self._lat_n <= self.inflight:
+                return
+            if self._lat_s == 0.0:
+                self._lat_s = lat
+            else:
+                self._lat_s = 0.9 * self._lat_s + 0.1 * min(lat, 2.0 * self._lat_s)
 
     def _finish(self, t: Ticket) -> Tuple[np.ndarray, ...]:
         slot = t.slot

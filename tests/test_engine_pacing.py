@@ -16,7 +16,7 @@ def _engine(inflight=5, pace=1.0, busy=4):
     e = object.__new__(GpuEngine)  # no device: only the pacing state
     e.inflight = inflight
     e._pace, e._fixed_gap_s = pace, 0.0
-    e._last_launch, e._lat_s = 0.0, 0.0
+    e._last_launch, e._lat_s, e._lat_n = 0.0, 0.0, 0
     e._pace_lock = threading.Lock()
     e._pace_min_busy = max(1, inflight - 2)
     e._free = queue.Queue()
@@ -27,12 +27,16 @@ def _engine(inflight=5, pace=1.0, busy=4):
 
 def test_latency_ewma_sets_the_gap():
     e = _engine()
-    now = time.perf_counter()
-    e._note_done(_T(now - 0.010))
+    for _ in range(e.inflight):  # the first pipeline turn is ignored (cold graphs)
+        e._note_done(_T(time.perf_counter() - 0.5))
+    assert e._lat_s == 0.0
+    e._note_done(_T(time.perf_counter() - 0.010))
     assert abs(e._lat_s - 0.010) < 1e-3
     for _ in range(50):
         e._note_done(_T(time.perf_counter() - 0.005))
     assert 0.0045 < e._lat_s < 0.0060  # converges to the new latency
+    e._note_done(_T(time.perf_counter() - 1.0))  # one stall moves it by at most 10 % of 2x
+    assert e._lat_s < 0.0065
 
 
 def test_waits_near_saturation():
