@@ -1,7 +1,7 @@
 """Flagship serving benchmark: ResNet-50 bs=32 requests/sec (whole node) + p50 latency.
 
 BASELINE.json metric: "requests/sec (whole node) + p50 latency, ResNet-50 bs=32 at 1/2/4/8
-MI355X".  One process per GPU (``torch.distributed.run``); every rank is an independent
+MI355X".  One process per GPU; every rank is an independent
 data-parallel serving replica (config 4 of BASELINE.json): rank 0 initialises the random
 ResNet-50 weights and RCCL-broadcasts them over xGMI (X1), every rank builds its fused engine
 and captures its hipGraph, then serves synthetic requests.
@@ -14,6 +14,15 @@ is how the server's batcher drives the engine.  Per-request latency = submit -> 
 
 Prints ONE JSON line on rank 0 (value = total requests/s over all ranks, computed from the
 max elapsed time over ranks).  Weights are random-init and inputs synthetic (no network).
+
+Launch modes:
+  * ``python bench.py --gpus N`` with no ``WORLD_SIZE`` in the environment: this process is a
+    pure launcher (it touches neither the GPU nor ``torch.cuda``) and starts N rank processes of
+    itself (``parallel/launch.py``), relays rank 0's JSON line, and exits non-zero if any rank
+    fails;
+  * under ``torch.distributed.run`` (``WORLD_SIZE`` set): runs as that rank; ``--gpus`` must
+    equal ``WORLD_SIZE`` or the bench refuses to run.
+``MLS_DIST_BACKEND=gloo`` rehearses N ranks sharing fewer GPUs (RCCL refuses duplicate devices).
 """
 from __future__ import annotations
 
@@ -23,15 +32,8 @@ import os
 import sys
 import time
 
-import numpy as np
-import torch
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-
-from mlmicroservicetemplate_amd.parallel import dist as mdist  # noqa: E402
-
-EAGER_BASELINE_IMG_S = 11249.9  # stock PyTorch-ROCm (MIOpen) ops in the same engine, bs=32 bf16, 5 in flight, 1x MI355X: profiles/r1_bench_eager_inflight.jsonl
 
 
 def log(*a):
@@ -39,6 +41,8 @@ def log(*a):
 
 
 def build_model(backend: str, device, batch: int, params):
+    import torch
+
     from mlmicroservicetemplate_amd.models import resnet
 
     if backend == "fused":
@@ -63,8 +67,8 @@ def build_model(backend: str, device, batch: int, params):
     return fwd
 
 
-def main(argv=None) -> int:
-    ap = argparse.ArgumentParser(description=__doc__)
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
@@ -74,12 +78,46 @@ def main(argv=None) -> int:
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--serial", action="store_true", help="one compute stream (no concurrent in-flight batches)")
     ap.add_argument("--seed", type=int, default=0)
-    args = ap.parse_args(argv)
+    ap.add_argument("--measure-eager", type=int, default=0, metavar="STEPS",
+                    help="after the timed run, time STEPS batches of the stock-PyTorch (MIOpen/hipBLASLt) "
+                         "engine in the same process and report vs_pytorch_eager_per_gpu")
+    ap.add_argument("--launch-timeout", type=float, default=1500.0,
+                    help="launcher mode: bound on the whole N-rank job (s)")
+    return ap.parse_args(argv)
+
+
+def launch_ranks(args, argv) -> int:
+    """Launcher mode: N rank processes of this script, rank 0's JSON relayed (no GPU touched here)."""
+    from mlmicroservicetemplate_amd.parallel.launch import spawn_ranks
+
+    cmd = [sys.executable, "-u", os.path.abspath(__file__), *argv]
+    log(f"bench: launching {args.gpus} ranks")
+    return spawn_ranks(cmd, args.gpus, timeout_s=args.launch_timeout)
+
+
+def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse_args(argv)
+    if args.gpus < 1:
+        log("--gpus must be >= 1")
+        return 2
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        return launch_ranks(args, argv)
+    if env_world is not None and int(env_world) != args.gpus:
+        log(f"error: --gpus {args.gpus} but WORLD_SIZE={env_world}; refusing to report a mislabelled run")
+        return 2
+    return run_rank(args)
+
+
+def run_rank(args) -> int:
+    import numpy as np
+    import torch
+
+    from mlmicroservicetemplate_amd.parallel import dist as mdist
 
     info = mdist.init_distributed()
     world = info.world_size
-    if world != args.gpus:
-        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     # one GPU per rank; with fewer visible GPUs than ranks (a gloo rehearsal on a 1-GPU box,
     # MLS_DIST_BACKEND=gloo) ranks share them round-robin
     ndev = max(1, torch.cuda.device_count())
@@ -163,6 +201,22 @@ def main(argv=None) -> int:
 
     total_req = world * args.batch * args.steps
     value = total_req / elapsed_max
+    eager = None
+    if args.measure_eager > 0:  # stock-PyTorch engine, same process / box / protocol (not the flagship)
+        efwd = build_model("eager", device, args.batch, params)
+        eeng = GpuEngine(efwd, device, (224, 224, 3), torch.uint8, buckets=[args.batch], inflight=args.inflight,
+                         use_graphs=not args.no_graphs, name=f"eager.r{info.rank}", concurrent=not args.serial)
+        eeng.warmup(capture=not args.no_graphs)
+        engine = eeng
+        run_steps(min(args.warmup, 5), [])
+        mdist.barrier()
+        torch.cuda.synchronize(device)
+        te = time.perf_counter()
+        run_steps(args.measure_eager, [])
+        torch.cuda.synchronize(device)
+        mdist.barrier()
+        eager = mdist.max_over_ranks(time.perf_counter() - te)
+        eager = args.batch * args.measure_eager / eager
     if info.rank == 0:
         out = {
             "metric": "requests/sec (whole node) + p50 latency, ResNet-50 bs=32",
@@ -184,7 +238,8 @@ def main(argv=None) -> int:
             "p50_latency_ms": round(p50_max, 3),
             "p99_latency_ms": round(p99_max, 3),
             "per_gpu_requests_per_s": round(value / world, 1),
-            "vs_pytorch_eager_per_gpu": round(value / world / EAGER_BASELINE_IMG_S, 3),
+            **({"pytorch_eager_per_gpu_requests_per_s": round(eager, 1),
+                "vs_pytorch_eager_per_gpu": round(value / world / eager, 3)} if eager else {}),
             "weight_broadcast_s": round(t_bcast, 3),
             "host_submit_ms_per_step": round(host_s[0] * 1e3 / args.steps, 4),
         }

@@ -4,7 +4,9 @@ Wraps the C++ pool in ``csrc/staging.cpp`` (built in-tree by ``frontend/build.py
 copy threads, GIL released, the calling thread copies too, 256 KiB chunks from an atomic cursor.
 ``MLS_STAGE_THREADS`` sets the number of pool threads (default 4, plus the caller);
 ``MLS_NATIVE_STAGING=0`` selects the Python thread-pool path (kept for A/B and for hosts where
-the module has not been built).
+the module has not been built).  A serving process never compiles: a missing module, or one whose
+build stamp does not match the current sources, falls back to the Python path with a warning
+(build it with ``python -m mlmicroservicetemplate_amd build``).
 """
 from __future__ import annotations
 
@@ -31,7 +33,9 @@ def _load():
     path = fbuild.staging_path()
     try:
         if not os.path.exists(path):
-            fbuild.build()  # host C++ only: seconds, no GPU toolchain involved
+            raise FileNotFoundError(f"{path} is not built")
+        if not fbuild.staging_current():
+            raise RuntimeError(f"{path} is stale (built from other staging sources); rebuild it")
         spec = importlib.util.spec_from_file_location("_staging", path)
         mod = importlib.util.module_from_spec(spec)
         spec.loader.exec_module(mod)
@@ -67,6 +71,10 @@ class HostStager:
     def gather(self, dst: np.ndarray, samples: Sequence[np.ndarray]) -> None:
         """``dst[i] = samples[i]`` for every request (``dst`` a pinned ``[max_b, ...]`` view)."""
         n = len(samples)
+        if n > dst.shape[0]:
+            raise ValueError(f"{n} samples do not fit a staging buffer of {dst.shape[0]} rows")
+        if not dst.flags.c_contiguous:
+            raise ValueError("staging destination must be C-contiguous")
         if self._native is not None and n > 0:
             each = dst[0].nbytes
             srcs = [s if (isinstance(s, np.ndarray) and s.dtype == dst.dtype and s.flags.c_contiguous)

@@ -123,6 +123,8 @@ class GpuEngine:
         # 4.8 MB ResNet batch every ~0.6 ms next to the rest of the host loop
         self._stager = HostStager(stage_workers, name=name)
         self.name = name
+        self._tr_stage, self._tr_h2d, self._tr_replay, self._tr_d2h, self._tr_wait = (
+            f"{name}.{k}" for k in ("stage", "h2d", "replay", "d2h", "d2h_wait"))
         self._enqueue_lock = threading.Lock()
         # Launch pacing.  Batches that become ready together (a closed loop, a burst, two slots
         # freed by one clump of completions) otherwise enter the network in lock step: all in the
@@ -209,7 +211,7 @@ class GpuEngine:
         pick_bucket(n, self.buckets)  # validate before taking a slot
         slot = self._free.get()  # blocks while `inflight` batches are outstanding
         try:
-            with tracing.range(f"{self.name}.stage"):
+            with tracing.range(self._tr_stage):
                 dst = slot.host_in.numpy() if self.sample_dtype != torch.bfloat16 else None
                 if isinstance(samples, np.ndarray):
                     dst[:n] = samples
@@ -270,29 +272,28 @@ class GpuEngine:
             bucket = pick_bucket(n, self.buckets)
             with self._enqueue_lock, torch.cuda.device(self.device):
                 self._pace_launch()
-                with tracing.range(f"{self.name}.enqueue"):
-                    s_h2d = slot.s_comp if self.copies_on_slot_stream else self.s_h2d
-                    s_d2h = slot.s_comp if self.copies_on_slot_stream else self.s_d2h
-                    with torch.cuda.stream(s_h2d):
-                        slot.dev_in[:bucket].copy_(slot.host_in[:bucket], non_blocking=True)
-                        slot.ev_h2d.record(s_h2d)
-                    slot.s_comp.wait_event(slot.ev_h2d)
-                    with torch.cuda.stream(slot.s_comp):
-                        if self.use_graphs and bucket in slot.graphs:
-                            slot.graphs[bucket].replay()
-                            outs = slot.outs[bucket]
-                        else:
-                            with torch.no_grad():
-                                outs = tuple(self.forward(slot.dev_in[:bucket]))
-                            slot.outs[bucket] = outs
-                            if bucket not in slot.host_out:
-                                self._alloc_host_out(slot, bucket, outs)
-                        slot.ev_comp.record(slot.s_comp)
-                    s_d2h.wait_event(slot.ev_comp)
-                    with torch.cuda.stream(s_d2h):
-                        for h, d in zip(slot.host_out[bucket], outs):
-                            h.copy_(d, non_blocking=True)
-                        slot.ev_done.record(s_d2h)
+                s_h2d = slot.s_comp if self.copies_on_slot_stream else self.s_h2d
+                s_d2h = slot.s_comp if self.copies_on_slot_stream else self.s_d2h
+                with tracing.range(self._tr_h2d), torch.cuda.stream(s_h2d):
+                    slot.dev_in[:bucket].copy_(slot.host_in[:bucket], non_blocking=True)
+                    slot.ev_h2d.record(s_h2d)
+                slot.s_comp.wait_event(slot.ev_h2d)
+                with tracing.range(self._tr_replay), torch.cuda.stream(slot.s_comp):
+                    if self.use_graphs and bucket in slot.graphs:
+                        slot.graphs[bucket].replay()
+                        outs = slot.outs[bucket]
+                    else:
+                        with torch.no_grad():
+                            outs = tuple(self.forward(slot.dev_in[:bucket]))
+                        slot.outs[bucket] = outs
+                        if bucket not in slot.host_out:
+                            self._alloc_host_out(slot, bucket, outs)
+                    slot.ev_comp.record(slot.s_comp)
+                s_d2h.wait_event(slot.ev_comp)
+                with tracing.range(self._tr_d2h), torch.cuda.stream(s_d2h):
+                    for h, d in zip(slot.host_out[bucket], outs):
+                        h.copy_(d, non_blocking=True)
+                    slot.ev_done.record(s_d2h)
         except BaseException as e:
             self._free.put(slot)
             self.last_error = f"{type(e).__name__}: {e}"
@@ -329,7 +330,8 @@ class GpuEngine:
         slot = t.slot
         try:
             try:
-                slot.ev_done.synchronize()
+                with tracing.range(self._tr_wait):
+                    slot.ev_done.synchronize()
                 if self._pace > 0 and self.inflight > 1:
                     self._note_done(t)
             except RuntimeError as e:  # device fault surfaced at the sync: this worker is dead

@@ -56,31 +56,57 @@ def _stamp(src: str, flags, deps=()) -> str:
     return h.hexdigest()[:16]
 
 
-def _build_one(src: str, out: str, flags, verbose: bool, force: bool, deps=()) -> str:
-    stamp = _stamp(src, flags, deps)
+def _current(src: str, out: str, flags, deps=()) -> bool:
     sf = out + ".stamp"
-    if not force and os.path.exists(out) and os.path.exists(sf):
-        with open(sf) as f:
-            if f.read().strip() == stamp:
-                return out
+    if not (os.path.exists(out) and os.path.exists(sf)):
+        return False
+    with open(sf) as f:
+        return f.read().strip() == _stamp(src, flags, deps)
+
+
+def _build_one(src: str, out: str, flags, verbose: bool, force: bool, deps=()) -> str:
+    """Compile under an exclusive lock on ``<out>.lock`` into a per-process temp name, then an
+    atomic rename: concurrent builders (several ranks starting together) never load or install a
+    half-written module."""
+    import fcntl
+
+    if not force and _current(src, out, flags, deps):
+        return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    cmd = [_cxx(), *flags, src, "-o", out + ".tmp"]
-    if verbose:
-        print(" ".join(cmd), flush=True)
-    r = subprocess.run(cmd, capture_output=True, text=True)
-    if r.returncode != 0:
-        raise RuntimeError(f"build failed for {src}:\n{r.stderr[-8000:]}")
-    os.replace(out + ".tmp", out)
-    with open(sf, "w") as f:
-        f.write(stamp)
+    with open(out + ".lock", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        if not force and _current(src, out, flags, deps):  # another process built it meanwhile
+            return out
+        tmp = f"{out}.{os.getpid()}.tmp"
+        cmd = [_cxx(), *flags, src, "-o", tmp]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            if os.path.exists(tmp):
+                os.unlink(tmp)
+            raise RuntimeError(f"build failed for {src}:\n{r.stderr[-8000:]}")
+        os.replace(tmp, out)
+        with open(out + ".stamp", "w") as f:
+            f.write(_stamp(src, flags, deps))
     return out
 
 
-def build(force: bool = False, verbose: bool = False):
+def _ext_flags():
     import pybind11
 
-    ext_flags = CXXFLAGS + ["-shared", "-fPIC", "-fvisibility=hidden", "-I", pybind11.get_include(),
-                            "-I", sysconfig.get_paths()["include"]]
+    return CXXFLAGS + ["-shared", "-fPIC", "-fvisibility=hidden", "-I", pybind11.get_include(),
+                       "-I", sysconfig.get_paths()["include"]]
+
+
+def staging_current() -> bool:
+    """Is the built staging module up to date with ``staging.cpp`` / ``staging_core.h``?"""
+    return _current(os.path.join(ENGINE_CSRC, "staging.cpp"), staging_path(), _ext_flags() + ["-O3"],
+                    (os.path.join(ENGINE_CSRC, "staging_core.h"),))
+
+
+def build(force: bool = False, verbose: bool = False):
+    ext_flags = _ext_flags()
     ext = _build_one(os.path.join(CSRC, "httpfront.cpp"), ext_path(), ext_flags, verbose, force)
     lg = _build_one(os.path.join(CSRC, "loadgen.cpp"), loadgen_path(), CXXFLAGS, verbose, force)
     stg = _build_one(os.path.join(ENGINE_CSRC, "staging.cpp"), staging_path(), ext_flags + ["-O3"], verbose, force,

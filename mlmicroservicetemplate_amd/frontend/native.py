@@ -38,6 +38,7 @@ from urllib.parse import parse_qs
 import numpy as np
 
 from .. import discovery
+from ..utils import tracing
 from ..api.multipart import MultipartError, Part, parse_multipart
 from ..api.state import ServiceState
 from . import build as fbuild
@@ -90,7 +91,8 @@ class HostReplica:
 
     def run(self, slot, n: int):
         try:
-            return self.fn(slot[:n])
+            with tracing.range("native.handoff"):
+                return self.fn(slot[:n])
         finally:
             self.release(slot)
 
@@ -118,7 +120,9 @@ class EngineReplica:
         return self.engine.host_buffer(slot)
 
     def run(self, slot, n: int):
-        return self.engine.launch(slot, n).wait()
+        with tracing.range("native.handoff"):
+            t = self.engine.launch(slot, n)
+        return t.wait()
 
 
 # --------------------------------------------------------------------------------- service

@@ -34,6 +34,7 @@ import torch.distributed as dist
 import torch.nn.functional as F
 
 from ..ops import reference as R
+from ..utils import tracing
 
 
 @dataclass
@@ -270,19 +271,28 @@ class TPComm:
 
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         if self.tp > 1:
-            if self.car is not None and self.car.eligible(t):
-                return self.car.all_reduce_(t)  # one-shot IPC path for small (decode) messages
-            if self.host_staged and t.is_cuda:
-                h = t.float().cpu()
-                dist.all_reduce(h, group=self.group)
-                t.copy_(h)
-                return t
-            dist.all_reduce(t, group=self.group)
+            with tracing.range("tp.all_reduce"):
+                return self._all_reduce(t)
+        return t
+
+    def _all_reduce(self, t: torch.Tensor) -> torch.Tensor:
+        if self.car is not None and self.car.eligible(t):
+            return self.car.all_reduce_(t)  # one-shot IPC path for small (decode) messages
+        if self.host_staged and t.is_cuda:
+            h = t.float().cpu()
+            dist.all_reduce(h, group=self.group)
+            t.copy_(h)
+            return t
+        dist.all_reduce(t, group=self.group)
         return t
 
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
         if self.tp == 1:
             return t.unsqueeze(0)
+        with tracing.range("tp.all_gather"):
+            return self._all_gather(t)
+
+    def _all_gather(self, t: torch.Tensor) -> torch.Tensor:
         if self.host_staged and t.is_cuda:
             h = t.contiguous().cpu()
             out = [torch.empty_like(h) for _ in range(self.tp)]
@@ -294,12 +304,17 @@ class TPComm:
 
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if self.tp > 1:
-            if self.host_staged and t.is_cuda:
-                h = t.cpu()
-                dist.broadcast(h, src=src, group=self.group)
-                t.copy_(h)
-                return t
-            dist.broadcast(t, src=src, group=self.group)
+            with tracing.range("tp.broadcast"):
+                return self._broadcast(t, src)
+        return t
+
+    def _broadcast(self, t: torch.Tensor, src: int) -> torch.Tensor:
+        if self.host_staged and t.is_cuda:
+            h = t.cpu()
+            dist.broadcast(h, src=src, group=self.group)
+            t.copy_(h)
+            return t
+        dist.broadcast(t, src=src, group=self.group)
         return t
 
 
@@ -686,10 +701,11 @@ class LlamaTP:
             self.pages.device_table()
         if slot_ids is not None:
             slot_ids = slot_ids.to(self.device).contiguous()
-        if self.backend == "fused":
-            return self._fused_forward(ids.to(torch.int32), positions.to(torch.int32), lens.to(torch.int32), B, S,
-                                       decode, k, slot_ids)
-        return self._ref_forward(ids, positions, lens, B, S, decode, k, slot_ids)
+        with tracing.range("llama.decode" if decode else "llama.prefill"):
+            if self.backend == "fused":
+                return self._fused_forward(ids.to(torch.int32), positions.to(torch.int32), lens.to(torch.int32), B,
+                                           S, decode, k, slot_ids)
+            return self._ref_forward(ids, positions, lens, B, S, decode, k, slot_ids)
 
     def gather_candidates(self, vals: torch.Tensor, idx: torch.Tensor):
         """X4 all-gather of every rank's local top-k -> ``[B, tp*k]`` values / ids (host tensors)."""
@@ -768,7 +784,8 @@ class LlamaTP:
             t_s.copy_(tok.view(B, 1))
             p_s.copy_(cur.view(B, 1))
             l_s.copy_(cur.view(B) + 1)
-            g.replay()
+            with tracing.range("llama.decode"):
+                g.replay()
             return v_s, i_s
         self._dec_ctx = ctx
         try:
@@ -789,10 +806,12 @@ class LlamaTP:
         ids = ids.to(dev)
         lens = lens.to(dev).to(torch.int32)
         k = max(1, min(gp.top_k, self.top_k_max))
-        if self.pages is not None:  # batch row b = slot b, pages for the prompt + the generation budget
-            for b in range(B):
-                self.pages.assign(b, S + gp.max_new_tokens)
+        assigned = 0
         try:
+            if self.pages is not None:  # batch row b = slot b, pages for the prompt + the generation budget
+                for b in range(B):
+                    self.pages.assign(b, S + gp.max_new_tokens)
+                    assigned = b + 1
             pos = torch.arange(S, device=dev, dtype=torch.int32).unsqueeze(0).expand(B, S).contiguous()
             vals, idx = self.step(ids, pos, lens, decode=False, k=k)
             out = []
@@ -807,8 +826,8 @@ class LlamaTP:
                 cur = cur + 1
             return torch.stack(out, dim=1)
         finally:
-            if self.pages is not None:
-                for b in range(B):
+            if self.pages is not None:  # also on OutOfPages part-way: release exactly the rows assigned
+                for b in range(assigned):
                     self.pages.release(b)
 
     def _sample_rows(self, vals, idx, gp: GenParams, step: int) -> torch.Tensor:

@@ -19,6 +19,8 @@ from typing import Dict, List, Optional, Tuple
 import torch
 import torch.distributed as dist
 
+from ..utils import tracing
+
 
 @dataclass
 class DistInfo:
@@ -44,15 +46,25 @@ def env_info() -> DistInfo:
     )
 
 
-def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0, device_id: Optional[int] = None) -> DistInfo:
-    """Initialise the default process group from the environment (no-op for world size 1)."""
+def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0, device_id: Optional[int] = None,
+                     force: bool = False) -> DistInfo:
+    """Initialise the default process group from the environment.  World size 1 is a no-op
+    unless ``force`` (or ``MLS_DIST_FORCE=1``): then a one-rank group is created too, which is how
+    the RCCL code paths (device-tensor broadcast / all-reduce / barrier) run on a one-GPU box."""
     info = env_info()
-    if info.world_size <= 1:
+    force = force or os.environ.get("MLS_DIST_FORCE", "0") == "1"
+    if info.world_size <= 1 and not force:
         return info
     if dist.is_initialized():
         info.backend = dist.get_backend()
         return info
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if "MASTER_PORT" not in os.environ:
+        if info.world_size > 1:
+            raise RuntimeError("MASTER_PORT must be set for a multi-rank process group")
+        from .launch import free_port
+
+        os.environ["MASTER_PORT"] = str(free_port())
     # dmabuf IPC only on this pool's host driver (RCCL / tensor sharing across processes)
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     if backend is None:  # MLS_DIST_BACKEND=gloo: rehearse several ranks on one GPU (RCCL refuses that)
@@ -77,10 +89,15 @@ def destroy() -> None:
 
 def barrier(group=None) -> None:
     if dist.is_initialized():
-        if dist.get_backend(group) == "nccl":
-            dist.barrier(group=group, device_ids=[torch.cuda.current_device()])
-        else:
-            dist.barrier(group=group)
+        with tracing.range("dist.barrier"):
+            _barrier(group)
+
+
+def _barrier(group=None) -> None:
+    if dist.get_backend(group) == "nccl":
+        dist.barrier(group=group, device_ids=[torch.cuda.current_device()])
+    else:
+        dist.barrier(group=group)
 
 
 def _group_by_dtype(tensors: Dict[str, torch.Tensor]) -> Dict[torch.dtype, List[str]]:
@@ -101,9 +118,14 @@ def broadcast_state(
     ``spec`` (shapes/dtypes, known from the architecture) -- or ``spec=None`` to receive it via
     a small object broadcast first.  Returns tensors on ``device`` on every rank."""
     rank = dist.get_rank(group) if dist.is_initialized() else 0
-    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+    if not dist.is_initialized():
         assert state is not None
         return {k: v.to(device) if device is not None else v for k, v in state.items()}
+    with tracing.range("dist.broadcast"):
+        return _broadcast_state(state, src, device, group, spec, rank)
+
+
+def _broadcast_state(state, src, device, group, spec, rank) -> Dict[str, torch.Tensor]:
     backend = dist.get_backend(group)
     comm_dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
     if spec is None:
@@ -135,7 +157,8 @@ def all_reduce_health(ok: bool, group=None) -> bool:
     backend = dist.get_backend(group)
     dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
     t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    with tracing.range("dist.health"):
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
     return bool(t.item())
 
 
@@ -145,5 +168,6 @@ def max_over_ranks(value: float, group=None) -> float:
     backend = dist.get_backend(group)
     dev = torch.device("cuda", torch.cuda.current_device()) if backend == "nccl" else torch.device("cpu")
     t = torch.tensor([value], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    with tracing.range("dist.max"):
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return float(t.item())

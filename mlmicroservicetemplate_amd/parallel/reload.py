@@ -8,7 +8,10 @@ pointing at valid weights and are replayed unchanged (no re-capture, no allocati
 
 Data-parallel service (one process per GPU, any rank may receive the HTTP request): the receiving
 rank writes the request to a small control directory shared by the service's ranks
-(``/dev/shm/mls-reload-<PORT>-<MASTER_PORT>``); every rank's watcher thread picks it up, rank 0
+(``/dev/shm/mls-reload-<PORT>-<MASTER_PORT>-<MLS_LAUNCH_ID>``: the launcher draws a random id per
+launch, so a crashed earlier run's state is never picked up and the path cannot be guessed in
+advance; the directory is created 0700 and refused if it is a symlink, owned by another user or
+group/world accessible); every rank's watcher thread picks it up, rank 0
 loads the checkpoint, broadcasts an ok flag and then the parameters as one flattened buffer per
 dtype over RCCL/xGMI (``dist.broadcast_state``), every rank applies them and acknowledges; the
 HTTP request returns once all ranks acknowledged.  The process group is otherwise idle in DP
@@ -17,11 +20,16 @@ serving, so the reload collectives never interleave with other collectives.
 Ordering: a new generation is only written (under an ``fcntl`` lock on the control directory)
 once every rank has acknowledged the previous one -- a second request meanwhile gets 409 -- so
 every watcher applies every generation, in order, and all ranks issue the same collectives.  Rank
-0 also broadcasts the generation it applies, and a rank that read another one fails loudly.
+0 also broadcasts the generation it applies; a rank that read another one acknowledges with an
+error instead of applying.  A watcher never dies on a failed generation (it writes an error ack),
+and a generation older than the request timeout that some rank never acknowledged may be replaced,
+so a lost rank cannot lock the endpoint into 409 for the life of the service.
 
 Security: the endpoint is off unless ``API_KEY`` is set (403), the ``api_key`` header must match
 it, and ``weights`` may only name a file under ``WEIGHTS_DIR`` (same 400 whether a path is outside
-it or missing, so the endpoint does not reveal which paths exist).
+it or missing, so the endpoint does not reveal which paths exist).  Rank 0 re-validates the path
+against ``WEIGHTS_DIR`` when it applies a generation, so a request that did not come through the
+HTTP handler cannot load an arbitrary file either.
 """
 from __future__ import annotations
 
@@ -80,6 +88,25 @@ def resolve_weights(settings, weights: Any) -> str:
     return path
 
 
+def secure_control_dir(path: str) -> str:
+    """Create ``path`` 0700 (if missing) and check it is a real directory owned by us and closed
+    to group / world -- the ranks trust what they read there."""
+    try:
+        os.mkdir(path, 0o700)
+    except FileExistsError:
+        pass
+    st = os.lstat(path)
+    import stat as _stat
+
+    if _stat.S_ISLNK(st.st_mode) or not _stat.S_ISDIR(st.st_mode):
+        raise PermissionError(f"reload control path {path} is not a plain directory")
+    if st.st_uid != os.getuid():
+        raise PermissionError(f"reload control directory {path} is owned by uid {st.st_uid}, not {os.getuid()}")
+    if st.st_mode & 0o077:
+        raise PermissionError(f"reload control directory {path} is accessible to other users ({oct(st.st_mode & 0o777)})")
+    return path
+
+
 def _atomic_write(path: str, obj: dict) -> None:
     tmp = f"{path}.{os.getpid()}.tmp"
     with open(tmp, "w") as f:
@@ -108,9 +135,11 @@ class ReloadCoordinator:
         self._thread: Optional[threading.Thread] = None
         self.ctl_dir: Optional[str] = None
         if ctx.world_size > 1:
-            base = "/dev/shm" if os.path.isdir("/dev/shm") else tempfile.gettempdir()
-            self.ctl_dir = os.path.join(base, f"mls-reload-{settings.PORT}-{os.environ.get('MASTER_PORT', '0')}")
-            os.makedirs(self.ctl_dir, exist_ok=True)
+            base = os.environ.get("MLS_RELOAD_BASE") or ("/dev/shm" if os.path.isdir("/dev/shm")
+                                                          else tempfile.gettempdir())
+            launch = os.environ.get("MLS_LAUNCH_ID", "0")
+            self.ctl_dir = secure_control_dir(os.path.join(
+                base, f"mls-reload-{settings.PORT}-{os.environ.get('MASTER_PORT', '0')}-{launch}"))
             self._thread = threading.Thread(target=self._watch, name="mls-reload-watch", daemon=True)
             self._thread.start()
 
@@ -126,7 +155,9 @@ class ReloadCoordinator:
             raise ReloadError("give 'weights' (a safetensors path on the server) or 'seed'")
         t0 = time.perf_counter()
         if self.ctl_dir is None:
-            with self._lock:
+            from ..utils import tracing
+
+            with self._lock, tracing.range("reload.apply"):
                 params = self.plugin.load_params(weights, seed)
                 self.plugin.apply_params(params)
                 self.generation += 1
@@ -135,11 +166,13 @@ class ReloadCoordinator:
         with self._lock, _DirLock(self.ctl_dir):
             cur = _read(os.path.join(self.ctl_dir, "request.json")) or {}
             prev = int(cur.get("generation", 0))
-            if prev and not all(os.path.exists(os.path.join(self.ctl_dir, f"ack-{prev}-{r}.json"))
-                                for r in range(self.ctx.world_size)):
+            stale = time.time() - float(cur.get("t", 0.0)) > float(cur.get("timeout", timeout))
+            if prev and not stale and not all(os.path.exists(os.path.join(self.ctl_dir, f"ack-{prev}-{r}.json"))
+                                              for r in range(self.ctx.world_size)):
                 raise ReloadBusy(f"reload generation {prev} is still being applied; retry later")
             gen = prev + 1
-            _atomic_write(os.path.join(self.ctl_dir, "request.json"), {"generation": gen, "weights": weights, "seed": seed})
+            _atomic_write(os.path.join(self.ctl_dir, "request.json"),
+                          {"generation": gen, "weights": weights, "seed": seed, "t": time.time(), "timeout": timeout})
         deadline = time.monotonic() + timeout
         while time.monotonic() < deadline:
             acks = [_read(os.path.join(self.ctl_dir, f"ack-{gen}-{r}.json")) for r in range(self.ctx.world_size)]
@@ -156,8 +189,18 @@ class ReloadCoordinator:
         req_path = os.path.join(self.ctl_dir, "request.json")
         while not self._stop.is_set():
             req = _read(req_path)
-            if req and int(req.get("generation", 0)) > self.generation:
-                self._apply_distributed(req)
+            try:
+                gen = int(req.get("generation", 0)) if req else 0
+            except (TypeError, ValueError):
+                gen = 0
+            if gen > self.generation:
+                try:
+                    self._apply_distributed(req)
+                except Exception as e:  # never let the watcher die silently: ack the failure
+                    logger.exception("reload generation %d failed on rank %d", gen, self.ctx.rank)
+                    self.generation = gen
+                    _atomic_write(os.path.join(self.ctl_dir, f"ack-{gen}-{self.ctx.rank}.json"),
+                                  {"rank": self.ctx.rank, "generation": gen, "error": f"{type(e).__name__}: {e}"})
             self._stop.wait(self.poll_s)
 
     def _apply_distributed(self, req: dict) -> None:
@@ -171,7 +214,10 @@ class ReloadCoordinator:
         params = None
         if self.ctx.rank == 0:
             try:
-                params = self.plugin.load_params(req.get("weights"), req.get("seed"))
+                weights = req.get("weights")
+                if weights is not None:  # re-check: the request file is not trusted to be from the handler
+                    weights = resolve_weights(self.settings, weights)
+                params = self.plugin.load_params(weights, req.get("seed"))
             except Exception as e:  # validated on rank 0 before any rank commits
                 err = f"{type(e).__name__}: {e}"
         backend = dist.get_backend()
@@ -180,13 +226,17 @@ class ReloadCoordinator:
         dist.broadcast(ok, src=0)
         flag, gen0 = (int(v) for v in ok.tolist())
         if gen0 != gen:  # cannot happen with the 409 gate; never apply out of step with rank 0
-            raise RuntimeError(f"reload: rank {self.ctx.rank} read generation {gen}, rank 0 applies {gen0}")
+            err = f"rank {self.ctx.rank} read generation {gen}, rank 0 applies {gen0}"
+            flag = 0
         if flag:
             try:
-                params = mdist.broadcast_state(params, src=0, device=None, spec=self.plugin.reload_spec())
-                with self._lock:
-                    self.plugin.apply_params(params)
-                    self.last = {"generation": gen, "weights": req.get("weights"), "seed": req.get("seed")}
+                from ..utils import tracing
+
+                with tracing.range("reload.apply"):
+                    params = mdist.broadcast_state(params, src=0, device=None, spec=self.plugin.reload_spec())
+                    with self._lock:
+                        self.plugin.apply_params(params)
+                        self.last = {"generation": gen, "weights": req.get("weights"), "seed": req.get("seed")}
             except Exception as e:
                 logger.exception("reload generation %d failed on rank %d", gen, self.ctx.rank)
                 err = f"{type(e).__name__}: {e}"

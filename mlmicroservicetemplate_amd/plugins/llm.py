@@ -58,7 +58,7 @@ class LlamaPlugin(ModelPlugin):
         source = llama.CheckpointSource(s.WEIGHTS, device=dev) if s.WEIGHTS else None
         params = llama.init_llama_shard(cfg, tp, ctx.rank, int(s.SEED), device=dev, source=source)
         max_batch, max_seq = int(s.MAX_BATCH) or 32, int(extra.get("max_seq", 2048))
-        kv_pages = self._kv_pages(extra.get("kv_pages", 0), cfg, tp, max_batch, max_seq, dev)
+        kv_pages = self._kv_pages(extra.get("kv_pages", 0), cfg, tp, max_batch, max_seq, dev, backend)
         if tp > 1 and kv_pages:  # the scheduler replays rank 0's admissions: every pool must be equal
             from ..parallel import dist as mdist
 
@@ -78,7 +78,7 @@ class LlamaPlugin(ModelPlugin):
         logger.info("llama ready: tp=%d rank=%d backend=%s device=%s", tp, ctx.rank, backend, dev)
 
     @staticmethod
-    def _kv_pages(spec, cfg, tp, max_batch, max_seq, dev) -> int:
+    def _kv_pages(spec, cfg, tp, max_batch, max_seq, dev, backend: str = "fused") -> int:
         """MODEL_CONFIG ``kv_pages``: 0 = per-slot caches (``max_batch x max_seq`` rows), N = a
         shared pool of N 64-row pages, ``auto`` = as many pages as half the free HBM holds, capped
         at what ``max_batch`` full-length sequences could use (+ the scratch page).  Under TP the
@@ -90,7 +90,8 @@ class LlamaPlugin(ModelPlugin):
             return int(spec)
         from ..models.llama import shard_dims
 
-        page_bytes = cfg.layers * 2 * 64 * shard_dims(cfg, tp, 0).hkv * cfg.head_dim * 2
+        elem = 2 if backend == "fused" else 4  # LlamaTP: bf16 caches when fused, fp32 for the reference backend
+        page_bytes = cfg.layers * 2 * 64 * shard_dims(cfg, tp, 0).hkv * cfg.head_dim * elem
         if torch.device(dev).type != "cuda":
             return full
         free, _total = torch.cuda.mem_get_info(torch.device(dev))

@@ -16,7 +16,9 @@ Design points:
     row's slot to fail just that request; a raised exception fails the whole batch;
   * admission control: more than ``max_queue`` waiting requests -> :class:`QueueFull`
     (HTTP 503) instead of unbounded latency;
-  * cancelled requests (client went away) are dropped before the batch is formed.
+  * cancelled requests (client went away) stop counting at once: ``queue_depth``, ``load`` and
+    ``max_queue`` admission count only live queued futures (a set maintained by a done-callback),
+    and the cancelled entries are swept from the deque when the next batch is formed.
 """
 from __future__ import annotations
 
@@ -27,6 +29,8 @@ import logging
 import threading
 import time
 from typing import Any, Callable, Deque, List, Optional, Sequence, Tuple
+
+from ..utils import tracing
 
 logger = logging.getLogger("mlsamd.batcher")
 
@@ -64,6 +68,9 @@ class DynamicBatcher:
         self._own_executor = executor is None
         self._executor = executor or cf.ThreadPoolExecutor(self.inflight, thread_name_prefix=f"{name}-exec")
         self._q: Deque[Tuple[Any, asyncio.Future, float]] = collections.deque()
+        # futures queued and not cancelled: what queue_depth / load / admission count (the deque
+        # may still hold cancelled entries until the collector sweeps them in _take)
+        self._queued: set = set()
         self._wake: Optional[asyncio.Event] = None
         self._full: Optional[asyncio.Event] = None
         self._sem: Optional[asyncio.Semaphore] = None
@@ -113,6 +120,7 @@ class DynamicBatcher:
             self._task = None
         while self._q:
             _s, fut, _t = self._q.popleft()
+            self._queued.discard(fut)
             if not fut.done():
                 fut.set_exception(BatcherClosed(f"{self.name} stopped"))
         if self._own_executor:
@@ -121,24 +129,41 @@ class DynamicBatcher:
     # ----------------------------------------------------------------- API
     @property
     def queue_depth(self) -> int:
-        return len(self._q)
+        return len(self._queued)
 
     @property
     def load(self) -> int:
         """Outstanding requests (queued + executing) -- the router's least-loaded key."""
-        return len(self._q) + self._inflight_now * self.max_batch
+        return len(self._queued) + self._inflight_now * self.max_batch
+
+    def _on_queued_done(self, fut: "asyncio.Future") -> None:
+        # runs on the loop when a queued future completes; only a cancellation can complete it
+        # while it is still queued (results are set after _take removed it from the set)
+        if fut in self._queued:
+            self._queued.discard(fut)
+            if not self._queued:
+                # nothing live is waiting: let the collector sweep the cancelled entries now
+                if self._wake is not None:
+                    self._wake.set()
+
+    def _enqueue(self, item) -> None:
+        self._q.append(item)
+        fut = item[1]
+        if fut not in self._queued and not fut.done():
+            self._queued.add(fut)
+            fut.add_done_callback(self._on_queued_done)
 
     def submit_nowait(self, sample: Any) -> "asyncio.Future":
         if self._closed:
             raise BatcherClosed(f"{self.name} is stopped")
         if self._task is None:
             raise RuntimeError("batcher not started")
-        if len(self._q) >= self.max_queue:
+        if len(self._queued) >= self.max_queue:
             self.rejected += 1
-            raise QueueFull(f"{self.name}: {len(self._q)} requests queued")
+            raise QueueFull(f"{self.name}: {len(self._queued)} requests queued")
         fut = self._loop.create_future()
-        self._q.append((sample, fut, time.perf_counter()))
-        n = len(self._q)
+        self._enqueue((sample, fut, time.perf_counter()))
+        n = len(self._queued)
         if n == 1:
             self._wake.set()
         if n >= self.max_batch:
@@ -154,8 +179,9 @@ class DynamicBatcher:
     def evict_queued(self) -> List[Tuple[Any, "asyncio.Future", float]]:
         """Remove and return every queued (not yet dispatched) request -- a drained replica's
         backlog, which the router hands to healthy replicas."""
-        items = list(self._q)
+        items = [it for it in self._q if not it[1].done()]
         self._q.clear()
+        self._queued.clear()
         if self._full is not None:
             self._full.clear()
         return items
@@ -163,10 +189,10 @@ class DynamicBatcher:
     def adopt(self, items) -> None:
         """Append requests evicted from another replica (their futures keep their waiters)."""
         for it in items:
-            self._q.append(it)
-        if self._q and self._wake is not None:
+            self._enqueue(it)
+        if self._queued and self._wake is not None:
             self._wake.set()
-            if len(self._q) >= self.max_batch:
+            if len(self._queued) >= self.max_batch:
                 self._full.set()
 
     # ----------------------------------------------------------------- internals
@@ -174,10 +200,13 @@ class DynamicBatcher:
         batch = []
         while self._q and len(batch) < self.max_batch:
             item = self._q.popleft()
-            if item[1].cancelled():
+            self._queued.discard(item[1])
+            if item[1].done():  # cancelled while queued
                 continue
             batch.append(item)
-        if len(self._q) < self.max_batch:
+        while self._q and self._q[0][1].done():  # sweep cancelled heads so the deadline is a live one
+            self._queued.discard(self._q.popleft()[1])
+        if len(self._queued) < self.max_batch:
             self._full.clear()
         if not self._q:
             self._wake.clear()
@@ -186,19 +215,22 @@ class DynamicBatcher:
     async def _collector(self) -> None:
         while True:
             await self._wake.wait()
+            while self._q and self._q[0][1].done():  # cancelled while queued
+                self._queued.discard(self._q.popleft()[1])
             if not self._q:
                 self._wake.clear()
                 continue
             # wait until full or until the oldest request's deadline
             oldest = self._q[0][2]
             remaining = oldest + self.max_wait - time.perf_counter()
-            if len(self._q) < self.max_batch and remaining > 0 and not self._closed:
+            if len(self._queued) < self.max_batch and remaining > 0 and not self._closed:
                 try:
                     await asyncio.wait_for(self._full.wait(), remaining)
                 except asyncio.TimeoutError:
                     pass
             await self._sem.acquire()
-            batch = self._take()
+            with tracing.range("batch.assemble"):
+                batch = self._take()
             if not batch:
                 self._sem.release()
                 continue
@@ -218,7 +250,7 @@ class DynamicBatcher:
         bid = self._next_id
         self._next_id += 1
         self._running[bid] = t0
-        cfut = self._executor.submit(self.run_batch, samples)
+        cfut = self._executor.submit(self._run_traced, samples)
 
         def done(f: cf.Future) -> None:
             try:
@@ -227,6 +259,10 @@ class DynamicBatcher:
                 pass
 
         cfut.add_done_callback(done)
+
+    def _run_traced(self, samples):
+        with tracing.range("batch.run"):
+            return self.run_batch(samples)
 
     def _resolve(self, batch, f: cf.Future, t0: float, bid: int = -1) -> None:
         self._running.pop(bid, None)
@@ -273,7 +309,7 @@ class DynamicBatcher:
     def stats(self) -> dict:
         return {
             "name": self.name,
-            "queue_depth": len(self._q),
+            "queue_depth": len(self._queued),
             "inflight": self._inflight_now,
             "batches": self.batches,
             "requests": self.requests,

@@ -35,6 +35,12 @@ logger = logging.getLogger("mlsamd.serve")
 DP_MODELS = {"resnet50", "bert", "identity", "stub", "toy_classifier"}
 
 
+def secrets_token() -> str:
+    import secrets  # stdlib (this package never shadows it: SURVEY.md §7.4)
+
+    return secrets.token_hex(8)
+
+
 def free_port() -> int:
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
@@ -130,6 +136,7 @@ def launch(args) -> int:
     procs: List[subprocess.Popen] = []
     base_env = dict(os.environ)
     base_env.update({"WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(master_port),
+                     "MLS_LAUNCH_ID": base_env.get("MLS_LAUNCH_ID") or secrets_token(),
                      "HSA_ENABLE_IPC_MODE_LEGACY": base_env.get("HSA_ENABLE_IPC_MODE_LEGACY", "0")})
     cmd = [sys.executable, "-m", "mlmicroservicetemplate_amd", "rank", *args.passthrough]
     for r in range(world):

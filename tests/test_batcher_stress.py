@@ -140,3 +140,36 @@ def test_router_stress_debug_loop(caplog):
     assert sorted(everything) == list(range(n)), "lost or duplicated requests across replicas"
     assert all(s < n // 2 for s in runners[1].seen[seen_before:]), "drained replica received new work"
     assert not [r for r in caplog.records if r.name == "asyncio"]
+
+
+def test_cancelled_requests_leave_the_accounting_at_once():
+    """A cancelled queued request stops counting toward queue_depth / load / max_queue admission
+    immediately (not only when the collector next forms a batch)."""
+    from mlmicroservicetemplate_amd.scheduler.batcher import QueueFull
+
+    gate = threading.Event()
+
+    def run(samples):
+        gate.wait(5)
+        return samples
+
+    async def main():
+        b = DynamicBatcher(run, max_batch=3, max_wait_us=10_000_000, inflight=1, max_queue=3)
+        await b.start()
+        futs = [b.submit_nowait(i) for i in range(3)]
+        assert b.queue_depth == 3
+        with pytest.raises(QueueFull):
+            b.submit_nowait(99)
+        for f in futs:
+            f.cancel()
+        await asyncio.sleep(0)  # done-callbacks run on the next loop iteration
+        assert b.queue_depth == 0 and b.load == 0 and b.stats()["queue_depth"] == 0
+        live = [b.submit_nowait(10 + i) for i in range(3)]  # admission capacity is back
+        assert b.queue_depth == 3  # and the 3 live requests fill one batch
+        gate.set()
+        res = await asyncio.gather(*live)
+        assert res == [10, 11, 12]
+        assert b.queue_depth == 0
+        await b.stop()
+
+    asyncio.run(main(), debug=True)

@@ -40,3 +40,63 @@ def test_concurrent_slots_match_serial():
         for (rv, ri), (ov, oi) in zip(ref, outs):
             np.testing.assert_array_equal(ri, oi)
             np.testing.assert_array_equal(rv, ov)
+
+
+def test_benchmarked_config_end_to_end_vs_fp32():
+    """The exact configuration bench.py times: ResNet50Fused(max_batch=32) with the shipped B=32
+    tuning table, GpuEngine(inflight=5, concurrent slots, hipGraphs), 5 batches of 32 in flight
+    -- every row compared with the fp32 PyTorch reference of the same weights."""
+    from mlmicroservicetemplate_amd.engine.worker import GpuEngine
+    from mlmicroservicetemplate_amd.models import resnet
+    from mlmicroservicetemplate_amd.ops.autotune import load_tuning
+
+    tuning = load_tuning("resnet50", 32)
+    assert tuning, "the shipped B=32 tuning table must load (tuned/resnet50_gfx950_b32.json)"
+    p = resnet.init_resnet50(0)
+    model = resnet.ResNet50Fused(p, DEV, max_batch=32, tuning=tuning)
+
+    def fwd(x):
+        logits = model(x)
+        v, i = model.ops.softmax_topk(logits, 5)
+        return logits, v, i
+
+    eng = GpuEngine(fwd, DEV, (224, 224, 3), torch.uint8, buckets=[32], inflight=5, concurrent=True,
+                    use_graphs=True, name="benchcfg")
+    eng.warmup(capture=True)
+    rng = np.random.default_rng(7)
+    batches = [rng.integers(0, 256, (32, 224, 224, 3), dtype=np.uint8) for _ in range(5)]
+    tickets = [eng.submit(b) for b in batches]  # 5 co-running batches
+    outs = [t.wait() for t in tickets]
+    pd = {k: v.to(DEV) for k, v in p.items()}
+    for b, (logits, vals, idx) in zip(batches, outs):
+        ref = resnet.resnet50_reference(pd, torch.from_numpy(b).to(DEV)).float().cpu()
+        lg = torch.from_numpy(logits).float()
+        rel = ((lg - ref).abs().max() / ref.abs().max()).item()
+        assert rel <= 2e-2, rel
+        top2 = ref.topk(2, dim=-1).values
+        margin = (top2[:, 0] - top2[:, 1]) / ref.abs().max()
+        sure = margin > 1e-2
+        assert sure.sum() >= 8, "too few rows with a clear reference top-1 to compare"
+        assert torch.equal(torch.from_numpy(idx[:, 0]).long()[sure], ref.argmax(-1)[sure])
+        # the fused softmax/top-5 head agrees with torch on the engine's own logits
+        pv, pi = torch.softmax(lg, -1).topk(5, dim=-1)
+        np.testing.assert_allclose(vals, pv.numpy(), rtol=2e-2, atol=1e-4)
+
+
+def test_engine_roctx_ranges():
+    """the engine's stage / h2d / replay / d2h / d2h_wait ranges are emitted."""
+    from mlmicroservicetemplate_amd.engine.worker import GpuEngine
+    from mlmicroservicetemplate_amd.utils import tracing
+
+    eng = GpuEngine(lambda x: (x.float().sum(dim=1),), DEV, (16,), torch.uint8, buckets=[4], inflight=2,
+                    concurrent=True, name="tr")
+    eng.warmup(capture=True)
+    tracing.set_enabled(True)  # real roctx push/pop too
+    try:
+        with tracing.record() as names:
+            (s,) = eng.run([np.full(16, 2, np.uint8)] * 3)
+    finally:
+        tracing.set_enabled(False)
+    assert s.tolist() == [32.0] * 3
+    for k in ("stage", "h2d", "replay", "d2h", "d2h_wait"):
+        assert f"tr.{k}" in names, (k, names)

@@ -110,3 +110,28 @@ def test_plugin_kv_pages_setting():
     assert LlamaPlugin._kv_pages(0, cfg, 1, 8, 1024, "cpu") == 0
     assert LlamaPlugin._kv_pages("12", cfg, 1, 8, 1024, "cpu") == 12
     assert LlamaPlugin._kv_pages("auto", cfg, 1, 8, 1000, "cpu") == 8 * 16 + 1  # full coverage + scratch
+
+
+def test_paged_generate_out_of_pages_releases_partial_assignments(params):
+    """OutOfPages part-way through the per-row assign loop must not leak the pages of
+    the rows already assigned -- afterwards the pool is whole and a fitting batch still runs."""
+    cfg, p = params
+    model = LlamaTP(p, cfg, max_batch=3, max_seq=192, kv_pages=5)  # 4 usable pages
+    start = model.pages.free_pages
+    ids = torch.randint(3, 2000, (3, 60), generator=torch.Generator().manual_seed(1))
+    lens = torch.tensor([60, 60, 60])
+    with pytest.raises(OutOfPages):  # 2 pages per row (60 + 9 rows) x 3 rows > 4
+        model.generate(ids, lens, GenParams(max_new_tokens=9))
+    assert model.pages.free_pages == start
+    out = model.generate(ids[:2], lens[:2], GenParams(max_new_tokens=9))
+    assert out.shape == (2, 9) and model.pages.free_pages == start
+
+
+def test_plugin_kv_pages_auto_uses_cache_dtype():
+    """``kv_pages: auto`` sizes pages by the cache element size LlamaTP will use."""
+    from mlmicroservicetemplate_amd.plugins.llm import LlamaPlugin
+
+    cfg = tiny_config(**CFG)
+    # CPU: the full-length cap either way, but the helper must accept the backend
+    assert LlamaPlugin._kv_pages("auto", cfg, 1, 2, 128, "cpu", "reference") == 2 * 2 + 1
+    assert LlamaPlugin._kv_pages(7, cfg, 1, 2, 128, "cpu", "fused") == 7

@@ -186,9 +186,11 @@ def test_resnet50_fused_matches_reference():
     model = ResNet50Fused(params, DEV, max_batch=32)
     logits = model(imgs).float()
     ref = resnet50_reference({k: v.to(DEV) for k, v in params.items()}, imgs)
-    assert rel_err(logits, ref) < 5e-2
+    assert rel_err(logits, ref) < 2e-2
     vals, idx = model.classify(imgs, 5)
-    assert (idx[:, 0].long() == ref.argmax(-1)).float().mean().item() >= 0.75
+    top2 = ref.float().topk(2, dim=-1).values
+    sure = (top2[:, 0] - top2[:, 1]) / ref.abs().max() > 1e-2
+    assert torch.equal(idx[:, 0].long()[sure], ref.argmax(-1)[sure])
 
 
 @pytest.mark.parametrize("rows,N,k", [(32, 1000, 5), (5, 8, 3), (7, 512, 50), (3, 2048, 10), (9, 1032, 1)])

@@ -189,3 +189,79 @@ def test_reload_two_ranks_broadcasts_to_every_rank(frontend):
             proc.wait(30)
         except subprocess.TimeoutExpired:
             os.killpg(proc.pid, signal.SIGKILL)
+
+
+def test_control_dir_refuses_symlinks_foreign_modes(tmp_path):
+    """the reload control directory is trusted by every rank, so it must be a 0700
+    directory of ours -- never a symlink or a group/world-writable directory someone pre-created."""
+    from mlmicroservicetemplate_amd.parallel.reload import secure_control_dir
+
+    d = secure_control_dir(str(tmp_path / "ctl"))
+    assert (os.stat(d).st_mode & 0o777) == 0o700
+    assert secure_control_dir(d) == d  # a second rank of the same launch reuses it
+    target = tmp_path / "elsewhere"
+    target.mkdir(mode=0o700)
+    os.symlink(target, tmp_path / "link")
+    with pytest.raises(PermissionError):
+        secure_control_dir(str(tmp_path / "link"))
+    loose = tmp_path / "loose"
+    loose.mkdir()
+    os.chmod(loose, 0o777)
+    with pytest.raises(PermissionError):
+        secure_control_dir(str(loose))
+
+
+class _FakePlugin:
+    name = "fake"
+
+    def __init__(self):
+        self.applied = []
+
+    def reload_spec(self):
+        return {}
+
+    def load_params(self, weights, seed):
+        return {}
+
+    def apply_params(self, params):
+        self.applied.append(params)
+
+
+def test_stale_generation_is_replaced_and_watcher_acks_failures(tmp_path, monkeypatch):
+    """A generation some rank never acknowledged blocks new ones (409) only until the request
+    timeout has passed; a watcher whose apply raises writes an error ack instead of dying."""
+    import json
+    import time
+    from types import SimpleNamespace
+
+    from mlmicroservicetemplate_amd.parallel import reload as rl
+
+    monkeypatch.setenv("MLS_RELOAD_BASE", str(tmp_path))
+    monkeypatch.setenv("MLS_LAUNCH_ID", "testlaunch")
+    ctx = SimpleNamespace(rank=1, world_size=2)
+    settings = SimpleNamespace(PORT=1, WEIGHTS_DIR="")
+    co = rl.ReloadCoordinator(_FakePlugin(), ctx, settings, poll_s=0.01)
+    try:
+        assert co.ctl_dir.startswith(str(tmp_path)) and co.ctl_dir.endswith("-testlaunch")
+        # the watcher (rank 1) will fail to apply: there is no process group here
+        req = os.path.join(co.ctl_dir, "request.json")
+        rl._atomic_write(req, {"generation": 1, "seed": 3, "t": time.time(), "timeout": 0.3})
+        ack = os.path.join(co.ctl_dir, "ack-1-1.json")
+        for _ in range(300):
+            if os.path.exists(ack):
+                break
+            time.sleep(0.01)
+        a = json.load(open(ack))
+        assert a["generation"] == 1 and a["error"]
+        assert co._thread.is_alive()  # the watcher survived its failed generation
+        # rank 0 never acked generation 1: a new request is refused until it is stale
+        co._stop.set()
+        co._thread.join(2)
+        with pytest.raises(rl.ReloadBusy):
+            co.request(seed=4, timeout=0.3)
+        time.sleep(0.35)
+        with pytest.raises(TimeoutError):  # accepted as generation 2 (no rank applies it here)
+            co.request(seed=4, timeout=0.2)
+        assert json.load(open(req))["generation"] == 2
+    finally:
+        co.close()
