@@ -136,6 +136,7 @@ def run_rank(args) -> int:
     if world > 1:
         spec = {k: (tuple(v.shape), v.dtype) for k, v in resnet.init_resnet50_spec().items()}
         params = mdist.broadcast_state(params, src=0, device=device, spec=spec)
+        torch.cuda.synchronize(device)  # X1 done before any graph capture starts
     t_bcast = time.perf_counter() - t0
 
     fwd = build_model(args.backend, device, args.batch, params)

@@ -104,7 +104,8 @@ class ServingRuntime:
         logger.debug("Beginning Model Initialization Process.")
         self.state.mark_init_started()
         try:
-            self.plugin.init(self.ctx)
+            if not self.ctx.extra.get("preinitialized"):  # a respawned replica ran init before listening
+                self.plugin.init(self.ctx)
             if self.plugin.batched:
                 fut = asyncio.run_coroutine_threadsafe(self._start_batchers(), self.loop)
                 fut.result(timeout=60)
@@ -124,6 +125,9 @@ class ServingRuntime:
             return
         self.state.mark_ready()
         self.metrics.ready.set(1)
+        from ..parallel.launch import mark_replica_ready
+
+        mark_replica_ready(self.ctx.rank)
         logger.debug("Finishing Model Initialization Process.")
         if self.ctx.rank == 0:
             discovery.start_heartbeat(self.state, self.settings)

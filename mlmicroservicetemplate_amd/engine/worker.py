@@ -190,7 +190,11 @@ class GpuEngine:
                 for slot in self.slots:
                     for b in self.buckets:
                         g = torch.cuda.CUDAGraph()
-                        with torch.cuda.graph(g, pool=slot.pool, stream=slot.s_comp):
+                        # thread_local: the RCCL watchdog thread (DP ranks keep a process group for
+                        # X1 / X6) queries its events concurrently; under the default global mode
+                        # that query is an illegal call during capture and aborts the process
+                        with torch.cuda.graph(g, pool=slot.pool, stream=slot.s_comp,
+                                              capture_error_mode="thread_local"):
                             outs = self.forward(slot.dev_in[:b])
                         slot.graphs[b] = g
                         slot.outs[b] = tuple(outs)

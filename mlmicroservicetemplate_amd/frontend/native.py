@@ -188,7 +188,8 @@ class NativeService:
         """Reference ``init_model_helper`` (main.py:77-82): init, ready, then register."""
         self.state.mark_init_started()
         try:
-            self.plugin.init(self.ctx)
+            if not self.ctx.extra.get("preinitialized"):  # a respawned replica ran init before listening
+                self.plugin.init(self.ctx)
             if self.ctx.world_size > 1:
                 from ..parallel import dist as mdist
 
@@ -214,6 +215,9 @@ class NativeService:
             return
         self.state.mark_ready()
         self.srv.set_ready(True)
+        from ..parallel.launch import mark_replica_ready
+
+        mark_replica_ready(self.ctx.rank)
         if self.ctx.rank == 0:
             discovery.start_heartbeat(self.state, self.settings)
 

@@ -765,7 +765,8 @@ class LlamaTP:
                     self.step(tok, pos, lens, decode=True, k=k)
             torch.cuda.current_stream(dev).wait_stream(side)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            # thread_local: the RCCL watchdog thread polls its events while this thread captures
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 vals, idx = self.step(tok, pos, lens, decode=True, k=k)
         finally:
             self._dec_ctx = None

@@ -120,3 +120,19 @@ def spawn_ranks(cmd: Sequence[str], world: int, timeout_s: Optional[float] = Non
         for s, h in old.items():
             signal.signal(s, h)
     return rc
+
+
+# ----------------------------------------------------------------------------- replica readiness
+def mark_replica_ready(rank: int) -> None:
+    """A serving rank reports "initialised and serving" to its supervisor (``serve.py``) by
+    creating ``<MLS_SUPERVISOR_DIR>/ready-<replica>``; the supervisor switches from fail-fast
+    (start-up, where a dead rank would hang the X1 / X6 collectives) to per-replica restart."""
+    d = os.environ.get("MLS_SUPERVISOR_DIR")
+    if not d:
+        return
+    replica = os.environ.get("MLS_REPLICA_ID", str(rank))
+    try:
+        with open(os.path.join(d, f"ready-{replica}"), "w") as f:
+            f.write(str(os.getpid()))
+    except OSError:
+        pass

@@ -163,6 +163,9 @@ class ReloadCoordinator:
                 self.generation += 1
                 self.last = {"generation": self.generation, "weights": weights, "seed": seed}
             return {"generation": self.generation, "ranks": 1, "seconds": round(time.perf_counter() - t0, 3)}
+        if os.path.exists(os.path.join(self.ctl_dir, "degraded")):
+            raise ReloadBusy("a replica was restarted outside the process group; distributed reload is "
+                             "unavailable until the service restarts")
         with self._lock, _DirLock(self.ctl_dir):
             cur = _read(os.path.join(self.ctl_dir, "request.json")) or {}
             prev = int(cur.get("generation", 0))

@@ -13,18 +13,31 @@ Replaces the reference's ``uvicorn src.server.main:app --port ${PORT}`` compose 
   broadcasts each request's tokens to the other ranks (X5), which run the TP forward in
   lockstep (config 5).
 
-The parent only supervises: it forwards SIGINT/SIGTERM, and if any rank dies the others are
-terminated (a dead rank would hang the collectives).
+The parent only supervises and forwards SIGINT/SIGTERM.  Failure policy:
+
+* start-up (before every rank reported ready) and TP groups: a dead rank stops the others -- it
+  would hang the X1 / X6 / X2 collectives;
+* DP replicas after start-up are independent (the process group is idle once the weights are
+  broadcast): a dead replica is restarted as a FRESH standalone process (``WORLD_SIZE=1`` on the
+  same GPU) that loads its own weights (``SEED`` / ``WEIGHTS``, or the last completed hot reload),
+  runs its init BEFORE accepting connections (``MLS_DEFER_LISTEN``: no 503 window), and then
+  shares the port again; the survivors keep serving throughout, so ``/status`` stays 200 while at
+  least one replica is up.  At most ``MAX_RESTARTS`` restarts per replica in ``RESTART_WINDOW_S``;
+  distributed hot reload is refused (409) once a replica has left the group.  Reference analogue:
+  independent replica containers (reference ``README.md:36-40``).
 """
 from __future__ import annotations
 
 import argparse
+import json
 import logging
 import os
+import shutil
 import signal
 import socket
 import subprocess
 import sys
+import tempfile
 import time
 from typing import Dict, List, Optional
 
@@ -94,6 +107,13 @@ def run_rank(args) -> int:
     ctx = PluginContext(settings=settings, rank=info.rank, world_size=info.world_size, local_rank=info.local_rank,
                         devices=devices)
     plugin = load_plugin(settings.MODEL)
+    if os.environ.get("MLS_DEFER_LISTEN") == "1":
+        # a respawned DP replica: initialise before the shared socket is served, so clients never
+        # see this process's not-ready 503 while the surviving replicas are answering 200
+        if hasattr(plugin, "configure"):
+            plugin.configure(settings)
+        plugin.init(ctx)
+        ctx.extra["preinitialized"] = True
     if info.world_size > 1 and settings.TP > 1 and info.rank != 0:
         # tensor-parallel follower: no HTTP, run the lockstep worker loop
         plugin.init(ctx)
@@ -139,6 +159,8 @@ def launch(args) -> int:
                      "MLS_LAUNCH_ID": base_env.get("MLS_LAUNCH_ID") or secrets_token(),
                      "HSA_ENABLE_IPC_MODE_LEGACY": base_env.get("HSA_ENABLE_IPC_MODE_LEGACY", "0")})
     cmd = [sys.executable, "-m", "mlmicroservicetemplate_amd", "rank", *args.passthrough]
+    sup_dir = tempfile.mkdtemp(prefix="mls-sup-")  # 0700: ready markers of the replicas
+    base_env["MLS_SUPERVISOR_DIR"] = sup_dir
     for r in range(world):
         env = dict(base_env, RANK=str(r), LOCAL_RANK=str(r))
         pass_fds = ()
@@ -146,30 +168,133 @@ def launch(args) -> int:
             env["MLS_LISTEN_FD"] = str(sock.fileno())
             pass_fds = (sock.fileno(),)
         procs.append(subprocess.Popen(cmd, env=env, pass_fds=pass_fds))
+    try:
+        if settings.TP <= 1:
+            return _supervise_dp(procs, cmd, base_env, sock, settings, sup_dir)
+        return _supervise(procs)
+    finally:
+        shutil.rmtree(sup_dir, ignore_errors=True)
+
+
+MAX_RESTARTS = 3
+RESTART_WINDOW_S = 300.0
+
+
+def _respawn_env(base_env: Dict[str, str], r: int, sock, settings) -> Dict[str, str]:
+    """Environment of a restarted DP replica: a standalone process on GPU ``r`` (no process
+    group), weights from the last completed hot reload if there was one."""
+    env = dict(base_env, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MLS_DEVICE=str(r), MLS_REPLICA_ID=str(r),
+               MLS_DEFER_LISTEN="1")
+    env.pop("MASTER_PORT", None)
+    if sock is not None:
+        env["MLS_LISTEN_FD"] = str(sock.fileno())
+    if r != 0:
+        env["REGISTER"] = "0"  # one registration heartbeat per service (rank 0's)
+    last = _last_reload(base_env, settings)
+    if last:
+        if last.get("weights"):
+            env["WEIGHTS"] = str(last["weights"])
+        elif last.get("seed") is not None:
+            env["SEED"] = str(int(last["seed"]))
+            env["WEIGHTS"] = ""
+    return env
+
+
+def _ctl_dir(base_env: Dict[str, str], settings) -> str:
+    base = base_env.get("MLS_RELOAD_BASE") or ("/dev/shm" if os.path.isdir("/dev/shm") else tempfile.gettempdir())
+    return os.path.join(base, f"mls-reload-{settings.PORT}-{base_env.get('MASTER_PORT', '0')}-"
+                              f"{base_env.get('MLS_LAUNCH_ID', '0')}")
+
+
+def _last_reload(base_env: Dict[str, str], settings) -> Optional[dict]:
+    """The newest reload generation every original rank acknowledged without error."""
+    d = _ctl_dir(base_env, settings)
+    try:
+        with open(os.path.join(d, "request.json")) as f:
+            req = json.load(f)
+        gen = int(req["generation"])
+        world = int(base_env["WORLD_SIZE"])
+        for r in range(world):
+            with open(os.path.join(d, f"ack-{gen}-{r}.json")) as f:
+                if json.load(f).get("error"):
+                    return None
+        return req
+    except (OSError, ValueError, KeyError, TypeError):
+        return None
+
+
+def _mark_degraded(base_env: Dict[str, str], settings, why: str) -> None:
+    d = _ctl_dir(base_env, settings)
+    if os.path.isdir(d) and not os.path.islink(d):
+        try:
+            with open(os.path.join(d, "degraded"), "w") as f:
+                f.write(why)
+        except OSError:
+            pass
+
+
+def _supervise_dp(procs: List[subprocess.Popen], cmd, base_env: Dict[str, str], sock, settings,
+                  sup_dir: str) -> int:
+    world = len(procs)
     stopping = {"flag": False}
+    restarts: Dict[int, List[float]] = {r: [] for r in range(world)}
+    gave_up = set()
 
     def forward(sig, _frame):
         stopping["flag"] = True
         for p in procs:
-            if p.poll() is None:
+            if p is not None and p.poll() is None:
                 p.send_signal(sig)
 
     signal.signal(signal.SIGINT, forward)
     signal.signal(signal.SIGTERM, forward)
+
+    def all_ready() -> bool:
+        return all(os.path.exists(os.path.join(sup_dir, f"ready-{r}")) for r in range(world))
+
+    started = False
     rc = 0
     try:
         while True:
+            started = started or all_ready()
             codes = [p.poll() for p in procs]
             if all(c is not None for c in codes):
-                rc = next((c for c in codes if c), 0)
+                if not stopping["flag"]:
+                    rc = next((c for c in codes if c), 0) or (1 if gave_up else 0)
                 break
-            if any(c not in (None, 0) for c in codes) and not stopping["flag"]:
-                logger.error("a rank exited with %s; stopping the others", codes)
-                forward(signal.SIGTERM, None)
-                stopping["flag"] = True
+            for r, c in enumerate(codes):
+                if c is None or c == 0 or stopping["flag"] or r in gave_up:
+                    continue
+                if not started:  # start-up: the others are (or will be) blocked in X1 / X6
+                    logger.error("rank %d exited with %s during start-up; stopping the others", r, c)
+                    forward(signal.SIGTERM, None)
+                    rc = c if c > 0 else 1
+                    break
+                now = time.monotonic()
+                recent = [t for t in restarts[r] if now - t < RESTART_WINDOW_S]
+                if len(recent) >= MAX_RESTARTS:
+                    logger.error("replica %d exited with %s; %d restarts in %.0f s -- leaving it down", r, c,
+                                 len(recent), RESTART_WINDOW_S)
+                    gave_up.add(r)
+                    continue
+                restarts[r] = recent + [now]
+                logger.error("replica %d exited with %s; restarting it (the other replicas keep serving)", r, c)
+                _mark_degraded(base_env, settings, f"replica {r} exited with {c}")
+                try:
+                    os.unlink(os.path.join(sup_dir, f"ready-{r}"))
+                except OSError:
+                    pass
+                pass_fds = (sock.fileno(),) if sock is not None else ()
+                procs[r] = subprocess.Popen(cmd, env=_respawn_env(base_env, r, sock, settings), pass_fds=pass_fds)
+            if len(gave_up) == world:
+                rc = 1
+                break
             time.sleep(0.2)
     finally:
         deadline = time.time() + 20
+        for p in procs:
+            if p.poll() is None and not stopping["flag"] and rc:
+                p.send_signal(signal.SIGTERM)
         for p in procs:
             try:
                 p.wait(max(0.1, deadline - time.time()))

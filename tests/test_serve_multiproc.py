@@ -93,3 +93,57 @@ def test_workers_per_gpu_share_the_port():
             proc.wait(30)
         except subprocess.TimeoutExpired:
             os.killpg(proc.pid, signal.SIGKILL)
+
+
+@pytest.mark.timeout(240)
+def test_dp_replica_fault_isolation_and_restart():
+    """in DP serving a dead replica must not take the others down.  3 identity
+    ranks; one is SIGKILLed after start-up; /status and /predict keep answering 200 from the
+    survivors throughout, and the supervisor's fresh replacement process serves again."""
+    port = _port()
+    env = dict(os.environ, PYTHONPATH=ROOT, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    proc = subprocess.Popen([sys.executable, "-m", "mlmicroservicetemplate_amd", "serve", "--model", "identity",
+                             "--gpus", "3", "--port", str(port), "--host", "127.0.0.1", "--no-register",
+                             "--env-file", "/nonexistent"], cwd=ROOT, env=env, start_new_session=True)
+    url = f"http://127.0.0.1:{port}"
+
+    def predict():
+        body, ct = encode_multipart({"image_file": ("x", b"abcd", "application/octet-stream")})
+        return requests.post(url + "/predict", data=body, headers={"content-type": ct, "connection": "close"},
+                             timeout=5)
+
+    try:
+        deadline = time.time() + 120
+        pids = set()
+        while time.time() < deadline and len(pids) < 3:
+            try:
+                h = requests.get(url + "/health", headers={"connection": "close"}, timeout=2).json()
+                if requests.get(url + "/status", headers={"connection": "close"}, timeout=2).status_code == 200:
+                    pids.add(h["pid"])
+            except requests.RequestException:
+                pass
+            time.sleep(0.05)
+        assert len(pids) == 3, f"not every rank became ready: {pids}"
+        victim = sorted(pids)[1]
+        os.kill(victim, signal.SIGKILL)
+        # the survivors answer throughout: every probe is 200 (no 503 window, no refused connection)
+        new_pids, t_end = set(), time.time() + 150
+        while time.time() < t_end:
+            st = requests.get(url + "/status", headers={"connection": "close"}, timeout=5)
+            assert st.status_code == 200, st.text
+            r = predict()
+            assert r.status_code == 200 and r.json()["result"]["result"]["bytes"] == 4
+            h = requests.get(url + "/health", headers={"connection": "close"}, timeout=5).json()
+            assert h["pid"] != victim
+            if h["pid"] not in pids:
+                new_pids.add(h["pid"])
+                break
+            time.sleep(0.02)
+        assert new_pids, "the replacement replica never served"
+        assert proc.poll() is None, "the supervisor exited"
+    finally:
+        os.killpg(proc.pid, signal.SIGTERM)
+        try:
+            proc.wait(30)
+        except subprocess.TimeoutExpired:
+            os.killpg(proc.pid, signal.SIGKILL)
