@@ -349,6 +349,28 @@ class GenParams:
     seed: int = 0
 
 
+_M64 = (1 << 64) - 1
+
+
+def _splitmix64(x: int) -> int:
+    x = (x + 0x9E3779B97F4A7C15) & _M64
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & _M64
+    return x ^ (x >> 31)
+
+
+def sample_uniform(seed: int, step: int) -> float:
+    """The sampling draw for (request seed, decode step): a counter-based hash, bit-identical to
+    the device pick kernel (ops/csrc/decode_pick.hip), independent of the row's batch position."""
+    h = _splitmix64(((int(seed) & _M64) * 0x9E3779B97F4A7C15 + int(step)) & _M64)
+    return float(h >> 40) / 16777216.0
+
+
+class TPCommError(RuntimeError):
+    """A tensor-parallel collective lost a peer (one-shot all-reduce / all-gather timed out): the
+    tokens of the affected generation are not trustworthy and the request fails."""
+
+
 class LlamaTP:
     """One rank of a tensor-parallel Llama with a KV cache ``[layers][max_batch, max_seq, hkv, D]``
     (or, paged, ``[layers][pages, 64, hkv, D]`` pools addressed through a page table)."""
@@ -450,6 +472,11 @@ class LlamaTP:
             or getattr(self.comm, "car", None) is not None)
         self._graphs: Dict[Tuple[int, int, int], tuple] = {}
         self._dec_ctx: Optional[int] = None  # host bound on decode context (sizes the split grid)
+        # device-resident decode loop (X4 on device, _generate_device): per-batch-size static state
+        # shared by the captured steps of every context bucket, so switching buckets copies nothing
+        self._dev_graphs: Dict[Tuple[int, int, int], torch.cuda.CUDAGraph] = {}
+        self._dev_state: Dict[int, Tuple[torch.Tensor, ...]] = {}
+        self.health_every = int(os.environ.get("MLS_TP_HEALTH_EVERY", "32"))
 
     # ---------------------------------------------------------------- shared pieces
     @property
@@ -479,21 +506,10 @@ class LlamaTP:
 
     def _merge_sample(self, vals: torch.Tensor, idx: torch.Tensor, gp: GenParams, step: int) -> torch.Tensor:
         """X4: all-gather the ranks' top-k candidates, merge, pick the next token (identical on
-        every rank: same inputs, same seeded generator -> no broadcast needed)."""
-        allv = self.comm.all_gather(vals)  # [tp, B, k]
-        alli = self.comm.all_gather(idx)
-        B = vals.shape[0]
-        cv = allv.permute(1, 0, 2).reshape(B, -1)
-        ci = alli.permute(1, 0, 2).reshape(B, -1)
-        if gp.top_k <= 1:
-            best = cv.argmax(-1, keepdim=True)
-            return ci.gather(1, best).squeeze(1)
-        k = min(gp.top_k, cv.shape[1])
-        tv, tpos = torch.topk(cv, k, dim=-1)
-        probs = torch.softmax(tv / max(gp.temperature, 1e-5), dim=-1).cpu()
-        g = torch.Generator().manual_seed(gp.seed * 1000003 + step)
-        pick = torch.multinomial(probs, 1, generator=g).to(tpos.device)
-        return ci.gather(1, tpos.gather(1, pick)).squeeze(1)
+        every rank: same inputs, same counter-based draw -> no broadcast needed)."""
+        cv, ci = self.gather_candidates(vals, idx)
+        return torch.tensor([self.pick_token(cv[b], ci[b], gp, step) for b in range(cv.shape[0])],
+                            dtype=torch.int32, device=vals.device)
 
     # ---------------------------------------------------------------- reference backend
     def _ref_layer(self, i: int, x: torch.Tensor, B: int, S: int, positions: torch.Tensor, lens: torch.Tensor,
@@ -716,16 +732,22 @@ class LlamaTP:
 
     @staticmethod
     def pick_token(cv: torch.Tensor, ci: torch.Tensor, gp: GenParams, step: int) -> int:
-        """One row's next token from its merged candidates -- the same rule (and the same seeded
-        generator per (seed, step)) as a batch-of-one :meth:`generate`."""
+        """One row's next token from its merged candidates -- the rule of the device pick kernel
+        (ops.decode_pick): greedy = the first maximum; sampled = the ``top_k`` largest (ties in
+        candidate order), softmax at ``temperature`` in fp32, the first cumulative weight above
+        ``sample_uniform(seed, step)`` of the total."""
         if gp.top_k <= 1:
             return int(ci[int(cv.argmax())])
-        k = min(gp.top_k, cv.shape[0])
-        tv, tpos = torch.topk(cv, k)
-        probs = torch.softmax(tv / max(gp.temperature, 1e-5), dim=-1).view(1, -1)
-        g = torch.Generator().manual_seed(gp.seed * 1000003 + step)
-        pick = int(torch.multinomial(probs, 1, generator=g)[0, 0])
-        return int(ci[int(tpos[pick])])
+        k = min(gp.top_k, cv.shape[0], 64)
+        v = cv.float()
+        order = torch.sort(v, descending=True, stable=True).indices[:k]
+        tv = v[order]
+        w = torch.exp((tv - tv[0]) / max(gp.temperature, 1e-5))
+        cdf = torch.cumsum(w, 0)
+        thr = torch.tensor(sample_uniform(gp.seed, step), dtype=torch.float32) * cdf[-1]
+        hit = (cdf > thr).nonzero()
+        pick = int(hit[0, 0]) if hit.numel() else k - 1
+        return int(ci[int(order[pick])])
 
     def ctx_bucket(self, max_ctx: Optional[int]) -> int:
         """Power-of-two context bound (>= 256, <= max_seq) a decode graph is captured for."""
@@ -807,6 +829,8 @@ class LlamaTP:
         ids = ids.to(dev)
         lens = lens.to(dev).to(torch.int32)
         k = max(1, min(gp.top_k, self.top_k_max))
+        if self._device_loop_ok(B, k):
+            return self._generate_device(ids, lens, gp, k)
         assigned = 0
         try:
             if self.pages is not None:  # batch row b = slot b, pages for the prompt + the generation budget
@@ -828,6 +852,149 @@ class LlamaTP:
             return torch.stack(out, dim=1)
         finally:
             if self.pages is not None:  # also on OutOfPages part-way: release exactly the rows assigned
+                for b in range(assigned):
+                    self.pages.release(b)
+
+    # ---------------------------------------------------------------- device-resident decode loop
+    def _gather_pad(self, k: int) -> int:
+        return (-2 * k) % 4  # [B, 2k + pad] fp32 rows: a 16-B multiple per row (one-shot all-gather)
+
+    def _device_loop_ok(self, B: int, k: int) -> bool:
+        """May generate() run the X4 merge + token pick inside the captured decode step?"""
+        if os.environ.get("MLS_DEVICE_PICK", "1") == "0":
+            return False
+        if not (self.backend == "fused" and self.device.type == "cuda" and self.use_graphs and self._graph_ok(B)):
+            return False
+        if self.tp * k > 512 or k > 64:
+            return False
+        if self.tp == 1 or getattr(self.comm, "graph_safe", False):
+            return True
+        car = getattr(self.comm, "car", None)
+        if car is not None:
+            return B * (2 * k + self._gather_pad(k)) * 4 <= car.cap
+        return self._rccl_graphs and not getattr(self.comm, "host_staged", False)
+
+    def _gather_dev(self, vals: torch.Tensor, idx: torch.Tensor):
+        """X4 on device: every rank's [B, k] candidates -> ([tp, B, k] f32, [tp, B, k] i32), one
+        collective (values and ids packed in one fp32 row); graph-capturable."""
+        if self.tp == 1:
+            return vals.unsqueeze(0), idx.unsqueeze(0)
+        B, k = vals.shape
+        pad = self._gather_pad(k)
+        parts = [vals.float(), idx.view(torch.float32)]
+        if pad:
+            parts.append(torch.zeros(B, pad, device=vals.device, dtype=torch.float32))
+        pack = torch.cat(parts, dim=1).contiguous()
+        car = getattr(self.comm, "car", None)
+        if car is not None and car.gather_eligible(pack):
+            with tracing.range("tp.all_gather"):
+                g = car.all_gather(pack)
+        elif getattr(self.comm, "graph_safe", False):
+            g = self.comm.all_gather(pack)
+        else:
+            g = torch.empty((self.tp, *pack.shape), device=pack.device, dtype=pack.dtype)
+            with tracing.range("tp.all_gather"):
+                dist.all_gather_into_tensor(g, pack, group=self.comm.group)
+        return g[..., :k].contiguous(), g[..., k: 2 * k].contiguous().view(torch.int32)
+
+    def _dev_buffers(self, B: int):
+        st = self._dev_state.get(B)
+        if st is None:
+            dev = self.device
+            z = lambda dt: torch.zeros(B, device=dev, dtype=dt)  # noqa: E731
+            st = (z(torch.int32), z(torch.int32), z(torch.int32), z(torch.int32),  # tok, pos, lens, step
+                  z(torch.int32), torch.ones(B, device=dev, dtype=torch.float32), z(torch.int64),  # topk, temp, seed
+                  torch.zeros(B, self.max_seq, device=dev, dtype=torch.int32))  # hist
+            self._dev_state[B] = st
+        return st
+
+    def _decode_graph_dev(self, B: int, k: int, ctx: int) -> torch.cuda.CUDAGraph:
+        """Captured decode step + X4 gather + on-device pick for batch B / context bound ctx: reads
+        tok / pos / lens of the shared per-B state and advances them for the next replay."""
+        key = (B, k, ctx)
+        g = self._dev_graphs.get(key)
+        if g is not None:
+            return g
+        dev = self.device
+        tok, pos, lens, step, topk, temp, seed, hist = self._dev_buffers(B)
+        # warm-up (kernel selection, workspaces) on scratch inputs at position ctx - 1: that cache row
+        # is either the one a replay under this bound writes anyway or a future row rewritten before
+        # it is read (see _decode_graph); the shared state is left alone
+        t_w = torch.zeros(B, 1, dtype=torch.int32, device=dev)
+        p_w = torch.full((B, 1), ctx - 1, dtype=torch.int32, device=dev)
+        l_w = torch.full((B,), ctx, dtype=torch.int32, device=dev)
+        self._dec_ctx = ctx
+        try:
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                for _ in range(2):
+                    v, i = self.step(t_w, p_w, l_w, decode=True, k=k)
+                    self._gather_dev(v, i)
+            torch.cuda.current_stream(dev).wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                v, i = self.step(tok.view(B, 1), pos.view(B, 1), lens, decode=True, k=k)
+                cv, ci = self._gather_dev(v, i)
+                self.ops.decode_pick(cv, ci, tok, pos, lens, step, topk=topk, temp=temp, seed=seed, hist=hist)
+        finally:
+            self._dec_ctx = None
+        self._dev_graphs[key] = g
+        return g
+
+    def check_comm_health(self) -> None:
+        """Collective (same decode step on every rank): did any one-shot collective lose a peer
+        since the last check?  On an error every rank resets the device protocol, drops the IPC
+        path (RCCL from now on) and its captured steps, and raises :class:`TPCommError`."""
+        car = getattr(self.comm, "car", None)
+        if self.tp == 1 or car is None:
+            return
+        err = car.errors()
+        backend = dist.get_backend(self.comm.group)
+        flag = torch.tensor([err], dtype=torch.int32, device=self.device if backend == "nccl" else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.comm.group)
+        if int(flag.item()):
+            car.reset()
+            self.comm.car = None
+            self._graphs.clear()
+            self._dev_graphs.clear()
+            raise TPCommError("a tensor-parallel peer missed a one-shot collective; falling back to RCCL")
+
+    def _generate_device(self, ids: torch.Tensor, lens: torch.Tensor, gp: GenParams, k: int) -> torch.Tensor:
+        """generate() with every decode step a graph replay that also merges the ranks' candidates
+        and picks the next token on device (X4 + P4): no host round trip until the end (and the
+        comm-health check every ``health_every`` steps)."""
+        B, S = ids.shape
+        dev = self.device
+        tok, pos, lens_s, step, topk, temp, seed, hist = self._dev_buffers(B)
+        step.zero_()
+        topk.fill_(int(gp.top_k))
+        temp.fill_(float(gp.temperature))
+        seed.fill_(int(gp.seed))
+        assigned = 0
+        try:
+            if self.pages is not None:
+                for b in range(B):
+                    self.pages.assign(b, S + gp.max_new_tokens)
+                    assigned = b + 1
+            posp = torch.arange(S, device=dev, dtype=torch.int32).unsqueeze(0).expand(B, S).contiguous()
+            vals, idx = self.step(ids, posp, lens, decode=False, k=k)
+            cv, ci = self._gather_dev(vals, idx)
+            pos.copy_(lens - 1)  # the pick advances them to (lens, lens + 1): the first decode position
+            lens_s.copy_(lens)
+            self.ops.decode_pick(cv, ci, tok, pos, lens_s, step, topk=topk, temp=temp, seed=seed, hist=hist)
+            for t in range(1, gp.max_new_tokens):
+                g = self._decode_graph_dev(B, k, self.ctx_bucket(S + t))
+                if self.pages is not None:
+                    self.pages.device_table()  # the graph reads the table buffer in place
+                with tracing.range("llama.decode"):
+                    g.replay()
+                if self.health_every > 0 and t % self.health_every == 0:
+                    self.check_comm_health()
+            self.check_comm_health()
+            return hist[:, : gp.max_new_tokens].cpu()
+        finally:
+            if self.pages is not None:
                 for b in range(assigned):
                     self.pages.release(b)
 

@@ -310,6 +310,47 @@ def gemm(
     return out
 
 
+GEMM_TILE_CFGS = {1: (256, 256), 2: (256, 128), 3: (128, 128), 4: (128, 128), 5: (128, 256), 6: (256, 256),
+                  7: (256, 128), 8: (256, 256), 9: (256, 128)}
+
+
+def gemm_tile(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, act=ACT_NONE,
+              residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None, cfg: int = 0,
+              grid_cap: int = 0) -> torch.Tensor:
+    """Large-M projection on the LDS-DMA MFMA tile kernel (csrc/gemm_tile.hip):
+    ``act(a @ w.T + bias) (+ residual)``; SiLU-mul for gate/up interleaved in groups of 8.
+    ``K % 64 == 0``, ``N % 16 == 0``; ``cfg`` selects the tile (:data:`GEMM_TILE_CFGS`, 0 = by shape)."""
+    dev = a.device
+    _need(a, "a", torch.bfloat16, dev)
+    _need(w, "w", torch.bfloat16, dev)
+    M, K = a.shape
+    N, K2 = w.shape
+    code = _act(act)
+    if K != K2 or K % 64 or N % 16:
+        raise ValueError(f"gemm_tile: K ({K} vs {K2}) % 64 == 0 and N ({N}) % 16 == 0")
+    if bias is not None:
+        _need(bias, "bias", torch.float32, dev)
+        if bias.numel() != N:
+            raise ValueError(f"bias must have {N} elements")
+    if residual is not None:
+        if code == ACT_SILU_MUL:
+            raise ValueError("silu_mul takes no residual")
+        _need(residual, "residual", torch.bfloat16, dev)
+        if tuple(residual.shape) != (M, N):
+            raise ValueError("residual must be [M, N]")
+    n_out = N // 2 if code == ACT_SILU_MUL else N
+    if out is None:
+        out = torch.empty(M, n_out, device=dev, dtype=torch.bfloat16)
+    else:
+        _need(out, "out", torch.bfloat16, dev)
+        if tuple(out.shape) != (M, n_out):
+            raise ValueError(f"out must be [M, {n_out}]")
+    rc = lib().mls_gemm_tile(a.data_ptr(), w.data_ptr(), _ptr(bias), _ptr(residual), out.data_ptr(), M, N, K, code,
+                             n_out, N, int(cfg), int(grid_cap), stream_ptr(dev))
+    check(rc, "mls_gemm_tile")
+    return out
+
+
 _TUNED_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned")
 def load_blas_tuning(path: Optional[str] = None) -> bool:
     """Make hipBLASLt use the solutions PyTorch TunableOp measured fastest on MI355X for the shapes
@@ -985,6 +1026,48 @@ def skinny_packed_combine(attn_out: torch.Tensor, parts: DecodePartials, wp: tor
                                          M, N, K, ACT_NONE, int(variant), stream_ptr(dev))
     check(rc, "mls_skinny_packed_combine")
     return out
+
+
+def decode_pick(cand_v: torch.Tensor, cand_i: torch.Tensor, tok: torch.Tensor, pos: torch.Tensor, lens: torch.Tensor,
+                step: torch.Tensor, *, topk: Optional[torch.Tensor] = None, temp: Optional[torch.Tensor] = None,
+                seed: Optional[torch.Tensor] = None, hist: Optional[torch.Tensor] = None) -> None:
+    """X4 merge + next-token pick on device (csrc/decode_pick.hip): ``cand_v`` / ``cand_i`` are the
+    all-gathered ``[tp, B, k]`` candidates; per row picks greedily (``topk[b] <= 1``) or samples
+    (top-k, temperature, counter-based ``seed`` x step draw -- :func:`models.llama.sample_uniform`),
+    then advances ``tok`` / ``pos`` / ``lens`` / ``step`` ``[B]`` in place and records the token in
+    ``hist[b, step[b]]``.  Capturable (the TP decode graph ends with it)."""
+    dev = cand_v.device
+    tp, B, k = cand_v.shape
+    _need(cand_v, "cand_v", torch.float32, dev)
+    _need(cand_i, "cand_i", torch.int32, dev)
+    if tuple(cand_i.shape) != (tp, B, k) or tp * k > 512:
+        raise ValueError("cand_i must match cand_v [tp, B, k] with tp * k <= 512")
+    for name, t, dt in (("tok", tok, torch.int32), ("pos", pos, torch.int32), ("lens", lens, torch.int32),
+                        ("step", step, torch.int32)):
+        _need(t, name, dt, dev)
+        if t.numel() != B:
+            raise ValueError(f"{name} must have {B} elements")
+    for name, t, dt in (("topk", topk, torch.int32), ("temp", temp, torch.float32), ("seed", seed, torch.int64)):
+        if t is not None:
+            _need(t, name, dt, dev)
+            if t.numel() != B:
+                raise ValueError(f"{name} must have {B} elements")
+    cols = 0
+    if hist is not None:
+        _need(hist, "hist", torch.int32, dev)
+        if hist.shape[0] != B:
+            raise ValueError("hist must be [B, cols]")
+        cols = hist.shape[1]
+    rc = lib().mls_decode_pick(cand_v.data_ptr(), cand_i.data_ptr(), tp, B, k, _ptr(topk), _ptr(temp), _ptr(seed),
+                               tok.data_ptr(), pos.data_ptr(), lens.data_ptr(), _ptr(hist), cols, step.data_ptr(),
+                               stream_ptr(dev))
+    check(rc, "mls_decode_pick")
+
+
+def gpu_sleep(us: int, device=None) -> None:
+    """Hold the current stream of ``device`` for ``us`` microseconds (fault injection in tests)."""
+    dev = torch.device(device if device is not None else "cuda")
+    check(lib().mls_gpu_sleep(int(us), stream_ptr(dev)), "mls_gpu_sleep")
 
 
 def topk_large(x: torch.Tensor, k: int, max_chunk: int = 16384, *, lo: int = 0,

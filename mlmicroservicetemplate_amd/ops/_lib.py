@@ -37,6 +37,8 @@ _SIGS = {
     "mls_conv_chain": [P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, P],
     "mls_gemm": [P, P, P, P, P, P, P, SZ, I, I, I, I, I, I, P],
     "mls_gemm_heuristic": [I, I, I, _c.POINTER(I), _c.POINTER(I)],
+    "mls_gemm_tile": [P, P, P, P, P, I, I, I, I, I, I, I, I, P],
+    "mls_gemm_tile_pick": [I, I],
     "mls_gemm_num_cfgs": [],
     "mls_normalize_u8": [P, P, I, I, I, I, FP, FP, P],
     "mls_maxpool2d": [P, P, I, I, I, I, I, I, I, P],
@@ -62,6 +64,10 @@ _SIGS = {
     "mls_ar_open": [P, P],
     "mls_ar_allreduce": [P, P, P, L, _c.c_longlong, P],
     "mls_ar_error": [P, P],
+    "mls_ar_allgather": [P, P, P, L, _c.c_longlong, P],
+    "mls_ar_reset": [P],
+    "mls_gpu_sleep": [L, P],
+    "mls_decode_pick": [P, P, I, I, I, P, P, P, P, P, P, P, I, P, P],
     "mls_ar_destroy": [P],
     "mls_rope_kv": [P, P, P, P, L, I, I, I, I, P, P, P, P, I, I, L, I, I, P],
     "mls_kv_append": [P, I, I, I, P, P, P, L, I, I, I, P],

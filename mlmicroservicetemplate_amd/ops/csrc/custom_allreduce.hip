@@ -125,6 +125,60 @@ __global__ __launch_bounds__(AR_THREADS) void oneshot_allreduce_kernel(const ArA
   }
 }
 
+// X4: one-shot all-gather of `nbytes` per rank (the decode step's top-k candidates, a few KB):
+// the same stage -> publish -> wait -> read protocol and per-block epochs as the all-reduce (every
+// rank issues the same sequence of calls, so block b's epoch advances identically everywhere), but
+// chunk b of every rank is copied to out[src] instead of summed.
+__global__ __launch_bounds__(AR_THREADS) void oneshot_allgather_kernel(const ArArgs a, const char* in, char* out,
+                                                                        long nbytes) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  __shared__ int s_epoch, s_ok;
+  if (tid == 0) {
+    s_epoch = a.epochs[b] + 1;
+    s_ok = 1;
+  }
+  __syncthreads();
+  const int e = s_epoch;
+  const int parity = e & 1;
+  const long off = (long)b * AR_THREADS * 16 + tid * 16;
+  const bool mine = off < nbytes;  // nbytes % 16 == 0 (host-checked)
+  if (tid < a.world && e > 2) {
+    if (!ar_wait_ge(ar_done(a.bufs[a.rank], a.cap, a.max_blocks, tid, b), e - 2, a.timeout)) s_ok = 0;
+  }
+  __syncthreads();
+  char* stage = a.bufs[a.rank] + parity * a.cap;
+  if (mine) st16(stage + off, ld16(in + off));
+  __threadfence_system();
+  __syncthreads();
+  if (tid < a.world)
+    __hip_atomic_store(ar_ready(a.bufs[tid], a.cap, a.max_blocks, a.rank, b), e, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  if (tid < a.world) {
+    if (!ar_wait_ge(ar_ready(a.bufs[a.rank], a.cap, a.max_blocks, tid, b), e, a.timeout)) s_ok = 0;
+  }
+  __syncthreads();
+  if (mine) {
+    for (int r = 0; r < a.world; ++r) {
+      const int src = (a.rank + r) % a.world;
+      st16(out + (long)src * nbytes + off, load_sys16(a.bufs[src] + parity * a.cap + off));
+    }
+  }
+  __syncthreads();
+  if (tid < a.world)
+    __hip_atomic_store(ar_done(a.bufs[tid], a.cap, a.max_blocks, a.rank, b), e, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  if (tid == 0) {
+    a.epochs[b] = e;
+    if (!s_ok) atomicOr(a.err, 1);
+  }
+}
+
+// fault injection for tests: hold the stream for `us` microseconds (bounded: <= 10 s)
+__global__ void gpu_sleep_kernel(long long ticks) {
+  const long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+
 }  // namespace
 
 extern "C" {
@@ -200,6 +254,48 @@ int mls_ar_allreduce(void* ctx, const void* in, void* out, long n, long long tim
   a.timeout = timeout > 0 ? timeout : (1LL << 24);
   const int blocks = (int)((n + AR_ELEMS_PER_BLOCK - 1) / AR_ELEMS_PER_BLOCK);
   hipLaunchKernelGGL(oneshot_allreduce_kernel, dim3(blocks), dim3(AR_THREADS), 0, (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}
+
+// X4: out[world][nbytes] = every rank's `in` (nbytes % 16 == 0, nbytes <= cap, out != in)
+int mls_ar_allgather(void* ctx, const void* in, void* out, long nbytes, long long timeout, void* stream) {
+  ArCtx* c = (ArCtx*)ctx;
+  if (!c->opened && c->world > 1) return MLS_BAD_ARG;
+  if (nbytes <= 0 || nbytes % 16 || (size_t)nbytes > c->cap) return MLS_BAD_ARG;
+  ArArgs a{};
+  a.rank = c->rank;
+  a.world = c->world;
+  a.max_blocks = c->max_blocks;
+  a.cap = c->cap;
+  for (int r = 0; r < AR_MAX_RANKS; ++r) a.bufs[r] = c->peers[r];
+  a.epochs = c->epochs;
+  a.err = c->err;
+  a.timeout = timeout > 0 ? timeout : (1LL << 24);
+  const int blocks = (int)((nbytes + AR_THREADS * 16 - 1) / (AR_THREADS * 16));
+  if (blocks > c->max_blocks) return MLS_BAD_ARG;
+  hipLaunchKernelGGL(oneshot_allgather_kernel, dim3(blocks), dim3(AR_THREADS), 0, (hipStream_t)stream, a,
+                     (const char*)in, (char*)out, nbytes);
+  return (int)hipGetLastError();
+}
+
+// After a peer-wait timeout the per-block epochs of the ranks may disagree: every rank calls this
+// between two process-group barriers (no kernel of the group in flight) to restart the protocol.
+int mls_ar_reset(void* ctx) {
+  ArCtx* c = (ArCtx*)ctx;
+  if (hipDeviceSynchronize() != hipSuccess) return MLS_UNSUPPORTED;
+  const size_t flags = (size_t)2 * AR_MAX_RANKS * c->max_blocks * sizeof(int);
+  const size_t bytes = flags + (size_t)c->max_blocks * sizeof(int) + 64;
+  if (hipMemset(c->local + 2 * c->cap, 0, bytes) != hipSuccess) return MLS_UNSUPPORTED;
+  return (int)hipDeviceSynchronize();
+}
+
+int mls_gpu_sleep(long us, void* stream) {
+  if (us < 0 || us > 10000000) return MLS_BAD_ARG;
+  int dev = 0, khz = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) !=
+      hipSuccess || khz <= 0)
+    khz = 100000;  // the gfx9 constant clock: 100 MHz
+  hipLaunchKernelGGL(gpu_sleep_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (long long)us * khz / 1000);
   return (int)hipGetLastError();
 }
 

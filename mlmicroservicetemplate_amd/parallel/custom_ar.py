@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import ctypes
 import logging
+import os
 from typing import Optional
 
 import torch
@@ -28,7 +29,7 @@ logger = logging.getLogger("mlsamd.custom_ar")
 
 class CustomAllReduce:
     def __init__(self, group=None, device=None, cap_bytes: int = 1 << 20, self_test: bool = True,
-                 timeout_iters: int = 1 << 24):
+                 timeout_iters: Optional[int] = None):
         from ..ops import _lib
 
         self.group = group
@@ -39,7 +40,9 @@ class CustomAllReduce:
             dev = torch.device("cuda", torch.cuda.current_device())
         self.device = dev
         self.cap = int(cap_bytes)
-        self.timeout = int(timeout_iters)
+        # peer-wait bound in spin iterations (~1 s by default); MLS_AR_TIMEOUT_ITERS shrinks it (tests)
+        self.timeout = int(timeout_iters if timeout_iters is not None
+                           else os.environ.get("MLS_AR_TIMEOUT_ITERS", str(1 << 24)))
         self.enabled = False
         self.reason = ""
         self._lib = _lib.lib()
@@ -104,6 +107,38 @@ class CustomAllReduce:
                                         torch.cuda.current_stream(self.device).cuda_stream)
         if rc != 0:
             raise RuntimeError(f"mls_ar_allreduce failed ({rc})")
+        return out
+
+    def errors(self) -> int:
+        """Read (and clear) the peer-wait timeout word: non-zero = some one-shot collective since the
+        last read completed with a peer missing (its output is partial).  A host sync."""
+        return self._errors() if self.enabled or self._ctx else 0
+
+    def reset(self) -> None:
+        """Restart the device protocol after a timeout (per-block epochs may disagree between ranks):
+        collective -- every rank calls it; process-group barriers on both sides guarantee no
+        one-shot kernel of the group is in flight while the flags are cleared."""
+        from . import dist as mdist
+
+        mdist.barrier(self.group)
+        rc = self._lib.mls_ar_reset(self._ctx)
+        if rc != 0:
+            raise RuntimeError(f"mls_ar_reset failed ({rc})")
+        mdist.barrier(self.group)
+
+    def gather_eligible(self, t: torch.Tensor) -> bool:
+        nbytes = t.numel() * t.element_size()
+        return self.enabled and t.is_contiguous() and t.device == self.device and nbytes % 16 == 0 and nbytes <= self.cap
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        """X4 one-shot all-gather: ``[world, *t.shape]`` of every rank's ``t`` (graph-safe)."""
+        if not self.gather_eligible(t):
+            raise ValueError("tensor not eligible for the one-shot all-gather")
+        out = torch.empty((self.world, *t.shape), dtype=t.dtype, device=t.device)
+        rc = self._lib.mls_ar_allgather(self._ctx, t.data_ptr(), out.data_ptr(), t.numel() * t.element_size(),
+                                        self.timeout, torch.cuda.current_stream(self.device).cuda_stream)
+        if rc != 0:
+            raise RuntimeError(f"mls_ar_allgather failed ({rc})")
         return out
 
     def eligible(self, t: torch.Tensor) -> bool:

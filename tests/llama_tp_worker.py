@@ -24,11 +24,39 @@ def main():
     vals, idx = m.step(ids.cuda(), pos, lens.cuda(), decode=False, k=8)
     allv = m.comm.all_gather(vals)
     alli = m.comm.all_gather(idx)
-    out = m.generate(ids, lens, GenParams(max_new_tokens=8))
-    info = torch.tensor([int(m.use_graphs), int(m.comm.car is not None), len(m._graphs)])
+    failed = ""
+    stall_rank = int(os.environ.get("STALL_RANK", "-1"))
+    if stall_rank >= 0:
+        # fault injection: one rank's stream stalls past the peers' one-shot wait bound; every rank
+        # must fail the request (TPCommError), not return tokens computed from partial sums
+        from mlmicroservicetemplate_amd import ops
+        from mlmicroservicetemplate_amd.models.llama import TPCommError
+
+        if rank == stall_rank:
+            ops.gpu_sleep(int(os.environ.get("STALL_US", "300000")))
+        try:
+            m.generate(ids, lens, GenParams(max_new_tokens=8))
+        except TPCommError as e:
+            failed = type(e).__name__
+    # count host round trips of the decode loop (.cpu() on device tensors)
+    calls = []
+    orig = torch.Tensor.cpu
+
+    def counting_cpu(self, *a, **kw):
+        if self.is_cuda:
+            calls.append(tuple(self.shape))
+        return orig(self, *a, **kw)
+
+    torch.Tensor.cpu = counting_cpu
+    try:
+        out = m.generate(ids, lens, GenParams(max_new_tokens=8))
+    finally:
+        torch.Tensor.cpu = orig
+    info = torch.tensor([int(m.use_graphs), int(m.comm.car is not None), len(m._graphs) + len(m._dev_graphs),
+                         len(calls)])
     if m.comm.car is not None:
-        info[1] += 10 * m.comm.car._errors()  # peer-wait timeouts would show here
-    torch.save({"tokens": out.cpu(), "vals": allv.cpu(), "idx": alli.cpu(), "info": info},
+        info[1] += 10 * m.comm.car.errors()  # peer-wait timeouts would show here
+    torch.save({"tokens": out.cpu(), "vals": allv.cpu(), "idx": alli.cpu(), "info": info, "failed": failed},
                os.environ["OUT"] + f".{rank}.pt")
     dist.destroy_process_group()
 

@@ -31,10 +31,16 @@ CASES = {
     2: (dict(layers=2, hidden=512, heads=8, kv_heads=2, head_dim=128, intermediate=1024), {"MLS_CUSTOM_AR": "0"}),
     8: (dict(layers=2, hidden=512, heads=32, kv_heads=8, head_dim=128, intermediate=2048),
         {"MLS_CUSTOM_AR": "1", "GPU_MAX_HW_QUEUES": "1"}),
+    # fault injection: rank 1 stalls 300 ms with the peer-wait bound at ~a few ms -> every rank's
+    # request fails with TPCommError; the next request runs on the RCCL / group fallback
+    "stall": (dict(layers=2, hidden=512, heads=8, kv_heads=2, head_dim=128, intermediate=1024),
+              {"MLS_CUSTOM_AR": "1", "GPU_MAX_HW_QUEUES": "1", "STALL_RANK": "1", "STALL_US": "300000",
+               "MLS_AR_TIMEOUT_ITERS": "20000"}),
 }
+WORLD = {2: 2, 8: 8, "stall": 2}
 
 
-@pytest.mark.parametrize("world", [2, 8])
+@pytest.mark.parametrize("world", [2, 8, "stall"])
 def test_fused_tp_matches_tp1(tmp_path, world):
     from mlmicroservicetemplate_amd.models.llama import GenParams, LlamaTP, init_llama_shard, tiny_config
 
@@ -52,6 +58,7 @@ def test_fused_tp_matches_tp1(tmp_path, world):
     port = _port()
     out = str(tmp_path / "tok")
     procs = []
+    case, world = world, WORLD[world]
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                    OUT=out, TP_CFG=json.dumps(cfg_kw), PYTHONPATH=os.pathsep.join([root, os.environ.get("PYTHONPATH", "")]),
@@ -81,7 +88,12 @@ def test_fused_tp_matches_tp1(tmp_path, world):
         # the greedy continuations agree (a near-tie may flip late tokens)
         agree = (d["tokens"] == want).float().mean().item()
         assert agree >= 0.6, (r, d["tokens"], want)
-        if extra_env.get("MLS_CUSTOM_AR") == "1":
-            use_graphs, car, graphs = d["info"].tolist()
+        use_graphs, car, graphs, host_trips = d["info"].tolist()
+        if case == "stall":
+            assert d["failed"] == "TPCommError", f"rank {r}: the stalled generation did not fail ({d['failed']!r})"
+            assert car == 0, f"rank {r}: the IPC path must be dropped after a peer timeout"
+        elif extra_env.get("MLS_CUSTOM_AR") == "1":
             assert car == 1, f"rank {r}: IPC all-reduce disabled or a peer wait timed out ({car})"
             assert use_graphs == 1 and graphs >= 1, f"rank {r}: decode steps were not captured ({d['info']})"
+            # X4 on device: the whole decode loop is graph replays; the one host copy is the result
+            assert host_trips == 1, f"rank {r}: {host_trips} host round trips in generate()"

@@ -1,0 +1,82 @@
+"""Large-M GEMM probe: ops.gemm_tile (csrc/gemm_tile.hip) per tile cfg vs torch.matmul (hipBLASLt)
+on the BERT / Llama prefill projection shapes -- numerics (vs fp32) and graph-timed throughput,
+alone (c1) and with 4 independent copies co-running on their own streams (c4, how the serving
+engine runs them).  One JSON line per (shape, impl, concurrency).  Random [-1, 1)-scale operands
+(never zero-filled: cdna_hip_programming.md §5.4 rule 25)."""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+SHAPES = {  # name: (M, N, K, act)
+    "bert32_qkv": (4096, 2304, 768, "none"), "bert32_o": (4096, 768, 768, "none"),
+    "bert32_ffn1": (4096, 3072, 768, "gelu"), "bert32_ffn2": (4096, 768, 3072, "none"),
+    "bert128_qkv": (16384, 2304, 768, "none"), "bert128_o": (16384, 768, 768, "none"),
+    "bert128_ffn1": (16384, 3072, 768, "gelu"), "bert128_ffn2": (16384, 768, 3072, "none"),
+    "llama_qkv": (4096, 6144, 4096, "none"), "llama_o": (4096, 4096, 4096, "none"),
+    "llama_gateup": (4096, 28672, 4096, "silu_mul"), "llama_down": (4096, 4096, 14336, "none"),
+    "llama16k_gateup": (16384, 28672, 4096, "silu_mul"), "sq8k": (8192, 8192, 8192, "none"),
+    "tp8_qkv": (16384, 768, 4096, "none"), "tp8_gateup": (16384, 3584, 4096, "silu_mul"),
+    "tp8_down": (16384, 4096, 1792, "none"), "tp8_o": (16384, 4096, 512, "none"),
+}
+
+
+def main():
+    from mlmicroservicetemplate_amd import ops
+    from mlmicroservicetemplate_amd.ops.autotune import _time_multi
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shapes", nargs="*", default=list(SHAPES))
+    ap.add_argument("--cfgs", type=int, nargs="*", default=[0, 1, 2, 3, 4, 5])
+    ap.add_argument("--conc", type=int, nargs="*", default=[1, 4])
+    ap.add_argument("--iters", type=int, default=10)
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    for name in a.shapes:
+        M, N, K, act = SHAPES[name]
+        code = {"none": ops.ACT_NONE, "gelu": ops.ACT_GELU, "silu_mul": ops.ACT_SILU_MUL}[act]
+        xs = [(torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16) for _ in range(max(a.conc))]
+        w = ((torch.rand(N, K, device=dev) * 2 - 1) / K ** 0.5).to(torch.bfloat16)
+        bias = torch.randn(N, device=dev) * 0.1
+        flop = 2.0 * M * N * K
+        # fp32 reference on a row slice (the full fp32 product of the big shapes is slow)
+        rows = slice(0, min(M, 1024))
+        ref = xs[0][rows].float() @ w.float().T + bias
+        if code == ops.ACT_GELU:
+            ref = torch.nn.functional.gelu(ref)
+        elif code == ops.ACT_SILU_MUL:
+            g, u = ref.view(ref.shape[0], N // 16, 2, 8).unbind(2)
+            ref = (torch.nn.functional.silu(g) * u).reshape(ref.shape[0], N // 2)
+
+        def blas(x):
+            if code == ops.ACT_GELU:
+                return torch._addmm_activation(bias.to(torch.bfloat16), x, w.t(), use_gelu=True)
+            y = torch.addmm(bias.to(torch.bfloat16), x, w.t())
+            return ops.silu_mul_interleaved(y) if code == ops.ACT_SILU_MUL else y
+
+        impls = [("hipblaslt", blas, None)]
+        for cfg in a.cfgs:
+            impls.append((f"tile{cfg}", (lambda x, c=cfg: ops.gemm_tile(x, w, bias, act=code, cfg=c)), cfg))
+        for impl, fn, cfg in impls:
+            try:
+                y = fn(xs[0])
+                torch.cuda.synchronize()
+            except Exception as e:
+                print(json.dumps({"shape": name, "impl": impl, "error": str(e)[:200]}), flush=True)
+                continue
+            err = ((y[rows].float() - ref).abs().max() / ref.abs().max()).item()
+            for c in a.conc:
+                t = _time_multi([lambda i=i: fn(xs[i]) for i in range(c)], iters=a.iters) * 1e-3
+                print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "act": act, "impl": impl, "conc": c,
+                                  "us": round(t * 1e6, 1), "tflops": round(flop / t / 1e12, 1),
+                                  "rel_err": round(err, 5),
+                                  "pick": ops.lib().mls_gemm_tile_pick(M, N) if cfg == 0 else cfg}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
