@@ -155,6 +155,9 @@ class Settings:
     WEIGHTS_DIR: str = ""  # POST /admin/reload may only load safetensors under this directory ("" = seed reloads only)
     IMAGE_DIR: str = "src/images"  # legacy /predict?filename= flow (old-rev main.pyc@L119-152)
     TOPK: int = 5
+    # image models: uploads become GPU image containers -- baseline JPEGs Huffman-decoded on the host
+    # (C++), IDCT / colour / resize on the GPU inside the serving graph (ops.image_decode)
+    GPU_IMAGE_DECODE: bool = True
     # --- GPU execution ---
     GPUS: int = 1
     WORKERS_PER_GPU: int = 1  # HTTP worker processes per GPU (DP models): front-end CPU scales, each owns an engine

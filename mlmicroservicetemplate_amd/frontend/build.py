@@ -107,7 +107,8 @@ def staging_current() -> bool:
 
 def build(force: bool = False, verbose: bool = False):
     ext_flags = _ext_flags()
-    ext = _build_one(os.path.join(CSRC, "httpfront.cpp"), ext_path(), ext_flags, verbose, force)
+    ext = _build_one(os.path.join(CSRC, "httpfront.cpp"), ext_path(), ext_flags, verbose, force,
+                     deps=(os.path.join(CSRC, "jpeg_coefs.h"),))
     lg = _build_one(os.path.join(CSRC, "loadgen.cpp"), loadgen_path(), CXXFLAGS, verbose, force)
     stg = _build_one(os.path.join(ENGINE_CSRC, "staging.cpp"), staging_path(), ext_flags + ["-O3"], verbose, force,
                      deps=(os.path.join(ENGINE_CSRC, "staging_core.h"),))

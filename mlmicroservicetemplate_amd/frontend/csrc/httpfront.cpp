@@ -47,6 +47,8 @@
 #include <utility>
 #include <vector>
 
+#include "jpeg_coefs.h"
+
 namespace py = pybind11;
 using Clock = std::chrono::steady_clock;
 
@@ -364,6 +366,9 @@ class Server {
     std::vector<std::string> cors_origins;
     double request_timeout_s = 30.0;
     bool python_decode = true;
+    // samples are GPU image containers (jpeg_coefs.h): raw RGB uploads are wrapped, baseline JPEGs
+    // Huffman-decoded here on the I/O thread; anything else goes to the Python decode threads
+    bool image_container = false;
   };
 
   explicit Server(Config c) : cfg_(std::move(c)) {}
@@ -624,6 +629,7 @@ class Server {
     s["rejected_overload"] = n_overload_;
     s["python_routed"] = n_python_;
     s["decode_routed"] = n_decode_;
+    s["jpeg_native"] = n_jpeg_native_;
     s["text_hashed"] = n_text_hash_;
     s["connections_open"] = n_conns_;
     {
@@ -662,6 +668,7 @@ class Server {
   std::atomic<uint64_t> next_id_{1};
   std::atomic<uint64_t> next_conn_{2};  // 0 = listen socket, 1 = eventfd
 
+  std::atomic<long long> n_jpeg_native_{0};
   std::atomic<long long> n_requests_{0}, n_batches_{0}, n_samples_{0}, n_overload_{0}, n_python_{0}, n_decode_{0}, n_text_hash_{0},
       n_conns_{0};
   std::mutex cmu_;
@@ -1123,7 +1130,27 @@ class Server {
       immediate(c, 503, NOT_READY_BODY, ref.keep_alive, cors);
       return;
     }
-    if (cfg_.raw_samples && cfg_.sample_bytes > 0 && (long long)payload.size() == cfg_.sample_bytes &&
+    if (cfg_.image_container) {
+      Pending p;
+      p.body.assign(mlsjpeg::CONTAINER_BYTES, '\0');
+      uint8_t* dst = reinterpret_cast<uint8_t*>(&p.body[0]);
+      bool ok = false;
+      if (payload.size() == mlsjpeg::PAYLOAD_BYTES && raw_content_type(pctype)) {
+        mlsjpeg::raw_container(reinterpret_cast<const uint8_t*>(payload.data()), dst);
+        ok = true;
+      } else if (payload.size() > 2 && (uint8_t)payload[0] == 0xFF && (uint8_t)payload[1] == 0xD8) {
+        ok = mlsjpeg::jpeg_to_container(reinterpret_cast<const uint8_t*>(payload.data()), payload.size(), dst);
+        if (ok) n_jpeg_native_++;
+      }
+      if (ok) {
+        p.ref = std::move(ref);
+        p.off = 0;
+        c.waiting = true;
+        enqueue_sample(std::move(p));
+        return;
+      }
+      // not raw, not a baseline JPEG this decoder takes: the Python (PIL) decode threads below
+    } else if (cfg_.raw_samples && cfg_.sample_bytes > 0 && (long long)payload.size() == cfg_.sample_bytes &&
         raw_content_type(pctype)) {
       Pending p;
       p.ref = std::move(ref);
@@ -1173,6 +1200,30 @@ py::bytes as_bytes(const std::string& s) { return py::bytes(s.data(), s.size());
 
 PYBIND11_MODULE(_httpfront, m) {
   m.doc() = "Native HTTP/1.1 front end: epoll I/O threads, multipart parsing, C++ dynamic batching";
+  m.def("jpeg_container",
+        [](py::bytes data) -> py::object {
+          std::string in = data;
+          std::string out(mlsjpeg::CONTAINER_BYTES, '\0');
+          std::string why;
+          bool ok;
+          {
+            py::gil_scoped_release rel;
+            ok = mlsjpeg::jpeg_to_container(reinterpret_cast<const uint8_t*>(in.data()), in.size(),
+                                            reinterpret_cast<uint8_t*>(&out[0]), &why);
+          }
+          if (!ok) return py::str(why);
+          return py::bytes(out);
+        },
+        "JPEG bytes -> GPU image container (bytes), or the reason (str) it is not handled");
+  m.def("raw_container",
+        [](py::bytes rgb) -> py::bytes {
+          std::string in = rgb;
+          if (in.size() != mlsjpeg::PAYLOAD_BYTES) throw std::invalid_argument("raw image must be 224 x 224 x 3 bytes");
+          std::string out(mlsjpeg::CONTAINER_BYTES, '\0');
+          mlsjpeg::raw_container(reinterpret_cast<const uint8_t*>(in.data()), reinterpret_cast<uint8_t*>(&out[0]));
+          return py::bytes(out);
+        });
+  m.attr("CONTAINER_BYTES") = (long long)mlsjpeg::CONTAINER_BYTES;
   m.def("hash_tokenize",
         [](std::string text, int vocab, int max_len, int seq) -> py::object {
           std::vector<int32_t> ids;
@@ -1185,7 +1236,7 @@ PYBIND11_MODULE(_httpfront, m) {
       .def(py::init([](std::string host, int port, int listen_fd, int io_threads, long long sample_bytes,
                        int max_batch, int max_wait_us, int max_queue, long long max_upload, std::string form_field,
                        std::vector<std::string> cors_origins, double request_timeout_s, bool python_decode,
-                       bool raw_samples, std::vector<int> text_hash) {
+                       bool raw_samples, std::vector<int> text_hash, bool image_container) {
              Server::Config c;
              c.host = std::move(host);
              c.port = port;
@@ -1201,6 +1252,9 @@ PYBIND11_MODULE(_httpfront, m) {
              c.request_timeout_s = request_timeout_s;
              c.python_decode = python_decode;
              c.raw_samples = raw_samples;
+             c.image_container = image_container;
+             if (image_container && c.sample_bytes != (long long)mlsjpeg::CONTAINER_BYTES)
+               throw std::invalid_argument("image_container needs sample_bytes == CONTAINER_BYTES");
              if (text_hash.size() == 5) {  // vocab, max_len, seq, cls, sep
                c.text_hash = TextHash{text_hash[0], text_hash[1], text_hash[2], text_hash[3], text_hash[4]};
                if (c.text_hash.vocab <= 1000 || c.text_hash.seq <= 0 || c.text_hash.max_len < 2 ||
@@ -1214,7 +1268,7 @@ PYBIND11_MODULE(_httpfront, m) {
            py::arg("max_queue") = 4096, py::arg("max_upload") = 32 << 20, py::arg("form_field") = "image_file",
            py::arg("cors_origins") = std::vector<std::string>{}, py::arg("request_timeout_s") = 30.0,
            py::arg("python_decode") = true, py::arg("raw_samples") = true,
-           py::arg("text_hash") = std::vector<int>{})
+           py::arg("text_hash") = std::vector<int>{}, py::arg("image_container") = false)
       .def("start", &Server::start, py::call_guard<py::gil_scoped_release>())
       .def("stop", &Server::stop, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("port", &Server::port)

@@ -154,7 +154,8 @@ class NativeService:
             max_queue=int(settings.MAX_QUEUE), max_upload=int(settings.MAX_UPLOAD_BYTES),
             form_field=plugin.form_field, cors_origins=list(settings.CORS_ORIGINS),
             request_timeout_s=float(settings.REQUEST_TIMEOUT_S), python_decode=True,
-            raw_samples=bool(spec.get("raw_samples", True)), text_hash=list(spec.get("text_hash", [])))
+            raw_samples=bool(spec.get("raw_samples", True)), text_hash=list(spec.get("text_hash", [])),
+            image_container=bool(spec.get("image_container", False)))
         self.replicas: List[Any] = []
         self.reloader = None  # parallel.reload.ReloadCoordinator, after init
         self._stop = threading.Event()

@@ -232,7 +232,6 @@ class BertEager:
     __call__ = forward
 
 
-NATIVE_MIN_M = int(os.environ.get("MLS_BERT_NATIVE_MIN_M", "2048"))
 
 
 class BertFused:
@@ -262,17 +261,6 @@ class BertFused:
         cb[:C] = self.w["cls.b"]
         self.cls_w, self.cls_b = cw, cb
         self._ws = ops.StreamWorkspace(16 << 20, self.device)  # per stream: concurrent engine slots
-        if self.device.type == "cuda":
-            ops.load_blas_tuning()  # TunableOp-measured hipBLASLt solutions (FFN-up)
-        # MLS_BERT_NATIVE_GEMM=1: from NATIVE_MIN_M tokens the four projections run on the native
-        # MFMA GEMM with explicit tile configs (bias / GELU / residual in the epilogue).  Four
-        # co-running copies of ONE shape favour them (4096 tokens: QKV 593 vs 545 TFLOP/s, o 306 vs
-        # 183, FFN-up 801 vs 751, FFN-down 1033 vs 742; profiles/r2_gemm256_probe_c1_c4.jsonl), but
-        # in the engine -- batches co-running at different layers -- the whole model is slower
-        # (1.28-1.29 vs 1.10-1.11 ms per batch, profiles/r2_bert_native_gemm_ab.jsonl), so the
-        # library path stays the default.
-        self.native_gemm = os.environ.get("MLS_BERT_NATIVE_GEMM", "0") == "1"
-        self.native_cfg = {"qkv": 31, "o": 12, "ffn1": 12, "ffn2": 12}
 
     def forward(self, ids: torch.Tensor, type_ids: Optional[torch.Tensor], lens: torch.Tensor) -> torch.Tensor:
         """ids/type_ids int32 ``[B, S]``, lens int32 ``[B]`` -> bf16 logits ``[B, Cpad]``."""
@@ -284,38 +272,16 @@ class BertFused:
         x = ops.embed_layernorm(ids_f, tt_f, w["emb.word"], w["emb.pos"], w["emb.type"], w["emb.ln.g"], w["emb.ln.b"],
                                 S, eps=cfg.eps)
         ws = self._ws.get()
-        native = self.native_gemm and B * S >= NATIVE_MIN_M
-        nc = self.native_cfg
         for i in range(cfg.layers):
-            if native:  # tuned native tiles, epilogues fused (module docstring of this block in __init__)
-                qkv = ops.gemm(x, w[f"l{i}.qkv.w"], w[f"l{i}.qkv.b"], workspace=ws, cfg=nc["qkv"], splitk=1)
-                a = ops.flash_attention(qkv, B, S, cfg.heads, cfg.heads, cfg.head_dim, kv_lens=lens)
-                h = ops.gemm(a, w[f"l{i}.o.w"], w[f"l{i}.o.b"], residual=x, workspace=ws, cfg=nc["o"], splitk=1)
-                x = ops.layernorm(h, w[f"l{i}.ln1.g"], w[f"l{i}.ln1.b"], eps=cfg.eps)
-                f1 = ops.gemm(x, w[f"l{i}.ffn1.w"], w[f"l{i}.ffn1.b"], act=ops.ACT_GELU, workspace=ws,
-                              cfg=nc["ffn1"], splitk=1)
-                h = ops.gemm(f1, w[f"l{i}.ffn2.w"], w[f"l{i}.ffn2.b"], residual=x, workspace=ws, cfg=nc["ffn2"],
-                             splitk=1)
-                x = ops.layernorm(h, w[f"l{i}.ln2.g"], w[f"l{i}.ln2.b"], eps=cfg.eps)
-                continue
-            # large token counts: library GEMMs with the residual folded into the LayerNorm;
-            # small ones: native GEMMs with the residual in the epilogue
-            blas = B * S >= ops.BLAS_MIN_M
+            # all four projections native (ops.linear: the LDS-DMA tile kernel from TILE_MIN_M tokens,
+            # the conv_gemm tiles below); the residual rides in the o / FFN-down epilogues
             qkv = ops.linear(x, w[f"l{i}.qkv.w"], w[f"l{i}.qkv.b"], workspace=ws)
             a = ops.flash_attention(qkv, B, S, cfg.heads, cfg.heads, cfg.head_dim, kv_lens=lens)
-            if blas:
-                h = ops.linear(a, w[f"l{i}.o.w"], w[f"l{i}.o.b"])
-                x = ops.layernorm(h, w[f"l{i}.ln1.g"], w[f"l{i}.ln1.b"], residual=x, eps=cfg.eps)
-            else:
-                h = ops.gemm(a, w[f"l{i}.o.w"], w[f"l{i}.o.b"], residual=x, workspace=ws)
-                x = ops.layernorm(h, w[f"l{i}.ln1.g"], w[f"l{i}.ln1.b"], eps=cfg.eps)
+            h = ops.linear(a, w[f"l{i}.o.w"], w[f"l{i}.o.b"], residual=x, workspace=ws)
+            x = ops.layernorm(h, w[f"l{i}.ln1.g"], w[f"l{i}.ln1.b"], eps=cfg.eps)
             f1 = ops.linear(x, w[f"l{i}.ffn1.w"], w[f"l{i}.ffn1.b"], act=ops.ACT_GELU, workspace=ws)
-            if blas:
-                h = ops.linear(f1, w[f"l{i}.ffn2.w"], w[f"l{i}.ffn2.b"])
-                x = ops.layernorm(h, w[f"l{i}.ln2.g"], w[f"l{i}.ln2.b"], residual=x, eps=cfg.eps)
-            else:
-                h = ops.gemm(f1, w[f"l{i}.ffn2.w"], w[f"l{i}.ffn2.b"], residual=x, workspace=ws)
-                x = ops.layernorm(h, w[f"l{i}.ln2.g"], w[f"l{i}.ln2.b"], eps=cfg.eps)
+            h = ops.linear(f1, w[f"l{i}.ffn2.w"], w[f"l{i}.ffn2.b"], residual=x, workspace=ws)
+            x = ops.layernorm(h, w[f"l{i}.ln2.g"], w[f"l{i}.ln2.b"], eps=cfg.eps)
         cls_rows = x.view(B, S, H)[:, 0].contiguous()
         pooled = ops.gemm(cls_rows, w["pooler.w"], w["pooler.b"], act=ops.ACT_TANH, workspace=ws)
         return ops.gemm(pooled, self.cls_w, self.cls_b, workspace=ws)

@@ -436,8 +436,6 @@ class LlamaTP:
                             if self.p[n].shape[0] % 16 == 0 and self.p[n].shape[1] % 64 == 0
                             and min_el <= self.p[n].numel() < (1 << 31)}
             self.ones = torch.ones(cfg.hidden, device=self.device, dtype=torch.bfloat16)
-            if self.device.type == "cuda":  # TunableOp-measured hipBLASLt/rocBLAS solutions, batch 64-128 decode
-                ops.load_blas_tuning()
             self.workspace = torch.empty(32 << 20, device=self.device, dtype=torch.float32)
             self.dec_chunk = int(os.environ.get("MLS_DEC_CHUNK", "0"))  # 0: auto (see _fused_forward)
             self.dec_ws = torch.empty(max_batch * self.sd.hq * (-(-max_seq // 64)) * (D + 2) + 16,
@@ -699,10 +697,9 @@ class LlamaTP:
                                        eps=eps, variant=self.pk_variant)
         elif B <= 16:
             logits = ops.gemm_rmsnorm(r, p["lm_head"], delta, eps=eps, workspace=ws)
-        else:  # 1 GB of weights: the native tile streams 5.4 TB/s up to 64 rows, hipBLASLt (tuned) from
-            # 128 (238 vs 318 us; profiles/r2_llama8b_tunableop_search.txt)
+        else:  # 1 GB of weights: the weight-streaming native tile up to 64 rows, the tile GEMM above
             xn = ops.rmsnorm(delta, self.ones, residual=r, eps=eps)
-            logits = ops.linear(xn, p["lm_head"], workspace=ws, impl="native" if B <= 64 else "blas")
+            logits = ops.linear(xn, p["lm_head"], workspace=ws, impl="native" if B <= 64 else "auto")
         return self._local_topk(logits, k)
 
     # ---------------------------------------------------------------- public

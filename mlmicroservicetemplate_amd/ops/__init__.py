@@ -525,16 +525,13 @@ def fold_norm(w: torch.Tensor, gain: torch.Tensor) -> torch.Tensor:
     return (w.float() * gain.float().view(1, -1)).to(w.dtype)
 
 
-# Plain library GEMMs go to hipBLASLt (through torch.addmm): on the transformer prefill shapes it
-# runs 1.4-1.5 PFLOP/s against 0.9-1.0 for the native 128x128-tile kernel (profiles/r1_gemm_probe.jsonl),
-# and from M = 64 up it wins or ties on every BERT / Llama shape measured
-# (profiles/r1_gemm_probe_small_m.jsonl).  The native kernels keep the decode-shaped products
-# (skinny M <= 16, tiled up to 32, where they tie and fuse SiLU-mul) and every fused epilogue
-# hipBLASLt cannot express (SiLU-mul runs as a native elementwise pass after it).
-BLAS_MIN_M = int(os.environ.get("MLS_BLAS_MIN_M", "33"))
-_BF16_BIAS: dict = {}
-
-
+# Large-M projections run on the native LDS-DMA MFMA tile kernel (gemm_tile: csrc/gemm_tile.hip),
+# the decode-shaped ones (M <= 32, and 33..TILE_MIN_M - 1 rows) on the skinny / conv_gemm kernels with
+# per-shape plans.  hipBLASLt (torch.addmm) is reachable only on request -- impl="blas" or
+# MLS_GEMM_IMPL=blas -- as the A/B reference of tools/gemm_tile_probe.py; no default path calls it.
+TILE_MIN_M = int(os.environ.get("MLS_TILE_MIN_M", "256"))
+BLAS_MIN_M = TILE_MIN_M  # kept for callers that split "large" from "small" token counts
+_GEMM_IMPL = os.environ.get("MLS_GEMM_IMPL", "native")
 def _bias_bf16(bias: torch.Tensor) -> torch.Tensor:
     key = (bias.data_ptr(), bias.numel(), bias.device)
     hit = _BF16_BIAS.get(key)
@@ -567,22 +564,47 @@ def gemm_plan() -> Dict[Tuple[int, int, int], Tuple[int, int]]:
     return {(e["M"], e["N"], e["K"]): (int(e["plan"][0]), int(e["plan"][1])) for e in doc["entries"]}
 
 
+def tile_cfg_for(M: int, N: int, K: int) -> int:
+    """gemm_tile config for a shape: measured choices first (``tuned/gemm_tile_gfx950.json``), else
+    the kernel's own pick (largest tile that still fills the chip)."""
+    e = gemm_tile_plan().get((M, N, K))
+    return e if e is not None else 0
+
+
+@functools.lru_cache(maxsize=None)
+def gemm_tile_plan() -> Dict[Tuple[int, int, int], int]:
+    path = os.path.join(_TUNED_DIR, "gemm_tile_gfx950.json")
+    if os.environ.get("MLS_GEMM_PLAN", "1") == "0" or not os.path.exists(path):
+        return {}
+    with open(path) as f:
+        doc = json.load(f)
+    return {(e["M"], e["N"], e["K"]): int(e["cfg"]) for e in doc["entries"]}
+
+
 def linear(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, act=ACT_NONE,
            residual: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
            impl: str = "auto") -> torch.Tensor:
-    """Transformer projection ``act(a @ w.T + bias (+ residual))`` with the implementation chosen by
-    shape: hipBLASLt for large-M plain GEMMs (bias and GELU as its epilogues, SiLU-mul as a native
-    pass), the native kernels otherwise (``impl`` = "auto" | "native" | "blas")."""
+    """Transformer projection ``act(a @ w.T + bias) (+ residual)``, all native: M >= TILE_MIN_M on the
+    persistent LDS-DMA tile kernel (:func:`gemm_tile`, bias / GELU / SiLU-mul / residual in its
+    epilogue), smaller M on the skinny / conv_gemm kernels (measured per-shape plans in
+    ``tuned/gemm_plan_gfx950.json``).  ``impl``: "auto" | "native" | "tile" | "blas" (hipBLASLt, the
+    A/B reference only; also ``MLS_GEMM_IMPL=blas``)."""
     code = _act(act)
-    M = a.shape[0]
-    blas = impl == "blas" or (impl == "auto" and M >= BLAS_MIN_M)
-    plan = gemm_plan().get((M, w.shape[0], w.shape[1])) if impl == "auto" else None
-    if plan is not None:
-        if plan[0] > 0 and not (code == ACT_SILU_MUL and residual is not None):
-            return gemm(a, w, bias, act=code, residual=residual, workspace=workspace, cfg=plan[0], splitk=plan[1])
-        blas = plan[0] == 0
-    if not blas or code not in (ACT_NONE, ACT_GELU, ACT_SILU_MUL) or a.device.type != "cuda":
-        return gemm(a, w, bias, act=code, residual=residual, workspace=workspace)
+    M, K = a.shape
+    N = w.shape[0]
+    if impl == "blas" or (impl == "auto" and _GEMM_IMPL == "blas"):
+        return _linear_blas(a, w, bias, code, residual)
+    if impl == "tile" or (impl == "auto" and M >= TILE_MIN_M and K % 64 == 0 and N % 16 == 0
+                          and a.device.type == "cuda" and a.is_contiguous() and w.is_contiguous()):
+        return gemm_tile(a, w, bias, act=code, residual=residual, cfg=tile_cfg_for(M, N, K))
+    plan = gemm_plan().get((M, N, K)) if impl == "auto" else None
+    if plan is not None and plan[0] > 0 and not (code == ACT_SILU_MUL and residual is not None):
+        return gemm(a, w, bias, act=code, residual=residual, workspace=workspace, cfg=plan[0], splitk=plan[1])
+    return gemm(a, w, bias, act=code, residual=residual, workspace=workspace)
+
+
+def _linear_blas(a, w, bias, code, residual):
+    """hipBLASLt through torch (A/B reference; bias / GELU epilogues, SiLU-mul as a native pass)."""
     b16 = _bias_bf16(bias) if bias is not None else None
     if code == ACT_GELU:
         y = torch._addmm_activation(b16 if b16 is not None else torch.zeros(w.shape[0], device=a.device,
@@ -594,6 +616,8 @@ def linear(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         y = torch.addmm(b16, a, w.t())
     else:
         y = torch.mm(a, w.t())
+    if code not in (ACT_NONE, ACT_GELU, ACT_SILU_MUL):
+        raise ValueError("blas path: act must be none / gelu / silu_mul")
     if residual is not None:
         y += residual
     if code == ACT_SILU_MUL:
@@ -1062,6 +1086,34 @@ def decode_pick(cand_v: torch.Tensor, cand_i: torch.Tensor, tok: torch.Tensor, p
                                tok.data_ptr(), pos.data_ptr(), lens.data_ptr(), _ptr(hist), cols, step.data_ptr(),
                                stream_ptr(dev))
     check(rc, "mls_decode_pick")
+
+
+IMAGE_CONTAINER_BYTES = 64 + 224 * 224 * 3  # frontend/csrc/jpeg_coefs.h CONTAINER_BYTES
+IMAGE_SCRATCH_PER_IMAGE = 8 << 20  # jpeg_coefs.h SCRATCH_PER_IMAGE
+
+
+def image_decode(containers: torch.Tensor, out: Optional[torch.Tensor] = None,
+                 err: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """GPU half of the image path (csrc/image_decode.hip): ``[B, IMAGE_CONTAINER_BYTES]`` uint8
+    containers (raw RGB, or host-Huffman-decoded JPEG coefficients + resize geometry) -> uint8
+    ``[B, 224, 224, 3]``: IDCT, libjpeg chroma upsampling + YCbCr->RGB, Pillow's bilinear resize and
+    the centre crop of ``plugins.builtin.decode_image``.  ``err`` (int32 [1], optional) is set to 1
+    when a container is unusable (that image comes out black).  Capturable (fixed launch geometry;
+    the scratch comes from the caller's -- in a graph, the graph pool's -- allocator)."""
+    dev = containers.device
+    _need(containers, "containers", torch.uint8, dev)
+    if containers.dim() != 2 or containers.shape[1] != IMAGE_CONTAINER_BYTES:
+        raise ValueError(f"containers must be [B, {IMAGE_CONTAINER_BYTES}]")
+    B = containers.shape[0]
+    if out is None:
+        out = torch.empty(B, 224, 224, 3, device=dev, dtype=torch.uint8)
+    scratch = torch.empty(B * IMAGE_SCRATCH_PER_IMAGE, device=dev, dtype=torch.uint8)
+    if err is not None:
+        _need(err, "err", torch.int32, dev)
+    rc = lib().mls_image_decode(containers.data_ptr(), out.data_ptr(), scratch.data_ptr(), IMAGE_SCRATCH_PER_IMAGE, B,
+                                _ptr(err), stream_ptr(dev))
+    check(rc, "mls_image_decode")
+    return out
 
 
 def gpu_sleep(us: int, device=None) -> None:

@@ -67,6 +67,24 @@ class IdentityPlugin(ModelPlugin):
 
 
 RAW_CONTENT_TYPES = ("application/octet-stream", "application/x-rgb8")
+IMAGE_CONTAINER_BYTES = 64 + 224 * 224 * 3  # frontend/csrc/jpeg_coefs.h
+
+
+def image_container(data: bytes, content_type: str = "") -> np.ndarray:
+    """Upload bytes -> GPU image container (``frontend/csrc/jpeg_coefs.h``) as a uint8 row: raw RGB8
+    wrapped, baseline JPEGs Huffman-decoded by the C++ decoder, anything else decoded by PIL
+    (:func:`decode_image`) and wrapped.  ``ops.image_decode`` turns a batch of them into pixels."""
+    from ..frontend.native import load_extension
+
+    ext = load_extension()
+    n = 224 * 224 * 3
+    if len(data) == n and (not content_type or content_type.split(";")[0].strip() in RAW_CONTENT_TYPES):
+        return np.frombuffer(ext.raw_container(data), dtype=np.uint8)
+    if data[:2] == b"\xff\xd8":
+        c = ext.jpeg_container(data)
+        if isinstance(c, bytes):
+            return np.frombuffer(c, dtype=np.uint8)
+    return np.frombuffer(ext.raw_container(decode_image(data, content_type).tobytes()), dtype=np.uint8)
 
 
 def decode_image(data: bytes, content_type: str = "", size: int = 224, resize: int = 256) -> np.ndarray:
@@ -130,9 +148,16 @@ class ResNet50Plugin(ModelPlugin):
         if int(s.MAX_BATCH) == 0:  # auto: plan from free HBM and the latency SLO (scheduler/capacity.py)
             self.plan_batch(s, devices[0], params)
         buckets = [b for b in s.GRAPH_BUCKETS if b <= s.MAX_BATCH]
+        # GPU image decode: engine rows are image containers, the graph starts with ops.image_decode
+        self.containers = bool(s.GPU_IMAGE_DECODE) and s.BACKEND == "fused"
+        shape = (IMAGE_CONTAINER_BYTES,) if self.containers else (224, 224, 3)
         for dev in devices:
             fwd = self._build_forward(s.BACKEND, dev, max(buckets), params)
-            eng = GpuEngine(fwd, dev, (224, 224, 3), torch.uint8, buckets=buckets, inflight=int(s.INFLIGHT),
+            if self.containers:
+                from .. import ops
+
+                fwd = (lambda f: (lambda x: f(ops.image_decode(x))))(fwd)
+            eng = GpuEngine(fwd, dev, shape, torch.uint8, buckets=buckets, inflight=int(s.INFLIGHT),
                             use_graphs=bool(s.USE_GRAPHS), name=f"resnet50.{dev}",
                             concurrent=bool(s.CONCURRENT_SLOTS))
             eng.warmup(capture=bool(s.USE_GRAPHS))
@@ -192,6 +217,8 @@ class ResNet50Plugin(ModelPlugin):
         raise ValueError(f"unknown BACKEND {backend}")
 
     def preprocess(self, part: Part) -> Any:
+        if getattr(self, "containers", False):
+            return image_container(part.data, part.content_type or "")
         return decode_image(part.data, part.content_type or "")
 
     def replica_probes(self):
@@ -210,7 +237,13 @@ class ResNet50Plugin(ModelPlugin):
     def postprocess(self, out: Any) -> dict:
         return topk_result(self.labels, *out)
 
+    def configure(self, settings) -> None:
+        # known before init(): the native front end sizes its rows from native_spec()
+        self.containers = bool(settings.GPU_IMAGE_DECODE) and settings.BACKEND == "fused"
+
     def native_spec(self) -> dict:
+        if getattr(self, "containers", False):
+            return {"sample_bytes": IMAGE_CONTAINER_BYTES, "result": "topk", "image_container": True}
         return {"sample_bytes": 224 * 224 * 3, "result": "topk"}
 
     def reload_spec(self):

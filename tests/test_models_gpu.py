@@ -109,9 +109,10 @@ def test_skinny_lds_wide_n(M, fused):
     assert rel(out, ref) < 2e-2
 
 
-@pytest.mark.parametrize("impl", ["blas", "native"])
+@pytest.mark.parametrize("impl", ["blas", "native", "tile", "auto"])
 def test_linear_dispatch(impl):
-    """ops.linear: hipBLASLt (+ native SiLU-mul pass) and native paths agree with fp32."""
+    """ops.linear: the native paths (conv_gemm tiles, the LDS-DMA tile kernel, the default routing)
+    and the hipBLASLt A/B reference agree with fp32."""
     from mlmicroservicetemplate_amd import ops
 
     torch.manual_seed(7)
@@ -162,27 +163,25 @@ def test_topk_large_shard_offset_and_tail(N, k, lo, valid):
     assert torch.allclose(x.float().gather(1, local), rv)
 
 
-# 256 tokens: native GEMMs; 1024: hipBLASLt + LN-fused residual; 4096 (the benchmark shape):
-# + the TunableOp-chosen hipBLASLt FFN-up solution (ops/tuned/tunableop_gfx950.csv)
+# 256 tokens: conv_gemm tiles; 1024 / 4096 (the benchmark shape): the LDS-DMA tile GEMM
 @pytest.mark.parametrize("B,S", [(4, 64), (16, 64), (32, 128)])
 def test_bert_fused_matches_reference(B, S):
-    from mlmicroservicetemplate_amd import ops
     from mlmicroservicetemplate_amd.models import bert
 
     cfg = bert.BertConfig(num_labels=3)
     p = bert.init_bert(cfg, 0)
     torch.manual_seed(1)
-    if B * S == 4096:
-        assert ops.load_blas_tuning()
     ids = torch.randint(1000, cfg.vocab, (B, S), device=DEV, dtype=torch.int32)
     tt = torch.zeros_like(ids)
     lens = torch.tensor(([64, 33, 10, 1] * (B // 4)), device=DEV, dtype=torch.int32)
     ref = bert.bert_reference({k: v.to(DEV) for k, v in p.items()}, ids, tt, lens, cfg)
     fused = bert.BertFused(p, DEV, cfg)
     out = fused(ids, tt, lens)[:, :3].float()
-    assert rel(out, ref) < 5e-2
+    assert rel(out, ref) < 2e-2
     vals, idx = fused.classify(ids, tt, lens, k=3)
-    assert (idx[:, 0].long() == ref.argmax(-1)).float().mean() >= 0.75
+    top2 = ref.topk(2, dim=-1).values
+    sure = (top2[:, 0] - top2[:, 1]) / ref.abs().max() > 1e-2
+    assert torch.equal(idx[:, 0].long()[sure], ref.argmax(-1)[sure])
     eager = bert.BertEager(p, DEV, cfg)
     assert rel(eager(ids, tt, lens).float(), ref) < 5e-2
 
