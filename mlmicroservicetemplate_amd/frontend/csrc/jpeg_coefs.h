@@ -45,7 +45,7 @@ constexpr size_t PAYLOAD_BYTES = (size_t)IMG_OUT * IMG_OUT * 3;
 constexpr size_t CONTAINER_BYTES = HDR_BYTES + PAYLOAD_BYTES;
 // device scratch per image (ops/csrc/image_decode.hip): component planes + RGB + the horizontal
 // resample pass must fit; decode_at() moves to a coarser DCT scale until they do
-constexpr size_t SCRATCH_PER_IMAGE = (size_t)8 << 20;
+constexpr size_t SCRATCH_PER_IMAGE = (size_t)2 << 20;  // fits PIL-drafted sizes (short side 256..511)
 enum Kind : uint32_t { KIND_RAW = 0, KIND_JPEG = 1 };
 
 #pragma pack(push, 1)

@@ -532,6 +532,7 @@ def fold_norm(w: torch.Tensor, gain: torch.Tensor) -> torch.Tensor:
 TILE_MIN_M = int(os.environ.get("MLS_TILE_MIN_M", "256"))
 BLAS_MIN_M = TILE_MIN_M  # kept for callers that split "large" from "small" token counts
 _GEMM_IMPL = os.environ.get("MLS_GEMM_IMPL", "native")
+_BF16_BIAS: dict = {}
 def _bias_bf16(bias: torch.Tensor) -> torch.Tensor:
     key = (bias.data_ptr(), bias.numel(), bias.device)
     hit = _BF16_BIAS.get(key)
@@ -1089,7 +1090,7 @@ def decode_pick(cand_v: torch.Tensor, cand_i: torch.Tensor, tok: torch.Tensor, p
 
 
 IMAGE_CONTAINER_BYTES = 64 + 224 * 224 * 3  # frontend/csrc/jpeg_coefs.h CONTAINER_BYTES
-IMAGE_SCRATCH_PER_IMAGE = 8 << 20  # jpeg_coefs.h SCRATCH_PER_IMAGE
+IMAGE_SCRATCH_PER_IMAGE = 2 << 20  # jpeg_coefs.h SCRATCH_PER_IMAGE
 
 
 def image_decode(containers: torch.Tensor, out: Optional[torch.Tensor] = None,

@@ -229,19 +229,28 @@ def test_resnet50_hot_reload_in_place_under_graphs():
                                                             "MAX_BATCH": 4, "GRAPH_BUCKETS": [4], "INFLIGHT": 2})
     plugin = ResNet50Plugin()
     plugin.init(PluginContext(settings=s, devices=["cuda:0"]))
+    from mlmicroservicetemplate_amd.plugins.builtin import image_container
+
     eng, model = plugin.engines[0], plugin.models[0]
     x = np.random.default_rng(3).integers(0, 256, (4, 224, 224, 3), dtype=np.uint8)
-    v0, i0 = eng.run(x)
+    assert plugin.containers  # engine rows are GPU image containers (raw uploads wrapped)
+    xc = np.stack([image_container(img.tobytes(), "application/octet-stream") for img in x])
+    v0, i0 = eng.run(xc)
     ptrs = {k: t.data_ptr() for k, t in model.w.items()}
     params1 = plugin.load_params(None, 1)
     plugin.apply_params(params1)
     assert {k: t.data_ptr() for k, t in model.w.items()} == ptrs
-    v1, i1 = eng.run(x)  # graph replay on the reloaded weights
+    v1, i1 = eng.run(xc)  # graph replay on the reloaded weights
     fresh = resnet.ResNet50Fused(params1, "cuda:0", max_batch=4, tuning=autotune.load_tuning("resnet50", 4))
     fv, fi = fresh.classify(torch.from_numpy(x).cuda(), 5)
     np.testing.assert_array_equal(i1, fi.cpu().numpy())
     np.testing.assert_allclose(v1, fv.cpu().numpy(), rtol=1e-3, atol=1e-4)
     assert not np.array_equal(i0, i1)
+
+
+class _Part:
+    def __init__(self, data: bytes):
+        self.data, self.content_type = data, "application/octet-stream"
 
 
 def test_resnet50_auto_batch_plan():
@@ -260,5 +269,5 @@ def test_resnet50_auto_batch_plan():
     assert s.MAX_BATCH == plan.max_batch and s.GRAPH_BUCKETS[-1] == plan.max_batch
     assert plugin.engines[0].max_batch == plan.max_batch
     x = np.random.default_rng(0).integers(0, 256, (plan.max_batch, 224, 224, 3), dtype=np.uint8)
-    v, i = plugin.engines[0].run(x)
+    v, i = plugin.engines[0].run(np.stack([plugin.preprocess(_Part(img.tobytes())) for img in x]))
     assert v.shape == (plan.max_batch, 5) and np.all(np.isfinite(v))
