@@ -311,7 +311,8 @@ def gemm(
 
 
 GEMM_TILE_CFGS = {1: (256, 256), 2: (256, 128), 3: (128, 128), 4: (128, 128), 5: (128, 256), 6: (256, 256),
-                  7: (256, 128), 8: (256, 256), 9: (256, 128)}
+                  7: (256, 128), 8: (256, 256), 9: (256, 128), 10: (256, 256), 11: (256, 256), 12: (256, 128),
+                  15: (256, 256), 16: (256, 128)}
 
 
 def gemm_tile(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, act=ACT_NONE,

@@ -164,6 +164,20 @@ MLS_DEV int xcd_remap(int bid, int nwg) {
 
 MLS_DEV float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 MLS_DEV float silu(float x) { return x / (1.f + __expf(-x)); }
+// GEMM-epilogue forms: no IEEE divide sequence, no ocml erff branches.  erf by Abramowitz & Stegun
+// 7.1.26 (|error| <= 1.5e-7, far below the bf16 output's half-ulp), one v_rcp + one v_exp each.
+MLS_DEV float erf_fast(float x) {
+  const float a = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float y = fmaf(-p * t, __expf(-a * a), 1.f);
+  return copysignf(y, x);
+}
+MLS_DEV float gelu_fast(float x) { return 0.5f * x * (1.f + erf_fast(x * 0.70710678118654752f)); }
+MLS_DEV float silu_fast(float x) { return x * __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_TANH = 3, ACT_SILU = 4, ACT_SILU_MUL = 5 };
 MLS_DEV float apply_act(float v, int act) {
@@ -172,6 +186,15 @@ MLS_DEV float apply_act(float v, int act) {
     case ACT_GELU: return gelu_erf(v);
     case ACT_TANH: return tanhf(v);
     case ACT_SILU: return silu(v);
+    default: return v;
+  }
+}
+MLS_DEV float apply_act_fast(float v, int act) {
+  switch (act) {
+    case ACT_RELU: return fmaxf(v, 0.f);
+    case ACT_GELU: return gelu_fast(v);
+    case ACT_TANH: return tanhf(v);
+    case ACT_SILU: return silu_fast(v);
     default: return v;
   }
 }

@@ -37,7 +37,13 @@ struct GemmTileArgs {
   int M, N, K, act, ldo, ldr;
   uint32_t a_bytes, w_bytes;
   int tiles_n;
+  int flags;  // probe-only ablations (GT_ABL_*), 0 in every real call
 };
+// ablation flags (tools/gemm_tile_probe.py --ablate; cfg bits 8+ of mls_gemm_tile): timing-only builds
+// of the same instruction stream (cdna_hip_programming.md §7, "price ONE buffer's traffic")
+constexpr int GT_ABL_NOLOAD = 1;   // zero-record A / W descriptors: every DMA dropped by the range check
+constexpr int GT_ABL_NOSTORE = 2;  // epilogue stores land on a zero-record descriptor (dropped)
+constexpr int GT_ABL_NOBIAS = 4;   // epilogue skips the bias loads
 
 MLS_DEV void gt_glds16(rsrc_t r, char* lds, int voff, int soff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (GLDS3 void*)lds, 16, voff, soff, 0, 0);
@@ -95,8 +101,224 @@ MLS_DEV void gt_wait_ring(int left) {
   }
 }
 
-template <int BM, int BN, int WM, int WN, int STAGES, int BKS>
-__global__ __launch_bounds__(WM * WN * 64) void gemm_tile_kernel(const GemmTileArgs g) {
+// Tile epilogue shared by every variant: lane (fr, fq) holds D[n = 4*fq + e][m = fr] of each 16 x 16
+// MFMA tile = row m, 4 consecutive output columns.  Written so no memory op sits behind a per-element
+// branch (cdna_hip_programming.md §5 item 4(c): hipcc would wait vmcnt(0) per element -- one
+// dependent L2 round trip per (i, jn), ~32 per tile, measured as ~15 us of a 40 us BERT GEMM):
+//  * bias: 16 values per 16-column tile, uniform per wave -> scalar loads (constant address space),
+//    the lane picks its 4 -- no VMEM op, so no vmcnt wait that would drain the DMA ring;
+//  * residual: range-checked buffer loads (OOB -> 0) issued as one batch of MT per column tile;
+//  * stores: range-checked buffer stores (rows >= M and columns >= N land on the OOB offset).
+#define GCONST4 __attribute__((address_space(4)))
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+// EPI: 0 bias (+ act), 1 bias + residual (+ act), 2 SiLU-mul.  One specialisation per kind so the
+// unrolled (i, pair) body is straight-line code: a runtime act / residual / SiLU branch inside it made
+// hipcc re-home all 128 accumulator registers at every join (~500 instructions per store, measured
+// by in-kernel stamps at 31-60k cycles per 256 x 256 tile epilogue).
+// 16-B stores (T21, on the 16x16 fragment): v_permlane16_swap over the column tiles (2p, 2p + 1)
+// gives each lane 8 consecutive columns of its row -- fq 0: tile 2p cols 0-7, fq 1: tile 2p+1 cols
+// 0-7, fq 2: tile 2p cols 8-15, fq 3: tile 2p+1 cols 8-15 -- so a wave stores 16 rows x 64 B per
+// instruction: half the store instructions of the bf16x4-per-lane layout (the tail is store-ISSUE
+// bound: MI355X_MICROARCH.md, 'attention epilogue store tail').  Bias and residual are loaded in
+// the same layout (16-B range-checked buffer loads, OOB -> 0).
+template <int MT, int NTL, int EPI, int ACT>
+MLS_DEV void gt_epilogue_t(f32x4 (&acc)[MT][NTL], const GemmTileArgs& g, int m0, int n0, int wrow, int wcol) {
+  static_assert(NTL % 2 == 0, "column tiles pair up");
+  const int lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4;
+  const int ldo2 = g.ldo * 2, ldr2 = g.ldr * 2;
+  const int rows = g.M - m0 < 256 ? g.M - m0 : 256;  // valid rows of this tile (tiles are <= 256 tall)
+  const bool nostore = g.flags & GT_ABL_NOSTORE;
+  const rsrc_t ro = make_rsrc(g.out + (size_t)m0 * g.ldo, nostore ? 0u : (uint32_t)(rows * ldo2));
+  const rsrc_t rr = make_rsrc(EPI == 1 ? g.res + (size_t)m0 * g.ldr : g.out, EPI == 1 ? (uint32_t)(rows * ldr2) : 0u);
+  const bool use_bias = g.bias && !(g.flags & GT_ABL_NOBIAS);
+  const rsrc_t rb = make_rsrc(use_bias ? (const void*)g.bias : (const void*)g.out, use_bias ? (uint32_t)g.N * 4u : 0u);
+  const int sub = (fq & 1) * 16 + (fq >> 1) * 8;  // this lane's 8 columns within the 32-column pair
+#pragma unroll
+  for (int p = 0; p < NTL / 2; ++p) {
+    const int c0 = n0 + wcol + p * 32, c = c0 + sub;
+    const bool col_ok = c < g.N;  // N % 16 == 0: an 8-column run is wholly in or out
+    const f32x4 b_lo = __builtin_bit_cast(f32x4, bload16(rb, col_ok ? c * 4 : OOB));
+    const f32x4 b_hi = __builtin_bit_cast(f32x4, bload16(rb, col_ok ? c * 4 + 16 : OOB));
+    // residual rows two 16-row blocks ahead (a whole column of them live would cost 32 VGPRs and
+    // spill the 256 x 256 tile)
+    const int roff = col_ok ? (wrow + fr) * ldr2 + c * 2 : OOB;
+    uint4 rv0 = {0, 0, 0, 0}, rv1 = {0, 0, 0, 0};
+    if constexpr (EPI == 1) {
+      rv0 = bload16(rr, roff);
+      if (MT > 1) rv1 = bload16(rr, col_ok ? roff + 16 * ldr2 : OOB);
+    }
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const int r = wrow + i * 16 + fr;  // row within the tile
+      uint4 rcur = rv0;
+      if constexpr (EPI == 1) {
+        rv0 = rv1;
+        if (i + 2 < MT) rv1 = bload16(rr, col_ok ? roff + (i + 2) * 16 * ldr2 : OOB);
+      }
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        // __float_as_uint, not __builtin_bit_cast: hipcc (ROCm 7.2) folds a bit_cast of an ext-vector
+        // element feeding this builtin to element 0 -- one swap for all four (checked in the .s)
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * p][e]),
+                                                         __float_as_uint(acc[i][2 * p + 1][e]), false, false);
+        v[e] = __uint_as_float(sw[0]) + b_lo[e];
+        v[4 + e] = __uint_as_float(sw[1]) + b_hi[e];
+      }
+      bf16x8 o;
+      int off;
+      if constexpr (EPI == 2) {
+        // gate lanes fq 0/1 (tile 2p / 2p+1 cols 0-7) pair with their up columns on lanes fq 2/3
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (bf16)(silu_fast(v[e]) * xor32_f(v[e]));
+        off = fq < 2 && col_ok ? r * ldo2 + ((c0 >> 1) + fq * 8) * 2 : OOB;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float x = v[e];
+          v[e] = ACT == ACT_GELU ? gelu_fast(x) : ACT == ACT_RELU ? fmaxf(x, 0.f) : ACT == ACT_SILU ? silu_fast(x)
+                 : ACT == ACT_TANH ? tanhf(x) : x;
+        }
+        if constexpr (EPI == 1) {
+          const bf16x8 rb8 = __builtin_bit_cast(bf16x8, rcur);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += (float)rb8[e];
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (bf16)v[e];
+        off = col_ok ? r * ldo2 + c * 2 : OOB;
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), ro, off, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);  // keep each row block's live range to itself
+    }
+  }
+}
+
+// The bf16x4-per-lane form of the epilogue (one 8-B store per (i, jn), scalar-loaded bias): kept as
+// the A/B arm of the 16-B form (cfg 19 = cfg 1 with it) -- probe only.
+template <int MT, int NTL, int EPI, int ACT>
+MLS_DEV void gt_epilogue_x2(f32x4 (&acc)[MT][NTL], const GemmTileArgs& g, int m0, int n0, int wrow, int wcol) {
+  const int lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4;
+  const int ldo2 = g.ldo * 2, ldr2 = g.ldr * 2;
+  const int rows = g.M - m0 < 256 ? g.M - m0 : 256;
+  const bool nostore = g.flags & GT_ABL_NOSTORE;
+  const rsrc_t ro = make_rsrc(g.out + (size_t)m0 * g.ldo, nostore ? 0u : (uint32_t)(rows * ldo2));
+  const rsrc_t rr = make_rsrc(EPI == 1 ? g.res + (size_t)m0 * g.ldr : g.out, EPI == 1 ? (uint32_t)(rows * ldr2) : 0u);
+#pragma unroll
+  for (int jn = 0; jn < NTL; ++jn) {
+    const int nt0 = n0 + wcol + jn * 16, n = nt0 + 4 * fq;
+    const bool col_ok = nt0 < g.N;
+    f32x4 bv = {0.f, 0.f, 0.f, 0.f}, bu = {0.f, 0.f, 0.f, 0.f};
+    if (g.bias && col_ok && !(g.flags & GT_ABL_NOBIAS)) {
+      const GCONST4 f32x4* bp = (const GCONST4 f32x4*)(g.bias + nt0);
+      const f32x4 b0 = bp[0], b1 = bp[1], b2 = bp[2], b3 = bp[3];
+      bv = fq == 0 ? b0 : fq == 1 ? b1 : fq == 2 ? b2 : b3;
+      bu = fq == 0 ? b2 : b3;
+    }
+    uint2 rv[MT];
+    if constexpr (EPI == 1) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i) rv[i] = bload8(rr, col_ok ? (wrow + i * 16 + fr) * ldr2 + n * 2 : OOB);
+    }
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const int r = wrow + i * 16 + fr;
+      const f32x4 v = acc[i][jn];
+      bf16x4 b;
+      int off;
+      if constexpr (EPI == 2) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) b[e] = (bf16)(silu_fast(v[e] + bv[e]) * (xor32_f(v[e]) + bu[e]));
+        off = fq < 2 && col_ok ? r * ldo2 + ((nt0 >> 1) + 4 * fq) * 2 : OOB;
+      } else {
+        f32x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float x = v[e] + bv[e];
+          o[e] = ACT == ACT_GELU ? gelu_fast(x) : ACT == ACT_RELU ? fmaxf(x, 0.f) : ACT == ACT_SILU ? silu_fast(x)
+                 : ACT == ACT_TANH ? tanhf(x) : x;
+        }
+        if constexpr (EPI == 1) {
+          const bf16x4 rb = __builtin_bit_cast(bf16x4, rv[i]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] += (float)rb[e];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) b[e] = (bf16)o[e];
+        off = col_ok ? r * ldo2 + n * 2 : OOB;
+      }
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, b), ro, off, 0, 0);
+    }
+  }
+}
+
+#define GT_EPI_CALL(ACTV)                                                   \
+  do {                                                                      \
+    if constexpr (X2) gt_epilogue_x2<MT, NTL, EPI, ACTV>(acc, g, m0, n0, wrow, wcol); \
+    else gt_epilogue_t<MT, NTL, EPI, ACTV>(acc, g, m0, n0, wrow, wcol);    \
+  } while (0)
+template <int MT, int NTL, int EPI, bool X2>
+MLS_DEV void gt_epilogue_a(f32x4 (&acc)[MT][NTL], const GemmTileArgs& g, int m0, int n0, int wrow, int wcol) {
+  switch (g.act) {
+    case ACT_GELU: GT_EPI_CALL(ACT_GELU); break;
+    case ACT_RELU: GT_EPI_CALL(ACT_RELU); break;
+    case ACT_SILU: GT_EPI_CALL(ACT_SILU); break;
+    case ACT_TANH: GT_EPI_CALL(ACT_TANH); break;
+    default: GT_EPI_CALL(ACT_NONE); break;
+  }
+}
+
+// dispatch once per tile, then zero the accumulators for the next tile in one straight run
+template <int MT, int NTL, bool X2 = false>
+MLS_DEV void gt_epilogue(f32x4 (&acc)[MT][NTL], const GemmTileArgs& g, int m0, int n0, int wrow, int wcol) {
+  if (g.act == ACT_SILU_MUL) {
+    if constexpr (X2) gt_epilogue_x2<MT, NTL, 2, ACT_NONE>(acc, g, m0, n0, wrow, wcol);
+    else gt_epilogue_t<MT, NTL, 2, ACT_NONE>(acc, g, m0, n0, wrow, wcol);
+  } else if (g.res) {
+    gt_epilogue_a<MT, NTL, 1, X2>(acc, g, m0, n0, wrow, wcol);
+  } else {
+    gt_epilogue_a<MT, NTL, 0, X2>(acc, g, m0, n0, wrow, wcol);
+  }
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int jn = 0; jn < NTL; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // retire the epilogue's VMEM ops with the BUILTIN wait (hipcc's waitcnt pass sees it; an asm one it
+  // does not): otherwise the pass carries the bias / residual load registers as possibly pending
+  // around the k-loop back edge and emits vmcnt(0) before the first ds_read of EVERY k-step --
+  // draining the DMA ring each step (+25-40 % k-step cycles, measured by stamps vs the x2 arm)
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
+}
+
+// In-kernel stamps (cdna_hip_programming.md §7) for the STAMP build of the tile kernel (cfg 13/14 =
+// cfg 1/2 + stamps, probe only): s_memtime with its own lgkmcnt wait, fenced by sched_barriers.
+MLS_DEV unsigned long long gt_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+MLS_DEV unsigned long long gt_realtime() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+
+template <int BM, int BN, int WM, int WN, int STAGES, int BKS, bool STAMP = false, bool PIPE = false, bool X2 = false>
+__global__ __launch_bounds__(WM * WN * 64) void gemm_tile_kernel(const GemmTileArgs g0) {
+  // STAMP: g0.res is the stamp buffer [grid][8] (u64): t0 start, t1 first k-step landed, t2 first
+  // tile's last MFMA, t3 its epilogue issued, t4 all stores retired, t5/t6 realtime at t0/t4, t7 tiles
+  unsigned long long st[5] = {0, 0, 0, 0, 0}, rt0 = 0;
+  GemmTileArgs g = g0;
+  if constexpr (STAMP) {
+    g.res = nullptr;
+    st[0] = gt_stamp();
+    rt0 = gt_realtime();
+  }
   constexpr int NT = WM * WN * 64;
   constexpr int WTM = BM / WM, WTN = BN / WN;  // wave tile: WTM rows (m) x WTN columns (n)
   constexpr int MT = WTM / 16, NTL = WTN / 16;
@@ -168,7 +390,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_tile_kernel(const GemmTileA
   const int fr = lane & 15, fq = lane >> 4;
   const int sw = gt_swz<BKS>(fr);  // tile rows are 16-aligned: swz(r) depends on r & 15 only
   const int a_rd = (wm * WTM + fr) * ROWB, w_rd = A_BYTES + (wn * WTN + fr) * ROWB;
-  const bool glu = g.act == ACT_SILU_MUL;
+
 
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
@@ -178,9 +400,39 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_tile_kernel(const GemmTileA
   for (int j = 0; j < nsteps; ++j) {
     gt_wait_ring<STAGES, LOADS>(nsteps - 1 - j);  // step j landed; later ones may still fly
     gt_barrier();  // step j visible to every wave; step j - 1 fully read by every wave
+    if constexpr (STAMP)
+      if (j == 0) st[1] = gt_stamp();
     if (j + STAGES - 1 < nsteps) stage();
     const char* base = smem + c_slot * STAGE_BYTES;
     c_slot = c_slot + 1 == STAGES ? 0 : c_slot + 1;
+    if constexpr (PIPE && BKS == 64) {
+      // fragment pipeline across the two 32-deep halves of the step: the k 32-63 W fragments are
+      // read up front, each A fragment of k 32-63 right after the last MFMA that reads its k 0-31
+      // register -- the second half's LDS latency hides under the first half's MFMAs instead of
+      // stalling both waves of the SIMD after them
+      const int coff0 = (fq ^ sw) << 4, coff1 = ((4 + fq) ^ sw) << 4;
+      bf16x8 af[MT], w0[NTL], w1[NTL];
+#pragma unroll
+      for (int jn = 0; jn < NTL; ++jn) w0[jn] = *reinterpret_cast<const bf16x8*>(base + w_rd + jn * 16 * ROWB + coff0);
+#pragma unroll
+      for (int i = 0; i < MT; ++i) af[i] = *reinterpret_cast<const bf16x8*>(base + a_rd + i * 16 * ROWB + coff0);
+#pragma unroll
+      for (int jn = 0; jn < NTL; ++jn) w1[jn] = *reinterpret_cast<const bf16x8*>(base + w_rd + jn * 16 * ROWB + coff1);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+#pragma unroll
+        for (int jn = 0; jn < NTL; ++jn)
+          acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0[jn], af[i], acc[i][jn], 0, 0, 0);
+        af[i] = *reinterpret_cast<const bf16x8*>(base + a_rd + i * 16 * ROWB + coff1);
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int jn = 0; jn < NTL; ++jn)
+          acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1[jn], af[i], acc[i][jn], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    } else {
 #pragma unroll
     for (int ks = 0; ks < BKS / 32; ++ks) {
       const int coff = ((ks * 4 + fq) ^ sw) << 4;
@@ -197,57 +449,30 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_tile_kernel(const GemmTileA
           acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[jn], af[i], acc[i][jn], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
+    }
     if (++c_kt < nk) continue;
     c_kt = 0;
 
     // ---- epilogue of this tile (the next tile's first k-steps are already in flight) ----
-    // lane holds D[n = 4*fq + r][m = fr] of each 16 x 16 tile -> row m, 4 consecutive columns
     int m0, n0;
+    if constexpr (STAMP)
+      if (c_ti == 0) st[2] = gt_stamp();
     tile_mn(c_ti++, m0, n0);
+    gt_epilogue<MT, NTL, X2>(acc, g, m0, n0, wm * WTM, wn * WTN);
+    if constexpr (STAMP)
+      if (c_ti == 1) st[3] = gt_stamp();
+  }
+  if constexpr (STAMP) {
+    gt_wait_vmcnt<0>();
+    st[4] = gt_stamp();
+    const unsigned long long rt1 = gt_realtime();
+    if (threadIdx.x == 0) {
+      unsigned long long* o = (unsigned long long*)g0.res + blockIdx.x * 8;
 #pragma unroll
-    for (int i = 0; i < MT; ++i) {
-      const int m = m0 + wm * WTM + i * 16 + fr;
-#pragma unroll
-      for (int jn = 0; jn < NTL; ++jn) {
-        const int nt0 = n0 + wn * WTN + jn * 16;  // first column of this 16-column tile
-        const int n = nt0 + 4 * fq;
-        float v[4] = {acc[i][jn][0], acc[i][jn][1], acc[i][jn][2], acc[i][jn][3]};
-        acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (glu) {
-          // columns nt0..nt0+7 are gate, nt0+8..nt0+15 up: lane l < 32 holds gate, lane l + 32 its up
-          float u[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) u[e] = xor32_f(v[e]);
-          if (fq < 2 && m < g.M && nt0 < g.N) {
-            float o[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float gt = v[e] + (g.bias ? g.bias[n + e] : 0.f);
-              const float up = u[e] + (g.bias ? g.bias[n + 8 + e] : 0.f);
-              o[e] = silu(gt) * up;
-            }
-            bf16x4 b = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
-            *reinterpret_cast<bf16x4*>(g.out + (size_t)m * g.ldo + (nt0 >> 1) + 4 * fq) = b;
-          }
-          continue;
-        }
-        if (m >= g.M || n >= g.N) continue;
-        if (g.bias) {
-          const float4 b = *reinterpret_cast<const float4*>(g.bias + n);
-          v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
-        }
-        if (g.act != ACT_NONE) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], g.act);
-        }
-        if (g.res) {
-          const bf16x4 r = *reinterpret_cast<const bf16x4*>(g.res + (size_t)m * g.ldr + n);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] += (float)r[e];
-        }
-        bf16x4 b = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-        *reinterpret_cast<bf16x4*>(g.out + (size_t)m * g.ldo + n) = b;
-      }
+      for (int k = 0; k < 5; ++k) o[k] = st[k];
+      o[5] = rt0;
+      o[6] = rt1;
+      o[7] = (unsigned long long)my_tiles;
     }
   }
 }
@@ -324,7 +549,7 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(const GemmTileArgs g) {
     for (int j = 0; j < NTL; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int fr = lane & 15, fq = lane >> 4, sw = gt_swz<64>(fr);
   const int a_rd = (wm * WTM + fr) * ROWB, w_rd = A_BYTES + (wn * WTN + fr) * ROWB;
-  const bool glu = g.act == ACT_SILU_MUL;
+
 
   // prologue: stage 0 (both halves), group 1's half of stage 1; stage 0 visible to all
   if (nsteps > 0) dma_half(0);
@@ -364,51 +589,159 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(const GemmTileArgs g) {
     if (j % nk == nk - 1) {
       int m0, n0;
       tile_mn(j / nk, m0, n0);
-#pragma unroll
-      for (int i = 0; i < MT; ++i) {
-        const int m = m0 + wm * WTM + i * 16 + fr;
-#pragma unroll
-        for (int jn = 0; jn < NTL; ++jn) {
-          const int nt0 = n0 + wn * WTN + jn * 16, n = nt0 + 4 * fq;
-          float v[4] = {acc[i][jn][0], acc[i][jn][1], acc[i][jn][2], acc[i][jn][3]};
-          acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
-          if (glu) {
-            float u[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) u[e] = xor32_f(v[e]);
-            if (fq < 2 && m < g.M && nt0 < g.N) {
-              float o[4];
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const float gt_ = v[e] + (g.bias ? g.bias[n + e] : 0.f);
-                const float up = u[e] + (g.bias ? g.bias[n + 8 + e] : 0.f);
-                o[e] = silu(gt_) * up;
-              }
-              bf16x4 b = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
-              *reinterpret_cast<bf16x4*>(g.out + (size_t)m * g.ldo + (nt0 >> 1) + 4 * fq) = b;
-            }
-            continue;
-          }
-          if (m >= g.M || n >= g.N) continue;
-          if (g.bias) {
-            const float4 b = *reinterpret_cast<const float4*>(g.bias + n);
-            v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
-          }
-          if (g.act != ACT_NONE) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], g.act);
-          }
-          if (g.res) {
-            const bf16x4 r = *reinterpret_cast<const bf16x4*>(g.res + (size_t)m * g.ldr + n);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] += (float)r[e];
-          }
-          bf16x4 b = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-          *reinterpret_cast<bf16x4*>(g.out + (size_t)m * g.ldo + n) = b;
-        }
-      }
+      gt_epilogue<MT, NTL>(acc, g, m0, n0, wm * WTM, wn * WTN);
     }
     if (grp == 0) gt_wait_vmcnt<0>();  // group 0's A half of stage j + 1
+    gt_barrier();
+  }
+  if (grp == 0) gt_barrier();  // balance group 1's stagger barrier
+}
+
+// ---------------------------------------------------------------------------------------------
+// Ring variant (cfg 10-12): the ping-pong stagger of gemm_pp_kernel on a DEEP LDS-DMA ring.
+//
+// Measured on the kernels above (profiles/r3_gemm_tile_probe_*.jsonl): the 2-stage 256 x 256 loop
+// runs at ~48 % of MFMA peak on 8192^3 -- the DMA of step j + 1 has one k-step (~0.85 us of MFMA)
+// to land, less than a loaded L2-miss round trip -- and the ping-pong kernel, whose DMA had even
+// less lead, was slower still.  This kernel keeps the stagger (one wave per SIMD in its MFMA section
+// while the other reads fragments, so barriers never empty the MFMA pipe) and gives every DMA
+// R - 1 sub-steps of lead:
+//  * sub-step = 32 of K: one 16x16x32 MFMA per (i, jn) per wave (32 per wave on the 256^2 tile);
+//    ring slot = A[BM][32] + W[BN][32] (24-32 KB, 64-B rows), R slots (160 KB for 256^2 x 5);
+//  * group 0 = waves 0-3, group 1 = waves 4-7 (one of each per SIMD); group 1 runs one barrier
+//    behind.  Barrier interval 2u: G0 reads slot u (L section) while G1 multiplies u - 1 (M
+//    section); interval 2u + 1: G0 multiplies u, G1 reads u;
+//  * G0 DMAs the A half of sub-step u + R - 1 in its L section of u, G1 the W half of u + R in its M
+//    section of u -- both into slot (u - 1) % R / u % R, free since the barrier that closed the
+//    last read of it; each wave retires its half of sub-step u + 1 (counted vmcnt, never 0 in steady
+//    state) before the barrier that precedes the first read of it, so a DMA has ~2(R - 2) barrier
+//    intervals of lead instead of 2;
+//  * epilogue bias through the scalar cache (constant address space, uniform per wave): a vector
+//    load there would make hipcc drain the whole DMA ring with vmcnt(0) at every tile end.
+template <int L, int MAXN>
+MLS_DEV void gt_wait_groups(int n) {  // wait until <= L * min(n, MAXN) of this wave's loads are in flight
+  if constexpr (MAXN == 0) {
+    gt_wait_vmcnt<0>();
+  } else {
+    if (n >= MAXN) gt_wait_vmcnt<L * MAXN>();
+    else gt_wait_groups<L, MAXN - 1>(n);
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int R>
+__global__ __launch_bounds__(512) void gemm_ring_kernel(const GemmTileArgs g) {
+  static_assert(WM * WN == 8, "8 waves");
+  constexpr int WTM = BM / WM, WTN = BN / WN, MT = WTM / 16, NTL = WTN / 16;
+  constexpr int ROWB = 64;  // 32 k of bf16
+  constexpr int A_BYTES = BM * ROWB, SLOT = (BM + BN) * ROWB;
+  constexpr int LA = A_BYTES / (256 * 16), LB = BN * ROWB / (256 * 16);  // DMAs per thread per half
+  static_assert(LA * 256 * 16 == A_BYTES && LB * 256 * 16 == BN * ROWB, "whole DMA rounds per group");
+  static_assert(R * SLOT <= 160 * 1024 && R >= 3, "ring");
+  static_assert(WTN == 64 || WTN == 32, "bias slice");
+  __shared__ __attribute__((aligned(16))) char smem[R * SLOT];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int grp = __builtin_amdgcn_readfirstlane(wid >> 2), gt = tid & 255, gw = wid & 3;
+  const int wm = wid / WN, wn = wid - wm * WN;
+  const int tiles_m = (g.M + BM - 1) / BM, ntiles = tiles_m * g.tiles_n;
+  const int G = gridDim.x, bq = xcd_remap(blockIdx.x, G);
+  const int my_tiles = bq < ntiles ? (ntiles - 1 - bq) / G + 1 : 0;
+  const int nk = g.K / 32, nsub = my_tiles * nk;
+  const rsrc_t ra = make_rsrc(g.a, g.a_bytes), rw = make_rsrc(g.w, g.w_bytes);
+  const int K2 = g.K * 2;
+
+  auto tile_mn = [&](int ti, int& m0, int& n0) {
+    int tm, tn;
+    gt_tile(bq + ti * G, tiles_m, g.tiles_n, tm, tn);
+    m0 = tm * BM;
+    n0 = tn * BN;
+  };
+  // this thread's DMA pieces (group 0: A rows, group 1: W rows): LDS byte i*4096 + gt*16 of the
+  // half = row (i*4096 + gt*16) / 64, lane-linear chunk gt & 3 = source chunk (gt & 3) ^ swz(row)
+  constexpr int LD = LA > LB ? LA : LB;
+  int d_off[LD];
+  const int lim = grp == 0 ? g.M : g.N;
+#pragma unroll
+  for (int i = 0; i < LD; ++i) {
+    const int row = i * 64 + (gt >> 2);
+    d_off[i] = row * K2 + (((gt & 3) ^ gt_swz<32>(row)) << 4);
+  }
+  // loader cursor of this group (its half of sub-step l_u goes to slot l_u % R)
+  int l_u = 0, l_kt = 0, l_ti = 0, l_m0 = 0, l_n0 = 0, l_slot = 0;
+  tile_mn(0, l_m0, l_n0);
+  auto issue = [&]() {
+    char* base = smem + l_slot * SLOT + gw * 1024;
+    if (grp == 0) {
+      const int so = l_m0 * K2 + l_kt * ROWB;
+#pragma unroll
+      for (int i = 0; i < LA; ++i)
+        gt_glds16(ra, base + i * 4096, l_m0 + i * 64 + (gt >> 2) < lim ? d_off[i] : OOB, so);
+    } else {
+      const int so = l_n0 * K2 + l_kt * ROWB;
+#pragma unroll
+      for (int i = 0; i < LB; ++i)
+        gt_glds16(rw, base + A_BYTES + i * 4096, l_n0 + i * 64 + (gt >> 2) < lim ? d_off[i] : OOB, so);
+    }
+    ++l_u;
+    l_slot = l_slot + 1 == R ? 0 : l_slot + 1;
+    if (++l_kt == nk) {
+      l_kt = 0;
+      if (++l_ti < my_tiles) tile_mn(l_ti, l_m0, l_n0);
+    }
+  };
+
+  f32x4 acc[MT][NTL];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NTL; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fq = lane >> 4;
+  const int coff = (fq ^ gt_swz<32>(fr)) << 4;
+  const int a_rd = (wm * WTM + fr) * ROWB + coff, w_rd = A_BYTES + (wn * WTN + fr) * ROWB + coff;
+
+
+  // prologue: G0 A halves of 0 .. R-2, G1 W halves of 0 .. R-1; sub-step 0 retired; G1 staggers
+  {
+    const int n_pro = grp == 0 ? R - 1 : R;
+    for (int u = 0; u < n_pro && u < nsub; ++u) issue();
+    const int after = l_u - 1;  // loads issued after sub-step 0's
+    if (grp == 0) gt_wait_groups<LA, R - 2>(after);
+    else gt_wait_groups<LB, R - 1>(after);
+  }
+  gt_barrier();
+  if (grp == 1) gt_barrier();
+
+  int c_slot = 0, c_kt = 0, c_ti = 0;
+  bf16x8 af[MT], wf[NTL];
+  for (int u = 0; u < nsub; ++u) {
+    // ---- L section ----
+    if (grp == 0 && l_u < nsub) issue();  // A half of u + R - 1
+    {
+      const char* base = smem + c_slot * SLOT;
+#pragma unroll
+      for (int jn = 0; jn < NTL; ++jn) wf[jn] = *reinterpret_cast<const bf16x8*>(base + w_rd + jn * 16 * ROWB);
+#pragma unroll
+      for (int i = 0; i < MT; ++i) af[i] = *reinterpret_cast<const bf16x8*>(base + a_rd + i * 16 * ROWB);
+    }
+    c_slot = c_slot + 1 == R ? 0 : c_slot + 1;
+    if (grp == 1 && u + 1 < nsub) gt_wait_groups<LB, R - 2>(l_u - 1 - (u + 1));  // W half of u + 1 retired
+    gt_barrier();
+    // ---- M section ----
+    if (grp == 1 && l_u < nsub) issue();  // W half of u + R
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int jn = 0; jn < NTL; ++jn)
+        acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[jn], af[i], acc[i][jn], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    if (++c_kt == nk) {
+      c_kt = 0;
+      int m0, n0;
+      tile_mn(c_ti++, m0, n0);
+      gt_epilogue<MT, NTL>(acc, g, m0, n0, wm * WTM, wn * WTN);
+    }
+    if (grp == 0 && u + 1 < nsub) gt_wait_groups<LA, R - 2>(l_u - 1 - (u + 1));  // A half of u + 1 retired
     gt_barrier();
   }
   if (grp == 0) gt_barrier();  // balance group 1's stagger barrier
@@ -424,6 +757,8 @@ struct GtCfg {
 //   3: 128x128, 4 waves 2x2, 2 x 64,  64 KB (2 blocks / CU)
 //   4: 128x128, 4 waves 2x2, 3 x 64,  96 KB      5: 128x256, 8 waves 2x4, 3 x 64, 144 KB
 //   8: 256x256 ping-pong (gemm_pp_kernel), 2 x 64, 128 KB    9: 256x128 ping-pong, 2 x 64, 96 KB
+//  10: 256x256 ring (gemm_ring_kernel), 5 x 32, 160 KB      11: 256x256 ring, 4 x 32, 128 KB
+//  12: 256x128 ring, 6 x 32, 144 KB
 GtCfg gt_cfg(int cfg) {
   switch (cfg) {
     case 1: return {256, 256, 512};
@@ -435,6 +770,17 @@ GtCfg gt_cfg(int cfg) {
     case 7: return {256, 128, 512};
     case 8: return {256, 256, 512};
     case 9: return {256, 128, 512};
+    case 10: return {256, 256, 512};
+    case 11: return {256, 256, 512};
+    case 12: return {256, 128, 512};
+    case 13: return {256, 256, 512};
+    case 14: return {256, 128, 512};
+    case 15: return {256, 256, 512};
+    case 16: return {256, 128, 512};
+    case 17: return {256, 256, 512};
+    case 18: return {256, 128, 512};
+    case 19: return {256, 256, 512};
+    case 20: return {256, 256, 512};
     default: return {0, 0, 0};
   }
 }
@@ -472,6 +818,17 @@ int gt_launch(const GemmTileArgs& g0, int cfg, int grid_cap, hipStream_t st) {
     case 7: hipLaunchKernelGGL((gemm_tile_kernel<256, 128, 4, 2, 4, 32>), grid, block, 0, st, g); break;
     case 8: hipLaunchKernelGGL((gemm_pp_kernel<256, 256, 2, 4>), grid, block, 0, st, g); break;
     case 9: hipLaunchKernelGGL((gemm_pp_kernel<256, 128, 4, 2>), grid, block, 0, st, g); break;
+    case 10: hipLaunchKernelGGL((gemm_ring_kernel<256, 256, 2, 4, 5>), grid, block, 0, st, g); break;
+    case 11: hipLaunchKernelGGL((gemm_ring_kernel<256, 256, 2, 4, 4>), grid, block, 0, st, g); break;
+    case 12: hipLaunchKernelGGL((gemm_ring_kernel<256, 128, 4, 2, 6>), grid, block, 0, st, g); break;
+    case 13: hipLaunchKernelGGL((gemm_tile_kernel<256, 256, 2, 4, 2, 64, true>), grid, block, 0, st, g); break;
+    case 14: hipLaunchKernelGGL((gemm_tile_kernel<256, 128, 4, 2, 3, 64, true>), grid, block, 0, st, g); break;
+    case 15: hipLaunchKernelGGL((gemm_tile_kernel<256, 256, 2, 4, 2, 64, false, true>), grid, block, 0, st, g); break;
+    case 16: hipLaunchKernelGGL((gemm_tile_kernel<256, 128, 4, 2, 3, 64, false, true>), grid, block, 0, st, g); break;
+    case 17: hipLaunchKernelGGL((gemm_tile_kernel<256, 256, 2, 4, 2, 64, true, true>), grid, block, 0, st, g); break;
+    case 18: hipLaunchKernelGGL((gemm_tile_kernel<256, 128, 4, 2, 3, 64, true, true>), grid, block, 0, st, g); break;
+    case 19: hipLaunchKernelGGL((gemm_tile_kernel<256, 256, 2, 4, 2, 64, false, false, true>), grid, block, 0, st, g); break;
+    case 20: hipLaunchKernelGGL((gemm_tile_kernel<256, 256, 2, 4, 2, 64, true, false, true>), grid, block, 0, st, g); break;
   }
   return hipGetLastError() == hipSuccess ? MLS_OK : MLS_BAD_ARG;
 }
@@ -499,6 +856,8 @@ int mls_gemm_tile(const void* A, const void* W, const float* bias, const void* r
   const size_t ab = (size_t)M * K * 2, wb = (size_t)N * K * 2;
   if (ab >= 0x7FFFFFFFull || wb >= 0x7FFFFFFFull || (size_t)M * ldo >= 0x7FFFFFFFFFull) return MLS_UNSUPPORTED;
   GemmTileArgs g{};
+  g.flags = cfg >> 8;
+  cfg &= 0xFF;
   g.a = (const bf16*)A;
   g.w = (const bf16*)W;
   g.bias = bias;
@@ -507,8 +866,8 @@ int mls_gemm_tile(const void* A, const void* W, const float* bias, const void* r
   g.M = M; g.N = N; g.K = K; g.act = act;
   g.ldo = ldo > 0 ? ldo : (act == ACT_SILU_MUL ? N / 2 : N);
   g.ldr = ldr > 0 ? ldr : N;
-  g.a_bytes = (uint32_t)ab;
-  g.w_bytes = (uint32_t)wb;
+  g.a_bytes = g.flags & GT_ABL_NOLOAD ? 0u : (uint32_t)ab;
+  g.w_bytes = g.flags & GT_ABL_NOLOAD ? 0u : (uint32_t)wb;
   return gt_launch(g, cfg > 0 ? cfg : gt_pick(M, N), grid_cap, (hipStream_t)stream);
 }
 

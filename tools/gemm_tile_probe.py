@@ -34,6 +34,10 @@ def main():
     ap.add_argument("--cfgs", type=int, nargs="*", default=[0, 1, 2, 3, 4, 5])
     ap.add_argument("--conc", type=int, nargs="*", default=[1, 4])
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--ablate", type=int, nargs="*", default=[],
+                    help="timing-only ablations per cfg (csrc/gemm_tile.hip GT_ABL_*: 1 = no loads, 2 = no stores)")
+    ap.add_argument("--stamps", type=int, nargs="*", default=[],
+                    help="stamped builds (cfg 13 = cfg 1, 14 = cfg 2): per-block phase cycles of the first tile")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.manual_seed(0)
@@ -59,9 +63,17 @@ def main():
             y = torch.addmm(bias.to(torch.bfloat16), x, w.t())
             return ops.silu_mul_interleaved(y) if code == ops.ACT_SILU_MUL else y
 
-        impls = [("hipblaslt", blas, None)]
+        for scfg in a.stamps:
+            for ab in [0] + a.ablate:
+                r = stamp_run(ops, xs[0], w, bias, code if code != ops.ACT_SILU_MUL else ops.ACT_NONE,
+                              scfg | (ab << 8), name)
+                print(json.dumps(dict(r, ablate=ab)), flush=True)
+        impls = [("hipblaslt", blas, None)] if a.cfgs else []
         for cfg in a.cfgs:
             impls.append((f"tile{cfg}", (lambda x, c=cfg: ops.gemm_tile(x, w, bias, act=code, cfg=c)), cfg))
+            for ab in a.ablate:
+                impls.append((f"tile{cfg}ab{ab}", (lambda x, c=cfg | (ab << 8): ops.gemm_tile(x, w, bias, act=code, cfg=c)),
+                              cfg))
         for impl, fn, cfg in impls:
             try:
                 y = fn(xs[0])
@@ -76,6 +88,32 @@ def main():
                                   "us": round(t * 1e6, 1), "tflops": round(flop / t / 1e12, 1),
                                   "rel_err": round(err, 5),
                                   "pick": ops.lib().mls_gemm_tile_pick(M, N) if cfg == 0 else cfg}), flush=True)
+
+
+def stamp_run(ops, x, w, bias, code, cfg, name):
+    """One stamped launch (after a warm one): medians over blocks of the first tile's phases in shader
+    cycles -- prologue (first k-step landed), per k-step, epilogue issue, store drain -- plus the
+    clock from s_memtime vs the 100 MHz s_memrealtime."""
+    M, K = x.shape
+    N = w.shape[0]
+    out = torch.empty(M, N, device=x.device, dtype=torch.bfloat16)
+    buf = torch.zeros(4096, 8, device=x.device, dtype=torch.int64)
+    for _ in range(2):
+        rc = ops.lib().mls_gemm_tile(x.data_ptr(), w.data_ptr(), bias.data_ptr(), buf.data_ptr(), out.data_ptr(), M, N,
+                                     K, code, N, N, cfg, 0, ops.stream_ptr(x.device))
+        ops.check(rc, "mls_gemm_tile")
+    torch.cuda.synchronize()
+    t = buf[buf[:, 7] > 0].cpu().double()
+    nk = K // 64
+    med = lambda v: round(float(v.median()), 1)
+    span_rt = (t[:, 6].max() - t[:, 5].min()) / 100.0  # us at 100 MHz
+    ghz = float(((t[:, 4] - t[:, 0]).sum() / ((t[:, 6] - t[:, 5]).sum() / 100e6)) / 1e9)
+    return {"shape": name, "stamp_cfg": cfg, "blocks": int(t.shape[0]), "tiles_per_block_max": int(t[:, 7].max()),
+            "clock_ghz": round(ghz, 3), "span_us": round(float(span_rt), 1),
+            "start_skew_us": round(float((t[:, 5].max() - t[:, 5].min()) / 100.0), 2),
+            "prologue_cyc": med(t[:, 1] - t[:, 0]), "kstep_cyc": med((t[:, 2] - t[:, 1]) / max(1, nk - 1)),
+            "epilogue_cyc": med(t[:, 3] - t[:, 2]), "drain_cyc": med(t[:, 4] - t[:, 3]),
+            "total_cyc": med(t[:, 4] - t[:, 0]), "ideal_kstep_cyc": None}
 
 
 if __name__ == "__main__":
