@@ -315,12 +315,30 @@ GEMM_TILE_CFGS = {1: (256, 256), 2: (256, 128), 3: (128, 128), 4: (128, 128), 5:
                   15: (256, 256), 16: (256, 128)}
 
 
+_SPLIT_COUNTERS: Dict[Tuple[int, int], torch.Tensor] = {}
+SPLIT_COUNTER_ELEMS = 1 << 14
+
+
+def split_counters(workspace: torch.Tensor) -> torch.Tensor:
+    """Zeroed int32 arrival counters of the in-launch split-K combine, one set per workspace buffer
+    (= per stream: StreamWorkspace), allocated on first use (eager warm-up, before graph capture).
+    Each tile's reducer resets its counter, so they stay zero between launches."""
+    key = (workspace.device.index or 0, workspace.data_ptr())
+    c = _SPLIT_COUNTERS.get(key)
+    if c is None:
+        c = torch.zeros(SPLIT_COUNTER_ELEMS, device=workspace.device, dtype=torch.int32)
+        _SPLIT_COUNTERS[key] = c
+    return c
+
+
 def gemm_tile(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, act=ACT_NONE,
               residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None, cfg: int = 0,
-              grid_cap: int = 0) -> torch.Tensor:
+              grid_cap: int = 0, splitk: int = 1, workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Large-M projection on the LDS-DMA MFMA tile kernel (csrc/gemm_tile.hip):
     ``act(a @ w.T + bias) (+ residual)``; SiLU-mul for gate/up interleaved in groups of 8.
-    ``K % 64 == 0``, ``N % 16 == 0``; ``cfg`` selects the tile (:data:`GEMM_TILE_CFGS`, 0 = by shape)."""
+    ``K % 64 == 0``, ``N % 16 == 0``; ``cfg`` selects the tile (:data:`GEMM_TILE_CFGS`, 0 = by shape).
+    ``splitk > 1`` splits K and combines in the launch through fp32 slabs in ``workspace`` (falls back
+    to no split when the workspace is missing or too small, or K does not divide)."""
     dev = a.device
     _need(a, "a", torch.bfloat16, dev)
     _need(w, "w", torch.bfloat16, dev)
@@ -346,8 +364,18 @@ def gemm_tile(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = N
         _need(out, "out", torch.bfloat16, dev)
         if tuple(out.shape) != (M, n_out):
             raise ValueError(f"out must be [M, {n_out}]")
+    sk, ws_ptr, ws_elems, cnt_ptr = 1, None, 0, None
+    if splitk > 1 and workspace is not None and (cfg & 0xFF) in GEMM_TILE_CFGS:
+        bm, bn = GEMM_TILE_CFGS[cfg & 0xFF]
+        bks = 32 if (cfg & 0xFF) in (6, 7) else 64
+        tiles = -(-M // bm) * -(-N // bn)
+        if (K // bks) % splitk == 0 and tiles * splitk * bm * bn <= workspace.numel() \
+                and tiles <= SPLIT_COUNTER_ELEMS and workspace.dtype == torch.float32:
+            sk, ws_ptr, ws_elems, cnt_ptr = int(splitk), workspace.data_ptr(), workspace.numel(), \
+                split_counters(workspace).data_ptr()
     rc = lib().mls_gemm_tile(a.data_ptr(), w.data_ptr(), _ptr(bias), _ptr(residual), out.data_ptr(), M, N, K, code,
-                             n_out, N, int(cfg), int(grid_cap), stream_ptr(dev))
+                             n_out, N, int(cfg), int(grid_cap), sk, ws_ptr, ws_elems, cnt_ptr, SPLIT_COUNTER_ELEMS,
+                             stream_ptr(dev))
     check(rc, "mls_gemm_tile")
     return out
 
@@ -566,21 +594,21 @@ def gemm_plan() -> Dict[Tuple[int, int, int], Tuple[int, int]]:
     return {(e["M"], e["N"], e["K"]): (int(e["plan"][0]), int(e["plan"][1])) for e in doc["entries"]}
 
 
-def tile_cfg_for(M: int, N: int, K: int) -> int:
-    """gemm_tile config for a shape: measured choices first (``tuned/gemm_tile_gfx950.json``), else
-    the kernel's own pick (largest tile that still fills the chip)."""
+def tile_cfg_for(M: int, N: int, K: int) -> Tuple[int, int]:
+    """gemm_tile (config, K splits) for a shape: measured choices first (``tuned/gemm_tile_gfx950.json``),
+    else the kernel's own pick (largest tile that still fills the chip), no split."""
     e = gemm_tile_plan().get((M, N, K))
-    return e if e is not None else 0
+    return e if e is not None else (0, 1)
 
 
 @functools.lru_cache(maxsize=None)
-def gemm_tile_plan() -> Dict[Tuple[int, int, int], int]:
-    path = os.path.join(_TUNED_DIR, "gemm_tile_gfx950.json")
+def gemm_tile_plan() -> Dict[Tuple[int, int, int], Tuple[int, int]]:
+    path = os.environ.get("MLS_GEMM_TILE_TABLE") or os.path.join(_TUNED_DIR, "gemm_tile_gfx950.json")
     if os.environ.get("MLS_GEMM_PLAN", "1") == "0" or not os.path.exists(path):
         return {}
     with open(path) as f:
         doc = json.load(f)
-    return {(e["M"], e["N"], e["K"]): int(e["cfg"]) for e in doc["entries"]}
+    return {(e["M"], e["N"], e["K"]): (int(e["cfg"]), int(e.get("splitk", 1))) for e in doc["entries"]}
 
 
 def linear(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, act=ACT_NONE,
@@ -598,7 +626,8 @@ def linear(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         return _linear_blas(a, w, bias, code, residual)
     if impl == "tile" or (impl == "auto" and M >= TILE_MIN_M and K % 64 == 0 and N % 16 == 0
                           and a.device.type == "cuda" and a.is_contiguous() and w.is_contiguous()):
-        return gemm_tile(a, w, bias, act=code, residual=residual, cfg=tile_cfg_for(M, N, K))
+        cfg, sk = tile_cfg_for(M, N, K)
+        return gemm_tile(a, w, bias, act=code, residual=residual, cfg=cfg, splitk=sk, workspace=workspace)
     plan = gemm_plan().get((M, N, K)) if impl == "auto" else None
     if plan is not None and plan[0] > 0 and not (code == ACT_SILU_MUL and residual is not None):
         return gemm(a, w, bias, act=code, residual=residual, workspace=workspace, cfg=plan[0], splitk=plan[1])

@@ -38,6 +38,9 @@ struct GemmTileArgs {
   uint32_t a_bytes, w_bytes;
   int tiles_n;
   int flags;  // probe-only ablations (GT_ABL_*), 0 in every real call
+  int splitk;  // K splits per output tile (>= 1); > 1: fp32 slabs in ws + per-tile arrival counters
+  float* ws;   // [tiles][splitk][BM * BN] fp32 partial tiles (fragment-linear)
+  int* cnt;    // [tiles] arrival counters: zero before the launch, reset to zero by each tile's reducer
 };
 // ablation flags (tools/gemm_tile_probe.py --ablate; cfg bits 8+ of mls_gemm_tile): timing-only builds
 // of the same instruction stream (cdna_hip_programming.md §7, "price ONE buffer's traffic")
@@ -291,6 +294,65 @@ MLS_DEV void gt_epilogue(f32x4 (&acc)[MT][NTL], const GemmTileArgs& g, int m0, i
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
 }
 
+// In-launch split-K combine (cdna_hip_programming.md §5 "Projection GEMM", item 2): each K-split
+// block writes its fp32 partial tile as a fragment-linear slab (lane-contiguous 16 B, 1 KB per wave
+// instruction), retires it, and one lane releases at agent scope and draws a ticket from the tile's
+// counter; the split that draws S - 1 is the reducer: acquire, add the other S - 1 slabs into its
+// accumulators, reset the counter for the next launch, and run the normal epilogue.  Returns true
+// for the reducer; the others return with zeroed accumulators.  Correct for any placement of a
+// tile's splits (adjacent units -> same XCD in practice, the fast case).
+template <int TILE_ELEMS, int MT, int NTL>
+MLS_DEV bool gt_splitk_arrive(f32x4 (&acc)[MT][NTL], const GemmTileArgs& g, int tile, int split, int* flag) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, S = g.splitk;
+  f32x4* const tile_ws = reinterpret_cast<f32x4*>(g.ws + (size_t)tile * S * TILE_ELEMS);
+  const int frag0 = wid * MT * NTL * 64 + lane;  // this lane's first f32x4 in a slab
+  f32x4* mine = tile_ws + (size_t)split * (TILE_ELEMS / 4) + frag0;
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int jn = 0; jn < NTL; ++jn) mine[(i * NTL + jn) * 64] = acc[i][jn];
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // every wave: its slab stores (and the ring's DMAs) retired
+  gt_barrier();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    const int old = __hip_atomic_fetch_add(g.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == S - 1;
+    if (last) {
+      __hip_atomic_store(g.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+    }
+    *flag = last;
+  }
+  gt_barrier();
+  const bool last = __builtin_amdgcn_readfirstlane(*flag) != 0;
+  gt_barrier();  // flag read by every wave before it can be rewritten by this block's next unit
+  if (!last) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int jn = 0; jn < NTL; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+    return false;
+  }
+  // sum ALL S slabs (its own re-read too) in split order: the result does not depend on which
+  // split arrived last, so repeated launches are bit-identical
+  for (int s2 = 0; s2 < S; ++s2) {
+    const f32x4* slab = tile_ws + (size_t)s2 * (TILE_ELEMS / 4) + frag0;
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      f32x4 t[NTL];
+#pragma unroll
+      for (int jn = 0; jn < NTL; ++jn) t[jn] = slab[(i * NTL + jn) * 64];
+#pragma unroll
+      for (int jn = 0; jn < NTL; ++jn) acc[i][jn] = s2 == 0 ? t[jn] : acc[i][jn] + t[jn];
+      __builtin_amdgcn_sched_barrier(0);  // NTL loads in flight at a time: the accumulators fill the file
+    }
+  }
+  return true;
+}
+
 // In-kernel stamps (cdna_hip_programming.md §7) for the STAMP build of the tile kernel (cfg 13/14 =
 // cfg 1/2 + stamps, probe only): s_memtime with its own lgkmcnt wait, fenced by sched_barriers.
 MLS_DEV unsigned long long gt_stamp() {
@@ -327,16 +389,20 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_tile_kernel(const GemmTileA
   constexpr int A_LD = A_BYTES / (NT * 16), B_LD = B_BYTES / (NT * 16), LOADS = A_LD + B_LD;
   static_assert(A_BYTES % (NT * 16) == 0 && B_BYTES % (NT * 16) == 0, "stage must split into whole DMA rounds");
   static_assert(BKS == 32 || BKS == 64, "stage depth");
-  __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE_BYTES];
+  // + 16 B: the split-K "last arriver" flag -- in the SAME __shared__ object as the ring (a second
+  // one can make hipcc wait vmcnt(0) before every k-step's first ds_read: §5 item 4(a))
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE_BYTES + 16];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid - wm * WN;
   const int tiles_m = (g.M + BM - 1) / BM, ntiles = tiles_m * g.tiles_n;
-  // persistent: block b takes logical tiles b', b' + G, b' + 2G, ... where b' = XCD-contiguous
-  // remap of b -- at every round an XCD works on a contiguous (N-fastest) run of tiles
+  // work unit = (tile, K split): unit u -> tile u / S, split u % S (the S splits of a tile are
+  // adjacent units, so they land on one XCD and its reducer reads same-XCD slabs).  Persistent:
+  // block b takes units b', b' + G, ... where b' = XCD-contiguous remap of b
+  const int S = g.splitk, nunits = ntiles * S;
   const int G = gridDim.x, bq = xcd_remap(blockIdx.x, G);
-  const int my_tiles = bq < ntiles ? (ntiles - 1 - bq) / G + 1 : 0;
-  const int nk = g.K / BKS, nsteps = my_tiles * nk;
+  const int my_tiles = bq < nunits ? (nunits - 1 - bq) / G + 1 : 0;  // units of this block
+  const int nk = g.K / BKS / S, nsteps = my_tiles * nk;              // k-steps per unit
 
   const rsrc_t ra = make_rsrc(g.a, g.a_bytes), rw = make_rsrc(g.w, g.w_bytes);
   // DMA source: LDS byte p = i*NT*16 + tid*16 of a stage image is row p / 128, lane-linear chunk
@@ -354,22 +420,25 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_tile_kernel(const GemmTileA
   }
   const int K2 = g.K * 2;
 
-  auto tile_mn = [&](int ti, int& m0, int& n0) {
+  // unit ui of this block -> tile origin (m0, n0) and its first k-step k0
+  auto tile_mn = [&](int ti, int& m0, int& n0, int& k0) {
+    const int u = bq + ti * G, t = S == 1 ? u : u / S;
     int tm, tn;
-    gt_tile(bq + ti * G, tiles_m, g.tiles_n, tm, tn);
+    gt_tile(t, tiles_m, g.tiles_n, tm, tn);
     m0 = tm * BM;
     n0 = tn * BN;
+    k0 = (u - t * S) * nk;
   };
-  // loader cursor: the (tile, k-step) of the next DMA, advanced without divisions
-  int l_ti = 0, l_kt = 0, l_m0 = 0, l_n0 = 0, l_slot = 0;
-  if (nsteps > 0) tile_mn(0, l_m0, l_n0);
+  // loader cursor: the (unit, k-step) of the next DMA, advanced without divisions
+  int l_ti = 0, l_kt = 0, l_m0 = 0, l_n0 = 0, l_k0 = 0, l_slot = 0;
+  if (nsteps > 0) tile_mn(0, l_m0, l_n0, l_k0);
   auto stage = [&]() {  // DMA the loader cursor's k-step into ring slot l_slot, then advance it
-    const int kt = l_kt, m0 = l_m0, n0 = l_n0;
+    const int kt = l_k0 + l_kt, m0 = l_m0, n0 = l_n0;
     char* base = smem + l_slot * STAGE_BYTES + wid * 1024;
     l_slot = l_slot + 1 == STAGES ? 0 : l_slot + 1;
     if (++l_kt == nk) {
       l_kt = 0;
-      if (++l_ti < my_tiles) tile_mn(l_ti, l_m0, l_n0);
+      if (++l_ti < my_tiles) tile_mn(l_ti, l_m0, l_n0, l_k0);
     }
     const int sa = m0 * K2 + kt * ROWB, sb = n0 * K2 + kt * ROWB;
 #pragma unroll
@@ -453,12 +522,15 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_tile_kernel(const GemmTileA
     if (++c_kt < nk) continue;
     c_kt = 0;
 
-    // ---- epilogue of this tile (the next tile's first k-steps are already in flight) ----
-    int m0, n0;
+    // ---- epilogue of this unit (the next unit's first k-steps are already in flight) ----
+    int m0, n0, k0;
     if constexpr (STAMP)
       if (c_ti == 0) st[2] = gt_stamp();
-    tile_mn(c_ti++, m0, n0);
-    gt_epilogue<MT, NTL, X2>(acc, g, m0, n0, wm * WTM, wn * WTN);
+    const int cu = bq + c_ti * G;
+    tile_mn(c_ti++, m0, n0, k0);
+    const bool reducer = S == 1 || gt_splitk_arrive<BM * BN, MT, NTL>(acc, g, cu / S, cu - (cu / S) * S,
+                                                                        (int*)(smem + STAGES * STAGE_BYTES));
+    if (reducer) gt_epilogue<MT, NTL, X2>(acc, g, m0, n0, wm * WTM, wn * WTN);
     if constexpr (STAMP)
       if (c_ti == 1) st[3] = gt_stamp();
   }
@@ -807,7 +879,13 @@ int gt_launch(const GemmTileArgs& g0, int cfg, int grid_cap, hipStream_t st) {
   const int per_cu = cfg == 3 ? 2 : 1;
   int cap = grid_cap > 0 ? grid_cap : gt_num_cus() * per_cu;
   const int ntiles = tiles_m * g.tiles_n;
-  const dim3 grid(ntiles < cap ? ntiles : cap), block(c.threads);
+  // split-K: tile-kernel cfgs only; whole k-steps per split, room for every slab and counter
+  const bool sk_ok = cfg <= 7 || cfg >= 13;
+  const int bks = cfg == 6 || cfg == 7 ? 32 : 64;
+  if (g.splitk < 1) g.splitk = 1;
+  if (g.splitk > 1 && (!sk_ok || (g.K / bks) % g.splitk || !g.ws || !g.cnt)) return MLS_BAD_ARG;
+  const int units = ntiles * g.splitk;
+  const dim3 grid(units < cap ? units : cap), block(c.threads);
   switch (cfg) {
     case 1: hipLaunchKernelGGL((gemm_tile_kernel<256, 256, 2, 4, 2, 64>), grid, block, 0, st, g); break;
     case 2: hipLaunchKernelGGL((gemm_tile_kernel<256, 128, 4, 2, 3, 64>), grid, block, 0, st, g); break;
@@ -837,8 +915,8 @@ int gt_launch(const GemmTileArgs& g0, int cfg, int grid_cap, hipStream_t st) {
 // one with the most blocks (the projection GEMMs run under 4-5-way stream concurrency in serving)
 int gt_pick(int M, int N) {
   auto blocks = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
-  if (blocks(256, 256) >= 256) return 1;
-  if (blocks(256, 128) >= 256) return 2;
+  if (blocks(256, 256) >= 256) return 15;  // cfg 1 + fragment pipeline (>= cfg 1 on every probed shape)
+  if (blocks(256, 128) >= 256) return 16;
   if (blocks(128, 256) >= 256) return 5;
   return 4;
 }
@@ -849,9 +927,12 @@ extern "C" {
 
 // out[M][N] = act(A[M][K] . W[N][K]^T + bias (+ res));  ACT_SILU_MUL: W rows gate/up interleaved in
 // groups of 8, out [M][N/2].  K % 64 == 0, N % 16 == 0; cfg 0 = pick by shape; grid_cap 0 = one
-// resident wave of persistent blocks.
+// resident wave of persistent blocks.  splitk > 1: K in that many whole-k-step splits combined in
+// the launch -- ws >= tiles * splitk * BM * BN fp32, cnt >= tiles int32, all ZERO before the first
+// launch (each tile's reducer resets its counter).
 int mls_gemm_tile(const void* A, const void* W, const float* bias, const void* res, void* out, int M, int N, int K,
-                  int act, int ldo, int ldr, int cfg, int grid_cap, void* stream) {
+                  int act, int ldo, int ldr, int cfg, int grid_cap, int splitk, void* ws, long long ws_elems,
+                  void* cnt, int cnt_elems, void* stream) {
   if (M <= 0 || N <= 0 || K <= 0 || K % 64 || N % 16 || (res && act == ACT_SILU_MUL)) return MLS_BAD_ARG;
   const size_t ab = (size_t)M * K * 2, wb = (size_t)N * K * 2;
   if (ab >= 0x7FFFFFFFull || wb >= 0x7FFFFFFFull || (size_t)M * ldo >= 0x7FFFFFFFFFull) return MLS_UNSUPPORTED;
@@ -868,7 +949,17 @@ int mls_gemm_tile(const void* A, const void* W, const float* bias, const void* r
   g.ldr = ldr > 0 ? ldr : N;
   g.a_bytes = g.flags & GT_ABL_NOLOAD ? 0u : (uint32_t)ab;
   g.w_bytes = g.flags & GT_ABL_NOLOAD ? 0u : (uint32_t)wb;
-  return gt_launch(g, cfg > 0 ? cfg : gt_pick(M, N), grid_cap, (hipStream_t)stream);
+  const int c = cfg > 0 ? cfg : gt_pick(M, N);
+  g.splitk = splitk > 1 ? splitk : 1;
+  if (g.splitk > 1) {
+    const GtCfg t = gt_cfg(c);
+    if (!t.bm) return MLS_BAD_ARG;
+    const long long tiles = (long long)((M + t.bm - 1) / t.bm) * ((N + t.bn - 1) / t.bn);
+    if (!ws || !cnt || tiles > cnt_elems || tiles * g.splitk * t.bm * t.bn > ws_elems) return MLS_BAD_ARG;
+    g.ws = (float*)ws;
+    g.cnt = (int*)cnt;
+  }
+  return gt_launch(g, c, grid_cap, (hipStream_t)stream);
 }
 
 int mls_gemm_tile_pick(int M, int N) { return gt_pick(M, N); }

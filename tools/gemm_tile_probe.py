@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--cfgs", type=int, nargs="*", default=[0, 1, 2, 3, 4, 5])
     ap.add_argument("--conc", type=int, nargs="*", default=[1, 4])
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--splitk", type=int, nargs="*", default=[1], help="K splits per tile cfg (in-launch combine)")
     ap.add_argument("--ablate", type=int, nargs="*", default=[],
                     help="timing-only ablations per cfg (csrc/gemm_tile.hip GT_ABL_*: 1 = no loads, 2 = no stores)")
     ap.add_argument("--stamps", type=int, nargs="*", default=[],
@@ -69,8 +70,12 @@ def main():
                               scfg | (ab << 8), name)
                 print(json.dumps(dict(r, ablate=ab)), flush=True)
         impls = [("hipblaslt", blas, None)] if a.cfgs else []
+        ws = torch.zeros(64 << 20, device=dev, dtype=torch.float32)
         for cfg in a.cfgs:
-            impls.append((f"tile{cfg}", (lambda x, c=cfg: ops.gemm_tile(x, w, bias, act=code, cfg=c)), cfg))
+            for sk in a.splitk:
+                tag = f"tile{cfg}" + (f"s{sk}" if sk > 1 else "")
+                impls.append((tag, (lambda x, c=cfg, k=sk: ops.gemm_tile(x, w, bias, act=code, cfg=c, splitk=k,
+                                                                         workspace=ws)), cfg))
             for ab in a.ablate:
                 impls.append((f"tile{cfg}ab{ab}", (lambda x, c=cfg | (ab << 8): ops.gemm_tile(x, w, bias, act=code, cfg=c)),
                               cfg))
@@ -100,7 +105,7 @@ def stamp_run(ops, x, w, bias, code, cfg, name):
     buf = torch.zeros(4096, 8, device=x.device, dtype=torch.int64)
     for _ in range(2):
         rc = ops.lib().mls_gemm_tile(x.data_ptr(), w.data_ptr(), bias.data_ptr(), buf.data_ptr(), out.data_ptr(), M, N,
-                                     K, code, N, N, cfg, 0, ops.stream_ptr(x.device))
+                                     K, code, N, N, cfg, 0, 1, None, 0, None, 0, ops.stream_ptr(x.device))
         ops.check(rc, "mls_gemm_tile")
     torch.cuda.synchronize()
     t = buf[buf[:, 7] > 0].cpu().double()
