@@ -38,6 +38,10 @@ def main() -> int:
     ap.add_argument("--ready-timeout", type=float, default=300)
     ap.add_argument("--jpeg", action="store_true", help="upload a 320x240 JPEG (server-side decode) instead of raw RGB8")
     ap.add_argument("--decode-workers", type=int, default=4)
+    ap.add_argument("--jpeg-kind", default="photo", choices=["photo", "noise"],
+                    help="photo: smooth gradients + texture + mild noise (a camera-like entropy); noise: uniform "
+                         "random pixels (worst case for the Huffman decoder)")
+    ap.add_argument("--jpeg-size", default="320x240")
     ap.add_argument("--text", action="store_true",
                     help="upload an English text (~110 tokens) as multipart field `text` (the bert plugin)")
     args = ap.parse_args()
@@ -53,7 +57,16 @@ def main() -> int:
         from PIL import Image
 
         buf = io.BytesIO()
-        img = np.random.default_rng(0).integers(0, 256, (240, 320, 3), dtype=np.uint8)
+        jw, jh = (int(v) for v in args.jpeg_size.split("x"))
+        rng = np.random.default_rng(0)
+        if args.jpeg_kind == "noise":
+            img = rng.integers(0, 256, (jh, jw, 3), dtype=np.uint8)
+        else:  # the fixture generator of tests/test_image_decode.py
+            x = np.linspace(0, 1, jw)[None, :, None]
+            y = np.linspace(0, 1, jh)[:, None, None]
+            base = rng.random((1, 1, 3)) * 150 + 40 * np.sin(6 * x + rng.random() * 3) * np.cos(4 * y) + 25 * np.sin(
+                18 * x * y + rng.random((1, 1, 3)))
+            img = np.clip(base + rng.normal(0, 3.0, (jh, jw, 3)) + 60 * x, 0, 255).astype(np.uint8)
         Image.fromarray(img).save(buf, format="JPEG", quality=90)
         path = os.path.join(ROOT, "gpurun_out", "http_bench_upload.jpg")
         os.makedirs(os.path.dirname(path), exist_ok=True)
@@ -104,7 +117,8 @@ def main() -> int:
             except (requests.RequestException, ValueError):
                 pass
             res.update({"model": args.model, "frontend": args.frontend, "workers_per_gpu": args.workers_per_gpu,
-                        "io_threads": args.io_threads, "gpus": 1, "payload": "text100w" if args.text else ("jpeg320x240" if args.jpeg else "raw-rgb8"),
+                        "io_threads": args.io_threads, "gpus": 1, "payload": "text100w" if args.text else (f"jpeg{args.jpeg_size}-{args.jpeg_kind}" if args.jpeg else "raw-rgb8"),
+                        "gpu_image_decode": os.environ.get("GPU_IMAGE_DECODE", "1"),
                         "decode_workers": args.decode_workers})
             print(json.dumps(res), flush=True)
     finally:
