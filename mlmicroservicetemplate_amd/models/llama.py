@@ -249,6 +249,34 @@ class LlamaTokenizer:
 
 
 # --------------------------------------------------------------------------- comm
+class _ARDone:
+    """A collective that already completed in stream order (or needed none)."""
+
+    __slots__ = ("t",)
+
+    def __init__(self, t: torch.Tensor):
+        self.t = t
+
+    def wait(self) -> torch.Tensor:
+        return self.t
+
+
+class _ARPending:
+    """An all-reduce in flight on the backend's own stream (RCCL: ProcessGroupNCCL's NCCL stream,
+    ordered after the producer on the current stream); :meth:`wait` orders the current stream
+    after it -- the compute between start and wait overlaps the transfer."""
+
+    __slots__ = ("t", "work")
+
+    def __init__(self, t: torch.Tensor, work):
+        self.t, self.work = t, work
+
+    def wait(self) -> torch.Tensor:
+        with tracing.range("tp.all_reduce_wait"):
+            self.work.wait()
+        return self.t
+
+
 class TPComm:
     """Tensor-parallel collectives over a torch.distributed group (RCCL on GPU, gloo on CPU)."""
 
@@ -285,6 +313,18 @@ class TPComm:
             return t
         dist.all_reduce(t, group=self.group)
         return t
+
+    def all_reduce_start(self, t: torch.Tensor):
+        """Start an in-place sum all-reduce and return a handle whose ``wait()`` yields ``t`` reduced.
+        Large (prefill) messages go to the backend asynchronously so the caller can run independent
+        work in between; the one-shot IPC path (an in-stream kernel) and host-staged gloo
+        complete before returning."""
+        if self.tp == 1:
+            return _ARDone(t)
+        with tracing.range("tp.all_reduce"):
+            if (self.car is not None and self.car.eligible(t)) or (self.host_staged and t.is_cuda):
+                return _ARDone(self._all_reduce(t))
+            return _ARPending(t, dist.all_reduce(t, group=self.group, async_op=True))
 
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
         if self.tp == 1:
@@ -333,6 +373,9 @@ class ShardEmulationComm:
 
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
         return t
+
+    def all_reduce_start(self, t: torch.Tensor):
+        return _ARDone(t)
 
     def all_gather(self, t: torch.Tensor) -> torch.Tensor:
         return t.unsqueeze(0).expand(self.tp, *t.shape)
@@ -384,6 +427,9 @@ class LlamaTP:
         self.sd = shard_dims(cfg, tp, rank)
         self.tp, self.rank = tp, rank
         self.comm = comm or TPComm(None, tp)
+        # TP prefill: two batch halves interleaved so each o / down all-reduce overlaps the other
+        # half's compute (_prefill_overlapped); MLS_TP_OVERLAP=0 runs the plain layer loop
+        self.tp_overlap = os.environ.get("MLS_TP_OVERLAP", "1") == "1"
         self.backend = backend
         self.device = torch.device(device)
         self.max_batch, self.max_seq = max_batch, max_seq
@@ -647,7 +693,11 @@ class LlamaTP:
                              residual_out=None if d is None else x, eps=eps)
             return ops.linear(xn, w, act=act, workspace=ws), x
 
-        for i in range(cfg.layers):
+        overlap = (not decode and self.tp > 1 and B >= 2 and T >= 64 and self.tp_overlap
+                   and not torch.cuda.is_current_stream_capturing())
+        if overlap:
+            r, delta = self._prefill_overlapped(r, pos, lens, B, S, explicit_slots, pre_norm, linear)
+        for i in range(0 if not overlap else cfg.layers, cfg.layers):
             qkv, r = pre_norm(r, f"l{i}.qkv", delta)
             parts = None
             if decode:  # RoPE + KV append ride inside the decode-attention launch
@@ -701,6 +751,51 @@ class LlamaTP:
             xn = ops.rmsnorm(delta, self.ones, residual=r, eps=eps)
             logits = ops.linear(xn, p["lm_head"], workspace=ws, impl="native" if B <= 64 else "auto")
         return self._local_topk(logits, k)
+
+    def _prefill_overlapped(self, r, pos, lens, B: int, S: int, explicit_slots, pre_norm, linear):
+        """TP prefill as two batch halves (micro-batches) interleaved layer by layer so that every
+        o / down all-reduce runs while the other half computes:
+
+            half 0: norm+QKV, RoPE/KV, attention, o -> start AR(o0)
+            half 1: norm+QKV, RoPE/KV, attention, o -> start AR(o1)     [overlaps AR(o0)]
+            half 0: wait AR(o0), norm+gate/up, down -> start AR(d0)     [overlaps AR(o1)]
+            half 1: wait AR(o1), norm+gate/up, down -> start AR(d1)     [overlaps AR(d0)]
+            next layer, half 0 waits AR(d0)                             [overlaps AR(d1)]
+
+        The residual stream rows of each half are updated in place (views of ``r``); returns the
+        full residual and the last layer's all-reduced delta."""
+        ops, cfg, sd = self.ops, self.cfg, self.sd
+        D = cfg.head_dim
+        if explicit_slots is None:  # plain cache: the token -> cache row map of rope_kv_'s implicit mode
+            b = torch.arange(B, device=r.device, dtype=torch.int64).repeat_interleave(S)
+            pl = pos.long()
+            valid = pl < lens.long()[b]
+            explicit_slots = torch.where(valid, b * self.max_seq + pl, torch.full_like(pl, -1)).to(torch.int32)
+        half = B // 2
+        parts = [(0, half), (half, B)]
+        res = [r[b0 * S:b1 * S] for b0, b1 in parts]
+        dlt = [None, None]
+        pend_d = [None, None]
+        for i in range(cfg.layers):
+            pend_o = [None, None]
+            for m, (b0, b1) in enumerate(parts):
+                lo, hi = b0 * S, b1 * S
+                if pend_d[m] is not None:
+                    dlt[m] = pend_d[m].wait()
+                qkv, res[m] = pre_norm(res[m], f"l{i}.qkv", dlt[m])
+                ops.rope_kv_(qkv, pos[lo:hi], self.cos, self.sin, sd.hq, sd.hkv, D, explicit_slots[lo:hi],
+                             self.k_cache[i], self.v_cache[i], lens=lens[b0:b1], seq=S, max_seq=self.max_seq,
+                             hm_rows=self.kv_hm_rows)
+                a = ops.flash_attention(qkv, b1 - b0, S, sd.hq, sd.hkv, D, kv_lens=lens[b0:b1], causal=True)
+                pend_o[m] = self.comm.all_reduce_start(linear(a, f"l{i}.o"))
+            for m in range(2):
+                o = pend_o[m].wait()
+                gu, res[m] = pre_norm(res[m], f"l{i}.gate_up", o, act=ops.ACT_SILU_MUL)
+                pend_d[m] = self.comm.all_reduce_start(linear(gu, f"l{i}.down"))
+        dlt = [p.wait() for p in pend_d]
+        if any(x.data_ptr() != y.data_ptr() for x, y in zip(res, (r[:half * S], r[half * S:]))):
+            r = torch.cat(res)  # pre_norm handed back new residual tensors instead of the views
+        return r, torch.cat(dlt)
 
     # ---------------------------------------------------------------- public
     @torch.no_grad()

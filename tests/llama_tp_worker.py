@@ -24,6 +24,12 @@ def main():
     vals, idx = m.step(ids.cuda(), pos, lens.cuda(), decode=False, k=8)
     allv = m.comm.all_gather(vals)
     alli = m.comm.all_gather(idx)
+    # the overlapped TP prefill (two batch halves, all-reduces started early) vs the plain layer loop
+    overlap_on = m.tp_overlap
+    m.tp_overlap = False
+    vals0, idx0 = m.step(ids.cuda(), pos, lens.cuda(), decode=False, k=8)
+    m.tp_overlap = overlap_on
+    overlap_diff = float((vals0.float() - vals.float()).abs().max())
     failed = ""
     stall_rank = int(os.environ.get("STALL_RANK", "-1"))
     if stall_rank >= 0:
@@ -56,7 +62,8 @@ def main():
                          len(calls)])
     if m.comm.car is not None:
         info[1] += 10 * m.comm.car.errors()  # peer-wait timeouts would show here
-    torch.save({"tokens": out.cpu(), "vals": allv.cpu(), "idx": alli.cpu(), "info": info, "failed": failed},
+    torch.save({"tokens": out.cpu(), "vals": allv.cpu(), "idx": alli.cpu(), "info": info, "failed": failed,
+                "overlap_diff": overlap_diff},
                os.environ["OUT"] + f".{rank}.pt")
     dist.destroy_process_group()
 

@@ -35,7 +35,16 @@ def _worker(rank, world, port, q):
         healthy_all = mdist.all_reduce_health(True)
         healthy_one_bad = mdist.all_reduce_health(rank != 1)
         mx = mdist.max_over_ranks(float(rank))
-        q.put((rank, ok, ok2, healthy_all, healthy_one_bad, mx))
+        # TPComm's split all-reduce (start now, wait later: the TP prefill overlap's primitive)
+        from mlmicroservicetemplate_amd.models.llama import TPComm, _ARPending
+
+        comm = TPComm(None, world)
+        t = torch.full((1000,), float(rank + 1))
+        h = comm.all_reduce_start(t)
+        busy = torch.randn(200, 200) @ torch.randn(200, 200)  # independent work while it flies
+        red = h.wait()
+        ok3 = isinstance(h, _ARPending) and red is t and bool((red == world * (world + 1) / 2).all()) and busy.numel() > 0
+        q.put((rank, ok and ok3, ok2, healthy_all, healthy_one_bad, mx))
     finally:
         mdist.destroy()
 

@@ -1,7 +1,9 @@
 """§5.2 race detection for the native host runtime: the engine's staging pool
 (engine/csrc/staging_core.h) built with ThreadSanitizer and with AddressSanitizer +
-UndefinedBehaviorSanitizer and driven from several submitter threads (tests/native/staging_sanitize.cpp).
-Host code only -- GPU sanitizers are not available on the test pool."""
+UndefinedBehaviorSanitizer and driven from several submitter threads (tests/native/staging_sanitize.cpp);
+the front end's JPEG coefficient decoder (frontend/csrc/jpeg_coefs.h) mutation-fuzzed under
+ASan + UBSan (tests/native/jpeg_fuzz.cpp).  Host code only -- GPU sanitizers are not available on
+the test pool."""
 import os
 import shutil
 import subprocess
@@ -26,3 +28,33 @@ def test_staging_pool_under_sanitizer(tmp_path, san):
                ASAN_OPTIONS="detect_leaks=1:halt_on_error=1:verify_asan_link_order=0", UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
     run = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=240)
     assert run.returncode == 0 and "staging sanitize: ok" in run.stdout, (run.stdout[-2000:], run.stderr[-6000:])
+
+
+@pytest.mark.timeout(300)
+def test_jpeg_decoder_fuzz_under_asan_ubsan(tmp_path):
+    cxx = shutil.which("g++") or shutil.which("clang++")
+    if cxx is None:
+        pytest.skip("no host C++ compiler")
+    import numpy as np
+
+    from test_image_decode import jpeg, photo
+
+    files = []
+    for i, kw in enumerate([dict(quality=90, subsampling=2), dict(quality=75, subsampling=0),
+                            dict(quality=90, subsampling=2, restart_marker_blocks=2), dict(quality=85, mode="L")]):
+        pth = tmp_path / f"f{i}.jpg"
+        pth.write_bytes(jpeg(photo(96 + 16 * i, 80, seed=i), **kw))
+        files.append(str(pth))
+    noise = tmp_path / "noise.jpg"
+    noise.write_bytes(jpeg(np.random.default_rng(0).integers(0, 256, (64, 80, 3), dtype=np.uint8), quality=95))
+    files.append(str(noise))
+    exe = str(tmp_path / "jpeg_fuzz")
+    inc = os.path.join(os.path.dirname(HERE), "mlmicroservicetemplate_amd", "frontend", "csrc")
+    build = subprocess.run([cxx, "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined",
+                            "-fno-omit-frame-pointer", "-I", inc, os.path.join(HERE, "native", "jpeg_fuzz.cpp"), "-o", exe],
+                           capture_output=True, text=True)
+    assert build.returncode == 0, build.stderr[-4000:]
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:halt_on_error=1:verify_asan_link_order=0",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    run = subprocess.run([exe, *files], capture_output=True, text=True, env=env, timeout=240)
+    assert run.returncode == 0 and "jpeg fuzz: ok" in run.stdout, (run.stdout[-2000:], run.stderr[-6000:])

@@ -53,6 +53,18 @@ SCRIPT = textwrap.dedent("""
     b = comm._broadcast(x[:3].clone(), 0)
     assert torch.equal(b, x[:3])
     stage("tpcomm")
+    # split all-reduce on the RCCL stream (the TP prefill overlap's primitive): start, queue
+    # independent work on the compute stream, wait; tp=2 forces the async path on the world-1 group
+    from mlmicroservicetemplate_amd.models.llama import _ARPending
+    comm2 = TPComm(None, 2, device=dev, custom_ar=False)
+    big = torch.randn(1024, 4096, device=dev).to(torch.bfloat16)
+    want = big.clone()
+    h = comm2.all_reduce_start(big)
+    z = torch.randn(2048, 2048, device=dev) @ torch.randn(2048, 2048, device=dev)
+    red = h.wait()
+    torch.cuda.synchronize()
+    assert isinstance(h, _ARPending) and red is big and torch.equal(red, want) and z.isfinite().all()
+    stage("async all-reduce")
     # RCCL inside a captured hipGraph (thread_local capture mode: the watchdog thread polls)
     s = torch.cuda.Stream()
     buf = torch.ones(8192, device=dev)
