@@ -35,32 +35,45 @@ struct Hdr {
 MLS_DEV uint32_t rd32(const uint8_t* p) { return p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24); }
 MLS_DEV int rd16(const uint8_t* p) { return p[0] | (p[1] << 8); }
 
-MLS_DEV Hdr parse(const uint8_t* c, long scratch_per_image) {
+MLS_DEV Hdr parse(const uint8_t* c0, long scratch_per_image) {
+  // the 64-B header in four 16-B loads (the container base is 16-B aligned), every field picked from
+  // those registers at a constant offset: ~40 byte loads per thread before, and no private array
+  const uint4* p4 = reinterpret_cast<const uint4*>(c0);
+  const uint4 q[4] = {p4[0], p4[1], p4[2], p4[3]};
+  auto b8 = [&](int off) -> int {
+    const uint4 v = q[off >> 4];
+    const int w = (off >> 2) & 3;
+    const uint32_t d = w == 0 ? v.x : w == 1 ? v.y : w == 2 ? v.z : v.w;
+    return (int)((d >> (8 * (off & 3))) & 0xFF);
+  };
+  auto r16 = [&](int off) { return b8(off) | (b8(off + 1) << 8); };
+  auto r32 = [&](int off) { return (uint32_t)r16(off) | ((uint32_t)r16(off + 2) << 16); };
   Hdr h;
-  h.ok = rd32(c) == IMG_MAGIC;
-  h.kind = rd32(c + 4);
-  h.W = rd16(c + 8);
-  h.H = rd16(c + 10);
-  h.nc = c[12];
-  h.s = c[13];
-  h.hmax = c[14];
-  h.vmax = c[15];
+  h.ok = r32(0) == IMG_MAGIC;
+  h.kind = r32(4);
+  h.W = r16(8);
+  h.H = r16(10);
+  h.nc = b8(12);
+  h.s = b8(13);
+  h.hmax = b8(14);
+  h.vmax = b8(15);
   long plane_px = 0;
+#pragma unroll
   for (int i = 0; i < 3; ++i) {
-    const uint8_t* q = c + 16 + 10 * i;
-    h.ch[i] = q[0];
-    h.cv[i] = q[1];
-    h.bw[i] = rd16(q + 2);
-    h.bh[i] = rd16(q + 4);
-    h.first[i] = (int)rd32(q + 6);
+    const int o = 16 + 10 * i;
+    h.ch[i] = b8(o);
+    h.cv[i] = b8(o + 1);
+    h.bw[i] = r16(o + 2);
+    h.bh[i] = r16(o + 4);
+    h.first[i] = (int)r32(o + 6);
     if (i < h.nc) plane_px += (long)h.bw[i] * h.bh[i] * h.s * h.s;
   }
-  h.rw = rd16(c + 46);
-  h.rh = rd16(c + 48);
-  h.left = rd16(c + 50);
-  h.top = rd16(c + 52);
-  h.nblocks = rd32(c + 55);
-  h.entries_off = rd32(c + 59);
+  h.rw = r16(46);
+  h.rh = r16(48);
+  h.left = r16(50);
+  h.top = r16(52);
+  h.nblocks = r32(55);
+  h.entries_off = r32(59);
   if (h.kind == 1) {
     const bool sgood = h.s == 1 || h.s == 2 || h.s == 4 || h.s == 8;
     const long need = plane_px + (long)h.W * h.H * 3 + (long)h.H * IMG_OUT * 3;
@@ -68,24 +81,38 @@ MLS_DEV Hdr parse(const uint8_t* c, long scratch_per_image) {
            need <= scratch_per_image && h.rw >= IMG_OUT && h.rh >= IMG_OUT && h.left + IMG_OUT <= h.rw &&
            h.top + IMG_OUT <= h.rh && 384 + 4 * (((long)h.nblocks + 63) / 64) + (long)h.nblocks <= (long)h.entries_off &&
            h.entries_off <= IMG_PAYLOAD;
-    for (int i = 0; i < h.nc && h.ok; ++i)
-      h.ok = h.ch[i] >= 1 && h.cv[i] >= 1 && (long)h.first[i] + (long)h.bw[i] * h.bh[i] <= (long)h.nblocks &&
-             h.bw[i] * h.s >= (h.W * h.ch[i] + h.hmax - 1) / h.hmax && h.bh[i] * h.s >= (h.H * h.cv[i] + h.vmax - 1) / h.vmax;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)  // constant indices: the header stays in registers
+      if (i < h.nc)
+        h.ok = h.ok && h.ch[i] >= 1 && h.cv[i] >= 1 && (long)h.first[i] + (long)h.bw[i] * h.bh[i] <= (long)h.nblocks &&
+               h.bw[i] * h.s >= (h.W * h.ch[i] + h.hmax - 1) / h.hmax &&
+               h.bh[i] * h.s >= (h.H * h.cv[i] + h.vmax - 1) / h.vmax;
   }
   return h;
 }
 
 // scratch layout per image: planes (component-major), then RGB [H][W][3], then hpass [H][224][3]
+// component-indexed header fields with a runtime index, kept in registers (a dynamically indexed
+// struct array goes to scratch memory)
+MLS_DEV int at3(const int (&a)[3], int i) { return i == 0 ? a[0] : i == 1 ? a[1] : a[2]; }
+
 MLS_DEV long plane_off(const Hdr& h, int comp) {
   long o = 0;
-  for (int i = 0; i < comp; ++i) o += (long)h.bw[i] * h.bh[i] * h.s * h.s;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    if (i < comp) o += (long)h.bw[i] * h.bh[i] * h.s * h.s;
   return o;
 }
 MLS_DEV long rgb_off(const Hdr& h) { return plane_off(h, h.nc); }
 MLS_DEV long hp_off(const Hdr& h) { return rgb_off(h) + (long)h.W * h.H * 3; }
 
-// ---- 1. IDCT: 4 blocks per 256-thread workgroup, one 64-lane slot each (grid-stride over the
-// image's blocks: the launch geometry is fixed, so it can be captured once for any container) ----
+// ---- 1. IDCT: 4 blocks per 256-thread workgroup, one 64-lane wave each (grid-stride over the
+// image's blocks: the launch geometry is fixed, so it can be captured once for any container).
+// Entry parsing is wave-parallel: the block's first unit = its group's start + an in-wave sum of the
+// group's earlier counts (one coalesced byte load per lane); each lane takes one 2-byte unit, and
+// the rare escapes (0x80 marker + an int16 in the next unit) are resolved on the ballot mask of
+// marker candidates -- a lane-0 scan of up to 63 counts and every entry (dependent byte loads)
+// measured ~70 % of this kernel before ----
 constexpr int IDCT_WG = 64;  // workgroups per image
 __global__ __launch_bounds__(256) void img_idct_kernel(const uint8_t* __restrict__ cont, uint8_t* __restrict__ scratch,
                                                        long scratch_per_image) {
@@ -93,66 +120,85 @@ __global__ __launch_bounds__(256) void img_idct_kernel(const uint8_t* __restrict
   const uint8_t* c = cont + (long)b * IMG_CONTAINER;
   __shared__ double F[4][64];
   __shared__ double T[4][64];
+  __shared__ double Mc[64];  // IDCT basis of this image's scale: Mc[x * s + u] = c(u)/2 cos((2x+1)u pi / 2s)
   const Hdr h = parse(c, scratch_per_image);
   if (!h.ok || h.kind != 1) return;
   const int slot = threadIdx.x >> 6, t = threadIdx.x & 63;
   const int s = h.s, ss = s * s;
   const int y = t / s, x = t - y * s;  // pass 1: thread = (v, x); pass 2: (y, x)
   const double PI = 3.14159265358979323846;
+  if (threadIdx.x < ss) {  // once per workgroup, not once per multiply (fp64 cos is a long software routine)
+    const int xx = threadIdx.x / s, uu = threadIdx.x - xx * s;
+    Mc[threadIdx.x] = (uu == 0 ? 0.70710678118654752440 : 1.0) * 0.5 * cos((2 * xx + 1) * uu * PI / (2 * s));
+  }
   uint8_t* sc = scratch + (long)b * scratch_per_image;
+  const uint8_t* pay = c + IMG_HDR;
+  const long groups = ((long)h.nblocks + 63) / 64, counts_off = 384 + 4 * groups;
+  const long cap = (IMG_PAYLOAD - (long)h.entries_off) / 2;  // units that fit the container
+  const uint8_t* ent = pay + h.entries_off;
   const long stride = (long)gridDim.x * 4;
   for (long base = (long)blockIdx.x * 4; base < (long)h.nblocks; base += stride) {  // uniform per workgroup
     const long blk = base + slot;
-    const bool live = blk < (long)h.nblocks;
+    const bool live = blk < (long)h.nblocks;  // uniform per wave
     F[slot][t] = 0.0;
-    int comp = 0;
-    while (comp + 1 < h.nc && blk >= h.first[comp + 1]) ++comp;
+    const int comp = (h.nc > 2 && blk >= h.first[2]) ? 2 : (h.nc > 1 && blk >= h.first[1]) ? 1 : 0;
     __syncthreads();
-    if (live && t == 0) {
-      // compact entries (jpeg_coefs.h): units of this block start at gstart[blk / 64] + the counts of
-      // the group's earlier blocks; int8 value x quantisation step, or the (0x80, pos) + int16 escape
-      const uint8_t* pay = c + IMG_HDR;
-      const long groups = ((long)h.nblocks + 63) / 64, counts_off = 384 + 4 * groups;
+    if (live) {
       const long g = blk >> 6;
-      long u = rd32(pay + 384 + 4 * g);
-      for (long k = g * 64; k < blk; ++k) u += pay[counts_off + k];
-      const long end = u + pay[counts_off + blk];
-      const long cap = (IMG_PAYLOAD - (long)h.entries_off) / 2;
-      const uint8_t* ent = pay + h.entries_off;
-      while (u < end && u < cap) {
-        int v = (int)(int8_t)ent[2 * u];
-        const int pos = ent[2 * u + 1];
-        if (v == -128) {
-          if (u + 1 >= cap) break;
-          v = (int)(int16_t)(ent[2 * u + 2] | (ent[2 * u + 3] << 8));
-          u += 2;
-        } else {
-          u += 1;
+      const int k = (int)(blk & 63);
+      // units before this block in its group: sum of counts[g*64 + L] over lanes L < k
+      int before = t < k ? pay[counts_off + g * 64 + t] : 0;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) before += __shfl_xor(before, o);
+      const long u0 = (long)rd32(pay + 384 + 4 * g) + before;
+      const int n = pay[counts_off + blk];
+      bool carry = false;  // the previous chunk ended on a marker: this chunk's unit 0 is its payload
+      for (int c0 = 0; c0 < n; c0 += 64) {
+        const long u = u0 + c0 + t;
+        const bool in = c0 + t < n && u < cap;
+        const int b0 = in ? ent[2 * u] : 0, b1 = in ? ent[2 * u + 1] : 0;
+        // true markers among the candidates (a payload unit is never a marker): scan the set bits
+        unsigned long long cand = __ballot(in && b0 == 0x80), mk = 0;
+        if (carry) cand &= ~1ull;
+        while (cand) {
+          const int q = __builtin_ctzll(cand);
+          mk |= 1ull << q;
+          cand &= q >= 62 ? 0ull : ~0ull << (q + 2);
         }
-        if (pos < ss) F[slot][pos] = (double)v * (double)rd16(pay + 2 * (comp * 64 + pos));
+        const bool is_payload = t == 0 ? carry : ((mk >> (t - 1)) & 1) != 0;
+        const bool is_marker = (mk >> t) & 1;
+        // the escape's int16 sits in the next unit -- held by lane t + 1 (chunk tail: read it)
+        const int nb0 = __shfl_down(b0, 1), nb1 = __shfl_down(b1, 1);
+        int v;
+        if (is_marker) {
+          v = t < 63 ? (int)(int16_t)(nb0 | (nb1 << 8))
+                     : (u + 1 < cap ? (int)(int16_t)(ent[2 * (u + 1)] | (ent[2 * (u + 1) + 1] << 8)) : 0);
+        } else {
+          v = (int)(int8_t)b0;
+        }
+        const int pos = b1;
+        if (in && !is_payload && pos < ss)
+          F[slot][pos] = (double)v * (double)rd16(pay + 2 * (comp * 64 + pos));
+        carry = (mk >> 63) & 1;
       }
     }
+    __syncthreads();
     if (live && t < ss) {  // T[v][x] = sum_u F[v][u] M[x][u]
       double acc = 0.0;
-      for (int u = 0; u < s; ++u) {
-        const double cu = u == 0 ? 0.70710678118654752440 : 1.0;
-        acc += F[slot][y * s + u] * (cu * 0.5 * cos((2 * x + 1) * u * PI / (2 * s)));
-      }
+      for (int u = 0; u < s; ++u) acc += F[slot][y * s + u] * Mc[x * s + u];
       T[slot][t] = acc;
     }
     __syncthreads();
     if (live && t < ss) {
       double acc = 0.0;  // P[y][x] = sum_v M[y][v] T[v][x]
-      for (int v = 0; v < s; ++v) {
-        const double cv = v == 0 ? 0.70710678118654752440 : 1.0;
-        acc += (cv * 0.5 * cos((2 * y + 1) * v * PI / (2 * s))) * T[slot][v * s + x];
-      }
+      for (int v = 0; v < s; ++v) acc += Mc[y * s + v] * T[slot][v * s + x];
       int px = (int)floor(acc + 128.0 + 0.5);
       px = px < 0 ? 0 : px > 255 ? 255 : px;
-      const long local = blk - h.first[comp];
-      const int row = (int)(local / h.bw[comp]), col = (int)(local - (long)row * h.bw[comp]);
-      if (row < h.bh[comp]) {
-        const long pw = (long)h.bw[comp] * s;
+      const int bwc = at3(h.bw, comp);
+      const long local = blk - at3(h.first, comp);
+      const int row = (int)(local / bwc), col = (int)(local - (long)row * bwc);
+      if (row < at3(h.bh, comp)) {
+        const long pw = (long)bwc * s;
         sc[plane_off(h, comp) + (long)(row * s + y) * pw + col * s + x] = (uint8_t)px;
       }
     }
@@ -196,8 +242,8 @@ __global__ __launch_bounds__(256) void img_color_kernel(const uint8_t* __restric
   if (!h.ok || h.kind != 1) return;
   const long n = (long)h.W * h.H;
   uint8_t* sc = scratch + (long)b * scratch_per_image;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
-    const int y = (int)(i / h.W), x = (int)(i - (long)y * h.W);
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < (int)n; i += gridDim.x * 256) {
+    const int y = i / h.W, x = i - y * h.W;
     const uint8_t* p0 = sc + plane_off(h, 0);
     const int Y = p0[(long)y * h.bw[0] * h.s + x];
     int r, g, bb;
@@ -219,6 +265,7 @@ __global__ __launch_bounds__(256) void img_color_kernel(const uint8_t* __restric
 
 // Pillow precompute_coeffs (bilinear) for output index xx: first source index, taps, fixed weights
 constexpr int MAX_TAPS = 33;
+template <int KSTRIDE = 1>  // kk[j * KSTRIDE]: 1 for one set, IMG_OUT for the hpass's per-column sets in LDS
 MLS_DEV int pil_coeffs(int in_size, int out_size, int xx, int* kk) {
   const double scale = (double)in_size / (double)out_size;
   const double filterscale = scale < 1.0 ? 1.0 : scale;
@@ -231,19 +278,20 @@ MLS_DEV int pil_coeffs(int in_size, int out_size, int xx, int* kk) {
   if (xmax > in_size) xmax = in_size;
   xmax -= xmin;
   if (xmax > MAX_TAPS) xmax = MAX_TAPS;
-  double k[MAX_TAPS];
-  double ww = 0.0;
-  for (int x = 0; x < xmax; ++x) {
+  // two passes recomputing the triangle weight (no local double array: it would live in scratch)
+  auto tri = [&](int x) {
     double t = (x + xmin - center + 0.5) * ss;
     t = t < 0 ? -t : t;
-    k[x] = t < 1.0 ? 1.0 - t : 0.0;
-    ww += k[x];
-  }
+    return t < 1.0 ? 1.0 - t : 0.0;
+  };
+  double ww = 0.0;
+  for (int x = 0; x < xmax; ++x) ww += tri(x);
   for (int x = 0; x < xmax; ++x) {
-    const double v = (ww != 0.0 ? k[x] / ww : k[x]) * (double)(1 << PRECISION_BITS);
-    kk[x] = v < 0 ? (int)(v - 0.5) : (int)(v + 0.5);
+    const double k = tri(x);
+    const double v = (ww != 0.0 ? k / ww : k) * (double)(1 << PRECISION_BITS);
+    kk[x * KSTRIDE] = v < 0 ? (int)(v - 0.5) : (int)(v + 0.5);
   }
-  kk[MAX_TAPS - 1] = xmax;  // tap count rides in the last slot
+  kk[(MAX_TAPS - 1) * KSTRIDE] = xmax;  // tap count rides in the last slot
   return xmin;
 }
 
@@ -270,16 +318,20 @@ __global__ __launch_bounds__(256) void img_hpass_kernel(const uint8_t* __restric
       for (int ch = 0; ch < 3; ++ch) hp[((long)y * IMG_OUT + ox) * 3 + ch] = rgb[((long)y * h.W + x) * 3 + ch];
     return;
   }
-  int kk[MAX_TAPS];
-  const int xmin = pil_coeffs(h.W, h.rw, x, kk);
-  const int taps = kk[MAX_TAPS - 1];
+  // this column's taps in LDS ([tap][column]: lanes read consecutive words), not a per-thread array
+  // (dynamically indexed -> scratch memory)
+  __shared__ int kks[MAX_TAPS * IMG_OUT];
+  int* kk = kks + ox;
+  const int xmin = pil_coeffs<IMG_OUT>(h.W, h.rw, x, kk);
+  const int taps = kk[(MAX_TAPS - 1) * IMG_OUT];
   for (int y = blockIdx.x; y < h.H; y += gridDim.x) {
     long a0 = 1L << (PRECISION_BITS - 1), a1 = a0, a2 = a0;
     const uint8_t* r = rgb + ((long)y * h.W + xmin) * 3;
     for (int j = 0; j < taps; ++j) {
-      a0 += (long)r[3 * j] * kk[j];
-      a1 += (long)r[3 * j + 1] * kk[j];
-      a2 += (long)r[3 * j + 2] * kk[j];
+      const long w = kk[j * IMG_OUT];
+      a0 += (long)r[3 * j] * w;
+      a1 += (long)r[3 * j + 1] * w;
+      a2 += (long)r[3 * j + 2] * w;
     }
     uint8_t* o = hp + ((long)y * IMG_OUT + ox) * 3;
     o[0] = clip8(a0);
@@ -301,9 +353,10 @@ __global__ __launch_bounds__(256) void img_vpass_kernel(const uint8_t* __restric
     if (threadIdx.x == 0 && oy == 0 && err) atomicOr(err, 1);
     return;
   }
-  if (h.kind == 0) {
-    for (int i = threadIdx.x; i < IMG_OUT * 3; i += 256)
-      o[(long)oy * IMG_OUT * 3 + i] = c[IMG_HDR + (long)oy * IMG_OUT * 3 + i];
+  if (h.kind == 0) {  // a row is 672 B = 42 x 16 B; the container payload starts 64-B aligned
+    const uint4* src = reinterpret_cast<const uint4*>(c + IMG_HDR + (long)oy * IMG_OUT * 3);
+    uint4* dst = reinterpret_cast<uint4*>(o + (long)oy * IMG_OUT * 3);
+    if (threadIdx.x < IMG_OUT * 3 / 16) dst[threadIdx.x] = src[threadIdx.x];
     return;
   }
   const uint8_t* hp = scratch + (long)b * scratch_per_image + hp_off(h);
