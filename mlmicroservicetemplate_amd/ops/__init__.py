@@ -312,7 +312,7 @@ def gemm(
 
 GEMM_TILE_CFGS = {1: (256, 256), 2: (256, 128), 3: (128, 128), 4: (128, 128), 5: (128, 256), 6: (256, 256),
                   7: (256, 128), 8: (256, 256), 9: (256, 128), 10: (256, 256), 11: (256, 256), 12: (256, 128),
-                  15: (256, 256), 16: (256, 128)}
+                  15: (256, 256), 16: (256, 128), 21: (192, 192), 22: (192, 192)}
 
 
 _SPLIT_COUNTERS: Dict[Tuple[int, int], torch.Tensor] = {}

@@ -831,6 +831,7 @@ struct GtCfg {
 //   8: 256x256 ping-pong (gemm_pp_kernel), 2 x 64, 128 KB    9: 256x128 ping-pong, 2 x 64, 96 KB
 //  10: 256x256 ring (gemm_ring_kernel), 5 x 32, 160 KB      11: 256x256 ring, 4 x 32, 128 KB
 //  12: 256x128 ring, 6 x 32, 144 KB
+//  21: 192x192, 8 waves 4x2, 3 x 64, 144 KB (a 3-deep ring at ~the 256^2 tile's reuse)   22: + PIPE
 GtCfg gt_cfg(int cfg) {
   switch (cfg) {
     case 1: return {256, 256, 512};
@@ -853,6 +854,8 @@ GtCfg gt_cfg(int cfg) {
     case 18: return {256, 128, 512};
     case 19: return {256, 256, 512};
     case 20: return {256, 256, 512};
+    case 21: return {192, 192, 512};
+    case 22: return {192, 192, 512};
     default: return {0, 0, 0};
   }
 }
@@ -907,6 +910,8 @@ int gt_launch(const GemmTileArgs& g0, int cfg, int grid_cap, hipStream_t st) {
     case 18: hipLaunchKernelGGL((gemm_tile_kernel<256, 128, 4, 2, 3, 64, true, true>), grid, block, 0, st, g); break;
     case 19: hipLaunchKernelGGL((gemm_tile_kernel<256, 256, 2, 4, 2, 64, false, false, true>), grid, block, 0, st, g); break;
     case 20: hipLaunchKernelGGL((gemm_tile_kernel<256, 256, 2, 4, 2, 64, true, false, true>), grid, block, 0, st, g); break;
+    case 21: hipLaunchKernelGGL((gemm_tile_kernel<192, 192, 4, 2, 3, 64>), grid, block, 0, st, g); break;
+    case 22: hipLaunchKernelGGL((gemm_tile_kernel<192, 192, 4, 2, 3, 64, false, true>), grid, block, 0, st, g); break;
   }
   return hipGetLastError() == hipSuccess ? MLS_OK : MLS_BAD_ARG;
 }

@@ -19,7 +19,7 @@ def _cfgs():
     return sorted(c for c in ops.GEMM_TILE_CFGS if c != 8)  # 8: ping-pong reference variant, spills
 
 
-@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6, 7, 9, 10, 11, 12, 15, 16])
+@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6, 7, 9, 10, 11, 12, 15, 16, 21, 22])
 @pytest.mark.parametrize("M,N,K,cap", [(300, 528, 192, 0), (1024, 1280, 512, 3), (4096, 768, 768, 0)])
 def test_gemm_tile_epilogues(cfg, M, N, K, cap):
     from mlmicroservicetemplate_amd import ops
