@@ -73,7 +73,10 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=32)
-    ap.add_argument("--inflight", type=int, default=int(os.environ.get("INFLIGHT", 5)))
+    ap.add_argument("--inflight", type=int, default=int(os.environ.get("INFLIGHT", 0)),
+                    help="batches in flight per GPU (0 = 4 with CU partitions, else 5)")
+    ap.add_argument("--cu-partition", type=int, default=int(os.environ.get("MLS_CU_PARTITION", 2)),
+                    help="spatial partitions of the CUs for the in-flight batches (engine/worker.py; 0 = off)")
     ap.add_argument("--backend", default="fused", choices=["fused", "eager"])
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--serial", action="store_true", help="one compute stream (no concurrent in-flight batches)")
@@ -140,8 +143,13 @@ def run_rank(args) -> int:
     t_bcast = time.perf_counter() - t0
 
     fwd = build_model(args.backend, device, args.batch, params)
+    if args.inflight <= 0:
+        args.inflight = 4 if args.cu_partition and not args.serial else 5
     engine = GpuEngine(fwd, device, (224, 224, 3), torch.uint8, buckets=[args.batch], inflight=args.inflight,
-                       use_graphs=not args.no_graphs, name=f"resnet50.r{info.rank}", concurrent=not args.serial)
+                       use_graphs=not args.no_graphs, name=f"resnet50.r{info.rank}", concurrent=not args.serial,
+                       cu_partitions=0 if args.serial else args.cu_partition)
+    args.inflight = engine.inflight  # a partitioned engine caps its slots at the hardware queues
+    cu_parts = engine.cu_partitions
     engine.warmup(capture=not args.no_graphs)
 
     rng = np.random.default_rng(1234 + info.rank)
@@ -206,7 +214,8 @@ def run_rank(args) -> int:
     if args.measure_eager > 0:  # stock-PyTorch engine, same process / box / protocol (not the flagship)
         efwd = build_model("eager", device, args.batch, params)
         eeng = GpuEngine(efwd, device, (224, 224, 3), torch.uint8, buckets=[args.batch], inflight=args.inflight,
-                         use_graphs=not args.no_graphs, name=f"eager.r{info.rank}", concurrent=not args.serial)
+                         use_graphs=not args.no_graphs, name=f"eager.r{info.rank}", concurrent=not args.serial,
+                         cu_partitions=0 if args.serial else args.cu_partition)
         eeng.warmup(capture=not args.no_graphs)
         engine = eeng
         run_steps(min(args.warmup, 5), [])
@@ -235,7 +244,7 @@ def run_rank(args) -> int:
             "config": {"model": "resnet50-v1.5", "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "seq_len": None, "image_size": 224, "parallelism": f"dp{world}",
                        "backend": args.backend, "hipgraph": not args.no_graphs, "inflight": args.inflight,
-                           "concurrent_slots": not args.serial},
+                       "concurrent_slots": not args.serial, "cu_partitions": cu_parts},
             "p50_latency_ms": round(p50_max, 3),
             "p99_latency_ms": round(p99_max, 3),
             "per_gpu_requests_per_s": round(value / world, 1),

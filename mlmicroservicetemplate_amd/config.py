@@ -171,6 +171,7 @@ class Settings:
     USE_GRAPHS: bool = True
     INFLIGHT: int = 5  # batches in flight per GPU worker: H2D/compute/D2H overlap + co-running graphs (r1 sweep)
     CONCURRENT_SLOTS: bool = True  # in-flight batches co-run on per-slot streams (+26 % ResNet-50 req/s)
+    CU_PARTITION: int = 2  # ResNet-50 engine: slot streams CU-masked into this many halves (0 = off; engine/worker.py)
     REQUEST_TIMEOUT_S: float = 30.0
     WATCHDOG_INTERVAL_S: float = 1.0  # replica liveness check period (0 disables the watchdog)
     WATCHDOG_STALL_S: float = 30.0  # a batch running longer than this drains its replica

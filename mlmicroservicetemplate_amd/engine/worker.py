@@ -100,6 +100,7 @@ class GpuEngine:
         concurrent: bool = False,
         stage_workers: Optional[int] = None,
         copies_on_slot_stream: Optional[bool] = None,
+        cu_partitions: Optional[int] = None,
     ):
         self.forward = forward
         self.device = torch.device(device)
@@ -110,6 +111,34 @@ class GpuEngine:
         self.inflight = max(1, int(inflight))
         self.use_graphs = use_graphs
         self.concurrent = bool(concurrent) and self.inflight > 1
+        # Spatial partitioning (cu_partitions / MLS_CU_PARTITION = 2, 4 or 8; 0 = off): concurrent
+        # slot i's stream is CU-masked to partition i % P (ops.partition_masks, csrc/partition.hip):
+        # with MLS_CU_PARTITION_MODE=intra (default) every partition holds 1 / P of the CUs of every
+        # XCD (a CU mask cannot confine a queue to whole XCDs: an XCD left without mask bits runs on
+        # all its CUs -- profiles/r3_cu_mask_census.txt).  Two halves x 2 batches each, unpaced:
+        # ResNet-50 bs=32 54.5-55.6k vs 52.8-53.1k req/s at 200 steps, 49.3-51.4k vs 48.0-49.6k at 20,
+        # p50 2.2-2.3 vs 2.55-2.8 ms (profiles/r3_cu_partition_ab.jsonl): the two batches of a half
+        # co-run on 128 CUs instead of five interleaving over 256.  A masked stream holds its own
+        # hardware queue, so a partitioned engine keeps at most MLS_HW_QUEUES (4) slots -- 5-8
+        # masked slots measured 35-44k.
+        if cu_partitions is None:
+            cu_partitions = int(os.environ.get("MLS_CU_PARTITION", "0"))
+        self.cu_partitions = int(cu_partitions) if self.concurrent else 0
+        part_masks = None
+        if self.cu_partitions:
+            from .. import ops
+
+            part_masks = ops.partition_masks(self.cu_partitions, self.device,
+                                             mode=os.environ.get("MLS_CU_PARTITION_MODE", "intra"))
+            if part_masks is None:
+                logger.warning("%s: CU partitioning unavailable (mask not verified); slots use all CUs", name)
+                self.cu_partitions = 0
+            else:
+                hwq = int(os.environ.get("MLS_HW_QUEUES", "4"))
+                if self.inflight > hwq:
+                    logger.info("%s: %d partitions -> %d slots in flight (one hardware queue each)", name,
+                                self.cu_partitions, hwq)
+                    self.inflight = hwq
         # concurrent slots: a slot's H2D and D2H ride its own compute stream instead of the shared
         # copy streams (those share the 4 hardware queues with the slot streams).  With native
         # staging + launch pacing this is +3-4 % req/s on ResNet-50 (20 steps 47.2-48.3k vs
@@ -134,14 +163,16 @@ class GpuEngine:
         # the previous launch.  The estimate shrinks when pacing shortens the latency, so it cannot
         # run away (an estimate from observed completion intervals does: pacing stretches them).
         # MLS_LAUNCH_PACE=0 disables, MLS_LAUNCH_GAP_US=<us> fixes the gap instead.
-        self._pace = float(os.environ.get("MLS_LAUNCH_PACE", "1.0"))
+        # (partitioned engines run unpaced unless MLS_LAUNCH_PACE says otherwise: each half holds
+        # only two batches, and pacing measured level-to-worse there)
+        self._pace = float(os.environ.get("MLS_LAUNCH_PACE", "0" if self.cu_partitions else "1.0"))
         self._fixed_gap_s = float(os.environ.get("MLS_LAUNCH_GAP_US", "0")) * 1e-6
         self._last_launch = 0.0
         self._lat_s = 0.0  # EWMA of launch -> done latency
         self._lat_n = 0  # completions seen
         self._pace_lock = threading.Lock()
         # pace only with at least this many other batches in flight (default: inflight - 2)
-        self._pace_min_busy = int(os.environ.get("MLS_PACE_MIN_BUSY", "0")) or max(1, int(inflight) - 2)
+        self._pace_min_busy = int(os.environ.get("MLS_PACE_MIN_BUSY", "0")) or max(1, self.inflight - 2)
         self._free: "queue.Queue[_Slot]" = queue.Queue()
         self.slots: List[_Slot] = []
         self.batches = 0
@@ -165,7 +196,12 @@ class GpuEngine:
                     ev_done=torch.cuda.Event(blocking=True),
                 )
                 if self.concurrent:
-                    slot.s_comp = torch.cuda.Stream(self.device)
+                    if part_masks is not None:
+                        from .. import ops
+
+                        slot.s_comp = ops.cu_masked_stream(part_masks[i % self.cu_partitions], self.device)
+                    else:
+                        slot.s_comp = torch.cuda.Stream(self.device)
                     slot.pool = torch.cuda.graph_pool_handle() if use_graphs else None
                 else:
                     slot.s_comp = self.s_comp
@@ -361,7 +397,8 @@ class GpuEngine:
     def stats(self) -> dict:
         return {"name": self.name, "device": str(self.device), "batches": self.batches, "samples": self.samples,
                 "inflight": self.inflight, "buckets": self.buckets, "graphs": self.use_graphs,
-                "concurrent": self.concurrent, "native_staging": self._stager.native,
+                "concurrent": self.concurrent, "cu_partitions": self.cu_partitions,
+                "native_staging": self._stager.native,
                 "pace_gap_us": round(self._pace * self._lat_s / max(1, self.inflight) * 1e6, 1),
                 "healthy": self.healthy, "last_error": self.last_error,
                 "free_slots": self._free.qsize()}

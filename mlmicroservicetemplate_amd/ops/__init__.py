@@ -13,7 +13,7 @@ import ctypes
 import functools
 import json
 import os
-from typing import Dict, Optional, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 
@@ -1151,6 +1151,109 @@ def gpu_sleep(us: int, device=None) -> None:
     """Hold the current stream of ``device`` for ``us`` microseconds (fault injection in tests)."""
     dev = torch.device(device if device is not None else "cuda")
     check(lib().mls_gpu_sleep(int(us), stream_ptr(dev)), "mls_gpu_sleep")
+
+
+MASK_WORDS = 8  # 256 CUs
+
+
+def cu_masked_stream(mask: Sequence[int], device=None) -> torch.cuda.ExternalStream:
+    """A new HIP stream restricted to the CUs whose bits are set in ``mask`` (``MASK_WORDS``
+    uint32 words; csrc/partition.hip).  The native stream lives for the process."""
+    import ctypes
+
+    dev = torch.device(device if device is not None else "cuda")
+    words = (ctypes.c_uint32 * len(mask))(*[int(m) & 0xFFFFFFFF for m in mask])
+    out = ctypes.c_void_p()
+    with torch.cuda.device(dev):
+        check(lib().mls_stream_create_cumask(ctypes.cast(words, ctypes.c_void_p), len(mask), ctypes.byref(out)),
+              "mls_stream_create_cumask")
+    return torch.cuda.ExternalStream(out.value, device=dev)
+
+
+def cu_census(stream: torch.cuda.Stream, blocks: int = 2048, spin: int = 64) -> torch.Tensor:
+    """(XCC_ID, HW_ID) of the CU each of ``blocks`` blocks ran on, launched on ``stream``: int32 [blocks, 2]."""
+    out = torch.full((blocks, 2), -1, device=stream.device, dtype=torch.int32)
+    with torch.cuda.stream(stream):
+        check(lib().mls_cu_census(out.data_ptr(), blocks, spin, stream.cuda_stream), "mls_cu_census")
+    stream.synchronize()
+    return out.cpu()
+
+
+_XCD_MASKS: Dict[int, Optional[List[List[int]]]] = {}
+
+
+def xcd_cu_masks(device=None) -> Optional[List[List[int]]]:
+    """Per XCD, the CU-mask words that select exactly that XCD's CUs, verified on the device with
+    :func:`cu_census` (every block of a masked stream must report one XCC id, and the 8 masks 8
+    distinct ids).  Logical mask bit ``b`` is tried as XCD ``b % 8`` (round-robin) and as
+    ``b // 32`` (contiguous); ``None`` when neither layout verifies."""
+    dev = torch.device(device if device is not None else "cuda")
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    if key in _XCD_MASKS:
+        return _XCD_MASKS[key]
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    result = None
+    if ncu == 256:
+        for layout in ("roundrobin", "contiguous"):
+            masks = []
+            for x in range(8):
+                bits = [b for b in range(ncu) if (b % 8 if layout == "roundrobin" else b // 32) == x]
+                w = [0] * MASK_WORDS
+                for b in bits:
+                    w[b // 32] |= 1 << (b % 32)
+                masks.append(w)
+            ids = []
+            for w in masks:
+                c = cu_census(cu_masked_stream(w, dev), blocks=256)
+                ids.append(set(c[:, 0].tolist()))
+            if all(len(s) == 1 for s in ids) and len(set().union(*ids)) == 8:
+                result = masks
+                break
+    _XCD_MASKS[key] = result
+    return result
+
+
+def census_cus(c: torch.Tensor) -> set:
+    """Distinct physical CUs in a :func:`cu_census` result: (XCC, SE, SH, CU) from HW_ID bits 8-15."""
+    return {(int(x), (int(h) >> 8) & 0xFF) for x, h in c.tolist()}
+
+
+def partition_masks(parts: int, device=None, mode: str = "xcd") -> Optional[List[List[int]]]:
+    """``parts`` (1, 2, 4 or 8) CU masks.  ``mode="xcd"``: each the union of 8 / parts whole XCDs
+    (needs :func:`xcd_cu_masks`).  ``mode="intra"``: each a 1 / parts share of the CUs of EVERY
+    XCD (CU ``c`` of every XCC with ``c % parts == p``; ``"intra_contig"``: ``c // (32 / parts) ==
+    p``), verified by census to select disjoint CU sets of the expected size."""
+    if parts not in (1, 2, 4, 8):
+        raise ValueError("parts must be 1, 2, 4 or 8")
+    if mode in ("intra", "intra_contig"):
+        dev = torch.device(device if device is not None else "cuda")
+        ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+        out, seen = [], set()
+        for p in range(parts):
+            # mask bit b -> XCC b % 8, CU b // 8 of that XCC (census: profiles/r3_cu_mask_census.txt);
+            # an XCC left without a bit runs on ALL its CUs, so every partition keeps bits on every XCC
+            w = [0] * MASK_WORDS
+            for b in range(ncu):
+                c = b // 8  # CU index inside its XCC
+                if (c % parts if mode == "intra" else c // (ncu // 8 // parts)) == p:
+                    w[b // 32] |= 1 << (b % 32)
+            cus = census_cus(cu_census(cu_masked_stream(w, dev), blocks=4096))
+            if len(cus) > ncu // parts or cus & seen:
+                return None
+            seen |= cus
+            out.append(w)
+        return out
+    xm = xcd_cu_masks(device)
+    if xm is None:
+        return None
+    per = 8 // parts
+    out = []
+    for p in range(parts):
+        w = [0] * MASK_WORDS
+        for x in range(p * per, (p + 1) * per):
+            w = [a | b for a, b in zip(w, xm[x])]
+        out.append(w)
+    return out
 
 
 def topk_large(x: torch.Tensor, k: int, max_chunk: int = 16384, *, lo: int = 0,

@@ -80,6 +80,10 @@ _SIGS = {
     "mls_decode_attention": [P, P, P, P, P, P, P, I, I, L, P, P, P, P, I, I, I, I, I, I, I, F, P, I, I, I, I, P],
     "mls_skinny_packed_combine": [P, P, P, P, I, I, I, I, P, P, P, P, I, I, I, I, I, P],
     "mls_skinny_fp8": [P, P, P, P, P, P, P, P, I, I, I, I, I, F, I, P],
+    "mls_stream_create_cumask": [P, I, _c.POINTER(P)],
+    "mls_stream_get_cumask": [P, P, I],
+    "mls_stream_destroy": [P],
+    "mls_cu_census": [P, I, I, P],
 }
 _OPTIONAL_SIGS: dict = {"mls_set_debug_flags": [I], "mls_chain_set_l2_cw": [I], "mls_skinny_set_variant": [I], "mls_skinny_set_max_split": [I]}
 

@@ -159,7 +159,7 @@ class ResNet50Plugin(ModelPlugin):
                 fwd = (lambda f: (lambda x: f(ops.image_decode(x))))(fwd)
             eng = GpuEngine(fwd, dev, shape, torch.uint8, buckets=buckets, inflight=int(s.INFLIGHT),
                             use_graphs=bool(s.USE_GRAPHS), name=f"resnet50.{dev}",
-                            concurrent=bool(s.CONCURRENT_SLOTS))
+                            concurrent=bool(s.CONCURRENT_SLOTS), cu_partitions=int(s.CU_PARTITION))
             eng.warmup(capture=bool(s.USE_GRAPHS))
             self.engines.append(eng)
         logger.info("resnet50 ready on %s (backend=%s buckets=%s)", devices, s.BACKEND, buckets)

@@ -44,8 +44,9 @@ def test_concurrent_slots_match_serial():
 
 def test_benchmarked_config_end_to_end_vs_fp32():
     """The exact configuration bench.py times: ResNet50Fused(max_batch=32) with the shipped B=32
-    tuning table, GpuEngine(inflight=5, concurrent slots, hipGraphs), 5 batches of 32 in flight
-    -- every row compared with the fp32 PyTorch reference of the same weights."""
+    tuning table, GpuEngine(4 slots on CU-masked streams in 2 partitions, hipGraphs), 5 batches of
+    32 submitted back to back -- every row compared with the fp32 PyTorch reference of the same
+    weights."""
     from mlmicroservicetemplate_amd.engine.worker import GpuEngine
     from mlmicroservicetemplate_amd.models import resnet
     from mlmicroservicetemplate_amd.ops.autotune import load_tuning
@@ -60,13 +61,18 @@ def test_benchmarked_config_end_to_end_vs_fp32():
         v, i = model.ops.softmax_topk(logits, 5)
         return logits, v, i
 
-    eng = GpuEngine(fwd, DEV, (224, 224, 3), torch.uint8, buckets=[32], inflight=5, concurrent=True,
-                    use_graphs=True, name="benchcfg")
+    eng = GpuEngine(fwd, DEV, (224, 224, 3), torch.uint8, buckets=[32], inflight=4, concurrent=True,
+                    use_graphs=True, name="benchcfg", cu_partitions=2)
+    assert eng.cu_partitions == 2 and eng.inflight == 4  # bench.py's defaults
     eng.warmup(capture=True)
     rng = np.random.default_rng(7)
     batches = [rng.integers(0, 256, (32, 224, 224, 3), dtype=np.uint8) for _ in range(5)]
-    tickets = [eng.submit(b) for b in batches]  # 5 co-running batches
-    outs = [t.wait() for t in tickets]
+    outs, pending = [], []
+    for b in batches:  # 4 co-running batches (one per slot), the 5th as soon as a slot frees
+        if len(pending) == eng.inflight:
+            outs.append(pending.pop(0).wait())
+        pending.append(eng.submit(b))
+    outs += [t.wait() for t in pending]
     pd = {k: v.to(DEV) for k, v in p.items()}
     for b, (logits, vals, idx) in zip(batches, outs):
         ref = resnet.resnet50_reference(pd, torch.from_numpy(b).to(DEV)).float().cpu()
@@ -100,3 +106,52 @@ def test_engine_roctx_ranges():
     assert s.tolist() == [32.0] * 3
     for k in ("stage", "h2d", "replay", "d2h", "d2h_wait"):
         assert f"tr.{k}" in names, (k, names)
+
+
+def test_cu_partition_masks_select_disjoint_halves():
+    """ops.partition_masks(mode="intra"): each mask's stream runs only on its own CUs -- 1 / P of
+    every XCD, disjoint across partitions -- as seen by the census kernel (csrc/partition.hip)."""
+    from mlmicroservicetemplate_amd import ops
+
+    full = ops.census_cus(ops.cu_census(torch.cuda.Stream(), blocks=4096))
+    assert len(full) == torch.cuda.get_device_properties(0).multi_processor_count
+    for parts in (2, 4):
+        masks = ops.partition_masks(parts, DEV, mode="intra")
+        assert masks is not None
+        seen = set()
+        for m in masks:
+            cus = ops.census_cus(ops.cu_census(ops.cu_masked_stream(m, DEV), blocks=4096))
+            assert len(cus) == len(full) // parts, (parts, len(cus))
+            assert {x for x, _ in cus} == {x for x, _ in full}  # every XCD keeps a share
+            assert not (cus & seen)
+            seen |= cus
+        assert seen == full
+
+
+def test_partitioned_engine_matches_serial():
+    """Slots on CU-masked streams (2 partitions) give exactly the results of one-at-a-time execution."""
+    from mlmicroservicetemplate_amd.engine.worker import GpuEngine
+    from mlmicroservicetemplate_amd.models import resnet
+    from mlmicroservicetemplate_amd.ops.autotune import load_tuning
+
+    p = resnet.init_resnet50(1)
+    model = resnet.ResNet50Fused(p, DEV, max_batch=8, tuning=load_tuning("resnet50", 8))
+    rng = np.random.default_rng(3)
+    batches = [rng.integers(0, 256, (8, 224, 224, 3), dtype=np.uint8) for _ in range(6)]
+    serial = GpuEngine(lambda x: model.classify(x, 5), DEV, (224, 224, 3), torch.uint8, buckets=[8], inflight=1,
+                       name="serial")
+    serial.warmup()
+    ref = [serial.run(b) for b in batches]
+    part = GpuEngine(lambda x: model.classify(x, 5), DEV, (224, 224, 3), torch.uint8, buckets=[8], inflight=6,
+                     concurrent=True, name="part", cu_partitions=2)
+    assert part.cu_partitions == 2 and part.inflight == 4 and part.stats()["cu_partitions"] == 2
+    part.warmup()
+    outs, pending = [], []
+    for b in batches:  # a slot returns on wait(): keep at most `inflight` batches outstanding
+        if len(pending) == part.inflight:
+            outs.append(pending.pop(0).wait())
+        pending.append(part.submit(b))
+    outs += [t.wait() for t in pending]
+    for (rv, ri), (ov, oi) in zip(ref, outs):
+        np.testing.assert_array_equal(ri, oi)
+        np.testing.assert_array_equal(rv, ov)
