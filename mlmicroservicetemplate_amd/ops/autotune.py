@@ -47,6 +47,9 @@ def _time(fn, iters: int = 20, warmup: int = 3) -> float:
     return start.elapsed_time(end) / iters
 
 
+_TUNE_STREAMS: list = []
+
+
 def _time_multi(fns, iters: int = 20, warmup: int = 3) -> float:
     """ms per call when ``len(fns)`` independent copies of a layer co-run on their own streams
     (each captured in its own hipGraph): the per-call cost under the engine's concurrent slots,
@@ -54,7 +57,23 @@ def _time_multi(fns, iters: int = 20, warmup: int = 3) -> float:
     if len(fns) == 1:
         return _time(fns[0], iters, warmup)
     main = torch.cuda.current_stream()
-    streams = [torch.cuda.Stream() for _ in fns]
+    # MLS_TUNE_PARTITIONS=P: the copies run on CU-masked streams, copy i in partition i % P -- how a
+    # partitioned serving engine (engine/worker.py, cu_partitions) co-runs its batches
+    parts = int(os.environ.get("MLS_TUNE_PARTITIONS", "0"))
+    masks = None
+    if parts:
+        from . import partition_masks
+
+        masks = partition_masks(parts, main.device, mode=os.environ.get("MLS_CU_PARTITION_MODE", "intra"))
+    if masks:
+        from . import cu_masked_stream
+
+        global _TUNE_STREAMS
+        if len(_TUNE_STREAMS) < len(fns):  # masked streams are created once (each holds a hardware queue)
+            _TUNE_STREAMS = [cu_masked_stream(masks[i % parts], main.device) for i in range(len(fns))]
+        streams = _TUNE_STREAMS[:len(fns)]
+    else:
+        streams = [torch.cuda.Stream() for _ in fns]
     graphs = []
     for fn, st in zip(fns, streams):
         st.wait_stream(main)

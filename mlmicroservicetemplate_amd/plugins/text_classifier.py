@@ -89,7 +89,11 @@ class BertPlugin(ModelPlugin):
 
                 eng = GpuEngine(fwd, dev, (2 * S + 1,), torch.int32, buckets=buckets, inflight=int(s.INFLIGHT),
                                 use_graphs=bool(s.USE_GRAPHS), name=f"bert.s{S}.{dev}",
-                                concurrent=bool(s.CONCURRENT_SLOTS))
+                                concurrent=bool(s.CONCURRENT_SLOTS),
+                                # CU-masked slot halves: B=32 30.4k vs 28.2k seq/s, B=128 level
+                                # (profiles/r3_bert_cu_partition_ab.jsonl); each masked slot holds a
+                                # hardware queue, so only with a single sequence-bucket engine
+                                cu_partitions=int(s.CU_PARTITION) if len(seqs) == 1 else 0)
                 eng.warmup(capture=bool(s.USE_GRAPHS))
                 per[S] = eng
             self.engines[dev] = per

@@ -51,12 +51,13 @@ def bench_bert(args):
                 pend = []
                 for _ in range(n):
                     pend.append(eng.submit(packed))
-                    if len(pend) >= args.inflight:
+                    if len(pend) >= eng.inflight:  # a partitioned engine may hold fewer slots
                         pend.pop(0).wait()
                 for t in pend:
                     t.wait()
                 dt = (time.perf_counter() - t0) / n
-                print(json.dumps({"bench": "bert-base", "backend": name, "batch": B, "seq": S, "inflight": args.inflight,
+                print(json.dumps({"bench": "bert-base", "backend": name, "batch": B, "seq": S, "inflight": eng.inflight,
+                                  "cu_partitions": eng.cu_partitions,
                                   "ms_per_batch": round(dt * 1e3, 3), "seq_per_s": round(B / dt, 1),
                                   "tokens_per_s": round(B * S / dt, 1)}), flush=True)
                 del eng
