@@ -41,7 +41,11 @@ constexpr int POOL_BYTES = NPOOL * COUT * 2;       // 4096: the pooled tile as t
 // bottleneck's 1x1 conv (64 -> 64, BN folded, ReLU) on each pooled tile while it is in LDS and
 // store its output t1 -- the layer1.0.conv1 launch and its 12.8 MB re-read of the pooled map go
 // away (the pooled map itself is still stored: the block's downsample branch reads it).
-template <int TILES_PER_BLOCK, bool CONV1>
+// SWAP: the MFMA computes D = W . Patch^T instead of Patch . W, so each lane holds 4 consecutive
+// output channels of one stem pixel and the epilogue writes 8 B per (row block, column block) --
+// 10 ds_write_b64 per lane per tile instead of 40 single-bf16 writes, one pixel-validity test per
+// row block instead of per element.
+template <int TILES_PER_BLOCK, bool CONV1, bool SWAP = true>
 __global__ __launch_bounds__(256, 3) void stem_pool_kernel(const uint8_t* __restrict__ img, const bf16* __restrict__ w,
                                                         const float* __restrict__ bias, bf16* __restrict__ out, int B,
                                                         int H, int W, int Po, float m0, float m1, float m2, float s0,
@@ -76,9 +80,14 @@ __global__ __launch_bounds__(256, 3) void stem_pool_kernel(const uint8_t* __rest
     for (int kh = 0; kh < 7; ++kh)
       bw[j][kh] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(w + (long)n * KTOT + kh * 32 + fq * 8));
   }
-  float bj[2];
+  float bj[2];      // !SWAP: this lane's output channel per column block
+  float bq[2][4];   // SWAP: this lane's 4 consecutive output channels per column block
 #pragma unroll
-  for (int j = 0; j < 2; ++j) bj[j] = bias[wn * 32 + j * 16 + fr];
+  for (int j = 0; j < 2; ++j) {
+    bj[j] = bias[wn * 32 + j * 16 + fr];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bq[j][r] = bias[wn * 32 + j * 16 + fq * 4 + r];
+  }
   // CONV1: wave w owns t1 columns w*16 .. w*16+15 of both 16-pixel row blocks; its B fragments
   // (64 input channels = 2 k-steps) and bias in registers for the whole block
   bf16x8 bw1[2];
@@ -99,16 +108,18 @@ __global__ __launch_bounds__(256, 3) void stem_pool_kernel(const uint8_t* __rest
 
   // epilogue row masks (bit i * 4 + r): padded rows, stem row 0, stem column 0 -- kept as bits so the
   // tile loop does not hold 20 row / column pairs in registers
+  // (SWAP: one bit per row block i -- the lane's pixel is wm * 80 + i * 16 + fr)
   uint32_t m_pad = 0, m_sr0 = 0, m_sc0 = 0;
 #pragma unroll
   for (int i = 0; i < 5; ++i)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = wm * 80 + i * 16 + fq * 4 + r;
+    for (int r = 0; r < (SWAP ? 1 : 4); ++r) {
+      const int row = wm * 80 + i * 16 + (SWAP ? fr : fq * 4 + r);
       const int sr = row / SC, sc = row - (row / SC) * SC;
-      m_pad |= (uint32_t)(row >= SP) << (i * 4 + r);
-      m_sr0 |= (uint32_t)(sr == 0) << (i * 4 + r);
-      m_sc0 |= (uint32_t)(sc == 0) << (i * 4 + r);
+      const int bit = SWAP ? i : i * 4 + r;
+      m_pad |= (uint32_t)(row >= SP) << bit;
+      m_sr0 |= (uint32_t)(sr == 0) << bit;
+      m_sc0 |= (uint32_t)(sc == 0) << bit;
     }
 
   // image bytes of a tile's patch -> registers (issued a tile ahead: software pipelined)
@@ -162,23 +173,46 @@ __global__ __launch_bounds__(256, 3) void stem_pool_kernel(const uint8_t* __rest
       for (int i = 0; i < 5; ++i) {
         const bf16x8 av = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(smem + abase[i] + kh * PC * 8));
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bw[j][kh], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = SWAP ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j][kh], av, acc[i][j], 0, 0, 0)
+                           : __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bw[j][kh], acc[i][j], 0, 0, 0);
       }
     }
 
     // bias + ReLU -> bf16 stem tile in LDS; stem pixels outside the image (row / column -1) -> 0
     const uint32_t zero = (sr0 < 0 ? m_sr0 : 0u) | (sc0 < 0 ? m_sc0 : 0u);
-    bf16* trow = tile + (wm * 80 + fq * 4) * TSTR + wn * 32 + fr;
+    if constexpr (SWAP) {
+      // lane: stem pixel wm*80 + i*16 + fr, channels wn*32 + j*16 + fq*4 .. +3 -> one 8-B write
+      // (pixel stride 144 B: the 16 lanes of a ds_write_b64 group land on disjoint bank pairs)
+      bf16* tp = tile + (wm * 80 + fr) * TSTR + wn * 32 + fq * 4;
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+      for (int i = 0; i < 5; ++i) {
+        if ((m_pad >> i) & 1u) continue;
+        const bool z = (zero >> i) & 1u;
 #pragma unroll
-      for (int i = 0; i < 5; ++i)
+        for (int j = 0; j < 2; ++j) {
+          bf16x4 v;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int k = i * 4 + r;
-          if (!((m_pad >> k) & 1u))
-            trow[(i * 16 + r) * TSTR + j * 16] = (bf16)(((zero >> k) & 1u) ? 0.f : fmaxf(acc[i][j][r] + bj[j], 0.f));
+          for (int r = 0; r < 4; ++r) {
+            const float e = acc[i][j][r];  // through a named float (ext-vector element bit-cast hazard)
+            v[r] = (bf16)(z ? 0.f : fmaxf(e + bq[j][r], 0.f));
+          }
+          *reinterpret_cast<uint2*>(tp + i * 16 * TSTR + j * 16) = __builtin_bit_cast(uint2, v);
         }
+      }
+    } else {
+      bf16* trow = tile + (wm * 80 + fq * 4) * TSTR + wn * 32 + fr;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 5; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int k = i * 4 + r;
+            if (!((m_pad >> k) & 1u))
+              trow[(i * 16 + r) * TSTR + j * 16] = (bf16)(((zero >> k) & 1u) ? 0.f : fmaxf(acc[i][j][r] + bj[j], 0.f));
+          }
+    }
     __syncthreads();
 
     // 3x3 / 2 max pool: thread = one pooled pixel x 8 channels
@@ -272,10 +306,15 @@ int mls_stem_pool_conv1(const void* images, const void* w, const float* bias, vo
   const long blocks = (long)B * (Po / TPH) * ((Po / TPW + tpb - 1) / tpb);
   if (blocks > 0x7fffffffL) return MLS_BAD_ARG;
   const bool c1 = w1 != nullptr && t1 != nullptr;
+  static const bool swap = [] {  // MLS_STEM_SWAP=0: the per-element epilogue (A/B)
+    const char* e = getenv("MLS_STEM_SWAP");
+    return !(e && e[0] == '0');
+  }();
   auto kernel = c1 ? (tpb == 1 ? stem_pool_kernel<1, true> : tpb == 2 ? stem_pool_kernel<2, true>
                                          : tpb == 7 ? stem_pool_kernel<7, true> : stem_pool_kernel<4, true>)
                    : (tpb == 1 ? stem_pool_kernel<1, false> : tpb == 2 ? stem_pool_kernel<2, false>
                                          : tpb == 7 ? stem_pool_kernel<7, false> : stem_pool_kernel<4, false>);
+  if (!swap && !c1 && tpb == 7) kernel = stem_pool_kernel<7, false, false>;
   hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)images,
                      (const bf16*)w, bias, (bf16*)out, B, H, W, Po, mean3[0], mean3[1], mean3[2], 1.f / std3[0],
                      1.f / std3[1], 1.f / std3[2], dbg, (const bf16*)w1, b1, (bf16*)t1);
