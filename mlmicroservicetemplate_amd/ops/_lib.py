@@ -129,6 +129,10 @@ def lib(build_if_missing: bool = True) -> ctypes.CDLL:
         if _LIB is not None:
             return _LIB
         path = _build.lib_path(DEBUG)
+        override = os.environ.get("MLS_LIB_OVERRIDE")  # A/B runs only: an alternative build of the same sources
+        if override:
+            build_if_missing = False
+            path = override
         if build_if_missing:
             # incremental: a no-op when the stamp matches the sources
             try:

@@ -45,6 +45,17 @@ constexpr int XL_PATCH = 648;                    // 8 images of 9 x 9, or 10 x 5
 
 #define LDS3 __attribute__((address_space(3)))
 
+// MFMA operand order: 1 D = W_tile . Patch^T -- a lane holds 4 consecutive output channels of one
+// pixel, so the epilogue parks a fragment with one 8-B LDS write (and a split-K slice with one
+// 16-B store) instead of four 2-B / 4-B ones.  0 (default): Patch . W_tile^T -- the swapped build
+// was level-to-slower on every 3x3 layer (layer1 12.6 vs 12.1 us co-running,
+// profiles/r3_swap_epilogue_component_costs.jsonl): the epilogue runs once per 2-16 chunks here,
+// unlike the stem's once per 70 MFMAs.  A/B build option (-DMLS_HALO_SWAP=1).
+#ifndef MLS_HALO_SWAP
+#define MLS_HALO_SWAP 0
+#endif
+typedef unsigned int halo_u32x4 __attribute__((__vector_size__(16)));
+
 MLS_DEV void glds16(rsrc_t r, char* lds, int voff, int soff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS3 void*)lds, 16, voff, soff, 0, 0);
 }
@@ -237,7 +248,8 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_halo_kernel(const HaloArgs a)
         if (C::CONTIG && !rb_on[i]) continue;  // wave-uniform: this row block is all padding
 #pragma unroll
         for (int j = 0; j < CB; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[cur][i], bf[cur][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = MLS_HALO_SWAP ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[cur][j], af[cur][i], acc[i][j], 0, 0, 0)
+                                    : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[cur][i], bf[cur][j], acc[i][j], 0, 0, 0);
       }
     }
   }
@@ -252,7 +264,15 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_halo_kernel(const HaloArgs a)
     for (int i = 0; i < RBW; ++i) {
       const int rb = rb_of(i);
 #pragma unroll
-      for (int j = 0; j < CB; ++j)
+      for (int j = 0; j < CB; ++j) {
+        if (MLS_HALO_SWAP) {  // lane: pixel rb*16 + fr, 4 consecutive channels -> one 16-B store
+          const int row = rb * 16 + fr;
+          const long idx = ((long)split * M + m_base + row) * a.N + n0 + j * 16 + fq * 4;
+          const float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
+          const halo_u32x4 q = {__float_as_uint(v0), __float_as_uint(v1), __float_as_uint(v2), __float_as_uint(v3)};
+          __builtin_amdgcn_raw_buffer_store_b128(q, wsr, row < R ? (int)(idx * 4) : OOB, 0, 16);
+          continue;
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = rb * 16 + fq * 4 + r;
@@ -262,6 +282,7 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_halo_kernel(const HaloArgs a)
           const float v = acc[i][j][r];
           __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), wsr, row < R ? (int)(idx * 4) : OOB, 0, 16);
         }
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -300,9 +321,15 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_halo_kernel(const HaloArgs a)
   }
 
   // epilogue: bias + act -> bf16 tile in LDS (reusing the stage buffer) -> 16-B stores
-  float bj[CB];
+  // bias of this lane's output channel(s): MLS_HALO_SWAP -> 4 consecutive channels fq*4 .. +3 per
+  // column block (the lane holds one pixel x 4 channels: one 8-B LDS write per fragment, pixel
+  // stride EPI_LD = BN + 8 bf16 so the 16-lane groups of a ds_write_b64 hit disjoint bank pairs)
+  float bj[CB][MLS_HALO_SWAP ? 4 : 1];
 #pragma unroll
-  for (int j = 0; j < CB; ++j) bj[j] = a.bias ? a.bias[n0 + j * 16 + fr] : 0.f;
+  for (int j = 0; j < CB; ++j)
+#pragma unroll
+    for (int r = 0; r < (MLS_HALO_SWAP ? 4 : 1); ++r)
+      bj[j][r] = a.bias ? a.bias[n0 + j * 16 + (MLS_HALO_SWAP ? fq * 4 + r : fr)] : 0.f;
   __syncthreads();  // every wave is done with the last chunk
   bf16* to = reinterpret_cast<bf16*>(smem);
 #pragma unroll
@@ -310,14 +337,27 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_halo_kernel(const HaloArgs a)
     if (!rb_on[i]) continue;
     const int rb = rb_of(i);
 #pragma unroll
-    for (int j = 0; j < CB; ++j)
+    for (int j = 0; j < CB; ++j) {
+      if (MLS_HALO_SWAP) {
+        bf16x4 q;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[i][j][r];  // through a named float (ext-vector element bit-cast hazard)
+          v += bj[j][r];
+          if (!a.res) v = apply_act(v, a.act);
+          q[r] = (bf16)v;
+        }
+        *reinterpret_cast<uint2*>(to + (rb * 16 + fr) * C::EPI_LD + j * 16 + fq * 4) = __builtin_bit_cast(uint2, q);
+        continue;
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = rb * 16 + fq * 4 + r;
-        float v = acc[i][j][r] + bj[j];
+        float v = acc[i][j][r] + bj[j][0];
         if (!a.res) v = apply_act(v, a.act);
         to[row * C::EPI_LD + j * 16 + fr] = (bf16)v;
       }
+    }
   }
   __syncthreads();
   constexpr int CPR = BN / 8;  // 16-B chunks per output row

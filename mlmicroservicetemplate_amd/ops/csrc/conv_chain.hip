@@ -37,6 +37,24 @@ MLS_DEV void glds16(rsrc_t r, char* lds, int voff, int soff) {
 
 typedef unsigned int u32x4v __attribute__((__vector_size__(16)));
 
+// SW (template parameter): MFMA operand order.  true: D = W . A^T, so a lane's 4 accumulators are
+// 4 consecutive output channels of one row -- pass 1 reads the residual and writes y as one 8-B
+// LDS access per fragment (instead of four 2-B read-modify-writes), the t1 epilogue parks 8 B per
+// fragment, and the biases come from wave-uniform scalar loads (no VGPR-resident bias table, no
+// VMEM op beside the DMA ring); false: D = A . W^T.  Per boundary from the per-call A/B
+// (profiles/r3_swap_epilogue_component_costs.jsonl): the single-slab (KS = 1) layer1 boundaries
+// take SW (layer1.1 -> 1.2: 27.4 -> 23.2 us co-running), the others measured level or slower.
+// MLS_CHAIN_SWAP=0/1 at build time forces one order everywhere (A/B builds).
+#define CONST4 __attribute__((address_space(4)))
+
+// the 4 biases of lane group fq in the 16 output channels starting at the wave-uniform nt0
+MLS_DEV f32x4 bias4(const float* b, int nt0, int fq) {
+  if (!b) return f32x4{0.f, 0.f, 0.f, 0.f};
+  const CONST4 f32x4* bp = (const CONST4 f32x4*)(b + nt0);
+  const f32x4 b0 = bp[0], b1 = bp[1], b2 = bp[2], b3 = bp[3];
+  return fq == 0 ? b0 : fq == 1 ? b1 : fq == 2 ? b2 : b3;
+}
+
 struct ChainArgs {
   const bf16* a1;   // [M][Ka]            (conv3 input, stride 1)
   const bf16* a2;   // [B][H2][W2][Kb]    (dual: the block input, sampled at stride2) or null
@@ -68,7 +86,7 @@ MLS_DEV int row_swz(int r) {
 // LDS-DMA: a plain global load consumed beside in-flight DMA makes hipcc wait vmcnt(0) and drain
 // the ring (cdna_hip_programming.md §5, "Projection GEMM" item 4(b)).  OCC = waves per SIMD the
 // register allocation must allow: 4 where the LDS footprint lets two blocks share a CU (<= 80 KB).
-template <int BM, int KS, int N1, int N2, int CW, int OCC>
+template <int BM, int KS, int N1, int N2, int CW, int OCC, bool SW>
 __global__ __launch_bounds__(512, OCC) void conv_chain_kernel(const ChainArgs a) {
   constexpr int NW = 8, NT = 512, WM = 4, WN = 2;
   constexpr int WTM = BM / WM, TM = WTM / 16;  // GEMM1 / GEMM2 wave rows
@@ -106,14 +124,16 @@ __global__ __launch_bounds__(512, OCC) void conv_chain_kernel(const ChainArgs a)
   const int K1 = a.Ka + a.Kb, KSA = a.Ka / 64;
   const bool has_res = a.res != nullptr;
 
-  // biases of every column this lane touches, before any DMA is in flight
-  float b3v[NJ][TN], b1v[TN2];
+  // (original order) biases of every column this lane touches, before any DMA is in flight
+  float b3v[SW ? 1 : NJ][TN], b1v[TN2];
+  if constexpr (!SW) {
 #pragma unroll
-  for (int j = 0; j < NJ; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
-    for (int jn = 0; jn < TN; ++jn) b3v[j][jn] = a.b3 ? a.b3[j * CW + wn * (CW / 2) + jn * 16 + fr] : 0.f;
+      for (int jn = 0; jn < TN; ++jn) b3v[j][jn] = a.b3 ? a.b3[j * CW + wn * (CW / 2) + jn * 16 + fr] : 0.f;
 #pragma unroll
-  for (int jn = 0; jn < TN2; ++jn) b1v[jn] = a.b1 ? a.b1[wn * (N2 / 2) + jn * 16 + fr] : 0.f;
+    for (int jn = 0; jn < TN2; ++jn) b1v[jn] = a.b1 ? a.b1[wn * (N2 / 2) + jn * 16 + fr] : 0.f;
+  }
 
   // DMA lane geometry.  128-B rows (A1, W3): 8 rows x 8 chunks per piece; CW-wide rows (W1,
   // residual): RPP rows x CPR chunks.  LDS chunk c of row r holds the logical chunk c ^ swz(r).
@@ -190,12 +210,14 @@ __global__ __launch_bounds__(512, OCC) void conv_chain_kernel(const ChainArgs a)
     if (j == 0) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       // the biases are retired too: pin their first use here, before stage 1 is issued
+      if constexpr (!SW) {
 #pragma unroll
-      for (int jj = 0; jj < NJ; ++jj)
+        for (int jj = 0; jj < NJ; ++jj)
 #pragma unroll
-        for (int jn = 0; jn < TN; ++jn) asm volatile("" ::"v"(b3v[jj][jn]));
+          for (int jn = 0; jn < TN; ++jn) asm volatile("" ::"v"(b3v[jj][jn]));
 #pragma unroll
-      for (int jn = 0; jn < TN2; ++jn) asm volatile("" ::"v"(b1v[jn]));
+        for (int jn = 0; jn < TN2; ++jn) asm volatile("" ::"v"(b1v[jn]));
+      }
     } else {
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Y_ST) : "memory");
     }
@@ -232,10 +254,37 @@ __global__ __launch_bounds__(512, OCC) void conv_chain_kernel(const ChainArgs a)
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int jn = 0; jn < TN; ++jn)
-          acc1[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[jn], acc1[i][jn], 0, 0, 0);
+          acc1[i][jn] = SW ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfv[jn], af[i], acc1[i][jn], 0, 0, 0)
+                                       : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[jn], acc1[i][jn], 0, 0, 0);
     }
 
     // ---- pass 1: y = relu(acc1 + b3 (+ res)) -> bf16, in place over the residual chunk
+    if constexpr (SW) {
+#pragma unroll
+      for (int jn = 0; jn < TN; ++jn) {
+        const int nt0 = wn * (CW / 2) + jn * 16, col = nt0 + fq * 4;  // col % 8 in {0, 4}: 8 B in one chunk
+        const f32x4 bb = bias4(a.b3, j * CW + nt0, fq);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int row = wm * WTM + i * 16 + fr;
+          uint2* p = reinterpret_cast<uint2*>(sR + row * (CW * 2) + (((col >> 3) ^ row_swz<CPR>(row)) << 4) +
+                                              (col & 7) * 2);
+          float rs[4] = {0.f, 0.f, 0.f, 0.f};
+          if (has_res) {
+            const bf16x4 rv = __builtin_bit_cast(bf16x4, *p);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) rs[r] = (float)rv[r];
+          }
+          bf16x4 q;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float e = acc1[i][jn][r];  // through a named float (ext-vector element bit-cast hazard)
+            q[r] = (bf16)fmaxf(e + bb[r] + rs[r], 0.f);
+          }
+          *p = __builtin_bit_cast(uint2, q);
+        }
+      }
+    } else
 #pragma unroll
     for (int jn = 0; jn < TN; ++jn) {
       const int col = wn * (CW / 2) + jn * 16 + fr;
@@ -288,7 +337,8 @@ __global__ __launch_bounds__(512, OCC) void conv_chain_kernel(const ChainArgs a)
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int jn = 0; jn < TN2; ++jn)
-          acc2[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[jn], acc2[i][jn], 0, 0, 0);
+          acc2[i][jn] = SW ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfv[jn], af[i], acc2[i][jn], 0, 0, 0)
+                                       : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[jn], acc2[i][jn], 0, 0, 0);
     }
   }
 
@@ -297,6 +347,25 @@ __global__ __launch_bounds__(512, OCC) void conv_chain_kernel(const ChainArgs a)
   __builtin_amdgcn_s_barrier();  // every wave is done reading the ring
   constexpr int TPR = N2 / 8;    // 16-B chunks per t1 row
   bf16* to = reinterpret_cast<bf16*>(smem);
+  if constexpr (SW) {
+#pragma unroll
+    for (int jn = 0; jn < TN2; ++jn) {
+      const int nt0 = wn * (N2 / 2) + jn * 16, col = nt0 + fq * 4;
+      const f32x4 bb = bias4(a.b1, nt0, fq);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * WTM + i * 16 + fr;
+        bf16x4 q;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = acc2[i][jn][r];
+          q[r] = (bf16)fmaxf(e + bb[r], 0.f);
+        }
+        *reinterpret_cast<uint2*>(to + row * N2 + ((((col >> 3) ^ (row & 7))) << 3) + (col & 7)) =
+            __builtin_bit_cast(uint2, q);
+      }
+    }
+  } else
 #pragma unroll
   for (int jn = 0; jn < TN2; ++jn) {
     const int col = wn * (N2 / 2) + jn * 16 + fr;
@@ -336,8 +405,13 @@ int launch_chain(const ChainArgs& a, hipStream_t st) {
   constexpr int BM = 128;
   constexpr int LDS = BM * KS * 128 + 2 * (CW * KS * 128 + N2 * CW * 2 + BM * CW * 2);
   constexpr int OCC = LDS <= 80 * 1024 ? 4 : 2;
-  hipLaunchKernelGGL((conv_chain_kernel<BM, KS, N1, N2, CW, OCC>), dim3((unsigned)((a.M + BM - 1) / BM)), dim3(512),
-                     0, st, a);
+#ifdef MLS_CHAIN_SWAP
+  constexpr bool SW = MLS_CHAIN_SWAP;
+#else
+  constexpr bool SW = KS == 1;
+#endif
+  hipLaunchKernelGGL((conv_chain_kernel<BM, KS, N1, N2, CW, OCC, SW>), dim3((unsigned)((a.M + BM - 1) / BM)),
+                     dim3(512), 0, st, a);
   return (int)hipGetLastError();
 }
 

@@ -154,6 +154,30 @@ MLS_DEV void splitk_finish_chunk(const ConvArgs& a, rsrc_t wr, int m, int n, boo
   st16(a.out + (size_t)m * a.ldo + n, pack8(v));
 }
 
+// MFMA operand order of conv_gemm_kernel.  1: D = B_tile . A_tile^T, so a lane's 4 accumulators
+// are 4 consecutive OUTPUT CHANNELS of one output pixel and parking a 16 x 16 fragment in LDS for
+// the epilogue is ONE ds_write_b128 per lane (row stride C_LD = BN + 4 floats: the 8-lane groups
+// of the write hit disjoint bank quads) instead of four ds_write_b32 down a column.  0 (default):
+// D = A_tile . B_tile^T -- the swapped build measured 2 % SLOWER over the forward's conv calls
+// co-running (397 vs 389 us, profiles/r3_swap_epilogue_component_costs.jsonl), so it stays an
+// A/B build option (-DMLS_CONV_SWAP=1).
+#ifndef MLS_CONV_SWAP
+#define MLS_CONV_SWAP 0
+#endif
+
+// Park one 16 x 16 fp32 accumulator fragment at (row0, col0) of the row-major LDS tile Cs.
+MLS_DEV void park_frag(float* Cs, int ld, int row0, int col0, int fr, int fq, const f32x4& v) {
+  if (MLS_CONV_SWAP) {
+    *reinterpret_cast<float4*>(Cs + (row0 + fr) * ld + col0 + fq * 4) = float4{v[0], v[1], v[2], v[3]};
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float e = v[r];  // through a named float (ext-vector element bit-cast hazard)
+      Cs[(row0 + fq * 4 + r) * ld + col0 + fr] = e;
+    }
+  }
+}
+
 // v2: LDS-DMA (buffer_load ... lds) into a STAGES-deep ring, counted vmcnt + raw s_barrier.
 // BKT (64 or 32) is the K depth of a stage: 32 halves the LDS ring, and with the accumulators
 // parked for the epilogue in EPI_PASSES row blocks, a block's LDS can shrink to ~24 KB -- twice
@@ -372,7 +396,8 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_kernel(const ConvArgs 
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = MLS_CONV_SWAP ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfv[j], af[i], acc[i][j], 0, 0, 0)
+                                    : __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
     }
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -384,13 +409,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_kernel(const ConvArgs 
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = wm * WTM + i * 16 + fq * 4 + r;
-          const int col = wn * WTN + j * 16 + fr;
-          Cs[row * C_LD + col] = acc[i][j][r];
-        }
+      for (int j = 0; j < TN; ++j) park_frag(Cs, C_LD, wm * WTM + i * 16, wn * WTN + j * 16, fr, fq, acc[i][j]);
     __syncthreads();
     // gate/up interleaved in 8-column groups: chunk 2p = gate, 2p+1 = up -> 8 outputs at n/2
     for (int q = tid; q < BM * (CPR / 2); q += NT) {
@@ -422,13 +441,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_kernel(const ConvArgs 
       const int frag_row = wm * WTM + i * 16;  // a fragment's 16 rows fall in one pass
       if (EPI_PASSES > 1 && (frag_row < row_lo || frag_row >= row_lo + PASS_ROWS)) continue;
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = frag_row + fq * 4 + r - row_lo;
-          const int col = wn * WTN + j * 16 + fr;
-          Cs[row * C_LD + col] = acc[i][j][r];
-        }
+      for (int j = 0; j < TN; ++j) park_frag(Cs, C_LD, frag_row - row_lo, wn * WTN + j * 16, fr, fq, acc[i][j]);
     }
     __syncthreads();
 #pragma unroll
