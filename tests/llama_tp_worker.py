@@ -38,6 +38,11 @@ def main():
         from mlmicroservicetemplate_amd import ops
         from mlmicroservicetemplate_amd.models.llama import TPCommError
 
+        # the prefill checks above ran with the default (~1 s) peer-wait bound: two ranks
+        # time-sharing one GPU can miss a few-ms bound on any small all-reduce; only the stalled
+        # request runs with the tight bound
+        if m.comm.car is not None and os.environ.get("MLS_AR_TIMEOUT_ITERS_STALL"):
+            m.comm.car.timeout = int(os.environ["MLS_AR_TIMEOUT_ITERS_STALL"])
         if rank == stall_rank:
             ops.gpu_sleep(int(os.environ.get("STALL_US", "300000")))
         try:

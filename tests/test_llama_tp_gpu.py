@@ -32,12 +32,14 @@ CASES = {
     8: (dict(layers=2, hidden=512, heads=32, kv_heads=8, head_dim=128, intermediate=2048),
         {"MLS_CUSTOM_AR": "1", "GPU_MAX_HW_QUEUES": "1"}),
     # fault injection: rank 1 stalls 300 ms with the peer-wait bound at ~a few ms -> every rank's
-    # request fails with TPCommError; the next request runs on the RCCL / group fallback.  The
-    # prefill runs the plain layer loop here: with a few-ms wait bound, two ranks time-sharing one
-    # GPU can time out on any of the prefill's small one-shot all-reduces before the injected stall
+    # request fails with TPCommError; the next request runs on the RCCL / group fallback.  The tight
+    # bound is set only for the stalled request (MLS_AR_TIMEOUT_ITERS_STALL, llama_tp_worker.py):
+    # with it from the start, two ranks time-sharing one GPU timed out on a small prefill
+    # all-reduce BEFORE the injected stall (a flaky partial-sum prefill).  The prefill runs the
+    # plain layer loop here.
     "stall": (dict(layers=2, hidden=512, heads=8, kv_heads=2, head_dim=128, intermediate=1024),
               {"MLS_CUSTOM_AR": "1", "GPU_MAX_HW_QUEUES": "1", "STALL_RANK": "1", "STALL_US": "300000",
-               "MLS_AR_TIMEOUT_ITERS": "20000", "MLS_TP_OVERLAP": "0"}),
+               "MLS_AR_TIMEOUT_ITERS_STALL": "20000", "MLS_TP_OVERLAP": "0"}),
 }
 WORLD = {2: 2, 8: 8, "stall": 2}
 
