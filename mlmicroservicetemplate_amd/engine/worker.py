@@ -199,7 +199,10 @@ class GpuEngine:
                     if part_masks is not None:
                         from .. import ops
 
-                        slot.s_comp = ops.cu_masked_stream(part_masks[i % self.cu_partitions], self.device)
+                        # pooled per (mask, slot-in-partition): engines built one after another in a
+                        # process reuse the queues
+                        slot.s_comp = ops.cu_masked_stream(part_masks[i % self.cu_partitions], self.device,
+                                                           key=i // self.cu_partitions)
                     else:
                         slot.s_comp = torch.cuda.Stream(self.device)
                     slot.pool = torch.cuda.graph_pool_handle() if use_graphs else None

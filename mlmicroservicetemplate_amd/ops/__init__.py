@@ -1156,18 +1156,32 @@ def gpu_sleep(us: int, device=None) -> None:
 MASK_WORDS = 8  # 256 CUs
 
 
-def cu_masked_stream(mask: Sequence[int], device=None) -> torch.cuda.ExternalStream:
-    """A new HIP stream restricted to the CUs whose bits are set in ``mask`` (``MASK_WORDS``
-    uint32 words; csrc/partition.hip).  The native stream lives for the process."""
+_MASKED_STREAMS: Dict[tuple, torch.cuda.ExternalStream] = {}
+_MASKED_LOCK = __import__("threading").Lock()
+
+
+def cu_masked_stream(mask: Sequence[int], device=None, key=0) -> torch.cuda.ExternalStream:
+    """The HIP stream restricted to the CUs whose bits are set in ``mask`` (``MASK_WORDS`` uint32
+    words; csrc/partition.hip) -- one per (device, mask, ``key``), created on first use and kept
+    for the process.  Every masked stream holds a hardware queue of its own, so they are pooled:
+    engines built one after another reuse them (``key`` tells apart the streams one engine needs
+    on the same mask) instead of piling up queues until queue creation fails."""
     import ctypes
 
     dev = torch.device(device if device is not None else "cuda")
-    words = (ctypes.c_uint32 * len(mask))(*[int(m) & 0xFFFFFFFF for m in mask])
-    out = ctypes.c_void_p()
-    with torch.cuda.device(dev):
-        check(lib().mls_stream_create_cumask(ctypes.cast(words, ctypes.c_void_p), len(mask), ctypes.byref(out)),
-              "mls_stream_create_cumask")
-    return torch.cuda.ExternalStream(out.value, device=dev)
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    ck = (dev.index, tuple(int(m) & 0xFFFFFFFF for m in mask), key)
+    with _MASKED_LOCK:
+        st = _MASKED_STREAMS.get(ck)
+        if st is None:
+            words = (ctypes.c_uint32 * len(mask))(*ck[1])
+            out = ctypes.c_void_p()
+            with torch.cuda.device(dev):
+                check(lib().mls_stream_create_cumask(ctypes.cast(words, ctypes.c_void_p), len(mask),
+                                                     ctypes.byref(out)), "mls_stream_create_cumask")
+            st = _MASKED_STREAMS[ck] = torch.cuda.ExternalStream(out.value, device=dev)
+        return st
 
 
 def cu_census(stream: torch.cuda.Stream, blocks: int = 2048, spin: int = 64) -> torch.Tensor:
@@ -1204,7 +1218,7 @@ def xcd_cu_masks(device=None) -> Optional[List[List[int]]]:
                 masks.append(w)
             ids = []
             for w in masks:
-                c = cu_census(cu_masked_stream(w, dev), blocks=256)
+                c = cu_census(cu_masked_stream(w, dev, key="census"), blocks=256)
                 ids.append(set(c[:, 0].tolist()))
             if all(len(s) == 1 for s in ids) and len(set().union(*ids)) == 8:
                 result = masks
@@ -1218,7 +1232,19 @@ def census_cus(c: torch.Tensor) -> set:
     return {(int(x), (int(h) >> 8) & 0xFF) for x, h in c.tolist()}
 
 
+_PARTITION_MASKS: Dict[tuple, Optional[List[List[int]]]] = {}
+
+
 def partition_masks(parts: int, device=None, mode: str = "xcd") -> Optional[List[List[int]]]:
+    """Cached :func:`_partition_masks` (the census verification runs once per device / mode / parts)."""
+    dev = torch.device(device if device is not None else "cuda")
+    ck = (dev.index if dev.index is not None else torch.cuda.current_device(), parts, mode)
+    if ck not in _PARTITION_MASKS:
+        _PARTITION_MASKS[ck] = _partition_masks(parts, dev, mode)
+    return _PARTITION_MASKS[ck]
+
+
+def _partition_masks(parts: int, device=None, mode: str = "xcd") -> Optional[List[List[int]]]:
     """``parts`` (1, 2, 4 or 8) CU masks.  ``mode="xcd"``: each the union of 8 / parts whole XCDs
     (needs :func:`xcd_cu_masks`).  ``mode="intra"``: each a 1 / parts share of the CUs of EVERY
     XCD (CU ``c`` of every XCC with ``c % parts == p``; ``"intra_contig"``: ``c // (32 / parts) ==
@@ -1237,7 +1263,7 @@ def partition_masks(parts: int, device=None, mode: str = "xcd") -> Optional[List
                 c = b // 8  # CU index inside its XCC
                 if (c % parts if mode == "intra" else c // (ncu // 8 // parts)) == p:
                     w[b // 32] |= 1 << (b % 32)
-            cus = census_cus(cu_census(cu_masked_stream(w, dev), blocks=4096))
+            cus = census_cus(cu_census(cu_masked_stream(w, dev, key="census"), blocks=4096))
             if len(cus) > ncu // parts or cus & seen:
                 return None
             seen |= cus

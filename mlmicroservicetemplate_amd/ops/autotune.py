@@ -70,7 +70,7 @@ def _time_multi(fns, iters: int = 20, warmup: int = 3) -> float:
 
         global _TUNE_STREAMS
         if len(_TUNE_STREAMS) < len(fns):  # masked streams are created once (each holds a hardware queue)
-            _TUNE_STREAMS = [cu_masked_stream(masks[i % parts], main.device) for i in range(len(fns))]
+            _TUNE_STREAMS = [cu_masked_stream(masks[i % parts], main.device, key=i // parts) for i in range(len(fns))]
         streams = _TUNE_STREAMS[:len(fns)]
     else:
         streams = [torch.cuda.Stream() for _ in fns]

@@ -120,7 +120,7 @@ def test_cu_partition_masks_select_disjoint_halves():
         assert masks is not None
         seen = set()
         for m in masks:
-            cus = ops.census_cus(ops.cu_census(ops.cu_masked_stream(m, DEV), blocks=4096))
+            cus = ops.census_cus(ops.cu_census(ops.cu_masked_stream(m, DEV, key="census"), blocks=4096))
             assert len(cus) == len(full) // parts, (parts, len(cus))
             assert {x for x, _ in cus} == {x for x, _ in full}  # every XCD keeps a share
             assert not (cus & seen)
