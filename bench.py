@@ -148,7 +148,6 @@ def run_rank(args) -> int:
     engine = GpuEngine(fwd, device, (224, 224, 3), torch.uint8, buckets=[args.batch], inflight=args.inflight,
                        use_graphs=not args.no_graphs, name=f"resnet50.r{info.rank}", concurrent=not args.serial,
                        cu_partitions=0 if args.serial else args.cu_partition)
-    args.inflight = engine.inflight  # a partitioned engine caps its slots at the hardware queues
     cu_parts = engine.cu_partitions
     engine.warmup(capture=not args.no_graphs)
 

@@ -119,11 +119,14 @@ class GpuEngine:
         # ResNet-50 bs=32 54.5-55.6k vs 52.8-53.1k req/s at 200 steps, 49.3-51.4k vs 48.0-49.6k at 20,
         # p50 2.2-2.3 vs 2.55-2.8 ms (profiles/r3_cu_partition_ab.jsonl): the two batches of a half
         # co-run on 128 CUs instead of five interleaving over 256.  A masked stream holds its own
-        # hardware queue, so a partitioned engine keeps at most MLS_HW_QUEUES (4) slots -- 5-8
-        # masked slots measured 35-44k.
+        # hardware queue, so a partitioned engine uses at most MLS_HW_QUEUES (4) masked streams --
+        # 5-8 of them measured 35-44k -- and slots beyond that share them round-robin (slot i on
+        # stream i % 4): their GPU work queues behind the stream-mate's while their host-side
+        # phases (staging, result hand-off) overlap, which the HTTP front end needs.
         if cu_partitions is None:
             cu_partitions = int(os.environ.get("MLS_CU_PARTITION", "0"))
         self.cu_partitions = int(cu_partitions) if self.concurrent else 0
+        self.part_streams = 0  # masked streams the slots are spread over
         part_masks = None
         if self.cu_partitions:
             from .. import ops
@@ -135,10 +138,8 @@ class GpuEngine:
                 self.cu_partitions = 0
             else:
                 hwq = int(os.environ.get("MLS_HW_QUEUES", "4"))
-                if self.inflight > hwq:
-                    logger.info("%s: %d partitions -> %d slots in flight (one hardware queue each)", name,
-                                self.cu_partitions, hwq)
-                    self.inflight = hwq
+                n = min(self.inflight, max(hwq, self.cu_partitions))
+                self.part_streams = max(self.cu_partitions, n - n % self.cu_partitions)
         # concurrent slots: a slot's H2D and D2H ride its own compute stream instead of the shared
         # copy streams (those share the 4 hardware queues with the slot streams).  With native
         # staging + launch pacing this is +3-4 % req/s on ResNet-50 (20 steps 47.2-48.3k vs
@@ -201,8 +202,9 @@ class GpuEngine:
 
                         # pooled per (mask, slot-in-partition): engines built one after another in a
                         # process reuse the queues
-                        slot.s_comp = ops.cu_masked_stream(part_masks[i % self.cu_partitions], self.device,
-                                                           key=i // self.cu_partitions)
+                        si = i % self.part_streams
+                        slot.s_comp = ops.cu_masked_stream(part_masks[si % self.cu_partitions], self.device,
+                                                           key=si // self.cu_partitions)
                     else:
                         slot.s_comp = torch.cuda.Stream(self.device)
                     slot.pool = torch.cuda.graph_pool_handle() if use_graphs else None

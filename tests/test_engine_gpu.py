@@ -144,7 +144,10 @@ def test_partitioned_engine_matches_serial():
     ref = [serial.run(b) for b in batches]
     part = GpuEngine(lambda x: model.classify(x, 5), DEV, (224, 224, 3), torch.uint8, buckets=[8], inflight=6,
                      concurrent=True, name="part", cu_partitions=2)
-    assert part.cu_partitions == 2 and part.inflight == 4 and part.stats()["cu_partitions"] == 2
+    # 6 slots over the 4 masked streams (slots 4, 5 share the streams of slots 0, 1)
+    assert part.cu_partitions == 2 and part.inflight == 6 and part.part_streams == 4
+    assert part.stats()["cu_partitions"] == 2
+    assert part.slots[4].s_comp.cuda_stream == part.slots[0].s_comp.cuda_stream
     part.warmup()
     outs, pending = [], []
     for b in batches:  # a slot returns on wait(): keep at most `inflight` batches outstanding
