@@ -1160,21 +1160,6 @@ _MASKED_STREAMS: Dict[tuple, torch.cuda.ExternalStream] = {}
 _MASKED_LOCK = __import__("threading").Lock()
 
 
-def _destroy_masked_streams() -> None:
-    """atexit: drain and destroy the pooled masked streams while the HIP runtime is still up (left
-    to the runtime's own teardown, a rocprofv3-traced process crashed in its exit handlers)."""
-    with _MASKED_LOCK:
-        items = list(_MASKED_STREAMS.items())
-        _MASKED_STREAMS.clear()
-    for (_dev, _mask, _key), st in items:
-        try:
-            st.synchronize()
-            lib().mls_stream_destroy(st.cuda_stream)
-        except Exception:
-            pass
-
-
-__import__("atexit").register(_destroy_masked_streams)
 
 
 def cu_masked_stream(mask: Sequence[int], device=None, key=0) -> torch.cuda.ExternalStream:
