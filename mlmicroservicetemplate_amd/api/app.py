@@ -123,6 +123,12 @@ class ServingRuntime:
             self.state.mark_failed(e)
             self.metrics.ready.set(0)
             return
+        # the model, engines and graphs are long-lived: move them out of the cyclic GC's young
+        # generations so a collection never walks them on the request path
+        import gc
+
+        gc.collect()
+        gc.freeze()
         self.state.mark_ready()
         self.metrics.ready.set(1)
         from ..parallel.launch import mark_replica_ready

@@ -204,6 +204,10 @@ class NativeService:
             labels = getattr(self.plugin, "labels", None)
             if labels:
                 self.srv.set_labels([str(x) for x in labels])
+            import gc
+
+            gc.collect()
+            gc.freeze()  # long-lived model / engine objects leave the collected generations
             for ri, rep in enumerate(self.replicas):
                 for si in range(max(1, int(getattr(rep, "inflight", 1)))):
                     with self._lock:
