@@ -90,10 +90,12 @@ class BertPlugin(ModelPlugin):
                 eng = GpuEngine(fwd, dev, (2 * S + 1,), torch.int32, buckets=buckets, inflight=int(s.INFLIGHT),
                                 use_graphs=bool(s.USE_GRAPHS), name=f"bert.s{S}.{dev}",
                                 concurrent=bool(s.CONCURRENT_SLOTS),
-                                # CU-masked slot halves: B=32 30.4k vs 28.2k seq/s, B=128 level
-                                # (profiles/r3_bert_cu_partition_ab.jsonl); each masked slot holds a
-                                # hardware queue, so only with a single sequence-bucket engine
-                                cu_partitions=int(s.CU_PARTITION) if len(seqs) == 1 else 0)
+                                # unpartitioned: CU-masked halves win the engine bench at B=32
+                                # (30.4k vs 28.2k seq/s, B=128 level) but lose over HTTP with the
+                                # per-sequence-bucket engines sharing the masked streams (18.8k vs
+                                # 24.1k req/s at 64 connections, 30.9k vs 32.5k at 256;
+                                # profiles/r3_bert_cu_partition_ab.jsonl); MLS_CU_PARTITION opts in
+                                cu_partitions=None)
                 eng.warmup(capture=bool(s.USE_GRAPHS))
                 per[S] = eng
             self.engines[dev] = per
