@@ -1234,6 +1234,26 @@ def census_cus(c: torch.Tensor) -> set:
     return {(int(x), (int(h) >> 8) & 0xFF) for x, h in c.tolist()}
 
 
+def intra_partition_words(parts: int, ncu: int = 256, mode: str = "intra", xccs: int = 8) -> List[List[int]]:
+    """The CU-mask words of ``parts`` intra-XCD partitions (pure; verified on the device by
+    :func:`partition_masks`).  Mask bit ``b`` is CU ``b // xccs`` of XCC ``b % xccs`` (census:
+    profiles/r3_cu_mask_census.txt); an XCC left without a bit runs on ALL its CUs, so every
+    partition keeps ``ncu / xccs / parts`` CUs on every XCC: CU ``c`` goes to partition ``c %
+    parts`` (``"intra"``) or ``c // (ncu / xccs / parts)`` (``"intra_contig"``)."""
+    per_xcc = ncu // xccs
+    if parts <= 0 or per_xcc % parts or mode not in ("intra", "intra_contig"):
+        raise ValueError(f"{parts} {mode} partitions of {per_xcc} CUs per XCC")
+    out = []
+    for p in range(parts):
+        w = [0] * max(MASK_WORDS, (ncu + 31) // 32)
+        for b in range(ncu):
+            c = b // xccs
+            if (c % parts if mode == "intra" else c // (per_xcc // parts)) == p:
+                w[b // 32] |= 1 << (b % 32)
+        out.append(w)
+    return out
+
+
 _PARTITION_MASKS: Dict[tuple, Optional[List[List[int]]]] = {}
 
 
@@ -1257,14 +1277,7 @@ def _partition_masks(parts: int, device=None, mode: str = "xcd") -> Optional[Lis
         dev = torch.device(device if device is not None else "cuda")
         ncu = torch.cuda.get_device_properties(dev).multi_processor_count
         out, seen = [], set()
-        for p in range(parts):
-            # mask bit b -> XCC b % 8, CU b // 8 of that XCC (census: profiles/r3_cu_mask_census.txt);
-            # an XCC left without a bit runs on ALL its CUs, so every partition keeps bits on every XCC
-            w = [0] * MASK_WORDS
-            for b in range(ncu):
-                c = b // 8  # CU index inside its XCC
-                if (c % parts if mode == "intra" else c // (ncu // 8 // parts)) == p:
-                    w[b // 32] |= 1 << (b % 32)
+        for p, w in enumerate(intra_partition_words(parts, ncu, mode)):
             cus = census_cus(cu_census(cu_masked_stream(w, dev, key="census"), blocks=4096))
             if len(cus) > ncu // parts or cus & seen:
                 return None
