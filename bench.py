@@ -144,6 +144,14 @@ def run_rank(args) -> int:
     t_bcast = time.perf_counter() - t0
 
     fwd = build_model(args.backend, device, args.batch, params)
+    if args.cu_partition and not args.serial:
+        from mlmicroservicetemplate_amd import ops
+
+        # the census-verified masks (cached for the engine); a device whose mask layout does not
+        # verify runs unpartitioned -- and then with the 5 slots of that mode
+        if ops.partition_masks(args.cu_partition, device, mode=os.environ.get("MLS_CU_PARTITION_MODE", "intra")) is None:
+            print(f"bench: CU partitions unavailable on {device}; unpartitioned", file=sys.stderr)
+            args.cu_partition = 0
     if args.inflight <= 0:
         args.inflight = 4 if args.cu_partition and not args.serial else 5
     engine = GpuEngine(fwd, device, (224, 224, 3), torch.uint8, buckets=[args.batch], inflight=args.inflight,
