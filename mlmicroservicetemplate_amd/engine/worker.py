@@ -140,6 +140,12 @@ class GpuEngine:
                 hwq = int(os.environ.get("MLS_HW_QUEUES", "4"))
                 n = min(self.inflight, max(hwq, self.cu_partitions))
                 self.part_streams = max(self.cu_partitions, n - n % self.cu_partitions)
+                try:  # create (or take from the pool) every masked stream up front
+                    masked = [ops.cu_masked_stream(part_masks[si % self.cu_partitions], self.device,
+                                                   key=si // self.cu_partitions) for si in range(self.part_streams)]
+                except Exception as e:  # e.g. no hardware queue left for another masked stream
+                    logger.warning("%s: CU-masked streams unavailable (%s); slots use all CUs", name, e)
+                    part_masks, self.cu_partitions, self.part_streams = None, 0, 0
         # concurrent slots: a slot's H2D and D2H ride its own compute stream instead of the shared
         # copy streams (those share the 4 hardware queues with the slot streams).  With native
         # staging + launch pacing this is +3-4 % req/s on ResNet-50 (20 steps 47.2-48.3k vs
@@ -198,13 +204,9 @@ class GpuEngine:
                 )
                 if self.concurrent:
                     if part_masks is not None:
-                        from .. import ops
-
                         # pooled per (mask, slot-in-partition): engines built one after another in a
-                        # process reuse the queues
-                        si = i % self.part_streams
-                        slot.s_comp = ops.cu_masked_stream(part_masks[si % self.cu_partitions], self.device,
-                                                           key=si // self.cu_partitions)
+                        # process reuse the queues; slots beyond them share round-robin
+                        slot.s_comp = masked[i % self.part_streams]
                     else:
                         slot.s_comp = torch.cuda.Stream(self.device)
                     slot.pool = torch.cuda.graph_pool_handle() if use_graphs else None
