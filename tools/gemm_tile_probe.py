@@ -22,6 +22,9 @@ SHAPES = {  # name: (M, N, K, act)
     "llama16k_gateup": (16384, 28672, 4096, "silu_mul"), "sq8k": (8192, 8192, 8192, "none"),
     "tp8_qkv": (16384, 768, 4096, "none"), "tp8_gateup": (16384, 3584, 4096, "silu_mul"),
     "tp8_down": (16384, 4096, 1792, "none"), "tp8_o": (16384, 4096, 512, "none"),
+    # Llama-3-8B prefill of one 512-token prompt (B=1 x 512 rows)
+    "llama512_qkv": (512, 6144, 4096, "none"), "llama512_o": (512, 4096, 4096, "none"),
+    "llama512_gateup": (512, 28672, 4096, "silu_mul"), "llama512_down": (512, 4096, 14336, "none"),
 }
 
 
