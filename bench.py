@@ -82,9 +82,11 @@ def parse_args(argv=None):
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--serial", action="store_true", help="one compute stream (no concurrent in-flight batches)")
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--measure-eager", type=int, default=0, metavar="STEPS",
-                    help="after the timed run, time STEPS batches of the stock-PyTorch (MIOpen/hipBLASLt) "
-                         "engine in the same process and report vs_pytorch_eager_per_gpu")
+    ap.add_argument("--measure-eager", type=int, default=int(os.environ.get("MLS_MEASURE_EAGER", 20)),
+                    metavar="STEPS",
+                    help="after the timed run (which it does not touch), time STEPS batches of the "
+                         "stock-PyTorch (MIOpen/hipBLASLt) engine in the same process and report "
+                         "vs_pytorch_eager_per_gpu -- BASELINE.md's config-2 bar; 0 = skip")
     ap.add_argument("--launch-timeout", type=float, default=1500.0,
                     help="launcher mode: bound on the whole N-rank job (s)")
     return ap.parse_args(argv)

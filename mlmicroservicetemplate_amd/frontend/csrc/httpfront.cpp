@@ -537,6 +537,10 @@ class Server {
       labels = labels_json_;
     }
     for (int r = 0; r < n; ++r) {
+      if (k > 0 && idx[r * k] < 0) {  // the GPU image decode flagged this upload (ids -1): as PIL's error
+        reply(refs[r], 500, failure_body("ValueError: undecodable image"));
+        continue;
+      }
       std::string body = "{\"status\":\"success\",\"result\":{\"classes\":[";
       for (int j = 0; j < k; ++j) {
         if (j) body += ',';

@@ -69,14 +69,18 @@ struct ImgHeader {
 #pragma pack(pop)
 static_assert(sizeof(ImgHeader) == HDR_BYTES, "container header");
 
-inline void fill_geometry(ImgHeader& h) {
+// false: the resized size does not fit the header's 16-bit fields (aspect ratio beyond ~256:1);
+// the caller then takes the PIL path
+inline bool fill_geometry(ImgHeader& h) {
   // decode_image: s = resize / min(w, h); nw, nh = max(size, round(w * s)), max(size, round(h * s))
   const double sc = (double)IMG_SHORT / (double)(h.width < h.height ? h.width : h.height);
   const double nw = std::nearbyint(h.width * sc), nh = std::nearbyint(h.height * sc);  // half-to-even
+  if (nw > 65535.0 || nh > 65535.0) return false;
   h.rw = (uint16_t)(nw < IMG_OUT ? IMG_OUT : nw);
   h.rh = (uint16_t)(nh < IMG_OUT ? IMG_OUT : nh);
   h.left = (uint16_t)((h.rw - IMG_OUT) / 2);
   h.top = (uint16_t)((h.rh - IMG_OUT) / 2);
+  return true;
 }
 
 // a raw 224 x 224 x 3 RGB upload -> container
@@ -173,6 +177,11 @@ struct BitReader {
   uint64_t acc = 0;
   int nbits = 0;
   bool marker = false;  // hit a marker: feed zeros
+  int zfill = 0;        // zero bits appended past the data / a marker (the newest bits of acc)
+  // the decoder consumed bits that were not in the stream: a truncated (or marker-cut) scan.
+  // PIL (no LOAD_TRUNCATED_IMAGES) rejects such a file, so the upload takes that path and fails
+  // the same way instead of classifying a grey tail.
+  bool overrun() const { return zfill > nbits; }
   void fill() {
     // bulk path: no 0xFF among the next 8 bytes (the usual case) -> one big-endian 64-bit load
     if (!marker && p + 8 <= end) {
@@ -189,20 +198,24 @@ struct BitReader {
     }
     while (nbits <= 56) {
       uint8_t b = 0;
+      bool real = false;
       if (!marker && p < end) {
         b = *p;
         if (b == 0xFF) {
           const uint8_t n = p + 1 < end ? p[1] : 0;
           if (n == 0x00) {
             p += 2;
+            real = true;
           } else {
             marker = true;  // RSTn / EOI: stop consuming
             b = 0;
           }
         } else {
           ++p;
+          real = true;
         }
       }
+      if (!real) zfill += 8;
       acc |= (uint64_t)b << (56 - nbits);
       nbits += 8;
     }
@@ -224,6 +237,7 @@ struct BitReader {
   void reset_at_marker() {  // byte-align and consume an RSTn marker
     acc = 0;
     nbits = 0;
+    zfill = 0;
     marker = false;
     while (p + 1 < end && !(p[0] == 0xFF && p[1] >= 0xD0 && p[1] <= 0xD7)) ++p;
     if (p + 1 < end) p += 2;
@@ -397,6 +411,7 @@ inline bool jpeg_to_container(const uint8_t* data, size_t n, uint8_t* out, std::
     for (int mcu = 0; mcu < total_mcu; ++mcu) {
       if (restart) {
         if (todo == 0) {
+          if (br.overrun()) return fail("truncated scan");
           br.reset_at_marker();
           pred[0] = pred[1] = pred[2] = 0;
           todo = restart;
@@ -474,6 +489,7 @@ inline bool jpeg_to_container(const uint8_t* data, size_t n, uint8_t* out, std::
           }
       }
     }
+    if (br.overrun()) return fail("truncated scan");
   }
 
   ImgHeader hd;
@@ -548,7 +564,7 @@ inline bool jpeg_to_container(const uint8_t* data, size_t n, uint8_t* out, std::
     hd.comp[c].bh = (uint16_t)(mcuy * cv[c]);
     hd.comp[c].offset = first[c];
   }
-  fill_geometry(hd);
+  if (!fill_geometry(hd)) return fail("aspect ratio beyond the container's resize range");
   std::memcpy(out, &hd, sizeof(hd));
   return true;
 }

@@ -346,6 +346,11 @@ class ResNet50Fused:
         self.std = IMAGENET_STD
         self.max_batch = max_batch
         self._ws = ops.StreamWorkspace(self._workspace_bytes(max_batch) // 4 + 1, self.device)
+        # fused head (MLS_FUSED_HEAD=0: avgpool + FC + softmax/top-k kernels): the last conv's
+        # epilogue accumulates the global average pool into a per-stream fp32 buffer, one kernel
+        # (csrc/head.hip) does FC + softmax + top-k and zeroes the buffer for the next forward
+        self.fuse_head = os.environ.get("MLS_FUSED_HEAD", "1") != "0"
+        self._pool = ops.StreamWorkspace(max_batch * self.fc_w.shape[1], self.device, zero=True)
 
     @property
     def workspace(self) -> torch.Tensor:
@@ -395,10 +400,13 @@ class ResNet50Fused:
             if b > batch:
                 continue
             for name, M, N, K in self.layer_gemm_shapes(b):
-                _cfg, sk = self._plan(name, M, N, K)
+                cfg, sk = self._plan(name, M, N, K)
+                if cfg in self.ops.PIPE_CFGS:  # splitk = K split + 16 * (items per block - 1)
+                    sk = sk % 16 or 1
                 if sk > 1:
                     need = max(need, sk * M * N * 4)
-        return max(need, 1 << 20)
+        # the fused head's logits scratch
+        return max(need, batch * NUM_CLASSES * 4, 1 << 20)
 
     # -- forward ----------------------------------------------------------------------------
     def _conv(self, x, name, act, residual=None, pad=None):
@@ -423,6 +431,40 @@ class ResNet50Fused:
 
     def forward(self, images_u8_nhwc: torch.Tensor) -> torch.Tensor:
         """uint8 ``[B,H,W,3]`` on device -> bf16 logits ``[B, num_classes]``."""
+        ops = self.ops
+        B = images_u8_nhwc.shape[0]
+        if self.fuse_head:
+            pooled = self._trunk(images_u8_nhwc, pool=True)
+            _v, _i, logits = ops.fc_head(pooled, self.fc_w, self.fc_b, 0, logits=self._logits_buf(B))
+            return logits.to(torch.bfloat16)
+        x = self._trunk(images_u8_nhwc, pool=False)
+        pooled = ops.avgpool_global_nhwc(x)
+        cfg, sk = self.tuning.get("fc", (0, 0))
+        return ops.gemm(pooled, self.fc_w, self.fc_b, workspace=self.workspace, cfg=cfg, splitk=sk)
+
+    __call__ = forward
+
+    def _logits_buf(self, B: int) -> torch.Tensor:
+        return self.workspace[: B * self.num_classes].view(B, self.num_classes)
+
+    def classify(self, images_u8_nhwc: torch.Tensor, k: int = 5, err: Optional[torch.Tensor] = None):
+        """Head: logits -> softmax -> top-k.  Returns (probs fp32 [B,k], ids int32 [B,k]).  ``err``
+        (int32 [B], ``ops.image_decode``'s per-image flags): flagged rows come back as ids -1 / NaN."""
+        if self.fuse_head:
+            pooled = self._trunk(images_u8_nhwc, pool=True)
+            B = images_u8_nhwc.shape[0]
+            vals, idx, _ = self.ops.fc_head(pooled, self.fc_w, self.fc_b, k, logits=self._logits_buf(B), err=err)
+            return vals, idx
+        vals, idx = self.ops.softmax_topk(self.forward(images_u8_nhwc), k)
+        if err is not None:  # unfused A/B path: same contract, torch ops
+            bad = (err[: idx.shape[0]] != 0).view(-1, 1)
+            idx = torch.where(bad, torch.full_like(idx, -1), idx)
+            vals = torch.where(bad, torch.full_like(vals, float("nan")), vals)
+        return vals, idx
+
+    def _trunk(self, images_u8_nhwc: torch.Tensor, pool: bool) -> torch.Tensor:
+        """Stem .. layer4: the last block output ``[B,7,7,2048]`` bf16, or with ``pool`` its global
+        average fp32 ``[B,2048]`` (fused into the last conv; the block output is never written)."""
         ops = self.ops
         B = images_u8_nhwc.shape[0]
         if B > self.max_batch:
@@ -463,16 +505,18 @@ class ResNet50Fused:
                                      act=ops.ACT_RELU, workspace=self.workspace, cfg=cfg, splitk=sk)
             else:
                 identity = self._conv(x, p + ".down", ops.ACT_NONE) if bi == 0 else x
+                if nxt is None and pool:  # the network's last conv: average pool in its epilogue
+                    pooled = self._pool.get()[: B * self.fc_w.shape[1]].view(B, -1)
+                    cfg, _sk = self.tuning.get(p + ".conv3", (0, 0))
+                    s3 = self.specs[p + ".conv3"]
+                    ops.conv2d_pool(t2, self.w[p + ".conv3"], self.b[p + ".conv3"], pooled, kernel=s3.k,
+                                    stride=s3.stride, pad=s3.pad, residual=identity, act=ops.ACT_RELU, cfg=cfg)
+                    return pooled
                 x = self._conv(t2, p + ".conv3", ops.ACT_RELU, residual=identity)
             if nxt is not None:
                 t1 = self._conv(x, nxt + ".conv1", ops.ACT_RELU)
-        pooled = ops.avgpool_global_nhwc(x)
-        cfg, sk = self.tuning.get("fc", (0, 0))
-        return ops.gemm(pooled, self.fc_w, self.fc_b, workspace=self.workspace, cfg=cfg, splitk=sk)
-
-    __call__ = forward
-
-    def classify(self, images_u8_nhwc: torch.Tensor, k: int = 5):
-        """Fused head: logits -> softmax -> top-k.  Returns (probs fp32 [B,k], ids int32 [B,k])."""
-        logits = self.forward(images_u8_nhwc)
-        return self.ops.softmax_topk(logits, k)
+        if pool:  # (the last block was a dual / chained one: not in ResNet-50, kept general)
+            pooled = self._pool.get()[: B * self.fc_w.shape[1]].view(B, -1)
+            pooled.copy_(ops.avgpool_global_nhwc(x).float())
+            return pooled
+        return x

@@ -52,16 +52,17 @@ class StreamWorkspace:
     streams (GpuEngine concurrent slots) must not share it.  A stream's buffer is allocated on
     its first use -- the engine's eager warm-up, before any graph capture."""
 
-    def __init__(self, elems: int, device):
+    def __init__(self, elems: int, device, zero: bool = False):
         self.elems = int(elems)
         self.device = torch.device(device)
+        self.zero = zero  # zero-initialised (an accumulator its consumer re-zeroes, e.g. the fused pool)
         self._bufs: dict = {}
 
     def get(self) -> torch.Tensor:
         key = torch.cuda.current_stream(self.device).cuda_stream if self.device.type == "cuda" else 0
         buf = self._bufs.get(key)
         if buf is None:
-            buf = torch.empty(self.elems, device=self.device, dtype=torch.float32)
+            buf = (torch.zeros if self.zero else torch.empty)(self.elems, device=self.device, dtype=torch.float32)
             self._bufs[key] = buf
         return buf
 
@@ -105,6 +106,12 @@ CFG_HALO = 100
 CFG_HALO_N32 = 101
 CFG_HALO_XL = 102  # 512 output pixels x 64 channels per block, 4 x 4 MFMA tiles per wave
 HALO_CFGS = (CFG_HALO, CFG_HALO_N32, CFG_HALO_XL)
+# cfg values that select the pipelined halo kernel (csrc/conv3x3_pipe.hip): CFG_PIPE + variant;
+# the tuning table's splitk carries the K split, MLS items per block ride in the upper digits of
+# splitk (splitk = ks + 16 * (ipb - 1)).
+CFG_PIPE = 110
+PIPE_VARIANTS = 6
+PIPE_CFGS = tuple(range(CFG_PIPE, CFG_PIPE + PIPE_VARIANTS))
 
 
 def conv2d_nhwc(
@@ -139,6 +146,12 @@ def conv2d_nhwc(
     if cout % 8:
         raise ValueError("Cout must be a multiple of 8")
     ho, wo = conv_out_hw(H, W, kernel, stride, pad)
+    if cfg in PIPE_CFGS:
+        if kernel != 3 or stride != 1 or pad != 1 or scale is not None or residual is not None:
+            raise ValueError("CFG_PIPE: 3x3 / stride 1 / pad 1 convolutions without a scale / residual only")
+        ks, ipb = max(1, int(splitk)) % 16 or 1, max(1, int(splitk)) // 16 + 1
+        return conv3x3_pipe(x, w, bias, act=act, out=out, variant=cfg - CFG_PIPE, splitk=ks, ipb=ipb,
+                            workspace=workspace)
     if cfg in HALO_CFGS:
         if kernel != 3 or stride != 1 or pad != 1 or scale is not None:
             raise ValueError("CFG_HALO: 3x3 / stride 1 / pad 1 convolutions without a scale only")
@@ -777,6 +790,115 @@ def conv3x3_halo(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] 
     return out
 
 
+def conv2d_pool(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], pool: torch.Tensor, *, kernel: int,
+                stride: int = 1, pad: int = 0, residual: Optional[torch.Tensor] = None, act=ACT_NONE,
+                out: Optional[torch.Tensor] = None, pool_only: bool = True, cfg: int = 0) -> Optional[torch.Tensor]:
+    """``conv2d_nhwc`` with the global average pool of its output fused into the epilogue (the
+    network's last convolution, csrc/conv_gemm.hip ``ConvArgs::pool``): ``pool`` fp32 ``[B, Cout]``
+    += the per-image mean of ``act(conv + bias (+ residual))``.  ``pool`` must be zero on entry
+    (:func:`fc_head` zeroes it after reading); with ``pool_only`` the output is not written."""
+    dev = x.device
+    _need(x, "x", torch.bfloat16, dev)
+    _need(w, "w", torch.bfloat16, dev)
+    _need(pool, "pool", torch.float32, dev)
+    B, H, W, C = x.shape
+    cout = w.shape[0]
+    if tuple(w.shape) != (cout, kernel, kernel, C) or C == 4:
+        raise ValueError(f"weight shape {tuple(w.shape)} != [{cout},{kernel},{kernel},{C}]")
+    ho, wo = conv_out_hw(H, W, kernel, stride, pad)
+    if pool.shape[0] < B or pool.shape[-1] != cout:
+        raise ValueError(f"pool must be [>= {B}, {cout}]")
+    if bias is not None:
+        _need(bias, "bias", torch.float32, dev)
+    if residual is not None:
+        _need(residual, "residual", torch.bfloat16, dev)
+        if tuple(residual.shape) != (B, ho, wo, cout):
+            raise ValueError("residual shape mismatch")
+    if not pool_only and out is None:
+        out = torch.empty(B, ho, wo, cout, device=dev, dtype=torch.bfloat16)
+    check(lib().mls_conv2d_pool(x.data_ptr(), w.data_ptr(), None, _ptr(bias), _ptr(residual), _ptr(out),
+                                pool.data_ptr(), int(pool_only), B, H, W, C, cout, kernel, kernel, stride, pad,
+                                _act(act), int(cfg), stream_ptr(dev)), "mls_conv2d_pool")
+    return out
+
+
+def fc_head(pooled: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], k: int, *,
+            logits: Optional[torch.Tensor] = None, softmax: bool = True, err: Optional[torch.Tensor] = None,
+            vals: Optional[torch.Tensor] = None, idx: Optional[torch.Tensor] = None):
+    """Classifier head in one launch (csrc/head.hip): ``pooled`` fp32 ``[B, K]`` (the fused average
+    pool; ZEROED by this call for the next forward) -> logits = pooled . w^T + bias (fp32, into
+    ``logits``) -> (softmax ->) top-``k``.  ``err`` int32 ``[B]``: rows flagged nonzero come back
+    with ids -1 and NaN values (an undecodable upload).  Returns (vals fp32 [B,k], ids int32 [B,k],
+    logits); with ``k == 0`` only the logits."""
+    dev = pooled.device
+    _need(pooled, "pooled", torch.float32, dev)
+    _need(w, "w", torch.bfloat16, dev)
+    B, K = pooled.shape
+    N = w.shape[0]
+    if w.shape[1] != K:
+        raise ValueError("w must be [N, K]")
+    if bias is not None:
+        _need(bias, "bias", torch.float32, dev)
+    if logits is None:
+        logits = torch.empty(B, N, device=dev, dtype=torch.float32)
+    _need(logits, "logits", torch.float32, dev)
+    if logits.numel() < B * N:
+        raise ValueError("logits buffer too small")
+    if err is not None:
+        _need(err, "err", torch.int32, dev)
+    if k > 0:
+        if vals is None:
+            vals = torch.empty(B, k, device=dev, dtype=torch.float32)
+        if idx is None:
+            idx = torch.empty(B, k, device=dev, dtype=torch.int32)
+    check(lib().mls_fc_head(pooled.data_ptr(), w.data_ptr(), _ptr(bias), logits.data_ptr(), _ptr(vals), _ptr(idx),
+                            _ptr(err), B, N, K, int(k), int(softmax), stream_ptr(dev)), "mls_fc_head")
+    return vals, idx, logits
+
+
+def conv3x3_pipe(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, act=ACT_NONE,
+                 out: Optional[torch.Tensor] = None, variant: int = 0, splitk: int = 1, ipb: int = 1,
+                 workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """3x3 / stride 1 / pad 1 NHWC conv on the pipelined halo kernel (csrc/conv3x3_pipe.hip):
+    x ``[B,H,W,Cin]`` bf16, w packed ``[N,3,3,Cin]`` bf16, bias fp32 ``[N]`` -> ``[B,H,W,N]``
+    ``act(conv + bias)`` (act: none / ReLU).  ``variant`` picks (channels per item, waves, row
+    blocks per wave, ring stages); ``splitk`` > 1 splits the input channels over that many items
+    per tile (in-launch reduction through fp32 slabs in ``workspace``, >= splitk * B*H*W*N floats;
+    otherwise one slice); ``ipb`` = consecutive items per block."""
+    dev = x.device
+    _need(x, "x", torch.bfloat16, dev)
+    _need(w, "w", torch.bfloat16, dev)
+    B, H, W, C = x.shape
+    N = w.shape[0]
+    if tuple(w.shape) != (N, 3, 3, C) or C % 32 or N % 32 or N > 512 or not 0 <= variant < PIPE_VARIANTS:
+        raise ValueError("conv3x3_pipe: w must be [N,3,3,Cin], Cin % 32 == 0, N % 32 == 0, N <= 512")
+    if act not in (ACT_NONE, ACT_RELU, "none", "relu"):
+        raise ValueError("conv3x3_pipe: act must be none or relu")
+    if bias is not None:
+        _need(bias, "bias", torch.float32, dev)
+        if bias.numel() != N:
+            raise ValueError("bias must have N elements")
+    shape = (B, H, W, N)
+    if out is None:
+        out = torch.empty(shape, device=dev, dtype=torch.bfloat16)
+    else:
+        _need(out, "out", torch.bfloat16, dev)
+        if tuple(out.shape) != shape:
+            raise ValueError(f"out must be {shape}")
+    wsp, wsb = _workspace_args(workspace)
+    check(lib().mls_conv3x3_pipe(x.data_ptr(), w.data_ptr(), _ptr(bias), out.data_ptr(), wsp, wsb, B, H, W, C, N,
+                                 _act(act), int(variant), max(1, int(splitk)), max(1, int(ipb)), stream_ptr(dev)),
+          "mls_conv3x3_pipe")
+    return out
+
+
+def conv3x3_pipe_geometry(B: int, H: int, W: int, variant: int = 0) -> Optional[Tuple[int, int]]:
+    """(output rows per item, images per item) of the pipelined kernel's variant, or None."""
+    th, nb = ctypes.c_int(0), ctypes.c_int(0)
+    rc = lib().mls_conv3x3_pipe_geometry(B, H, W, variant, ctypes.byref(th), ctypes.byref(nb))
+    return (th.value, nb.value) if rc == 0 else None
+
+
 def conv3x3_halo_geometry(B: int, H: int, W: int, variant: int = 0) -> Optional[Tuple[int, int]]:
     """(output rows per tile, images per tile) the halo kernel uses for this shape, or None."""
     th, nb = ctypes.c_int(0), ctypes.c_int(0)
@@ -1128,9 +1250,11 @@ def image_decode(containers: torch.Tensor, out: Optional[torch.Tensor] = None,
     """GPU half of the image path (csrc/image_decode.hip): ``[B, IMAGE_CONTAINER_BYTES]`` uint8
     containers (raw RGB, or host-Huffman-decoded JPEG coefficients + resize geometry) -> uint8
     ``[B, 224, 224, 3]``: IDCT, libjpeg chroma upsampling + YCbCr->RGB, Pillow's bilinear resize and
-    the centre crop of ``plugins.builtin.decode_image``.  ``err`` (int32 [1], optional) is set to 1
-    when a container is unusable (that image comes out black).  Capturable (fixed launch geometry;
-    the scratch comes from the caller's -- in a graph, the graph pool's -- allocator)."""
+    the centre crop of ``plugins.builtin.decode_image``.  ``err`` (int32 ``[B]``, optional): row b is
+    set to 1 when container b is unusable (that image comes out black), else 0 -- every launch, so
+    a captured graph needs no clearing; :func:`fc_head` turns flagged rows into id -1 / NaN.
+    Capturable (fixed launch geometry; the scratch comes from the caller's -- in a graph, the graph
+    pool's -- allocator)."""
     dev = containers.device
     _need(containers, "containers", torch.uint8, dev)
     if containers.dim() != 2 or containers.shape[1] != IMAGE_CONTAINER_BYTES:
@@ -1141,6 +1265,8 @@ def image_decode(containers: torch.Tensor, out: Optional[torch.Tensor] = None,
     scratch = torch.empty(B * IMAGE_SCRATCH_PER_IMAGE, device=dev, dtype=torch.uint8)
     if err is not None:
         _need(err, "err", torch.int32, dev)
+        if err.numel() < B:
+            raise ValueError(f"err must have >= {B} elements (one flag per image)")
     rc = lib().mls_image_decode(containers.data_ptr(), out.data_ptr(), scratch.data_ptr(), IMAGE_SCRATCH_PER_IMAGE, B,
                                 _ptr(err), stream_ptr(dev))
     check(rc, "mls_image_decode")

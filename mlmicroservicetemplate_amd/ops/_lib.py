@@ -47,6 +47,11 @@ _SIGS = {
     "mls_conv3x3_halo": [P, P, P, P, P, P, SZ, I, I, I, I, I, I, I, I, P],
     "mls_conv3x3_halo_geometry": [I, I, I, _c.POINTER(I), _c.POINTER(I)],
     "mls_conv3x3_halo_geometry_v": [I, I, I, I, _c.POINTER(I), _c.POINTER(I)],
+    "mls_conv2d_pool": [P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P],
+    "mls_fc_head": [P, P, P, P, P, P, P, I, I, I, I, I, P],
+    "mls_conv3x3_pipe": [P, P, P, P, P, SZ, I, I, I, I, I, I, I, I, I, P],
+    "mls_conv3x3_pipe_geometry": [I, I, I, I, _c.POINTER(I), _c.POINTER(I)],
+    "mls_conv3x3_pipe_num_variants": [],
     "mls_avgpool_global": [P, P, I, I, I, P],
     "mls_bn_act": [P, P, P, P, L, I, I, P],
     "mls_silu_mul_interleaved": [P, P, L, I, P],

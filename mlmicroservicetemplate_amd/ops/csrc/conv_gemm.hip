@@ -65,6 +65,12 @@ struct ConvArgs {
   // slice block of each tile sums the slabs and runs the epilogue in-launch (no reduce kernel)
   int* cnt;
   uint32_t ws_bytes;  // slab extent (sc1 buffer accesses of the in-launch reduction)
+  // fused global average pool (the network's last convolution): pool[b][n] += pool_scale * sum of
+  // the image's post-activation rows (one fp32 atomic per image segment and column of a tile);
+  // pool_only: the output itself is not stored.  splitk == 1 only.
+  float* pool;
+  float pool_scale;
+  int pool_hw, pool_only;
 };
 
 int g_dbg_flags = 0;  // set via mls_set_debug_flags (tools/conv_ablate.py); 0 in production
@@ -479,7 +485,34 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_kernel(const ConvArgs 
         if (v[0] == 12345.678f) st16(a.out, pack8(v));  // keep the value live, never true
         continue;
       }
+      if (a.pool) {  // the pooled values: post-activation, back into this thread's own LDS slots
+        float* cp = Cs + (row - row_lo) * C_LD + c8 * 8;
+        *reinterpret_cast<float4*>(cp) = float4{v[0], v[1], v[2], v[3]};
+        *reinterpret_cast<float4*>(cp + 4) = float4{v[4], v[5], v[6], v[7]};
+        if (a.pool_only) continue;
+      }
       st16(a.out + (size_t)m * a.ldo + n, pack8(v));
+    }
+    if (a.pool && a.splitk == 1) {
+      // global average pool: a thread per column walks the pass's rows, one atomic per image segment
+      __syncthreads();
+      const int n = n0 + tid;
+      if (tid < BN && n < a.N) {
+        float sum = 0.f;
+        int cur = -1;
+        for (int r = 0; r < PASS_ROWS; ++r) {
+          const int m = m0 + row_lo + r;
+          if (m >= a.M) break;
+          const int b = m / a.pool_hw;
+          if (b != cur) {
+            if (cur >= 0) atomicAdd(a.pool + (size_t)cur * a.N + n, sum * a.pool_scale);
+            sum = 0.f;
+            cur = b;
+          }
+          sum += Cs[r * C_LD + tid];
+        }
+        if (cur >= 0) atomicAdd(a.pool + (size_t)cur * a.N + n, sum * a.pool_scale);
+      }
     }
   }
   if (a.splitk > 1 && a.cnt != nullptr) {
@@ -1018,6 +1051,51 @@ int mls_conv2d(const void* x, const void* w, const float* scale, const float* bi
   if (wb >= 0x7FFFFFFFull) return MLS_UNSUPPORTED;
   a.w_bytes = (uint32_t)wb;
   return launch_conv(a, mode, cfg, splitk, ws_bytes, (hipStream_t)stream);
+}
+
+// mls_conv2d + the fused global average pool of the output: pool [B][Cout] fp32 += mean over the
+// Ho*Wo pixels of each image (the caller zeroes it; ops.fc_head does so after reading it);
+// pool_only: `out` is not written (may be null).  No split-K, no persistent config.
+int mls_conv2d_pool(const void* x, const void* w, const float* scale, const float* bias, const void* res, void* out,
+                    float* pool, int pool_only, int B, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                    int pad, int act, int cfg, void* stream) {
+  if (!pool || act == ACT_SILU_MUL || (!out && !pool_only)) return MLS_BAD_ARG;
+  if (cfg >= 20 && cfg <= 22) cfg = 0;
+  ConvArgs a{};
+  a.x = (const bf16*)x;
+  a.w = (const bf16*)w;
+  a.scale = scale;
+  a.bias = bias;
+  a.res = (const bf16*)res;
+  a.out = (bf16*)out;
+  a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.N = Cout; a.KH = KH; a.KW = KW; a.stride = stride; a.pad = pad;
+  a.Ho = (H + 2 * pad - KH) / stride + 1;
+  a.Wo = (W + 2 * pad - KW) / stride + 1;
+  a.M = B * a.Ho * a.Wo;
+  a.act = act;
+  a.ldo = Cout;
+  a.ldr = Cout;
+  a.pool = pool;
+  a.pool_hw = a.Ho * a.Wo;
+  a.pool_scale = 1.f / (float)(a.Ho * a.Wo);
+  a.pool_only = pool_only;
+  const size_t xb = (size_t)B * H * W * Cin * 2;
+  if (xb >= 0x7FFFFFFFull) return MLS_UNSUPPORTED;
+  a.x_bytes = (uint32_t)xb;
+  int mode;
+  if (KH == 1 && KW == 1 && pad == 0) {
+    mode = MODE_1X1;
+    a.K = Cin;
+  } else if (Cin % 64 == 0 && KH * KW <= 32 && Cin != 4) {
+    mode = MODE_GENERIC;
+    a.K = KH * KW * Cin;
+  } else {
+    return MLS_UNSUPPORTED;
+  }
+  const size_t wb = (size_t)Cout * a.K * 2;
+  if (wb >= 0x7FFFFFFFull) return MLS_UNSUPPORTED;
+  a.w_bytes = (uint32_t)wb;
+  return launch_conv(a, mode, cfg, 1, 0, (hipStream_t)stream);
 }
 
 // out = act(conv1x1(y, W[:, :Cin1]) + conv1x1_stride2(x, W[:, Cin1:]) + bias): y [B][Ho][Wo][Cin1],

@@ -1,0 +1,200 @@
+// Fused classifier head of ResNet-50 (K2 + K6 + K7 of SURVEY.md §2.E.1 in ONE launch):
+//   logits = pooled . W^T + b  ->  softmax  ->  top-k  (+ per-row decode-error flags)
+// where `pooled` [B][K] fp32 is the global average pool, accumulated by the LAST convolution's
+// epilogue (conv_gemm.hip, ConvArgs::pool: per-image column sums of the post-ReLU tile, one fp32
+// atomic per (image segment, column) of a tile) -- the [B][7][7][2048] block output is never written
+// to HBM nor read back, and avgpool / FC / softmax-top-k stop being three launches (~31 us serial,
+// round 3's profiles/r3_resnet50_b32_serial_kernel_summary_final.txt).
+//
+// Grid (ceil(N / 16) class groups) x (ceil(B / 16) row groups), 4 waves.  A block computes the
+// 16 x 16 logit tile of its classes x rows on MFMA (D = W_tile . pooled^T, K split over the waves,
+// pooled converted to bf16 on load -- the precision of the unfused bf16 GEMM), reduces the waves
+// through LDS, adds the bias and writes the tile through (sc1) to `logits`.  One ticket per row
+// group: the block that completes a row group (the last of its class groups) runs softmax + top-k
+// for those rows from the written-through logits (sc1 loads, no acquire: guide §6 Guideline 16 R1)
+// and zeroes the rows' pooled sums for the next launch (the convolution accumulates into them).
+// Counters are this stream's self-resetting split-K counters (conv_gemm.hip).
+#include "common.h"
+
+int* mls_stream_splitk_counters(void* stream, long ntiles);  // conv_gemm.hip
+
+namespace {
+
+constexpr int HT = 16;     // classes x rows per block tile
+constexpr int MAXV = 32;   // logits per lane in the finishing pass (N <= 2048)
+
+struct HeadArgs {
+  const float* pooled;  // [B][K] fp32 (zeroed again by this kernel)
+  const bf16* w;        // [N][K]
+  const float* bias;    // [N] or null
+  float* logits;        // [B][N] fp32 scratch / output
+  float* vals;          // [B][k] fp32 (k > 0)
+  int* idx;             // [B][k] int32
+  const int* err;       // [B] int32 or null: rows flagged nonzero get idx -1, vals NaN
+  int* cnt;             // [ceil(B/16)] arrival counters, zero between launches
+  int B, N, K, k, softmax;
+  uint32_t pooled_bytes, w_bytes, logits_bytes;
+};
+
+typedef unsigned int head_u32x4 __attribute__((__vector_size__(16)));
+
+__global__ __launch_bounds__(256) void fc_head_kernel(const HeadArgs a) {
+  __shared__ float red[4][HT][HT + 1];
+  __shared__ int flag;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int c0 = blockIdx.x * HT, r0 = blockIdx.y * HT;
+  const rsrc_t wr = make_rsrc(a.w, a.w_bytes);
+  const rsrc_t pr = make_rsrc(a.pooled, a.pooled_bytes);
+  const rsrc_t lr = make_rsrc(a.logits, a.logits_bytes);
+
+  // ---- 16 x 16 logit tile: wave w sums k in [w * K/4, (w + 1) * K/4) ----
+  const int kw = a.K / 4;  // host: K % 128 == 0
+  const int kb = wid * kw;
+  const int cl = c0 + fr, rw = r0 + fr;
+  const int woff = cl < a.N ? (cl * a.K + kb + fq * 8) * 2 : OOB;
+  const int poff = rw < a.B ? (rw * a.K + kb + fq * 8) * 4 : OOB;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < kw; k0 += 128) {  // 4 k-steps of 32 per trip: 4 x (16 B + 32 B) in flight per lane
+    uint4 wv[4];
+    float4 pv[4][2];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      wv[s] = bload16(wr, woff == OOB ? OOB : woff + (k0 + 32 * s) * 2);
+      pv[s][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(pr, poff == OOB ? OOB : poff + (k0 + 32 * s) * 4, 0, 0));
+      pv[s][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(pr, poff == OOB ? OOB : poff + (k0 + 32 * s) * 4 + 16, 0, 0));
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      bf16x8 b;
+      b[0] = (bf16)pv[s][0].x; b[1] = (bf16)pv[s][0].y; b[2] = (bf16)pv[s][0].z; b[3] = (bf16)pv[s][0].w;
+      b[4] = (bf16)pv[s][1].x; b[5] = (bf16)pv[s][1].y; b[6] = (bf16)pv[s][1].z; b[7] = (bf16)pv[s][1].w;
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wv[s]), b, acc, 0, 0, 0);
+    }
+  }
+  // D[class fq*4 + i][row fr]
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float v = acc[i];
+    red[wid][fq * 4 + i][fr] = v;
+  }
+  __syncthreads();
+  {
+    const int c = tid >> 4, r = tid & 15;
+    const int cg = c0 + c, rg = r0 + r;
+    const float v = red[0][c][r] + red[1][c][r] + red[2][c][r] + red[3][c][r] + (a.bias && cg < a.N ? a.bias[cg] : 0.f);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), lr, cg < a.N && rg < a.B ? (rg * a.N + cg) * 4 : OOB, 0, 16);
+  }
+  // publish: every wave's write-through stores drained, then one ticket for this row group
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    int* c = a.cnt + blockIdx.y;
+    const int prev = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == (int)gridDim.x - 1;
+    if (last) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
+    flag = last;
+  }
+  __syncthreads();
+  if (!flag) return;
+
+  // ---- the row group's finisher: softmax + top-k per row (wave w: rows r0 + 4w .. 4w + 3) ----
+  if (a.k > 0) {
+    const int nv = (a.N + 63) / 64;
+    for (int i = 0; i < 4; ++i) {
+      const int row = r0 + wid * 4 + i;
+      if (row >= a.B) break;  // wave-uniform
+      float v[MAXV];
+#pragma unroll
+      for (int j = 0; j < MAXV; ++j) {
+        const int c = lane + 64 * j;
+        v[j] = j < nv && c < a.N ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(lr, (row * a.N + c) * 4, 0, 16))
+                                 : -INFINITY;
+      }
+      float m = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < MAXV; ++j) m = fmaxf(m, v[j]);
+      m = wave_max(m);
+      float s = 0.f;
+      if (a.softmax) {
+#pragma unroll
+        for (int j = 0; j < MAXV; ++j) s += v[j] == -INFINITY ? 0.f : __expf(v[j] - m);
+        s = wave_sum(s);
+      }
+      const bool bad = a.err && a.err[row] != 0;
+      for (int t = 0; t < a.k; ++t) {
+        float bv = -INFINITY;
+        int bj = 0;
+#pragma unroll
+        for (int j = 0; j < MAXV; ++j)
+          if (v[j] > bv) {
+            bv = v[j];
+            bj = j;
+          }
+        int bc = bv == -INFINITY ? 0x7fffffff : lane + 64 * bj;
+        // wave arg-max: larger value wins, ties to the smaller class id
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          const float ov = __shfl_xor(bv, o, 64);
+          const int oc = __shfl_xor(bc, o, 64);
+          if (ov > bv || (ov == bv && oc < bc)) {
+            bv = ov;
+            bc = oc;
+          }
+        }
+        if (lane == (bc & 63)) {  // the owner removes the winner from its candidates
+#pragma unroll
+          for (int j = 0; j < MAXV; ++j)
+            if (lane + 64 * j == bc) v[j] = -INFINITY;
+        }
+        if (lane == 0) {
+          const float p = a.softmax ? __expf(bv - m) / s : bv;
+          a.vals[row * a.k + t] = bad ? __builtin_nanf("") : p;
+          a.idx[row * a.k + t] = bad ? -1 : (bc < a.N ? bc : -1);
+        }
+      }
+    }
+  }
+  // zero the row group's pooled sums for the next launch (every class group has read them: they
+  // arrived before this ticket)
+  const int nrows = min(HT, a.B - r0);
+  const int n4 = nrows * (a.K / 4);
+  float4* pz = reinterpret_cast<float4*>(const_cast<float*>(a.pooled) + (long)r0 * a.K);
+  for (int i = tid; i < n4; i += 256) pz[i] = float4{0.f, 0.f, 0.f, 0.f};
+}
+
+}  // namespace
+
+extern "C" {
+
+// pooled [B][K] fp32 (averages, zeroed on return), w [N][K] bf16, bias [N] fp32 or null ->
+// logits [B][N] fp32 (caller's scratch or output) and, for k > 0, vals / idx [B][k] of the
+// (softmax of the) logits' top-k.  err [B] int32 or null.  K % 128 == 0, N <= 2048, k <= 64.
+int mls_fc_head(const float* pooled, const void* w, const float* bias, float* logits, float* vals, int* idx,
+                const int* err, int B, int N, int K, int k, int softmax, void* stream) {
+  if (B <= 0 || N <= 0 || N > 64 * MAXV || K <= 0 || K % 128 || k < 0 || k > 64 || k > N) return MLS_BAD_ARG;
+  if (k > 0 && (!vals || !idx)) return MLS_BAD_ARG;
+  const long pb = (long)B * K * 4, wb = (long)N * K * 2, lb = (long)B * N * 4;
+  if (pb >= 0x7fffffffL || wb >= 0x7fffffffL || lb >= 0x7fffffffL) return MLS_UNSUPPORTED;
+  const int nrg = (B + HT - 1) / HT;
+  int* cnt = mls_stream_splitk_counters(stream, nrg);
+  if (!cnt) return MLS_UNSUPPORTED;  // counters must exist before graph capture (eager warm-up)
+  HeadArgs a;
+  a.pooled = pooled;
+  a.w = (const bf16*)w;
+  a.bias = bias;
+  a.logits = logits;
+  a.vals = vals;
+  a.idx = idx;
+  a.err = err;
+  a.cnt = cnt;
+  a.B = B, a.N = N, a.K = K, a.k = k, a.softmax = softmax;
+  a.pooled_bytes = (uint32_t)pb;
+  a.w_bytes = (uint32_t)wb;
+  a.logits_bytes = (uint32_t)lb;
+  hipLaunchKernelGGL(fc_head_kernel, dim3((N + HT - 1) / HT, nrg), dim3(256), 0, (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -348,9 +348,10 @@ __global__ __launch_bounds__(256) void img_vpass_kernel(const uint8_t* __restric
   uint8_t* o = out + (long)b * IMG_PAYLOAD;
   const Hdr h = parse(c, scratch_per_image);
   const int oy = blockIdx.x;  // one output row per workgroup
-  if (!h.ok || (h.kind != 0 && h.kind != 1)) {  // unusable container: a black image + the error flag
+  const bool bad = !h.ok || (h.kind != 0 && h.kind != 1);
+  if (threadIdx.x == 0 && oy == 0 && err) err[b] = bad ? 1 : 0;  // per image: every row written each launch
+  if (bad) {  // unusable container: a black image + its error flag
     for (int i = threadIdx.x; i < IMG_OUT * 3; i += 256) o[(long)oy * IMG_OUT * 3 + i] = 0;
-    if (threadIdx.x == 0 && oy == 0 && err) atomicOr(err, 1);
     return;
   }
   if (h.kind == 0) {  // a row is 672 B = 42 x 16 B; the container payload starts 64-B aligned
@@ -383,7 +384,8 @@ extern "C" {
 
 // containers [B][64 + 224*224*3] uint8 -> out [B][224][224][3] uint8.  scratch: B * scratch_per_image
 // bytes (planes + RGB + the horizontal pass of one image; a container needing more is reported).
-// err (nullable): set to 1 when a container is unusable (that image comes out black).  Fixed launch
+// err (nullable): int32 [B], err[b] = 1 when container b is unusable (that image comes out black), else 0
+// (written every launch: no clearing needed inside a graph).  Fixed launch
 // geometry (grid-stride loops), so one captured graph serves any mix of containers.
 int mls_image_decode(const void* cont, void* out, void* scratch, long scratch_per_image, int B, int* err,
                      void* stream) {

@@ -134,6 +134,8 @@ class ReloadCoordinator:
         self._stop = threading.Event()
         self._thread: Optional[threading.Thread] = None
         self.ctl_dir: Optional[str] = None
+        # set by serve.py's supervisor in a restarted DP replica's environment (serve._respawn_env)
+        self.respawned = os.environ.get("MLS_RESPAWNED_REPLICA", "") == "1"
         if ctx.world_size > 1:
             base = os.environ.get("MLS_RELOAD_BASE") or ("/dev/shm" if os.path.isdir("/dev/shm")
                                                           else tempfile.gettempdir())
@@ -154,6 +156,11 @@ class ReloadCoordinator:
         if weights is None and seed is None:
             raise ReloadError("give 'weights' (a safetensors path on the server) or 'seed'")
         t0 = time.perf_counter()
+        if self.respawned:
+            # a DP replica serve.py restarted runs outside the process group: a local reload here
+            # would leave it serving other weights than the surviving replicas (which answer 409)
+            raise ReloadBusy("this replica was restarted outside the process group; distributed reload is "
+                             "unavailable until the service restarts")
         if self.ctl_dir is None:
             from ..utils import tracing
 

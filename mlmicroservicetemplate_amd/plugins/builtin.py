@@ -145,18 +145,24 @@ class ResNet50Plugin(ModelPlugin):
         if ctx.world_size > 1:
             spec = {k: (tuple(v.shape), v.dtype) for k, v in resnet.init_resnet50_spec().items()}
             params = mdist.broadcast_state(params, src=0, device=torch.device(devices[0]), spec=spec)
+        # GPU image decode: engine rows are image containers, the graph starts with ops.image_decode
+        self.containers = bool(s.GPU_IMAGE_DECODE) and s.BACKEND == "fused"
         if int(s.MAX_BATCH) == 0:  # auto: plan from free HBM and the latency SLO (scheduler/capacity.py)
             self.plan_batch(s, devices[0], params)
         buckets = [b for b in s.GRAPH_BUCKETS if b <= s.MAX_BATCH]
-        # GPU image decode: engine rows are image containers, the graph starts with ops.image_decode
-        self.containers = bool(s.GPU_IMAGE_DECODE) and s.BACKEND == "fused"
         shape = (IMAGE_CONTAINER_BYTES,) if self.containers else (224, 224, 3)
         for dev in devices:
             fwd = self._build_forward(s.BACKEND, dev, max(buckets), params)
             if self.containers:
                 from .. import ops
 
-                fwd = (lambda f: (lambda x: f(ops.image_decode(x))))(fwd)
+                model = self.models[-1]
+
+                def fwd(x, model=model, k=self.topk):
+                    # per-image decode flags ride into the fused head: an unusable container comes
+                    # back as ids -1 (the request fails) instead of a black image's top-5
+                    err = torch.empty(x.shape[0], dtype=torch.int32, device=x.device)
+                    return model.classify(ops.image_decode(x, err=err), k, err=err)
             eng = GpuEngine(fwd, dev, shape, torch.uint8, buckets=buckets, inflight=int(s.INFLIGHT),
                             use_graphs=bool(s.USE_GRAPHS), name=f"resnet50.{dev}",
                             concurrent=bool(s.CONCURRENT_SLOTS), cu_partitions=int(s.CU_PARTITION))
@@ -176,10 +182,24 @@ class ResNet50Plugin(ModelPlugin):
         probe = resnet.ResNet50Fused(params, dev, max_batch=32) if fused else resnet.ResNet50Eager(params, dev)
         gen = torch.Generator(device="cpu").manual_seed(0)
 
+        containers = getattr(self, "containers", False)
+
         def make(b):
-            return torch.randint(0, 256, (b, 224, 224, 3), dtype=torch.uint8, generator=gen).to(dev)
+            imgs = torch.randint(0, 256, (b, 224, 224, 3), dtype=torch.uint8, generator=gen)
+            if containers:  # the served rows: image containers (their decode scratch counts too)
+                from ..frontend.native import load_extension
+
+                ext = load_extension()
+                rows = [np.frombuffer(ext.raw_container(im.numpy().tobytes()), dtype=np.uint8) for im in imgs]
+                return torch.from_numpy(np.stack(rows)).to(dev)
+            return imgs.to(dev)
 
         def fwd(x):
+            if containers:
+                from .. import ops
+
+                err = torch.empty(x.shape[0], dtype=torch.int32, device=x.device)
+                return probe.classify(ops.image_decode(x, err=err), self.topk, err=err)
             return probe.classify(x, self.topk) if fused else probe(x)
 
         with torch.no_grad():
@@ -235,7 +255,10 @@ class ResNet50Plugin(ModelPlugin):
         return out
 
     def postprocess(self, out: Any) -> dict:
-        return topk_result(self.labels, *out)
+        vals, idx = out
+        if len(idx) and int(idx[0]) < 0:  # ops.image_decode flagged the container (fused head: ids -1)
+            raise ValueError("undecodable image")
+        return topk_result(self.labels, vals, idx)
 
     def configure(self, settings) -> None:
         # known before init(): the native front end sizes its rows from native_spec()
@@ -328,7 +351,10 @@ class ToyClassifierPlugin(ModelPlugin):
         return [run_batch]
 
     def postprocess(self, out: Any) -> dict:
-        return topk_result(self.labels, *out)
+        vals, idx = out
+        if len(idx) and int(idx[0]) < 0:  # ops.image_decode flagged the container (fused head: ids -1)
+            raise ValueError("undecodable image")
+        return topk_result(self.labels, vals, idx)
 
     def native_spec(self) -> dict:
         return {"sample_bytes": self.size * self.size * 3, "result": "topk"}

@@ -184,7 +184,7 @@ def _respawn_env(base_env: Dict[str, str], r: int, sock, settings) -> Dict[str, 
     """Environment of a restarted DP replica: a standalone process on GPU ``r`` (no process
     group), weights from the last completed hot reload if there was one."""
     env = dict(base_env, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MLS_DEVICE=str(r), MLS_REPLICA_ID=str(r),
-               MLS_DEFER_LISTEN="1")
+               MLS_DEFER_LISTEN="1", MLS_RESPAWNED_REPLICA="1")
     env.pop("MASTER_PORT", None)
     if sock is not None:
         env["MLS_LISTEN_FD"] = str(sock.fileno())

@@ -120,3 +120,35 @@ def test_large_image_goes_coarser_but_fits():
     assert out.shape == (224, 224, 3)
     ref = decode_image(data, "image/jpeg")
     assert np.abs(out.astype(int) - ref.astype(int)).mean() < 8.0
+
+
+def test_truncated_jpeg_is_refused_like_pil():
+    """A JPEG cut inside its entropy-coded scan: the C++ decoder reports the overrun (it used to
+    feed zero bits and return a grey-tailed container), so the upload takes the PIL path, which
+    raises -- the same error the reference's PIL decode gives (no 200 with a made-up image)."""
+    ext = load_extension()
+    data = jpeg(photo(256, 256), quality=90, subsampling=2)
+    for cut in (len(data) // 2, len(data) - 200):
+        r = ext.jpeg_container(data[:cut])
+        assert isinstance(r, str) and "truncated" in r, r
+        with pytest.raises(Exception):
+            decode_image(data[:cut], "image/jpeg")
+        with pytest.raises(Exception):
+            image_container(data[:cut], "image/jpeg")
+    # restart markers: a cut in a later interval is caught at the next interval boundary / the end
+    rst = jpeg(photo(256, 256, seed=4), quality=90, subsampling=2, restart_marker_blocks=4)
+    r = ext.jpeg_container(rst[: len(rst) // 2])
+    assert isinstance(r, str) and "truncated" in r, r
+    # the untruncated files still decode
+    assert isinstance(ext.jpeg_container(data), bytes) and isinstance(ext.jpeg_container(rst), bytes)
+
+
+def test_extreme_aspect_ratio_takes_pil_path():
+    """Resized width beyond the container header's 16-bit field (aspect > 256:1): refused by the
+    C++ decoder (no uint16 wrap / zero width), decoded by PIL instead."""
+    ext = load_extension()
+    data = jpeg(photo(4096, 8, noise=1.0), quality=90)
+    r = ext.jpeg_container(data)
+    assert isinstance(r, str), "an aspect ratio of 512:1 must not produce a container"
+    c = image_container(data, "image/jpeg")
+    assert R.parse_header(c)["kind"] == 0

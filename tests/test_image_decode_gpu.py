@@ -36,9 +36,9 @@ def test_image_decode_matches_spec_and_pil():
     from mlmicroservicetemplate_amd.ops import image_reference as R
 
     conts, refs = _fixture_batch()
-    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    err = torch.full((len(conts),), 7, dtype=torch.int32, device=DEV)
     out = ops.image_decode(torch.from_numpy(conts).to(DEV), err=err).cpu().numpy()
-    assert int(err.item()) == 0
+    assert err.tolist() == [0] * len(conts)
     for i, c in enumerate(conts):
         spec = R.decode_container(c)
         d = np.abs(out[i].astype(int) - spec.astype(int))
@@ -53,9 +53,9 @@ def test_image_decode_bad_container_is_black_and_flagged():
     conts, _ = _fixture_batch()
     bad = conts[:2].copy()
     bad[1, :4] = 0  # wrong magic
-    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    err = torch.full((2,), 7, dtype=torch.int32, device=DEV)
     out = ops.image_decode(torch.from_numpy(bad).to(DEV), err=err).cpu().numpy()
-    assert int(err.item()) == 1 and out[1].max() == 0 and out[0].max() > 0
+    assert err.tolist() == [0, 1] and out[1].max() == 0 and out[0].max() > 0
 
 
 def test_resnet_top1_unchanged_vs_pil_decode():

@@ -265,3 +265,21 @@ def test_stale_generation_is_replaced_and_watcher_acks_failures(tmp_path, monkey
         assert json.load(open(req))["generation"] == 2
     finally:
         co.close()
+
+
+def test_respawned_replica_refuses_reload(tmp_path, monkeypatch):
+    """A DP replica restarted by serve.py runs standalone (WORLD_SIZE=1, no control dir): it must
+    answer 409 like the surviving replicas instead of loading weights only it would serve
+    (serve._respawn_env sets MLS_RESPAWNED_REPLICA)."""
+    from mlmicroservicetemplate_amd import serve
+
+    env = serve._respawn_env({"WORLD_SIZE": "4", "MASTER_PORT": "1"}, 2, None, settings())
+    assert env["MLS_RESPAWNED_REPLICA"] == "1" and env["WORLD_SIZE"] == "1"
+    monkeypatch.setenv("MLS_RESPAWNED_REPLICA", "1")
+    a = img(1)
+    with TestClient(create_app(settings(API_KEY="sekret", WEIGHTS_DIR=str(tmp_path)), ToyClassifierPlugin())) as c:
+        assert _ready(c.get)
+        r = c.post("/admin/reload", json={"seed": 3}, headers={"api_key": "sekret"})
+        assert r.status_code == 409 and "restarted" in r.json()["detail"]
+        body, h = upload(a)  # still serving the weights it started with
+        assert c.post("/predict", content=body, headers=h).json()["result"]["classes"] == expected_classes(0, a)

@@ -1,0 +1,51 @@
+"""Pipelined 3x3 conv (csrc/conv3x3_pipe.hip) variants x split-K x items-per-block vs the shipped
+table entry on the four ResNet-50 conv2 shapes at bs=32: graph-timed per call alone (c1) and as 4
+co-running copies (c4: group time / 4 = the throughput cost per call)."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+
+from mlmicroservicetemplate_amd import ops  # noqa: E402
+from mlmicroservicetemplate_amd.ops import autotune  # noqa: E402
+
+dev = torch.device("cuda:0")
+tuning = autotune.load_tuning("resnet50", 32)
+B = 32
+CONC = [int(c) for c in os.environ.get("CONC", "1,4").split(",")]
+VARIANTS = [int(v) for v in os.environ.get("VARIANTS", "0,1,2,3,4,5").split(",")]
+for layer, (H, C) in {"layer1.1.conv2": (56, 64), "layer2.1.conv2": (28, 128), "layer3.1.conv2": (14, 256),
+                      "layer4.1.conv2": (7, 512)}.items():
+    x = torch.randn(B, H, H, C, device=dev).to(torch.bfloat16)
+    w = ops.pack_conv_weight((torch.randn(C, C, 3, 3, device=dev) * 0.02).to(torch.bfloat16))
+    b = torch.randn(C, device=dev) * 0.1
+    cfg, sk = tuning.get(layer, (0, 0))
+    fl = 2 * B * H * H * C * C * 9
+    for conc in CONC:
+        outs = [torch.empty(B, H, H, C, device=dev, dtype=torch.bfloat16) for _ in range(conc)]
+        wss = [torch.empty(4 * B * H * H * C, device=dev, dtype=torch.float32) for _ in range(conc)]
+
+        def run(cf, s):
+            return autotune._time_multi([lambda o=o, ws=ws: ops.conv2d_nhwc(x, w, b, kernel=3, stride=1, pad=1,
+                                                                            act=ops.ACT_RELU, out=o, workspace=ws,
+                                                                            cfg=cf, splitk=s)
+                                         for o, ws in zip(outs, wss)], 20) * 1e3
+
+        rows = [("table", cfg, sk, run(cfg, sk))]
+        for v in VARIANTS:
+            for ks in (1, 2, 4):
+                if (C // 32) % ks:
+                    continue
+                for ipb in (1, 2):
+                    try:
+                        rows.append((f"pipe{v}", ops.CFG_PIPE + v, ks + 16 * (ipb - 1), run(ops.CFG_PIPE + v, ks + 16 * (ipb - 1))))
+                    except Exception as e:  # noqa: BLE001
+                        print(json.dumps({"layer": layer, "variant": v, "error": str(e)}), flush=True)
+        best = min(rows, key=lambda r: r[3])
+        for name, cf, s, us in rows:
+            print(json.dumps({"layer": layer, "conc": conc, "kernel": name, "cfg": cf, "splitk": s,
+                              "us": round(us, 2), "tflops": round(fl / us / 1e6, 1), "best": (cf, s) == best[1:3]}),
+                  flush=True)
