@@ -2,7 +2,8 @@
 
 Wraps the C++ pool in ``csrc/staging.cpp`` (built in-tree by ``frontend/build.py``): persistent
 copy threads, GIL released, the calling thread copies too, 256 KiB chunks from an atomic cursor.
-``MLS_STAGE_THREADS`` sets the number of pool threads (default 4, plus the caller);
+``MLS_STAGE_THREADS`` sets the number of pool threads (default 4, plus the caller; with several
+ranks per node the budget ``parallel.affinity.bind_to_gpu`` derives from the rank's CPU share);
 ``MLS_NATIVE_STAGING=0`` selects the Python thread-pool path (kept for A/B and for hosts where
 the module has not been built).  A serving process never compiles: a missing module, or one whose
 build stamp does not match the current sources, falls back to the Python path with a warning
@@ -51,7 +52,13 @@ class HostStager:
 
     def __init__(self, threads: Optional[int] = None, name: str = "engine", native: Optional[bool] = None):
         if threads is None:
-            threads = int(os.environ.get("MLS_STAGE_THREADS", "4"))
+            env = os.environ.get("MLS_STAGE_THREADS")
+            if env is not None:
+                threads = int(env)
+            else:  # multi-rank: this rank's share of its NUMA node's CPUs (parallel/affinity.py)
+                from ..parallel.affinity import STAGE_THREADS_CAP, stage_threads_hint
+
+                threads = stage_threads_hint() or STAGE_THREADS_CAP
         if native is None:
             native = os.environ.get("MLS_NATIVE_STAGING", "1") != "0"
         self.threads = max(0, int(threads))

@@ -520,6 +520,9 @@ class LlamaTP:
         # shared by the captured steps of every context bucket, so switching buckets copies nothing
         self._dev_graphs: Dict[Tuple[int, int, int], torch.cuda.CUDAGraph] = {}
         self._dev_state: Dict[int, Tuple[torch.Tensor, ...]] = {}
+        self._serve: Dict[int, Dict[str, torch.Tensor]] = {}
+        self.keep_logits = False
+        self.last_logits: Optional[torch.Tensor] = None
         self.health_every = int(os.environ.get("MLS_TP_HEALTH_EVERY", "32"))
 
     # ---------------------------------------------------------------- shared pieces
@@ -538,6 +541,8 @@ class LlamaTP:
         return self.comm.all_reduce_(x)
 
     def _local_topk(self, logits: torch.Tensor, k: int):
+        if self.keep_logits:  # tests: the full (shard-local) last-token logits of the latest step
+            self.last_logits = logits
         if self.backend == "fused":  # shard offset + padded-tail mask inside the merge launch
             return self.ops.topk_large(logits, k, lo=self.sd.vocab_lo, valid=self.cfg.vocab - self.sd.vocab_lo)
         else:
@@ -1029,6 +1034,58 @@ class LlamaTP:
                 v, i = self.step(tok.view(B, 1), pos.view(B, 1), lens, decode=True, k=k)
                 cv, ci = self._gather_dev(v, i)
                 self.ops.decode_pick(cv, ci, tok, pos, lens, step, topk=topk, temp=temp, seed=seed, hist=hist)
+        finally:
+            self._dec_ctx = None
+        self._dev_graphs[key] = g
+        return g
+
+    # ---------------------------------------------------------------- serving (ContinuousLlama) on device
+    def serve_state(self, B: int) -> Dict[str, torch.Tensor]:
+        """Per-slot device state of the continuous-batching decode loop (models/llama_serving.py):
+        ``E`` int32 [2, B] is the one per-iteration read-back -- row 0 the prefill picks of the
+        iteration's new sequences, row 1 (= ``tok``, the decode graph's input and output token) the
+        decode picks; ``active`` masks idle slots out of the pick (they decode a dummy token into
+        their own cache row / the scratch page and keep pos 0)."""
+        st = self._serve.get(B)
+        if st is None:
+            dev = self.device
+            z = lambda dt: torch.zeros(B, device=dev, dtype=dt)  # noqa: E731
+            E = torch.zeros(2, B, device=dev, dtype=torch.int32)
+            st = {"E": E, "tok": E[1], "pos": z(torch.int32), "lens": torch.ones(B, device=dev, dtype=torch.int32),
+                  "step": z(torch.int32), "topk": torch.ones(B, device=dev, dtype=torch.int32),
+                  "temp": torch.ones(B, device=dev, dtype=torch.float32), "seed": z(torch.int64),
+                  "active": z(torch.int32)}
+            self._serve[B] = st
+        return st
+
+    def serve_graph(self, B: int, k: int, ctx: int) -> torch.cuda.CUDAGraph:
+        """Captured serving decode step over all B slots: forward + X4 gather + the on-device pick
+        of the ACTIVE slots (``ops.decode_pick(active=...)``), advancing their state in place."""
+        key = ("serve", B, k, ctx)
+        g = self._dev_graphs.get(key)
+        if g is not None:
+            return g
+        dev = self.device
+        st = self.serve_state(B)
+        # warm-up on scratch inputs at position ctx - 1 (see _decode_graph): the shared state is not touched
+        t_w = torch.zeros(B, 1, dtype=torch.int32, device=dev)
+        p_w = torch.full((B, 1), ctx - 1, dtype=torch.int32, device=dev)
+        l_w = torch.full((B,), ctx, dtype=torch.int32, device=dev)
+        self._dec_ctx = ctx
+        try:
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                for _ in range(2):
+                    v, i = self.step(t_w, p_w, l_w, decode=True, k=k)
+                    self._gather_dev(v, i)
+            torch.cuda.current_stream(dev).wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                v, i = self.step(st["tok"].view(B, 1), st["pos"].view(B, 1), st["lens"], decode=True, k=k)
+                cv, ci = self._gather_dev(v, i)
+                self.ops.decode_pick(cv, ci, st["tok"], st["pos"], st["lens"], st["step"], topk=st["topk"],
+                                     temp=st["temp"], seed=st["seed"], active=st["active"])
         finally:
             self._dec_ctx = None
         self._dev_graphs[key] = g

@@ -21,12 +21,28 @@ Each sequence samples with its own parameters and the same seeded rule as a batc
 Tensor parallelism: rank 0 runs the scheduler and broadcasts each iteration's admissions; every
 rank then executes the identical iteration (same prefills, same decode steps, the same sampled
 tokens from the all-gathered candidates), so followers need no other coordination.
+
+Device-resident iterations (default whenever ``LlamaTP._device_loop_ok`` holds -- the fused
+backend on a GPU with graph-capturable collectives; ``MLS_SERVE_DEVICE_PICK=0`` forces the host
+path): every slot's next-token state (token, position, length, step, sampling parameters, an
+active mask) lives on the device (``LlamaTP.serve_state``).  The prefill of new sequences ends
+with the X4 merge + pick writing straight into their slots (``ops.decode_pick(rows=...)``), the
+decode step is ONE captured graph (forward + on-device all-gather + pick of the active slots,
+``LlamaTP.serve_graph``), and the host reads back one ``[2, B]`` int32 tensor per iteration for
+end-of-sequence / retirement -- no uncaptured collectives, no host token picking.
+
+Failure detection: every ``MLS_TP_HEALTH_EVERY`` iterations all ranks poll the one-shot
+all-reduce's error word (``LlamaTP.check_comm_health``, a collective); a peer that missed a
+collective fails every in-flight request (rank 0's futures get ``TPCommError``), the IPC path is
+dropped and serving continues on RCCL.  Followers run the same :meth:`ContinuousLlama.run_iteration`
+(same checks, same slot resets), so the ranks stay in step.
 """
 from __future__ import annotations
 
 import collections
 import concurrent.futures as cf
 import logging
+import os
 import threading
 import time
 from dataclasses import dataclass, field
@@ -70,6 +86,12 @@ class ContinuousLlama:
         self.iterations = 0
         self.tokens = 0
         self.eos = set(model.cfg.eos_ids)
+        self.health_every = max(0, int(getattr(model, "health_every", 32)))
+        self.failures = 0
+        # device-resident iterations (module docstring); re-decided only while no sequence is in flight
+        self._want_dev = os.environ.get("MLS_SERVE_DEVICE_PICK", "1") != "0"
+        self.dev_mode = False
+        self.host_reads = 0  # device -> host copies made by the iterations (diagnostics / tests)
 
     # ---------------------------------------------------------------- client side
     def start(self) -> "ContinuousLlama":
@@ -92,6 +114,9 @@ class ContinuousLlama:
         pages = self.m.pages
         if pages is not None and pages.pages_for(len(ids) + gp.max_new_tokens) > pages.num_pages - 1:
             raise ValueError("prompt + max_new_tokens exceeds the whole KV page pool")
+        # the temperature every rank samples with: the followers receive it in 1/1000 units
+        # (plugins/llm.py _broadcast_iter), so rank 0 uses the same quantised value
+        gp = GenParams(gp.max_new_tokens, gp.top_k, round(float(gp.temperature) * 1000) / 1000.0, gp.seed)
         fut: cf.Future = cf.Future()
         with self._wake:
             if self._stop:
@@ -143,22 +168,133 @@ class ContinuousLlama:
                 self.broadcast(admit)  # None = stop, announced to the followers too
             if admit is None:
                 break
-            try:
-                self.iteration(admit)
-            except BaseException as e:  # fail everything in flight, keep serving
-                logger.exception("generate iteration failed")
-                for i, s in enumerate(self.slots):
-                    if s is not None:
-                        if s.future is not None and not s.future.done():
-                            s.future.set_exception(e)
-                        self.slots[i] = None
-                        if self.m.pages is not None:
-                            self.m.pages.release(i)
+            self.run_iteration(admit)
+
+    def run_iteration(self, admit: List[_Seq]) -> None:
+        """One iteration + the periodic comm-health check; on any failure every in-flight request
+        fails and the slots are freed (rank 0 and the followers alike, so the ranks stay in step)."""
+        finished: List[_Seq] = []
+        try:
+            finished = self.iteration(admit)
+            # a result leaves only after a health check that covers the steps which produced it (a
+            # peer that missed a one-shot all-reduce leaves partial sums behind): every iteration
+            # that retires a sequence, and every health_every-th one (all ranks: same decisions)
+            if self.m.tp > 1 and (finished or (self.health_every and self.iterations % self.health_every == 0)):
+                self.m.check_comm_health()
+            for q in finished:
+                if q.future is not None and not q.future.done():
+                    q.future.set_result(list(q.out))
+        except BaseException as e:  # fail everything in flight, keep serving
+            logger.exception("generate iteration failed")
+            self.failures += 1
+            for q in finished:
+                if q.future is not None and not q.future.done():
+                    q.future.set_exception(e)
+            for i, s in enumerate(self.slots):
+                if s is not None:
+                    if s.future is not None and not s.future.done():
+                        s.future.set_exception(e)
+                    self.slots[i] = None
+                    if self.m.pages is not None:
+                        self.m.pages.release(i)
+            if self.dev_mode:
+                st = self.m.serve_state(self.B)
+                st["active"].zero_()
+                st["pos"].zero_()
+                st["lens"].fill_(1)
 
     # ---------------------------------------------------------------- one iteration (all ranks)
+    def _dev_ok(self) -> bool:
+        if not self._want_dev:
+            return False
+        if any(s is not None for s in self.slots):  # sequences in flight keep their mode
+            return self.dev_mode
+        return self.m._device_loop_ok(self.B, self.m.top_k_max)
+
     @torch.no_grad()
-    def iteration(self, admit: List[_Seq]) -> None:
+    def iteration(self, admit: List[_Seq]) -> List[_Seq]:
+        """Admit, decode one step, retire.  Returns the retired sequences (slots already freed);
+        :meth:`run_iteration` resolves their futures once the comm-health check has passed."""
+        self.dev_mode = self._dev_ok()
+        if self.dev_mode:
+            return self._iteration_dev(admit)
+        return self._iteration_host(admit)
+
+    @torch.no_grad()
+    def _iteration_dev(self, admit: List[_Seq]) -> List[_Seq]:
         m = self.m
+        dev = m.device
+        st = m.serve_state(self.B)
+        ops = m.ops
+        if admit:
+            for seq in admit:
+                self.slots[seq.slot] = seq
+                if m.pages is not None:
+                    m.pages.assign(seq.slot, len(seq.ids) + seq.gp.max_new_tokens)
+            S = max(len(s.ids) for s in admit)
+            ids = torch.zeros(len(admit), S, dtype=torch.int32)
+            for j, s in enumerate(admit):
+                ids[j, : len(s.ids)] = torch.tensor(s.ids, dtype=torch.int32)
+            # one H2D of the new slots' state: slot, pos (the pick advances it to the prompt length),
+            # lens, top_k, seed; temperatures separately (fp32)
+            meta = torch.tensor([[s.slot, len(s.ids) - 1, len(s.ids), s.gp.top_k, s.gp.seed] for s in admit],
+                                dtype=torch.int64).to(dev, non_blocking=True)
+            temps = torch.tensor([s.gp.temperature for s in admit], dtype=torch.float32).to(dev, non_blocking=True)
+            slot_ids = meta[:, 0].to(torch.int32)
+            lens = meta[:, 2].to(torch.int32)
+            pos = torch.arange(S, dtype=torch.int32, device=dev).unsqueeze(0).expand(len(admit), S).contiguous()
+            k = max(1, min(max(s.gp.top_k for s in admit), m.top_k_max))
+            vals, idx = m.step(ids.to(dev), pos, lens, decode=False, k=k, slot_ids=slot_ids)
+            cv, ci = m._gather_dev(vals, idx)
+            sl = meta[:, 0]
+            st["pos"][sl] = meta[:, 1].to(torch.int32)
+            st["lens"][sl] = lens
+            st["step"][sl] = 0
+            st["topk"][sl] = meta[:, 3].to(torch.int32)
+            st["seed"][sl] = meta[:, 4]
+            st["temp"][sl] = temps
+            st["active"][sl] = 1
+            ops.decode_pick(cv, ci, st["tok"], st["pos"], st["lens"], st["step"], topk=st["topk"], temp=st["temp"],
+                            seed=st["seed"], rows=slot_ids, emit=st["E"][0])
+            for s in admit:
+                s.cur = len(s.ids)
+        active = [s for s in self.slots if s is not None]
+        if active:
+            k = max(1, min(max(s.gp.top_k for s in active), m.top_k_max))
+            max_ctx = max(s.cur for s in active) + 1
+            g = m.serve_graph(self.B, k, m.ctx_bucket(max_ctx))
+            if m.pages is not None:
+                m.pages.device_table()  # the graph reads the table buffer in place
+            g.replay()
+        if admit or active:
+            E = st["E"].cpu()  # the iteration's one device -> host copy
+            self.host_reads += 1
+            e0, e1 = E[0].tolist(), E[1].tolist()
+            new = {id(s) for s in admit}
+            for s in admit:
+                s.out.append(int(e0[s.slot]))
+                self.tokens += 1
+            for s in active:
+                if id(s) in new and (len(s.out) >= s.gp.max_new_tokens or s.out[-1] in self.eos):
+                    continue  # finished on its prefill token: the decode pick is discarded
+                s.out.append(int(e1[s.slot]))
+                s.cur += 1
+                self.tokens += 1
+            done = self._retire()
+            if done:
+                idx_t = torch.tensor([q.slot for q in done], dtype=torch.int64).to(dev, non_blocking=True)
+                st["active"][idx_t] = 0
+                st["pos"][idx_t] = 0
+                st["lens"][idx_t] = 1
+        else:
+            done = []
+        self.iterations += 1
+        return done
+
+    @torch.no_grad()
+    def _iteration_host(self, admit: List[_Seq]) -> List[_Seq]:
+        m = self.m
+        done: List[_Seq] = []
         if admit:
             for seq in admit:
                 self.slots[seq.slot] = seq
@@ -178,7 +314,7 @@ class ContinuousLlama:
                 s.out.append(t)
                 s.cur = len(s.ids)
             self.tokens += len(admit)
-            self._retire()
+            done += self._retire()
         active = [s for s in self.slots if s is not None]
         if active:
             # host lists -> one tensor each (per-element tensor writes cost ~us apiece at 128 slots)
@@ -197,8 +333,9 @@ class ContinuousLlama:
                 s.out.append(t)
                 s.cur += 1
             self.tokens += len(active)
-            self._retire()
+            done += self._retire()
         self.iterations += 1
+        return done
 
     def _pick_rows(self, cv: torch.Tensor, ci: torch.Tensor, rows) -> List[int]:
         """Next token of each ``(row, gen params, step)``: the greedy rows in one vectorised
@@ -215,13 +352,15 @@ class ContinuousLlama:
                 out[j] = self.m.pick_token(cv[r], ci[r], gp, step)
         return out  # type: ignore[return-value]
 
-    def _retire(self) -> None:
+    def _retire(self) -> List[_Seq]:
+        """Free the slots of finished sequences (their futures are resolved by run_iteration)."""
+        done = []
         for i, s in enumerate(self.slots):
             if s is None:
                 continue
             if len(s.out) >= s.gp.max_new_tokens or (s.out and s.out[-1] in self.eos):
                 self.slots[i] = None
+                done.append(s)
                 if self.m.pages is not None:
                     self.m.pages.release(i)
-                if s.future is not None and not s.future.done():
-                    s.future.set_result(list(s.out))
+        return done

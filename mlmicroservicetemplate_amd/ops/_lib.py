@@ -73,7 +73,7 @@ _SIGS = {
     "mls_ar_reset": [P],
     "mls_gpu_sleep": [L, P],
     "mls_image_decode": [P, P, P, L, I, P, P],
-    "mls_decode_pick": [P, P, I, I, I, P, P, P, P, P, P, P, I, P, P],
+    "mls_decode_pick": [P, P, I, I, I, P, P, P, P, P, P, P, I, P, P, P, P, P],
     "mls_ar_destroy": [P],
     "mls_rope_kv": [P, P, P, P, L, I, I, I, I, P, P, P, P, I, I, L, I, I, P],
     "mls_kv_append": [P, I, I, I, P, P, P, L, I, I, I, P],

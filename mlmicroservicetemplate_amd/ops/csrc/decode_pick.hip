@@ -46,9 +46,15 @@ __global__ __launch_bounds__(64) void decode_pick_kernel(const float* __restrict
                                                          int tp, int B, int k, const int* __restrict__ topk,
                                                          const float* __restrict__ temp,
                                                          const long long* __restrict__ seed, int* tok, int* pos,
-                                                         int* lens, int* hist, int hist_cols, int* step) {
+                                                         int* lens, int* hist, int hist_cols, int* step,
+                                                         const int* __restrict__ rows,
+                                                         const int* __restrict__ active, int* emit) {
   const int b = blockIdx.x, lane = threadIdx.x;
   const int n = tp * k;
+  // per-sequence state row of candidate row b: rows[b] (a prefill of new sequences into their
+  // serving slots) or b; inactive state rows (an idle serving slot) are left untouched
+  const int sr = rows ? rows[b] : b;
+  if (active && !active[sr]) return;
   __shared__ float sv[PICK_MAX_CAND];
   __shared__ int sj[PICK_MAX_CAND];
   for (int j = lane; j < n; j += 64) {
@@ -57,7 +63,7 @@ __global__ __launch_bounds__(64) void decode_pick_kernel(const float* __restrict
     sj[j] = ci[((long)r * B + b) * k + c];
   }
   __syncthreads();
-  const int want = topk ? topk[b] : 1;
+  const int want = topk ? topk[sr] : 1;
   int token;
   if (want <= 1) {
     VI best{-INFINITY, 0x7fffffff};
@@ -81,7 +87,7 @@ __global__ __launch_bounds__(64) void decode_pick_kernel(const float* __restrict
       __syncthreads();
     }
     if (lane == 0) {
-      const float t = fmaxf(temp ? temp[b] : 1.f, 1e-5f);
+      const float t = fmaxf(temp ? temp[sr] : 1.f, 1e-5f);
       const float mx = tv[0];
       float p[PICK_MAX_TOPK];
       float cdf = 0.f;
@@ -91,7 +97,7 @@ __global__ __launch_bounds__(64) void decode_pick_kernel(const float* __restrict
         p[s] = cdf;  // running sum (same order as the host's cumsum)
       }
       const unsigned long long h =
-          splitmix64((unsigned long long)(seed ? seed[b] : 0) * 0x9E3779B97F4A7C15ull + (unsigned long long)step[b]);
+          splitmix64((unsigned long long)(seed ? seed[sr] : 0) * 0x9E3779B97F4A7C15ull + (unsigned long long)step[sr]);
       const float u = (float)(h >> 40) * (1.f / 16777216.f);
       int pick = kk - 1;
       for (int s = 0; s < kk; ++s)
@@ -108,12 +114,13 @@ __global__ __launch_bounds__(64) void decode_pick_kernel(const float* __restrict
     token = sj[0];
   }
   if (lane == 0) {
-    const int s = step[b];
-    if (hist && s < hist_cols) hist[(long)b * hist_cols + s] = token;
-    step[b] = s + 1;
-    tok[b] = token;
-    pos[b] += 1;
-    lens[b] += 1;
+    const int s = step[sr];
+    if (hist && s < hist_cols) hist[(long)sr * hist_cols + s] = token;
+    step[sr] = s + 1;
+    tok[sr] = token;
+    pos[sr] += 1;
+    lens[sr] += 1;
+    if (emit) emit[sr] = token;
   }
 }
 
@@ -123,12 +130,16 @@ extern "C" {
 
 // cv [tp][B][k] f32, ci [tp][B][k] i32; per-row params topk / temp / seed (nullptr: greedy, 1.0, 0);
 // tok / pos / lens [B] i32 advanced in place; hist [B][hist_cols] (nullable); step [B] i32.
+// Serving extensions (all nullable): rows [B] i32 maps candidate row b to state row rows[b] (the
+// state arrays then have the serving batch's size, indices < state_rows); active [state rows] i32
+// skips idle state rows; emit [state rows] i32 receives each picked token (a per-iteration
+// read-back buffer next to the decode graph's own tok).
 int mls_decode_pick(const float* cv, const int* ci, int tp, int B, int k, const int* topk, const float* temp,
                     const long long* seed, int* tok, int* pos, int* lens, int* hist, int hist_cols, int* step,
-                    void* stream) {
+                    const int* rows, const int* active, int* emit, void* stream) {
   if (tp <= 0 || B <= 0 || k <= 0 || tp * k > PICK_MAX_CAND || !tok || !pos || !lens || !step) return MLS_BAD_ARG;
   hipLaunchKernelGGL(decode_pick_kernel, dim3(B), dim3(64), 0, (hipStream_t)stream, cv, ci, tp, B, k, topk, temp, seed,
-                     tok, pos, lens, hist, hist_cols, step);
+                     tok, pos, lens, hist, hist_cols, step, rows, active, emit);
   return (int)hipGetLastError();
 }
 

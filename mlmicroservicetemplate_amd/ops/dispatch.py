@@ -1,0 +1,73 @@
+"""Projection dispatch policy (``linear``): which GEMM kernel a transformer projection runs on."""
+from __future__ import annotations
+
+import ctypes  # noqa: F401
+import functools  # noqa: F401
+import json  # noqa: F401
+import os  # noqa: F401
+from typing import Dict, List, Optional, Sequence, Tuple  # noqa: F401
+
+import torch
+
+from ._lib import NativeError, available, check, lib, stream_ptr  # noqa: F401
+from ._core import ACT_GELU, ACT_NONE, ACT_SILU_MUL, _act  # noqa: F401
+from .gemm_ops import _bias_bf16, gemm, gemm_tile, silu_mul_interleaved  # noqa: F401
+from .tables import small_m_plan_for, tile_cfg_for  # noqa: F401
+
+
+# Large-M projections run on the native LDS-DMA MFMA tile kernel (gemm_tile: csrc/gemm_tile.hip),
+# the decode-shaped ones (M <= 32, and 33..TILE_MIN_M - 1 rows) on the skinny / conv_gemm kernels with
+# per-shape plans.  hipBLASLt (torch.addmm) is reachable only on request -- impl="blas" or
+# MLS_GEMM_IMPL=blas -- as the A/B reference of tools/gemm_tile_probe.py; no default path calls it.
+TILE_MIN_M = int(os.environ.get("MLS_TILE_MIN_M", "256"))
+
+
+BLAS_MIN_M = TILE_MIN_M  # kept for callers that split "large" from "small" token counts
+
+
+_GEMM_IMPL = os.environ.get("MLS_GEMM_IMPL", "native")
+
+
+def linear(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, act=ACT_NONE,
+           residual: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
+           impl: str = "auto") -> torch.Tensor:
+    """Transformer projection ``act(a @ w.T + bias) (+ residual)``, all native: M >= TILE_MIN_M on the
+    persistent LDS-DMA tile kernel (:func:`gemm_tile`, bias / GELU / SiLU-mul / residual in its
+    epilogue), smaller M on the skinny / conv_gemm kernels (measured per-shape plans in
+    ``tuned/gemm_plan_gfx950.json``).  ``impl``: "auto" | "native" | "tile" | "blas" (hipBLASLt, the
+    A/B reference only; also ``MLS_GEMM_IMPL=blas``)."""
+    code = _act(act)
+    M, K = a.shape
+    N = w.shape[0]
+    if impl == "blas" or (impl == "auto" and _GEMM_IMPL == "blas"):
+        return _linear_blas(a, w, bias, code, residual)
+    if impl == "tile" or (impl == "auto" and M >= TILE_MIN_M and K % 64 == 0 and N % 16 == 0
+                          and a.device.type == "cuda" and a.is_contiguous() and w.is_contiguous()):
+        cfg, sk = tile_cfg_for(M, N, K)
+        return gemm_tile(a, w, bias, act=code, residual=residual, cfg=cfg, splitk=sk, workspace=workspace)
+    plan = small_m_plan_for(M, N, K) if impl == "auto" else None
+    if plan is not None and plan[0] > 0 and not (code == ACT_SILU_MUL and residual is not None):
+        return gemm(a, w, bias, act=code, residual=residual, workspace=workspace, cfg=plan[0], splitk=plan[1])
+    return gemm(a, w, bias, act=code, residual=residual, workspace=workspace)
+
+
+def _linear_blas(a, w, bias, code, residual):
+    """hipBLASLt through torch (A/B reference; bias / GELU epilogues, SiLU-mul as a native pass)."""
+    b16 = _bias_bf16(bias) if bias is not None else None
+    if code == ACT_GELU:
+        y = torch._addmm_activation(b16 if b16 is not None else torch.zeros(w.shape[0], device=a.device,
+                                    dtype=torch.bfloat16), a, w.t(), use_gelu=True)
+    elif residual is not None and b16 is None:
+        y = torch.addmm(residual, a, w.t())
+        residual = None
+    elif b16 is not None:
+        y = torch.addmm(b16, a, w.t())
+    else:
+        y = torch.mm(a, w.t())
+    if code not in (ACT_NONE, ACT_GELU, ACT_SILU_MUL):
+        raise ValueError("blas path: act must be none / gelu / silu_mul")
+    if residual is not None:
+        y += residual
+    if code == ACT_SILU_MUL:
+        y = silu_mul_interleaved(y)
+    return y

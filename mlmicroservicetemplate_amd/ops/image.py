@@ -1,0 +1,53 @@
+"""GPU image decode (JPEG coefficient containers -> pixels) and test hooks."""
+from __future__ import annotations
+
+import ctypes  # noqa: F401
+import functools  # noqa: F401
+import json  # noqa: F401
+import os  # noqa: F401
+from typing import Dict, List, Optional, Sequence, Tuple  # noqa: F401
+
+import torch
+
+from ._lib import NativeError, available, check, lib, stream_ptr  # noqa: F401
+from ._core import _need, _ptr  # noqa: F401
+
+
+IMAGE_CONTAINER_BYTES = 64 + 224 * 224 * 3  # frontend/csrc/jpeg_coefs.h CONTAINER_BYTES
+
+
+IMAGE_SCRATCH_PER_IMAGE = 2 << 20  # jpeg_coefs.h SCRATCH_PER_IMAGE
+
+
+def image_decode(containers: torch.Tensor, out: Optional[torch.Tensor] = None,
+                 err: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """GPU half of the image path (csrc/image_decode.hip): ``[B, IMAGE_CONTAINER_BYTES]`` uint8
+    containers (raw RGB, or host-Huffman-decoded JPEG coefficients + resize geometry) -> uint8
+    ``[B, 224, 224, 3]``: IDCT, libjpeg chroma upsampling + YCbCr->RGB, Pillow's bilinear resize and
+    the centre crop of ``plugins.builtin.decode_image``.  ``err`` (int32 ``[B]``, optional): row b is
+    set to 1 when container b is unusable (that image comes out black), else 0 -- every launch, so
+    a captured graph needs no clearing; :func:`fc_head` turns flagged rows into id -1 / NaN.
+    Capturable (fixed launch geometry; the scratch comes from the caller's -- in a graph, the graph
+    pool's -- allocator)."""
+    dev = containers.device
+    _need(containers, "containers", torch.uint8, dev)
+    if containers.dim() != 2 or containers.shape[1] != IMAGE_CONTAINER_BYTES:
+        raise ValueError(f"containers must be [B, {IMAGE_CONTAINER_BYTES}]")
+    B = containers.shape[0]
+    if out is None:
+        out = torch.empty(B, 224, 224, 3, device=dev, dtype=torch.uint8)
+    scratch = torch.empty(B * IMAGE_SCRATCH_PER_IMAGE, device=dev, dtype=torch.uint8)
+    if err is not None:
+        _need(err, "err", torch.int32, dev)
+        if err.numel() < B:
+            raise ValueError(f"err must have >= {B} elements (one flag per image)")
+    rc = lib().mls_image_decode(containers.data_ptr(), out.data_ptr(), scratch.data_ptr(), IMAGE_SCRATCH_PER_IMAGE, B,
+                                _ptr(err), stream_ptr(dev))
+    check(rc, "mls_image_decode")
+    return out
+
+
+def gpu_sleep(us: int, device=None) -> None:
+    """Hold the current stream of ``device`` for ``us`` microseconds (fault injection in tests)."""
+    dev = torch.device(device if device is not None else "cuda")
+    check(lib().mls_gpu_sleep(int(us), stream_ptr(dev)), "mls_gpu_sleep")

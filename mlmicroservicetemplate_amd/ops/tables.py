@@ -1,0 +1,93 @@
+"""Measured per-shape dispatch tables (ops/tuned/*.json) and their lookups -- a served shape that misses a table is logged once per process."""
+from __future__ import annotations
+
+import ctypes  # noqa: F401
+import functools  # noqa: F401
+import json  # noqa: F401
+import os  # noqa: F401
+from typing import Dict, List, Optional, Sequence, Tuple  # noqa: F401
+
+import torch
+
+from ._lib import NativeError, available, check, lib, stream_ptr  # noqa: F401
+
+
+_TUNED_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned")
+
+
+def load_blas_tuning(path: Optional[str] = None) -> bool:
+    """Make hipBLASLt use the solutions PyTorch TunableOp measured fastest on MI355X for the shapes
+    in ``tuned/tunableop_gfx950.csv`` (BERT FFN-up + GELU: 26.4 vs 30.1 us at 4-way concurrency,
+    ``profiles/r1_bert_gemm_probe.jsonl``).  Lookup only -- tuning stays off, so nothing is timed or
+    written at run time, and untuned shapes keep the library default.  ``MLS_BLAS_TUNING=0``
+    disables it; ``MLS_BLAS_TUNING_FILE`` reads another table (A/B).  Returns whether it loaded."""
+    if os.environ.get("MLS_BLAS_TUNING", "1") == "0" or not torch.cuda.is_available():
+        return False
+    from torch.cuda import tunable
+
+    tunable.enable(True)
+    tunable.tuning_enable(False)
+    path = path or os.environ.get("MLS_BLAS_TUNING_FILE") or os.path.join(_TUNED_DIR, "tunableop_gfx950.csv")
+    ok = bool(tunable.read_file(path))
+    if not ok:
+        tunable.enable(False)
+    return ok
+
+
+@functools.lru_cache(maxsize=None)
+def gemm_plan() -> Dict[Tuple[int, int, int], Tuple[int, int]]:
+    """Measured per-shape choices for :func:`linear` (``tuned/gemm_plan_gfx950.json``): exact
+    ``(M, N, K)`` -> ``(cfg, splitk)`` of the native kernel, cfg 0 = hipBLASLt.  ``MLS_GEMM_PLAN=0``
+    disables it."""
+    if os.environ.get("MLS_GEMM_PLAN", "1") == "0":
+        return {}
+    with open(os.path.join(_TUNED_DIR, "gemm_plan_gfx950.json")) as f:
+        doc = json.load(f)
+    return {(e["M"], e["N"], e["K"]): (int(e["plan"][0]), int(e["plan"][1])) for e in doc["entries"]}
+
+
+_TABLE_MISSES: set = set()
+
+
+_ops_log = __import__("logging").getLogger("mlsamd.ops")
+
+
+def _note_miss(table: str, M: int, N: int, K: int) -> None:
+    """Log ONCE per process and shape when a served GEMM shape is not in a tuning table (it then
+    runs the kernel's heuristic tile, which can be far off the measured best)."""
+    key = (table, M, N, K)
+    if key in _TABLE_MISSES:
+        return
+    _TABLE_MISSES.add(key)
+    _ops_log.warning("GEMM shape M=%d N=%d K=%d is not in %s: heuristic config (tune it with "
+                     "tools/gemm_tile_probe.py / ops.autotune)", M, N, K, table)
+
+
+def tile_cfg_for(M: int, N: int, K: int) -> Tuple[int, int]:
+    """gemm_tile (config, K splits) for a shape: measured choices first (``tuned/gemm_tile_gfx950.json``),
+    else the kernel's own pick (largest tile that still fills the chip), no split -- logged once."""
+    e = gemm_tile_plan().get((M, N, K))
+    if e is None:
+        _note_miss("gemm_tile_gfx950.json", M, N, K)
+        return (0, 1)
+    return e
+
+
+def small_m_plan_for(M: int, N: int, K: int) -> Optional[Tuple[int, int]]:
+    """The measured (cfg, splitk) of a small-M projection (``tuned/gemm_plan_gfx950.json``), or
+    None (logged once: the conv_gemm heuristic runs it)."""
+    plan = gemm_plan()
+    e = plan.get((M, N, K))
+    if e is None and plan:
+        _note_miss("gemm_plan_gfx950.json", M, N, K)
+    return e
+
+
+@functools.lru_cache(maxsize=None)
+def gemm_tile_plan() -> Dict[Tuple[int, int, int], Tuple[int, int]]:
+    path = os.environ.get("MLS_GEMM_TILE_TABLE") or os.path.join(_TUNED_DIR, "gemm_tile_gfx950.json")
+    if os.environ.get("MLS_GEMM_PLAN", "1") == "0" or not os.path.exists(path):
+        return {}
+    with open(path) as f:
+        doc = json.load(f)
+    return {(e["M"], e["N"], e["K"]): (int(e["cfg"]), int(e.get("splitk", 1))) for e in doc["entries"]}

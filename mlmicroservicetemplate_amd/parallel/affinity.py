@@ -10,6 +10,12 @@ may use.  Call before allocating pinned memory so first-touch places it on the l
 
 ``MLS_NUMA_BIND=0`` disables; ``=1`` forces it for single-process runs (default: only with
 several ranks, where it matters).
+
+Host-thread budget: on an 8-GPU node four ranks share each socket's CPUs, and every rank's
+engine would otherwise start 4 staging copy threads regardless (plus the submitting thread, the
+Python loop and HIP's own threads).  :func:`bind_to_gpu` also records how many CPUs this rank
+may use and how many local ranks share them; :func:`stage_threads_hint` turns that into the
+engine's copy-thread count (``engine/staging.HostStager``'s default).
 """
 from __future__ import annotations
 
@@ -55,14 +61,74 @@ def gpu_local_cpus(pci_addr: str, sysfs_root: str = "/sys") -> Optional[Set[int]
     return cpus or None
 
 
+STAGE_THREADS_CAP = 4  # copy threads that saturate one batch's memcpy (docs/PERF_NOTES.md, round 2)
+_hint: Optional[int] = None
+
+
+def stage_thread_budget(n_cpus: int, ranks_sharing: int, cap: int = STAGE_THREADS_CAP) -> int:
+    """Staging copy threads for one rank: its share of the CPUs it may use (``n_cpus`` shared by
+    ``ranks_sharing`` local ranks) minus one for the submitting thread (which copies too), at
+    least 1 and at most ``cap``."""
+    share = max(1, int(n_cpus)) // max(1, int(ranks_sharing))
+    return max(1, min(int(cap), share - 1))
+
+
+def ranks_sharing_cpus(device_index: int, local_world: int, sysfs_root: str = "/sys",
+                       pci_of=None) -> int:
+    """How many of the node's ``local_world`` ranks (rank r drives GPU ``r % ngpus``) have
+    their GPU on the same NUMA node as ``device_index`` -- i.e. share its local CPU list.  Unknown
+    topology: all of them."""
+    pci_of = pci_of or pci_address
+    mine_addr = pci_of(device_index)
+    mine = gpu_local_cpus(mine_addr, sysfs_root) if mine_addr else None
+    if not mine:
+        return max(1, local_world)
+    try:
+        import torch
+
+        ngpu = max(1, torch.cuda.device_count())
+    except Exception:
+        ngpu = 1
+    if pci_of is not pci_address:  # an explicit map (tests): one GPU per local rank
+        ngpu = max(1, local_world)
+    n = 0
+    for r in range(max(1, local_world)):
+        addr = pci_of(r % ngpu)
+        cpus = gpu_local_cpus(addr, sysfs_root) if addr else None
+        n += 1 if cpus == mine else 0
+    return max(1, n)
+
+
+def stage_threads_hint() -> Optional[int]:
+    """The copy-thread budget :func:`bind_to_gpu` computed for this process (None: not computed)."""
+    return _hint
+
+
 def bind_to_gpu(device_index: int, world_size: int = 1, sysfs_root: str = "/sys",
-                pci_addr: Optional[str] = None) -> Optional[List[int]]:
+                pci_addr: Optional[str] = None, local_world: Optional[int] = None,
+                pci_of=None) -> Optional[List[int]]:
     """Restrict this process's (calling thread's) CPU affinity to the GPU's local CPUs.
-    Returns the CPU list applied, or None when binding is disabled / impossible."""
+    Returns the CPU list applied, or None when binding is disabled / impossible.  With several
+    ranks it also sets :func:`stage_threads_hint` from the CPUs left to this rank."""
+    global _hint
+    if world_size > 1:
+        lw = int(local_world or os.environ.get("LOCAL_WORLD_SIZE", world_size))
+        try:
+            allowed0 = os.sched_getaffinity(0)
+        except (AttributeError, OSError):
+            allowed0 = set(range(os.cpu_count() or 1))
+        pci_of = pci_of or pci_address
+        addr0 = pci_addr or pci_of(device_index)
+        local0 = gpu_local_cpus(addr0, sysfs_root) if addr0 else None
+        usable = (local0 & allowed0) if local0 and (local0 & allowed0) else allowed0
+        sharing = ranks_sharing_cpus(device_index, lw, sysfs_root, pci_of=pci_of) if local0 else lw
+        _hint = stage_thread_budget(len(usable), sharing)
+        logger.info("GPU %d: %d usable CPUs shared by %d local ranks -> %d staging threads", device_index,
+                    len(usable), sharing, _hint)
     mode = os.environ.get("MLS_NUMA_BIND", "")
     if mode == "0" or (mode != "1" and world_size <= 1):
         return None
-    addr = pci_addr or pci_address(device_index)
+    addr = pci_addr or (pci_of or pci_address)(device_index)
     if addr is None:
         return None
     local = gpu_local_cpus(addr, sysfs_root)

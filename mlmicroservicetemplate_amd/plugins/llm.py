@@ -200,7 +200,7 @@ class LlamaPlugin(ModelPlugin):
         hdr[:3] = torch.tensor([OP_ITER, n, S])
         dist.broadcast(hdr, src=0)
         if n:
-            meta = torch.tensor([[a.slot, len(a.ids), a.gp.max_new_tokens, a.gp.top_k, int(a.gp.temperature * 1000),
+            meta = torch.tensor([[a.slot, len(a.ids), a.gp.max_new_tokens, a.gp.top_k, round(a.gp.temperature * 1000),
                                   a.gp.seed] for a in admit], dtype=torch.int64, device=self.comm_dev)
             ids = torch.zeros(n, S, dtype=torch.int64, device=self.comm_dev)
             for j, a in enumerate(admit):
@@ -234,7 +234,7 @@ class LlamaPlugin(ModelPlugin):
                         seq = _Seq(ids[j, :n].tolist(), GenParams(mnt_j, topk_j, temp_j / 1000.0, seed_j), None)
                         seq.slot = slot
                         admit.append(seq)
-                self.engine.iteration(admit)
+                self.engine.run_iteration(admit)  # same failure handling / health checks as rank 0
                 continue
             ids = torch.zeros(B, S, dtype=torch.int32, device=self.comm_dev)
             lens = torch.zeros(B, dtype=torch.int32, device=self.comm_dev)

@@ -70,9 +70,11 @@ def test_llama8b_4layer_fused_vs_reference():
     lens = torch.tensor([200, 131, 17], device=DEV, dtype=torch.int32)
     pos = torch.arange(S, device=DEV, dtype=torch.int32).unsqueeze(0).expand(B, S).contiguous()
     k = 8
+    ref.keep_logits = fus.keep_logits = True  # the full last-token logits of every step
     rv, ri = ref.step(ids, pos, lens, decode=False, k=k)
     fv, fi = fus.step(ids, pos, lens, decode=False, k=k)
     assert _rel(fv, rv) <= 3e-2
+    assert _rel(fus.last_logits[:, : cfg.vocab], ref.last_logits[:, : cfg.vocab]) <= 3e-2
     gap = (rv[:, 0] - rv[:, 1]) / rv.abs().max()
     assert torch.equal(fi[:, 0][gap > 1e-2], ri[:, 0][gap > 1e-2])
     cur = lens.clone()
@@ -81,6 +83,7 @@ def test_llama8b_4layer_fused_vs_reference():
         rv, ri = ref.step(tok.view(B, 1), cur.view(B, 1), cur + 1, decode=True, k=k)
         fv, fi = fus.step(tok.view(B, 1), cur.view(B, 1), cur + 1, decode=True, k=k)
         assert _rel(fv, rv) <= 3e-2
+        assert _rel(fus.last_logits[:, : cfg.vocab], ref.last_logits[:, : cfg.vocab]) <= 3e-2
         gap = (rv[:, 0] - rv[:, 1]) / rv.abs().max()
         assert torch.equal(fi[:, 0][gap > 1e-2], ri[:, 0][gap > 1e-2])
         tok, cur = ri[:, 0], cur + 1

@@ -124,4 +124,9 @@ def test_resnet_fused_head_vs_unfused_and_graph():
     vu, iu = mu.classify(imgs, 5)
     torch.cuda.synchronize()
     assert torch.equal(iu[:, 0][sure], i1[:, 0][sure])
-    assert (vu - v1).abs().max().item() < 2e-2
+    # probabilities against the fp32 reference at the returned classes: the fused head (fp32 pool
+    # sums, one bf16 rounding) must be at least as close as the unfused one (bf16 pool output)
+    pref = torch.softmax(ref, -1)
+    ef = (v1 - pref.gather(1, i1.long())).abs().max().item()
+    eu = (vu - pref.gather(1, iu.long())).abs().max().item()
+    assert ef < 5e-2 and ef <= eu + 1e-2, (ef, eu)

@@ -60,10 +60,14 @@ def test_resnet50_service_matches_direct_model():
         assert all(len(r["classes"]) == 5 for r in res)
         # the same images through the model directly (same seed-0 weights, fp32 reference)
         x = torch.from_numpy(np.stack([decode_image(b, "image/png") for b in imgs])).cuda()
-        ref = resnet.resnet50_reference({k: v.cuda() for k, v in resnet.init_resnet50(0).items()}, x)
-        top1 = ref.argmax(-1).tolist()
-        got = [int(r["classes"][0].split("_")[1]) for r in res]
-        assert np.mean([a == b for a, b in zip(top1, got)]) >= 0.75
+        ref = resnet.resnet50_reference({k: v.cuda() for k, v in resnet.init_resnet50(0).items()}, x).float()
+        got = torch.tensor([int(r["classes"][0].split("_")[1]) for r in res], device=ref.device)
+        # margin rule: exact top-1 on every image whose reference top-2 gap exceeds 1e-2 of the
+        # largest logit (a near-tie may flip under bf16 rounding and batch-bucket tile choices)
+        top2 = ref.topk(2, dim=-1).values
+        sure = (top2[:, 0] - top2[:, 1]) / ref.abs().max() > 1e-2
+        assert sure.sum() >= len(imgs) // 2, "too few decisive images to test anything"
+        assert torch.equal(got[sure], ref.argmax(-1)[sure]), (got, ref.argmax(-1), sure)
         h = c.get("/health").json()
         assert h["replicas"][0]["healthy"] and h["replicas"][0]["batches"] >= 2
         assert c.get("/info").json()["model"]["engines"][0]["concurrent"]
@@ -153,7 +157,20 @@ def test_resnet50_native_frontend_matches_python_frontend():
             outs = list(ex.map(lambda u: requests.post(url + "/predict", data=u[0], headers={"content-type": u[1]},
                                                        timeout=60), ups()))
         assert all(o.status_code == 200 for o in outs), [o.text for o in outs]
-        assert np.mean([a["classes"][0] == o.json()["result"]["classes"][0] for a, o in zip(py, outs)]) >= 0.75
+        # margin rule against the fp32 reference of the same uploads (decoded as the service does)
+        from mlmicroservicetemplate_amd.models import resnet
+        from mlmicroservicetemplate_amd.plugins.builtin import decode_image
+
+        x = torch.from_numpy(np.stack([a for a in raws] + [decode_image(b, "image/png") for b in pngs])).cuda()
+        ref = resnet.resnet50_reference({k: v.cuda() for k, v in resnet.init_resnet50(0).items()}, x).float()
+        top2 = ref.topk(2, dim=-1).values
+        sure = ((top2[:, 0] - top2[:, 1]) / ref.abs().max() > 1e-2).tolist()
+        want = ref.argmax(-1).tolist()
+        assert sum(sure) >= 4, "too few decisive images to test anything"
+        for i, o in enumerate(outs):
+            cls = int(o.json()["result"]["classes"][0].split("_")[1])
+            if sure[i]:
+                assert cls == want[i], (i, cls, want[i])
         lg = subprocess.run([fbuild.loadgen_path(), "--port", str(svc.port), "--conns", "32", "--threads", "2",
                              "--duration", "2", "--warmup", "0.5"], capture_output=True, text=True, timeout=60)
         res = json.loads(lg.stdout)
