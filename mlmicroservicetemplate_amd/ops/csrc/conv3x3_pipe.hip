@@ -38,8 +38,7 @@ int* mls_stream_splitk_counters(void* stream, long ntiles);  // conv_gemm.hip
 namespace {
 
 constexpr int CK = 32;         // input channels per chunk (one MFMA k-slab, 64 B per pixel)
-constexpr int PMAX = 384;      // patch pixels per item
-constexpr int PP = PMAX / 16;  // 1-KiB patch DMA pieces per stage
+constexpr int PMAX = 384;      // patch pixels per item (the largest patch area: PPC = 24 pieces)
 constexpr int MAX_ROWS = 256;  // output pixels per item (16 row blocks)
 constexpr int NMAX = 512;      // output channels (bias staged in LDS)
 
@@ -73,8 +72,11 @@ MLS_DEV void wait_vm() {
 typedef unsigned int pipe_u32x4 __attribute__((__vector_size__(16)));
 typedef unsigned int pipe_u32x2 __attribute__((__vector_size__(8)));
 
-template <int BN, int NW, int RBW, int STAGES>
+// PPC: 1-KiB patch DMA pieces per stage (16 px each): 24 (<= 384 patch pixels) or 16 (<= 256,
+// smaller items but a 3rd stage fits; no all-padding pieces issued for the 14x14 layer)
+template <int BN, int NW, int RBW, int STAGES, int PPC>
 struct PipeCfg {
+  static constexpr int PP = PPC;
   static constexpr int CB = BN / 16;
   static constexpr int W_PIECES = 9 * BN * CK * 2 / 1024;  // 36 (BN 64) / 18 (BN 32)
   static constexpr int PATCH_BYTES = PP * 1024;
@@ -87,15 +89,15 @@ struct PipeCfg {
   static constexpr int FLAG_OFF = BIAS_OFF + NMAX * 4;
   static constexpr int DUMMY_OFF = FLAG_OFF + 16;  // 1-KiB sink of the branch-free tail DMAs
   static constexpr int LDS = DUMMY_OFF + 1024;
-  static_assert(PP % NW == 0, "patch pieces split evenly over the waves");
+  static_assert(PP % NW == 0 || PP < NW, "patch pieces split evenly over the waves");
   static_assert(RBW * NW >= 1 && RBW * NW * 16 <= 2 * MAX_ROWS, "row blocks");
   static_assert(LDS <= 160 * 1024, "LDS");
   static_assert(LPS * (STAGES - 1) + NST < 64, "vmcnt range");
 };
 
-template <int BN, int NW, int RBW, int STAGES>
+template <int BN, int NW, int RBW, int STAGES, int PPC>
 __global__ __launch_bounds__(NW * 64) void conv3x3_pipe_kernel(const PipeArgs a) {
-  using C = PipeCfg<BN, NW, RBW, STAGES>;
+  using C = PipeCfg<BN, NW, RBW, STAGES, PPC>;
   constexpr int CB = C::CB, LPS = C::LPS, NST = C::NST;
   __shared__ __attribute__((aligned(16))) char smem[C::LDS];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -362,13 +364,13 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_pipe_kernel(const PipeArgs a)
 
 // Item geometry as conv3x3_halo.hip: the largest th dividing H with th * W <= max_rows and
 // (th + 2) * (W + 2) <= PMAX; whole images (th == H) packed nb per item (nb | B).
-bool pipe_geometry(int B, int H, int W, int max_rows, int* th, int* nb) {
+bool pipe_geometry(int B, int H, int W, int max_rows, int pmax, int* th, int* nb) {
   for (int t = H; t >= 1; --t) {
-    if (H % t || t * W > max_rows || (t + 2) * (W + 2) > PMAX) continue;
+    if (H % t || t * W > max_rows || (t + 2) * (W + 2) > pmax) continue;
     int n = 1;
     if (t == H)
       for (int c = 8; c >= 1; --c)
-        if (B % c == 0 && c * H * W <= max_rows && c * (H + 2) * (W + 2) <= PMAX) {
+        if (B % c == 0 && c * H * W <= max_rows && c * (H + 2) * (W + 2) <= pmax) {
           n = c;
           break;
         }
@@ -379,23 +381,30 @@ bool pipe_geometry(int B, int H, int W, int max_rows, int* th, int* nb) {
   return false;
 }
 
-// variant -> (BN, NW, RBW, STAGES); max_rows of the geometry = 16 * NW * RBW (<= 256)
+// variant -> (BN, NW, RBW, STAGES, PPC); max_rows of the geometry = 16 * NW * RBW (<= 256),
+// patch pixels <= 16 * PPC
 struct PipeVariant {
-  int bn, nw, rbw, stages;
+  int bn, nw, rbw, stages, ppc;
 };
 constexpr PipeVariant kPipeVariants[] = {
-    {64, 4, 4, 2},  // 0: 256-pixel items x 64 channels, 4 waves of 4 x 4 tiles
-    {32, 4, 4, 2},  // 1: x 32 channels (2x the items of the small-M layers)
-    {32, 4, 4, 3},  // 2: x 32 channels, 3-stage ring
-    {64, 8, 2, 2},  // 3: 8 waves of 2 x 4 tiles
-    {64, 4, 2, 2},  // 4: 128-pixel items x 64 channels (layer1 / layer2: 2x the items)
-    {32, 4, 2, 3},  // 5: 128-pixel items x 32 channels, 3 stages
+    {64, 4, 4, 2, 24},  // 0: 256-pixel items x 64 channels, 4 waves of 4 x 4 tiles
+    {32, 4, 4, 2, 24},  // 1: x 32 channels (2x the items of the small-M layers)
+    {32, 4, 4, 3, 24},  // 2: x 32 channels, 3-stage ring
+    {64, 8, 2, 2, 24},  // 3: 8 waves of 2 x 4 tiles
+    {64, 4, 2, 2, 24},  // 4: 128-pixel items x 64 channels (layer1 / layer2: 2x the items)
+    {32, 4, 2, 3, 24},  // 5: 128-pixel items x 32 channels, 3 stages
+    {64, 8, 2, 3, 16},  // 6: <= 256-pixel patches, 8 waves, 3 stages (52 KB each)
+    {64, 4, 2, 3, 16},  // 7: 128-pixel items, 4 waves of 2 x 4, 3 stages
+    {64, 8, 1, 3, 16},  // 8: 128-pixel items, 8 waves of 1 x 4, 3 stages
+    {32, 8, 2, 3, 16},  // 9: x 32 channels, 8 waves, 3 stages
+    {32, 8, 2, 4, 16},  // 10: x 32 channels, 8 waves, 4 stages (34 KB each)
+    {64, 8, 2, 2, 16},  // 11: variant 6 with 2 stages
 };
 constexpr int kNumPipeVariants = sizeof(kPipeVariants) / sizeof(kPipeVariants[0]);
 
-template <int BN, int NW, int RBW, int STAGES>
+template <int BN, int NW, int RBW, int STAGES, int PPC>
 void launch_pipe(dim3 grid, hipStream_t st, const PipeArgs& a) {
-  hipLaunchKernelGGL((conv3x3_pipe_kernel<BN, NW, RBW, STAGES>), grid, dim3(NW * 64), 0, st, a);
+  hipLaunchKernelGGL((conv3x3_pipe_kernel<BN, NW, RBW, STAGES, PPC>), grid, dim3(NW * 64), 0, st, a);
 }
 
 }  // namespace
@@ -415,7 +424,7 @@ int mls_conv3x3_pipe(const void* x, const void* w, const float* bias, void* out,
   if (act != ACT_NONE && act != ACT_RELU) return MLS_UNSUPPORTED;
   int th = 0, nb = 0;
   const int max_rows = 16 * v.nw * v.rbw;
-  if (!pipe_geometry(B, H, W, max_rows < MAX_ROWS ? max_rows : MAX_ROWS, &th, &nb)) return MLS_UNSUPPORTED;
+  if (!pipe_geometry(B, H, W, max_rows < MAX_ROWS ? max_rows : MAX_ROWS, 16 * v.ppc, &th, &nb)) return MLS_UNSUPPORTED;
   const long xb = (long)B * H * W * Cin * 2, wb = (long)N * 9 * Cin * 2, ob = (long)B * H * W * N * 2;
   if (xb >= 0x7fffffffL || wb >= 0x7fffffffL || ob >= 0x7fffffffL) return MLS_UNSUPPORTED;
   PipeArgs a;
@@ -449,12 +458,18 @@ int mls_conv3x3_pipe(const void* x, const void* w, const float* bias, void* out,
   const dim3 grid((unsigned)((a.nitems + ipb - 1) / ipb));
   hipStream_t st = (hipStream_t)stream;
   switch (variant) {
-    case 0: launch_pipe<64, 4, 4, 2>(grid, st, a); break;
-    case 1: launch_pipe<32, 4, 4, 2>(grid, st, a); break;
-    case 2: launch_pipe<32, 4, 4, 3>(grid, st, a); break;
-    case 3: launch_pipe<64, 8, 2, 2>(grid, st, a); break;
-    case 4: launch_pipe<64, 4, 2, 2>(grid, st, a); break;
-    case 5: launch_pipe<32, 4, 2, 3>(grid, st, a); break;
+    case 0: launch_pipe<64, 4, 4, 2, 24>(grid, st, a); break;
+    case 1: launch_pipe<32, 4, 4, 2, 24>(grid, st, a); break;
+    case 2: launch_pipe<32, 4, 4, 3, 24>(grid, st, a); break;
+    case 3: launch_pipe<64, 8, 2, 2, 24>(grid, st, a); break;
+    case 4: launch_pipe<64, 4, 2, 2, 24>(grid, st, a); break;
+    case 5: launch_pipe<32, 4, 2, 3, 24>(grid, st, a); break;
+    case 6: launch_pipe<64, 8, 2, 3, 16>(grid, st, a); break;
+    case 7: launch_pipe<64, 4, 2, 3, 16>(grid, st, a); break;
+    case 8: launch_pipe<64, 8, 1, 3, 16>(grid, st, a); break;
+    case 9: launch_pipe<32, 8, 2, 3, 16>(grid, st, a); break;
+    case 10: launch_pipe<32, 8, 2, 4, 16>(grid, st, a); break;
+    case 11: launch_pipe<64, 8, 2, 2, 16>(grid, st, a); break;
     default: return MLS_BAD_ARG;
   }
   return (int)hipGetLastError();
@@ -465,7 +480,7 @@ int mls_conv3x3_pipe_geometry(int B, int H, int W, int variant, int* th, int* nb
   if (variant < 0 || variant >= kNumPipeVariants) return MLS_BAD_ARG;
   const PipeVariant v = kPipeVariants[variant];
   const int max_rows = 16 * v.nw * v.rbw;
-  return pipe_geometry(B, H, W, max_rows < MAX_ROWS ? max_rows : MAX_ROWS, th, nb) ? 0 : MLS_UNSUPPORTED;
+  return pipe_geometry(B, H, W, max_rows < MAX_ROWS ? max_rows : MAX_ROWS, 16 * v.ppc, th, nb) ? 0 : MLS_UNSUPPORTED;
 }
 
 int mls_conv3x3_pipe_num_variants() { return kNumPipeVariants; }

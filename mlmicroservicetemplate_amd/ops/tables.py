@@ -53,14 +53,16 @@ _ops_log = __import__("logging").getLogger("mlsamd.ops")
 
 
 def _note_miss(table: str, M: int, N: int, K: int) -> None:
-    """Log ONCE per process and shape when a served GEMM shape is not in a tuning table (it then
-    runs the kernel's heuristic tile, which can be far off the measured best)."""
-    key = (table, M, N, K)
+    """Log ONCE per process and projection (N, K) when a served GEMM shape is not in a tuning table
+    (it then runs the kernel's heuristic tile, which can be far off the measured best)."""
+    # one line per projection (N, K) and table: a prefill sees a new M for nearly every batch
+    key = (table, N, K)
     if key in _TABLE_MISSES:
         return
     _TABLE_MISSES.add(key)
     _ops_log.warning("GEMM shape M=%d N=%d K=%d is not in %s: heuristic config (tune it with "
-                     "tools/gemm_tile_probe.py / ops.autotune)", M, N, K, table)
+                     "tools/gemm_tile_probe.py / ops.autotune; further misses of this N x K not logged)",
+                     M, N, K, table)
 
 
 def tile_cfg_for(M: int, N: int, K: int) -> Tuple[int, int]:

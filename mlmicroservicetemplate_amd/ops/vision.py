@@ -43,7 +43,7 @@ HALO_CFGS = (CFG_HALO, CFG_HALO_N32, CFG_HALO_XL)
 CFG_PIPE = 110
 
 
-PIPE_VARIANTS = 6
+PIPE_VARIANTS = 12
 
 
 PIPE_CFGS = tuple(range(CFG_PIPE, CFG_PIPE + PIPE_VARIANTS))

@@ -2,8 +2,6 @@
 on the GPU, prefill picks written into the slots, the decode step + X4 + pick as ONE captured
 graph, one [2, B] read-back per iteration) against the host-pick path on the same fused model:
 identical tokens for staggered greedy / sampled requests, with per-slot and paged KV caches."""
-import time
-
 import pytest
 import torch
 
@@ -16,11 +14,11 @@ def _serve(m, reqs, dev_mode: bool):
 
     eng = ContinuousLlama(m)
     eng._want_dev = dev_mode
+    # every request queued before the scheduler starts: the admission order (first 4, then one per
+    # freed slot) is then a function of the tokens alone, so both modes run the same prefill
+    # batches (staggered arrivals: tests/test_continuous_batching.py)
+    futs = [eng.submit(ids, gp) for ids, gp in reqs]
     eng.start()
-    futs = []
-    for ids, gp in reqs:
-        futs.append(eng.submit(ids, gp))
-        time.sleep(0.005)  # arrive while others are mid-decode
     outs = [f.result(timeout=120) for f in futs]
     eng.stop()
     return outs, eng

@@ -10,6 +10,7 @@ def test_untuned_shape_logged_once(caplog):
     ops._TABLE_MISSES.clear()
     assert ops.tile_cfg_for(1234, 4096, 4160) == (0, 1)
     assert ops.tile_cfg_for(1234, 4096, 4160) == (0, 1)
+    assert ops.tile_cfg_for(999, 4096, 4160) == (0, 1)  # same projection, another M: not logged again
     msgs = [r.getMessage() for r in caplog.records if "not in gemm_tile_gfx950.json" in r.getMessage()]
     assert len(msgs) == 1 and "M=1234 N=4096 K=4160" in msgs[0]
 

@@ -16,7 +16,7 @@ dev = torch.device("cuda:0")
 tuning = autotune.load_tuning("resnet50", 32)
 B = 32
 CONC = [int(c) for c in os.environ.get("CONC", "1,4").split(",")]
-VARIANTS = [int(v) for v in os.environ.get("VARIANTS", "0,1,2,3,4,5").split(",")]
+VARIANTS = [int(v) for v in os.environ.get("VARIANTS", "0,1,2,3,4,5,6,7,8,9,10,11").split(",")]
 for layer, (H, C) in {"layer1.1.conv2": (56, 64), "layer2.1.conv2": (28, 128), "layer3.1.conv2": (14, 256),
                       "layer4.1.conv2": (7, 512)}.items():
     x = torch.randn(B, H, H, C, device=dev).to(torch.bfloat16)
