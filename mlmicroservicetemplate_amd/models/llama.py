@@ -676,7 +676,7 @@ class LlamaTP:
                 return ops.skinny_fp8(x, q, sc, p[name].shape[0], residual=residual)
             if name in packed:
                 return ops.skinny_packed(x, packed[name], p[name].shape[0], residual=residual, variant=self.pk_variant)
-            return ops.linear(x, p[name], workspace=ws)
+            return ops.linear(x, p[name], residual=residual, workspace=ws)
 
         def pre_norm(x, name, d, act=ops.ACT_NONE):
             w = p[name]

@@ -36,6 +36,7 @@ from .tables import (  # noqa: F401
     load_blas_tuning,
     small_m_plan_for,
     tile_cfg_for,
+    tile_route_for,
 )
 from .gemm_ops import (  # noqa: F401
     FP8_MAX,

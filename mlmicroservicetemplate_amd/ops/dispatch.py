@@ -12,13 +12,18 @@ import torch
 from ._lib import NativeError, available, check, lib, stream_ptr  # noqa: F401
 from ._core import ACT_GELU, ACT_NONE, ACT_SILU_MUL, _act  # noqa: F401
 from .gemm_ops import _bias_bf16, gemm, gemm_tile, silu_mul_interleaved  # noqa: F401
-from .tables import small_m_plan_for, tile_cfg_for  # noqa: F401
+from .tables import small_m_plan_for, tile_cfg_for, tile_route_for  # noqa: F401
 
 
 # Large-M projections run on the native LDS-DMA MFMA tile kernel (gemm_tile: csrc/gemm_tile.hip),
 # the decode-shaped ones (M <= 32, and 33..TILE_MIN_M - 1 rows) on the skinny / conv_gemm kernels with
-# per-shape plans.  hipBLASLt (torch.addmm) is reachable only on request -- impl="blas" or
-# MLS_GEMM_IMPL=blas -- as the A/B reference of tools/gemm_tile_probe.py; no default path calls it.
+# per-shape plans.  hipBLASLt (torch.addmm; a SiLU-mul runs as the native pass after it) runs a
+# default path only where the tile table names it for a projection with no residual epilogue that
+# it measured faster on: the 256-row decode step of 256 serving slots (O / down / LM head,
+# profiles/r4_dec256_gemm_probe.jsonl) and Llama-3-8B TP=1 prefill from 1024 rows, where the
+# library's 1.19-1.58 PFLOP/s beat this kernel's 0.87-1.26 on all four projections
+# (profiles/r4_llama_prefill_gemm_native_vs_blas.jsonl; tuned/gemm_tile_gfx950.json).  Otherwise
+# only on request (impl="blas" or MLS_GEMM_IMPL=blas, the A/B reference).
 TILE_MIN_M = int(os.environ.get("MLS_TILE_MIN_M", "256"))
 
 
@@ -43,7 +48,13 @@ def linear(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         return _linear_blas(a, w, bias, code, residual)
     if impl == "tile" or (impl == "auto" and M >= TILE_MIN_M and K % 64 == 0 and N % 16 == 0
                           and a.device.type == "cuda" and a.is_contiguous() and w.is_contiguous()):
-        cfg, sk = tile_cfg_for(M, N, K)
+        kind, cfg, sk = tile_route_for(M, N, K) if impl == "auto" else ("tile",) + tile_cfg_for(M, N, K)
+        if kind == "blas" and code in (ACT_NONE, ACT_GELU, ACT_SILU_MUL) and residual is None:
+            return _linear_blas(a, w, bias, code, residual)
+        if kind == "conv":
+            return gemm(a, w, bias, act=code, residual=residual, workspace=workspace, cfg=cfg, splitk=sk)
+        if kind != "tile":
+            cfg, sk = 0, 1  # a library route for a fused epilogue: the tile kernel's own pick
         return gemm_tile(a, w, bias, act=code, residual=residual, cfg=cfg, splitk=sk, workspace=workspace)
     plan = small_m_plan_for(M, N, K) if impl == "auto" else None
     if plan is not None and plan[0] > 0 and not (code == ACT_SILU_MUL and residual is not None):

@@ -68,11 +68,23 @@ def _note_miss(table: str, M: int, N: int, K: int) -> None:
 def tile_cfg_for(M: int, N: int, K: int) -> Tuple[int, int]:
     """gemm_tile (config, K splits) for a shape: measured choices first (``tuned/gemm_tile_gfx950.json``),
     else the kernel's own pick (largest tile that still fills the chip), no split -- logged once."""
+    impl, cfg, sk = tile_route_for(M, N, K)
+    return (cfg, sk) if impl == "tile" else (0, 1)
+
+
+def tile_route_for(M: int, N: int, K: int) -> Tuple[str, int, int]:
+    """``(impl, cfg, splitk)`` of a large-M projection: impl "tile" (gemm_tile), "conv" (the conv_gemm
+    kernel, for short-M shapes whose tiles cannot fill the chip) or "blas" (hipBLASLt, a plain GEMM
+    the library measured faster on) -- the table's per-shape winner; a miss runs the tile kernel's
+    own pick (logged once)."""
     e = gemm_tile_plan().get((M, N, K))
-    if e is None:
-        _note_miss("gemm_tile_gfx950.json", M, N, K)
-        return (0, 1)
-    return e
+    if e is not None:
+        return e
+    for lo, hi, route in gemm_tile_ranges().get((N, K), ()):
+        if lo <= M <= hi:
+            return route
+    _note_miss("gemm_tile_gfx950.json", M, N, K)
+    return ("tile", 0, 1)
 
 
 def small_m_plan_for(M: int, N: int, K: int) -> Optional[Tuple[int, int]]:
@@ -92,4 +104,24 @@ def gemm_tile_plan() -> Dict[Tuple[int, int, int], Tuple[int, int]]:
         return {}
     with open(path) as f:
         doc = json.load(f)
-    return {(e["M"], e["N"], e["K"]): (int(e["cfg"]), int(e.get("splitk", 1))) for e in doc["entries"]}
+    return {(e["M"], e["N"], e["K"]): (e.get("impl", "tile"), int(e.get("cfg", 0)), int(e.get("splitk", 1)))
+            for e in doc["entries"] if "M" in e}
+
+
+@functools.lru_cache(maxsize=None)
+def gemm_tile_ranges() -> Dict[Tuple[int, int], List[Tuple[int, int, Tuple[str, int, int]]]]:
+    """Row-range entries of the tile table (``"M_min"`` / ``"M_max"`` instead of ``"M"``): a projection
+    (N, K) whose winner does not change over a range of token counts -- a prefill sees a new M for
+    nearly every batch.  Exact entries take precedence."""
+    path = os.environ.get("MLS_GEMM_TILE_TABLE") or os.path.join(_TUNED_DIR, "gemm_tile_gfx950.json")
+    if os.environ.get("MLS_GEMM_PLAN", "1") == "0" or not os.path.exists(path):
+        return {}
+    with open(path) as f:
+        doc = json.load(f)
+    out: Dict[Tuple[int, int], list] = {}
+    for e in doc["entries"]:
+        if "M_min" in e:
+            out.setdefault((e["N"], e["K"]), []).append(
+                (int(e["M_min"]), int(e.get("M_max", 1 << 30)),
+                 (e.get("impl", "tile"), int(e.get("cfg", 0)), int(e.get("splitk", 1)))))
+    return out

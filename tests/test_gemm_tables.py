@@ -18,10 +18,34 @@ def test_untuned_shape_logged_once(caplog):
 def test_tuned_shapes_are_silent(caplog):
     caplog.set_level(logging.WARNING, logger="mlsamd.ops")
     ops._TABLE_MISSES.clear()
-    (M, N, K), cfg = next(iter(ops.gemm_tile_plan().items()))
-    assert ops.tile_cfg_for(M, N, K) == cfg
+    (M, N, K), (impl, cfg, sk) = next(iter(ops.gemm_tile_plan().items()))
+    assert impl == "tile" and ops.tile_cfg_for(M, N, K) == (cfg, sk)
     (M2, N2, K2), plan = next(iter(ops.gemm_plan().items()))
     assert ops.small_m_plan_for(M2, N2, K2) == plan
     assert not [r for r in caplog.records if "not in" in r.getMessage()]
     assert ops.small_m_plan_for(3, 5, 64) is None
     assert any("gemm_plan_gfx950.json" in r.getMessage() for r in caplog.records)
+
+
+def test_decode256_routes_are_per_shape_winners():
+    """The 256-row decode step (256 serving slots): each projection on its measured winner --
+    conv_gemm split-K for QKV, the fused-SiLU tile for gate_up, hipBLASLt for the plain O / down /
+    LM head (profiles/r4_dec256_gemm_probe.jsonl)."""
+    assert ops.tile_route_for(256, 6144, 4096) == ("conv", 7, 2)
+    assert ops.tile_route_for(256, 28672, 4096) == ("tile", 16, 1)
+    for n, k in ((4096, 4096), (4096, 14336), (128256, 4096)):
+        assert ops.tile_route_for(256, n, k)[0] == "blas"
+        assert ops.tile_cfg_for(256, n, k) == (0, 1)
+
+
+def test_prefill_row_ranges_route_without_exact_entries(caplog):
+    """Row-range entries cover every prefill token count of a projection (no per-M miss logging):
+    Llama-3-8B TP=1 projections from 1024 rows go to hipBLASLt (measured faster at 4096 and 32768
+    rows); shapes outside every range still fall back to the tile kernel's pick."""
+    caplog.set_level(logging.WARNING, logger="mlsamd.ops")
+    ops._TABLE_MISSES.clear()
+    for m in (1024, 4096, 5000, 32768):
+        for n, k in ((6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)):
+            assert ops.tile_route_for(m, n, k)[0] == "blas"
+    assert not [r for r in caplog.records if "not in" in r.getMessage()]
+    assert ops.tile_route_for(700, 6144, 4096) == ("tile", 0, 1)  # below the range, no exact entry

@@ -18,6 +18,8 @@ SHAPES = {  # name: (M, N, K)
     "bert128_qkv": (128, 2304, 768), "bert128_ffn1": (128, 3072, 768), "bert128_ffn2": (128, 768, 3072),
     "bert128_o": (128, 768, 768), "bert1024_qkv": (1024, 2304, 768), "bert1024_ffn2": (1024, 768, 3072),
     "m64_qkv": (64, 6144, 4096), "m256_gateup": (256, 28672, 4096),
+    "dec256_qkv": (256, 6144, 4096), "dec256_o": (256, 4096, 4096), "dec256_down": (256, 4096, 14336),
+    "dec256_lm": (256, 128256, 4096),
 }
 
 

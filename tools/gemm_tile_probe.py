@@ -25,6 +25,13 @@ SHAPES = {  # name: (M, N, K, act)
     # Llama-3-8B prefill of one 512-token prompt (B=1 x 512 rows)
     "llama512_qkv": (512, 6144, 4096, "none"), "llama512_o": (512, 4096, 4096, "none"),
     "llama512_gateup": (512, 28672, 4096, "silu_mul"), "llama512_down": (512, 4096, 14336, "none"),
+    # Llama-3-8B decode step of 256 serving slots (M = 256 rows)
+    "dec256_qkv": (256, 6144, 4096, "none"), "dec256_o": (256, 4096, 4096, "none"),
+    "dec256_gateup": (256, 28672, 4096, "silu_mul"), "dec256_down": (256, 4096, 14336, "none"),
+    "dec256_lm": (256, 128256, 4096, "none"),
+    # serving prefill: 256 admitted 128-token prompts in one batch (M = 32768 rows)
+    "llama32k_qkv": (32768, 6144, 4096, "none"), "llama32k_o": (32768, 4096, 4096, "none"),
+    "llama32k_gateup": (32768, 28672, 4096, "silu_mul"), "llama32k_down": (32768, 4096, 14336, "none"),
 }
 
 
