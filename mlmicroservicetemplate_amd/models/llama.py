@@ -860,7 +860,10 @@ class LlamaTP:
         if self.tp == 1 or getattr(self.comm, "graph_safe", False) or self._rccl_graphs:
             return True
         car = getattr(self.comm, "car", None)
-        return car is not None and B * self.cfg.hidden * 2 <= car.cap
+        if car is None:
+            return False
+        probe = torch.empty(B * self.cfg.hidden, dtype=torch.bfloat16, device=car.device)
+        return car.eligible(probe)  # one-shot or two-shot: both are in-stream kernels
 
     def _decode_graph(self, B: int, k: int, ctx: int):
         """Captured decode step for batch B and context bound ctx (static token / position / length

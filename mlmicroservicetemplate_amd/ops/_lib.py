@@ -64,6 +64,8 @@ _SIGS = {
     "mls_embedding": [P, P, P, L, I, I, I, P],
     "mls_rope": [P, P, P, P, L, I, I, I, P],
     "mls_ar_create": [I, I, L, P],
+    "mls_ar_create2": [I, I, L, L, P],
+    "mls_ar_allreduce2": [P, P, P, L, _c.c_longlong, P],
     "mls_ar_handle": [P, P],
     "mls_ar_handle_size": [],
     "mls_ar_open": [P, P],

@@ -35,9 +35,15 @@ struct ArCtx {
   int* epochs;                   // [max_blocks] device-side per-block epoch (local)
   int* err;                      // local error word
   bool opened;
+  // two-shot region (its own staging halves, flags and epochs: the protocols never share memory)
+  size_t cap2;                   // bytes per two-shot staging half (0 = no two-shot path)
+  size_t off2;                   // byte offset of the region in every rank's allocation
+  int max_blocks2;
+  int* epochs2;
 };
 
 // allocation layout: [2][cap] staging | ready[AR_MAX_RANKS][max_blocks] | done[...] | epochs | err
+// | (4 KiB aligned, off2) [2][cap2] two-shot staging | ready2 / red2 / done2 [AR_MAX_RANKS][max_blocks2] | epochs2
 __host__ __device__ inline size_t ar_flags_off(size_t cap) { return 2 * cap; }
 
 struct ArArgs {
@@ -173,6 +179,106 @@ __global__ __launch_bounds__(AR_THREADS) void oneshot_allgather_kernel(const ArA
   }
 }
 
+// Two-shot all-reduce (reduce-scatter + all-gather in one launch) for the mid-size messages -- TP
+// decode at 32-256 rows (0.25-2 MiB per all-reduce) -- where the one-shot's (N - 1) x n bytes of
+// peer reads per rank outgrow xGMI: here each rank reads 2 (N - 1) / N x n.  The n elements are
+// N segments of n / N; block b owns chunk b of EVERY segment:
+//   1. stage chunk b of all N segments into this rank's two-shot buffer (half `parity`), publish
+//      ready2[rank][b] everywhere;
+//   2. once every peer's ready2 arrived, sum chunk b of segment `rank` over all ranks' buffers
+//      (fp32), write the bf16 result to `out` AND back into this rank's own staging copy of that
+//      chunk (no peer reads it during step 2: peer p reads segment p), publish red2[rank][b];
+//   3. once every peer's red2 arrived, copy chunk b of every other segment s from rank s's buffer
+//      (its reduced copy) to `out`; publish done2[rank][b] -- the restage guard two epochs later.
+// Every rank writes identical bf16 bytes for every element (one reducer per segment).  Same epoch,
+// bounded-spin and error-word rules as the one-shot kernel, in a disjoint region of the allocation.
+constexpr int AR2_CH = AR_THREADS * 8;  // elements of each segment per block
+
+struct Ar2Args {
+  const bf16* in;
+  bf16* out;
+  long n, seg;
+  int rank, world, max_blocks;
+  size_t cap, off;
+  char* bufs[AR_MAX_RANKS];
+  int* epochs;
+  int* err;
+  long long timeout;
+};
+
+MLS_DEV int* ar2_flag(char* base, const Ar2Args& a, int kind, int src, int b) {
+  return reinterpret_cast<int*>(base + a.off + 2 * a.cap) + (kind * AR_MAX_RANKS + src) * a.max_blocks + b;
+}
+
+__global__ __launch_bounds__(AR_THREADS) void twoshot_allreduce_kernel(const Ar2Args a) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  __shared__ int s_epoch, s_ok;
+  if (tid == 0) {
+    s_epoch = a.epochs[b] + 1;
+    s_ok = 1;
+  }
+  __syncthreads();
+  const int e = s_epoch, parity = e & 1;
+  const long c0 = (long)b * AR2_CH + tid * 8;  // this lane's 8 elements within each segment
+  const bool mine = c0 < a.seg;                // seg % 8 == 0 (host-checked)
+  char* const own = a.bufs[a.rank] + a.off + parity * a.cap;
+  if (tid < a.world && e > 2) {
+    if (!ar_wait_ge(ar2_flag(a.bufs[a.rank], a, 2, tid, b), e - 2, a.timeout)) s_ok = 0;
+  }
+  __syncthreads();
+  // (1) stage chunk b of every segment
+  if (mine)
+    for (int s = 0; s < a.world; ++s) {
+      const long i = s * a.seg + c0;
+      st16(reinterpret_cast<bf16*>(own) + i, ld16(a.in + i));
+    }
+  __threadfence_system();
+  __syncthreads();
+  if (tid < a.world)
+    __hip_atomic_store(ar2_flag(a.bufs[tid], a, 0, a.rank, b), e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (tid < a.world) {
+    if (!ar_wait_ge(ar2_flag(a.bufs[a.rank], a, 0, tid, b), e, a.timeout)) s_ok = 0;
+  }
+  __syncthreads();
+  // (2) reduce this rank's segment
+  if (mine) {
+    const long i = a.rank * a.seg + c0;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < a.world; ++r) {
+      const int src = (a.rank + r) % a.world;
+      float x[8];
+      unpack8(load_sys16(reinterpret_cast<const bf16*>(a.bufs[src] + a.off + parity * a.cap) + i), x);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += x[k];
+    }
+    const uint4 v = pack8(acc);
+    st16(a.out + i, v);
+    st16(reinterpret_cast<bf16*>(own) + i, v);
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (tid < a.world)
+    __hip_atomic_store(ar2_flag(a.bufs[tid], a, 1, a.rank, b), e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (tid < a.world) {
+    if (!ar_wait_ge(ar2_flag(a.bufs[a.rank], a, 1, tid, b), e, a.timeout)) s_ok = 0;
+  }
+  __syncthreads();
+  // (3) gather the other segments' reduced chunks from their owners
+  if (mine)
+    for (int r = 1; r < a.world; ++r) {
+      const int src = (a.rank + r) % a.world;
+      const long i = src * a.seg + c0;
+      st16(a.out + i, load_sys16(reinterpret_cast<const bf16*>(a.bufs[src] + a.off + parity * a.cap) + i));
+    }
+  __syncthreads();
+  if (tid < a.world)
+    __hip_atomic_store(ar2_flag(a.bufs[tid], a, 2, a.rank, b), e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (tid == 0) {
+    a.epochs[b] = e;
+    if (!s_ok) atomicOr(a.err, 1);
+  }
+}
+
 // fault injection for tests: hold the stream for `us` microseconds (bounded: <= 10 s)
 __global__ void gpu_sleep_kernel(long long ticks) {
   const long long t0 = wall_clock64();
@@ -184,15 +290,31 @@ __global__ void gpu_sleep_kernel(long long ticks) {
 extern "C" {
 
 // cap: bytes per message (messages above it use RCCL); returns an opaque context
-int mls_ar_create(int rank, int world, long cap, void** ctx_out) {
-  if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world || cap <= 0 || cap % 4096) return MLS_BAD_ARG;
+static size_t ar_region1_bytes(const ArCtx* c) {
+  const size_t flags = (size_t)2 * AR_MAX_RANKS * c->max_blocks * sizeof(int);
+  return 2 * c->cap + flags + (size_t)c->max_blocks * sizeof(int) + 64;
+}
+static size_t ar_region2_bytes(const ArCtx* c) {
+  const size_t flags = (size_t)3 * AR_MAX_RANKS * c->max_blocks2 * sizeof(int);
+  return 2 * c->cap2 + flags + (size_t)c->max_blocks2 * sizeof(int);
+}
+
+// cap: bytes per one-shot message; cap2: bytes per two-shot message (0 = none; messages above the
+// caps use RCCL); returns an opaque context
+int mls_ar_create2(int rank, int world, long cap, long cap2, void** ctx_out) {
+  if (world < 1 || world > AR_MAX_RANKS || rank < 0 || rank >= world || cap <= 0 || cap % 4096 || cap2 < 0 ||
+      cap2 % 4096)
+    return MLS_BAD_ARG;
   ArCtx* c = new ArCtx{};
   c->rank = rank;
   c->world = world;
   c->cap = (size_t)cap;
   c->max_blocks = (int)((cap / 2 + AR_ELEMS_PER_BLOCK - 1) / AR_ELEMS_PER_BLOCK);
-  const size_t flags = (size_t)2 * AR_MAX_RANKS * c->max_blocks * sizeof(int);
-  const size_t bytes = 2 * c->cap + flags + (size_t)c->max_blocks * sizeof(int) + 64;
+  c->cap2 = (size_t)cap2;
+  // a segment is <= cap2 / 2 / world elements; one block per AR2_CH of it
+  c->max_blocks2 = cap2 ? (int)((cap2 / 2 / world + AR2_CH - 1) / AR2_CH) : 0;
+  c->off2 = (ar_region1_bytes(c) + 4095) / 4096 * 4096;
+  const size_t bytes = c->off2 + (cap2 ? ar_region2_bytes(c) : 0);
   if (hipExtMallocWithFlags((void**)&c->local, bytes, hipDeviceMallocUncached) != hipSuccess) {
     delete c;
     return MLS_UNSUPPORTED;
@@ -202,13 +324,19 @@ int mls_ar_create(int rank, int world, long cap, void** ctx_out) {
     delete c;
     return MLS_UNSUPPORTED;
   }
+  const size_t flags = (size_t)2 * AR_MAX_RANKS * c->max_blocks * sizeof(int);
   c->epochs = reinterpret_cast<int*>(c->local + 2 * c->cap + flags);
   c->err = c->epochs + c->max_blocks;
+  c->epochs2 = cap2 ? reinterpret_cast<int*>(c->local + c->off2 + 2 * c->cap2 +
+                                             (size_t)3 * AR_MAX_RANKS * c->max_blocks2 * sizeof(int))
+                    : nullptr;
   for (int i = 0; i < AR_MAX_RANKS; ++i) c->peers[i] = nullptr;
   c->peers[rank] = c->local;
   *ctx_out = c;
   return 0;
 }
+
+int mls_ar_create(int rank, int world, long cap, void** ctx_out) { return mls_ar_create2(rank, world, cap, 0, ctx_out); }
 
 int mls_ar_handle(void* ctx, void* handle_out /* HIP_IPC_HANDLE_SIZE bytes */) {
   ArCtx* c = (ArCtx*)ctx;
@@ -257,6 +385,31 @@ int mls_ar_allreduce(void* ctx, const void* in, void* out, long n, long long tim
   return (int)hipGetLastError();
 }
 
+// two-shot: in/out n bf16 elements, n % (8 * world) == 0, n * 2 <= cap2; in may alias out
+int mls_ar_allreduce2(void* ctx, const void* in, void* out, long n, long long timeout, void* stream) {
+  ArCtx* c = (ArCtx*)ctx;
+  if (!c->opened && c->world > 1) return MLS_BAD_ARG;
+  if (!c->cap2 || n <= 0 || n % (8L * c->world) || (size_t)n * 2 > c->cap2) return MLS_BAD_ARG;
+  Ar2Args a{};
+  a.in = (const bf16*)in;
+  a.out = (bf16*)out;
+  a.n = n;
+  a.seg = n / c->world;
+  a.rank = c->rank;
+  a.world = c->world;
+  a.max_blocks = c->max_blocks2;
+  a.cap = c->cap2;
+  a.off = c->off2;
+  for (int r = 0; r < AR_MAX_RANKS; ++r) a.bufs[r] = c->peers[r];
+  a.epochs = c->epochs2;
+  a.err = c->err;
+  a.timeout = timeout > 0 ? timeout : (1LL << 24);
+  const int blocks = (int)((a.seg + AR2_CH - 1) / AR2_CH);
+  if (blocks > c->max_blocks2) return MLS_BAD_ARG;
+  hipLaunchKernelGGL(twoshot_allreduce_kernel, dim3(blocks), dim3(AR_THREADS), 0, (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}
+
 // X4: out[world][nbytes] = every rank's `in` (nbytes % 16 == 0, nbytes <= cap, out != in)
 int mls_ar_allgather(void* ctx, const void* in, void* out, long nbytes, long long timeout, void* stream) {
   ArCtx* c = (ArCtx*)ctx;
@@ -286,6 +439,10 @@ int mls_ar_reset(void* ctx) {
   const size_t flags = (size_t)2 * AR_MAX_RANKS * c->max_blocks * sizeof(int);
   const size_t bytes = flags + (size_t)c->max_blocks * sizeof(int) + 64;
   if (hipMemset(c->local + 2 * c->cap, 0, bytes) != hipSuccess) return MLS_UNSUPPORTED;
+  if (c->cap2) {
+    const size_t f2 = (size_t)3 * AR_MAX_RANKS * c->max_blocks2 * sizeof(int) + (size_t)c->max_blocks2 * sizeof(int);
+    if (hipMemset(c->local + c->off2 + 2 * c->cap2, 0, f2) != hipSuccess) return MLS_UNSUPPORTED;
+  }
   return (int)hipDeviceSynchronize();
 }
 

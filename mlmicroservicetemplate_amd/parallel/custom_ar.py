@@ -6,7 +6,10 @@ is what an 8 KiB decode message pays for.  This module does the bootstrap -- all
 the IPC handle, all-gather the handles over the existing process group, open the peers -- and
 a start-up self-test against the group's own all-reduce.  Anything unexpected (IPC
 unavailable, a timeout, a wrong sum) leaves :attr:`CustomAllReduce.enabled` False and callers
-keep RCCL; messages larger than ``cap`` always use RCCL (bandwidth-bound: the ring wins there).
+keep RCCL.  Messages up to ``two_shot_min`` bytes take the one-shot kernel (every rank reads all
+N - 1 peers' copies: (N - 1) x n bytes per rank, one synchronisation); larger ones up to ``cap2``
+the two-shot kernel (reduce-scatter + all-gather in one launch: 2 (N - 1) / N x n bytes per rank,
+two synchronisations) -- TP decode at 32-256 rows; beyond ``cap2`` RCCL (bandwidth-bound prefill).
 
 ``TPComm`` uses it for TP > 1 on GPUs unless ``MLS_CUSTOM_AR=0``.  Being graph-safe, it is also
 what lets ``LlamaTP`` capture the TP decode step (RCCL inside graphs stays opt-in,
@@ -29,7 +32,8 @@ logger = logging.getLogger("mlsamd.custom_ar")
 
 class CustomAllReduce:
     def __init__(self, group=None, device=None, cap_bytes: int = 1 << 20, self_test: bool = True,
-                 timeout_iters: Optional[int] = None):
+                 timeout_iters: Optional[int] = None, cap2_bytes: Optional[int] = None,
+                 two_shot_min: Optional[int] = None):
         from ..ops import _lib
 
         self.group = group
@@ -40,6 +44,10 @@ class CustomAllReduce:
             dev = torch.device("cuda", torch.cuda.current_device())
         self.device = dev
         self.cap = int(cap_bytes)
+        # two-shot message range (MLS_AR_TWO_SHOT_CAP=0 disables the path)
+        self.cap2 = int(cap2_bytes if cap2_bytes is not None else os.environ.get("MLS_AR_TWO_SHOT_CAP", 4 << 20))
+        self.two_shot_min = int(two_shot_min if two_shot_min is not None
+                                else os.environ.get("MLS_AR_TWO_SHOT_MIN", 128 << 10))
         # peer-wait bound in spin iterations (~1 s by default); MLS_AR_TIMEOUT_ITERS shrinks it (tests)
         self.timeout = int(timeout_iters if timeout_iters is not None
                            else os.environ.get("MLS_AR_TIMEOUT_ITERS", str(1 << 24)))
@@ -59,7 +67,7 @@ class CustomAllReduce:
     def _setup(self) -> None:
         L = self._lib
         with torch.cuda.device(self.device):
-            rc = L.mls_ar_create(self.rank, self.world, self.cap, ctypes.byref(self._ctx))
+            rc = L.mls_ar_create2(self.rank, self.world, self.cap, self.cap2, ctypes.byref(self._ctx))
             if rc != 0:
                 raise RuntimeError(f"mls_ar_create failed ({rc})")
             hs = L.mls_ar_handle_size()
@@ -80,14 +88,17 @@ class CustomAllReduce:
     def _self_test(self) -> None:
         g = torch.Generator().manual_seed(1234 + self.rank)
         ok = True
-        for n in (8, 4096, 4096 * 3 + 8, self.cap // 2):
+        sizes = [(n, False) for n in (8, 4096, 4096 * 3 + 8, self.cap // 2)]
+        if self.cap2:
+            sizes += [(n - n % (8 * self.world), True) for n in (8 * self.world, 100000, self.cap2 // 2)]
+        for n, two in sizes:
             x = torch.randn(n, generator=g).to(torch.bfloat16)
             ref = x.float().clone()
             if dist.get_backend(self.group) == "nccl":
                 ref = ref.to(self.device)
             dist.all_reduce(ref, group=self.group)  # the group's own backend (RCCL, or gloo on CPU)
             ref = ref.cpu()
-            y = self._run(x.to(self.device))
+            y = self._run2(x.to(self.device)) if two else self._run(x.to(self.device))
             torch.cuda.synchronize(self.device)
             err = (y.float().cpu() - ref).abs().max().item() / (ref.abs().max().item() + 1e-6)
             ok = ok and err < 2e-2
@@ -107,6 +118,14 @@ class CustomAllReduce:
                                         torch.cuda.current_stream(self.device).cuda_stream)
         if rc != 0:
             raise RuntimeError(f"mls_ar_allreduce failed ({rc})")
+        return out
+
+    def _run2(self, t: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        out = t if out is None else out
+        rc = self._lib.mls_ar_allreduce2(self._ctx, t.data_ptr(), out.data_ptr(), t.numel(), self.timeout,
+                                         torch.cuda.current_stream(self.device).cuda_stream)
+        if rc != 0:
+            raise RuntimeError(f"mls_ar_allreduce2 failed ({rc})")
         return out
 
     def errors(self) -> int:
@@ -141,13 +160,30 @@ class CustomAllReduce:
             raise RuntimeError(f"mls_ar_allgather failed ({rc})")
         return out
 
+    def _two_shot(self, t: torch.Tensor) -> bool:
+        nbytes = t.numel() * 2
+        return (self.cap2 > 0 and nbytes >= self.two_shot_min and nbytes <= self.cap2
+                and t.numel() % (8 * self.world) == 0)
+
     def eligible(self, t: torch.Tensor) -> bool:
-        return (self.enabled and t.dtype == torch.bfloat16 and t.is_contiguous() and t.device == self.device
-                and t.numel() % 8 == 0 and t.numel() * 2 <= self.cap)
+        if not (self.enabled and t.dtype == torch.bfloat16 and t.is_contiguous() and t.device == self.device
+                and t.numel() % 8 == 0):
+            return False
+        return self._two_shot(t) or t.numel() * 2 <= self.cap
+
+    def path(self, t: torch.Tensor) -> str:
+        """Which kernel :meth:`all_reduce_` runs for ``t``: "two_shot", "one_shot" or "backend"."""
+        if not self.eligible(t):
+            return "backend"
+        return "two_shot" if self._two_shot(t) else "one_shot"
 
     def all_reduce_(self, t: torch.Tensor) -> torch.Tensor:
-        """In-place sum across the group (one-shot path when eligible, else the group's backend)."""
-        if self.eligible(t):
+        """In-place sum across the group: one-shot for small messages, two-shot for the mid range,
+        else the group's backend."""
+        p = self.path(t)
+        if p == "two_shot":
+            return self._run2(t)
+        if p == "one_shot":
             return self._run(t)
         dist.all_reduce(t, group=self.group)
         return t

@@ -13,18 +13,41 @@ def main():
     from mlmicroservicetemplate_amd.parallel.custom_ar import CustomAllReduce
 
     dev = torch.device("cuda:0")
-    car = CustomAllReduce(None, dev, cap_bytes=1 << 20)
+    car = CustomAllReduce(None, dev, cap_bytes=1 << 20, cap2_bytes=4 << 20, two_shot_min=128 << 10)
     assert car.enabled, car.reason
     g = torch.Generator().manual_seed(rank)
     fails = 0
-    for n in (8, 4096, 4104, 65536, 300000):
+    paths = set()
+    # one-shot sizes, then two-shot ones (>= 128 KiB, multiples of 8 x world)
+    for n in (8, 4096, 4104, 65536, 300000, 8 * world * 8192, 256 * 4096, 8 * world * 25003):
         x = torch.randn(n, generator=g).to(torch.bfloat16)
         ref = x.float().clone()
         dist.all_reduce(ref)
+        paths.add(car.path(x.to(dev)))
         y = car.all_reduce_(x.to(dev))
         torch.cuda.synchronize()
         err = (y.float().cpu() - ref).abs().max().item() / ref.abs().max().item()
         fails += err > 2e-2
+        # every rank holds the same bytes (one reducer per element)
+        yy = y.float().cpu()
+        first = yy.clone()
+        dist.broadcast(first, 0)
+        fails += int(not torch.equal(first, yy))
+    fails += int(paths != {"one_shot", "two_shot"})
+    # two-shot inside a captured graph as well (256 decode rows x 4096 hidden = 2 MiB)
+    big = torch.zeros(256 * 4096, device=dev, dtype=torch.bfloat16)
+    s2 = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s2):
+        g2 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g2, stream=s2):
+            car.all_reduce_(big)
+    for it in range(3):
+        big.copy_(torch.full((256 * 4096,), float(rank + it), dtype=torch.bfloat16).to(dev))
+        torch.cuda.synchronize()
+        dist.barrier()
+        g2.replay()
+        torch.cuda.synchronize()
+        fails += int(not torch.all(big.float() == sum(r + it for r in range(world))).item())
     # captured in a graph: three all-reduces per replay, replayed twice (device-side epochs)
     bufs = [torch.zeros(4096, device=dev, dtype=torch.bfloat16) for _ in range(3)]
     s = torch.cuda.Stream(dev)

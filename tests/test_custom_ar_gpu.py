@@ -20,7 +20,7 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_custom_allreduce_multiprocess(world):
     root = os.path.dirname(HERE)
     port = _port()
