@@ -455,6 +455,8 @@ class LlamaTP:
             self.packed: Dict[str, torch.Tensor] = {}
             self.pk_variant = int(os.environ.get("MLS_PACKED_VARIANT", "9"))
             self.pk_fold = os.environ.get("MLS_PACKED_FOLD", "1") == "1"
+            self.ar_fuse = os.environ.get("MLS_AR_FUSE", "1") == "1"  # GEMM-fused TP all-reduce (decode)
+            self.ar_fused_calls = 0  # projections issued with the fused all-reduce (eager + captured)
             self.fuse_combine = os.environ.get("MLS_FUSE_COMBINE", "1") == "1"
             mode = os.environ.get("MLS_PACKED_DECODE", "auto")
             if self.device.type == "cuda" and mode != "0":
@@ -670,6 +672,22 @@ class LlamaTP:
         def use_fp8(name, K):
             return name in fp8 and T * K * 2 <= 65536
 
+        # TP > 1 decode: the row-parallel o / down projections run their all-reduce in their own
+        # epilogue (ops.skinny_packed_ar / skinny_packed_combine_ar, csrc/ar_protocol.h): one launch
+        # per projection + all-reduce instead of two, and each 2048-element chunk of the output is
+        # reduced as soon as the blocks producing it finish.  MLS_AR_FUSE=0: separate kernels.
+        car = getattr(self.comm, "car", None)
+        ar_fuse = (self.tp > 1 and car is not None and getattr(self, "ar_fuse", False) and bool(packed)
+                   and car.fusable(T * self.cfg.hidden))
+
+        def row_parallel(x, name):
+            """sum over the TP ranks of x @ W_name^T (W row-parallel: each rank holds a K slice)."""
+            if ar_fuse and name in packed and not use_fp8(name, x.shape[1]):
+                self.ar_fused_calls += 1
+                with tracing.range("tp.gemm_all_reduce"):
+                    return ops.skinny_packed_ar(x, packed[name], p[name].shape[0], car, variant=self.pk_variant)
+            return self.comm.all_reduce_(linear(x, name))
+
         def linear(x, name, residual=None):
             if use_fp8(name, x.shape[1]):
                 q, sc = fp8[name]
@@ -722,24 +740,31 @@ class LlamaTP:
                 a = ops.flash_attention(qkv, B, S, sd.hq, sd.hkv, D, kv_lens=lens, causal=True)
             if parts is not None:  # split-KV combine in the o-projection's prologue (one launch, not two)
                 o_w = p[f"l{i}.o"]
-                o = ops.skinny_packed_combine(a, parts, packed[f"l{i}.o"], o_w.shape[0], residual=r if fold else None,
-                                              variant=self.pk_variant)
+                if ar_fuse:  # ... and the all-reduce in its epilogue
+                    self.ar_fused_calls += 1
+                    with tracing.range("tp.gemm_all_reduce"):
+                        o = ops.skinny_packed_combine_ar(a, parts, packed[f"l{i}.o"], o_w.shape[0], car,
+                                                         variant=self.pk_variant)
+                else:
+                    o = ops.skinny_packed_combine(a, parts, packed[f"l{i}.o"], o_w.shape[0],
+                                                  residual=r if fold else None, variant=self.pk_variant)
                 if fold:
                     gu, _ = pre_norm(o, f"l{i}.gate_up", None, act=ops.ACT_SILU_MUL)
                     r = linear(gu, f"l{i}.down", residual=o)
                     continue
-                o = self.comm.all_reduce_(o)
+                if not ar_fuse:
+                    o = self.comm.all_reduce_(o)
                 gu, r = pre_norm(r, f"l{i}.gate_up", o, act=ops.ACT_SILU_MUL)
-                delta = self.comm.all_reduce_(linear(gu, f"l{i}.down"))
+                delta = row_parallel(gu, f"l{i}.down")
                 continue
             if fold:
                 h = linear(a, f"l{i}.o", residual=r)
                 gu, _ = pre_norm(h, f"l{i}.gate_up", None, act=ops.ACT_SILU_MUL)
                 r = linear(gu, f"l{i}.down", residual=h)
                 continue
-            o = self.comm.all_reduce_(linear(a, f"l{i}.o"))
+            o = row_parallel(a, f"l{i}.o")
             gu, r = pre_norm(r, f"l{i}.gate_up", o, act=ops.ACT_SILU_MUL)
-            delta = self.comm.all_reduce_(linear(gu, f"l{i}.down"))
+            delta = row_parallel(gu, f"l{i}.down")
         if not decode:
             last = (torch.arange(B, device=r.device, dtype=torch.int64) * S + lens.long() - 1)
             r = r.index_select(0, last)

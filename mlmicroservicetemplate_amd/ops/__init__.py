@@ -58,6 +58,7 @@ from .gemm_ops import (  # noqa: F401
     silu_mul_interleaved,
     skinny_fp8,
     skinny_packed,
+    skinny_packed_ar,
     split_counters,
 )
 from .dispatch import (  # noqa: F401
@@ -112,6 +113,7 @@ from .transformer import (  # noqa: F401
     rope_,
     rope_kv_,
     skinny_packed_combine,
+    skinny_packed_combine_ar,
 )
 from .image import (  # noqa: F401
     IMAGE_CONTAINER_BYTES,

@@ -86,6 +86,8 @@ _SIGS = {
     "mls_skinny_packed": [P, P, P, P, P, P, P, I, I, I, I, I, F, I, P],
     "mls_decode_attention": [P, P, P, P, P, P, P, I, I, L, P, P, P, P, I, I, I, I, I, I, I, F, P, I, I, I, I, P],
     "mls_skinny_packed_combine": [P, P, P, P, I, I, I, I, P, P, P, P, I, I, I, I, I, P],
+    "mls_skinny_packed_ar": [P, P, P, P, P, I, I, I, I, F, I, P, P],
+    "mls_skinny_packed_combine_ar": [P, P, P, P, I, I, I, I, P, P, I, I, I, I, P, P],
     "mls_skinny_fp8": [P, P, P, P, P, P, P, P, I, I, I, I, I, F, I, P],
     "mls_stream_create_cumask": [P, I, _c.POINTER(P)],
     "mls_stream_get_cumask": [P, P, I],

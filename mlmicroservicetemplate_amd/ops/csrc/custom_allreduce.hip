@@ -19,13 +19,9 @@
 // side self-tests the path at start-up against RCCL and keeps RCCL if anything is off.
 #include <cstring>
 
-#include "common.h"
+#include "ar_protocol.h"
 
 namespace {
-
-constexpr int AR_MAX_RANKS = 8;
-constexpr int AR_THREADS = 256;
-constexpr int AR_ELEMS_PER_BLOCK = AR_THREADS * 8;  // 4 KiB of bf16 per block per call
 
 struct ArCtx {
   int rank, world, max_blocks;
@@ -40,11 +36,11 @@ struct ArCtx {
   size_t off2;                   // byte offset of the region in every rank's allocation
   int max_blocks2;
   int* epochs2;
+  int* fuse_cnt;                 // [max_blocks] arrival counters of the GEMMs that fuse the one-shot
 };
 
 // allocation layout: [2][cap] staging | ready[AR_MAX_RANKS][max_blocks] | done[...] | epochs | err
 // | (4 KiB aligned, off2) [2][cap2] two-shot staging | ready2 / red2 / done2 [AR_MAX_RANKS][max_blocks2] | epochs2
-__host__ __device__ inline size_t ar_flags_off(size_t cap) { return 2 * cap; }
 
 struct ArArgs {
   const bf16* in;
@@ -58,77 +54,22 @@ struct ArArgs {
   long long timeout;  // spin iterations
 };
 
-MLS_DEV int* ar_ready(char* base, size_t cap, int max_blocks, int src, int b) {
-  return reinterpret_cast<int*>(base + ar_flags_off(cap)) + src * max_blocks + b;
-}
-MLS_DEV int* ar_done(char* base, size_t cap, int max_blocks, int src, int b) {
-  return reinterpret_cast<int*>(base + ar_flags_off(cap)) + (AR_MAX_RANKS + src) * max_blocks + b;
-}
-
-MLS_DEV bool ar_wait_ge(int* flag, int want, long long timeout) {
-  for (long long i = 0; i < timeout; ++i) {
-    if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >= want) return true;
-    __builtin_amdgcn_s_sleep(2);
-  }
-  return false;
-}
-
-MLS_DEV uint4 load_sys16(const void* p) {  // system-coherent 16-B load (peer memory over xGMI)
-  const rsrc_t r = make_rsrc(p, 16);
-  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, 0, 0, 17));
+MLS_DEV ArFuse ar_view(const ArArgs& a) {
+  ArFuse f{};
+  for (int r = 0; r < AR_MAX_RANKS; ++r) f.bufs[r] = a.bufs[r];
+  f.cap = a.cap;
+  f.rank = a.rank;
+  f.world = a.world;
+  f.max_blocks = a.max_blocks;
+  f.epochs = a.epochs;
+  f.err = a.err;
+  f.cnt = nullptr;
+  f.timeout = a.timeout;
+  return f;
 }
 
 __global__ __launch_bounds__(AR_THREADS) void oneshot_allreduce_kernel(const ArArgs a) {
-  const int b = blockIdx.x, tid = threadIdx.x;
-  __shared__ int s_epoch, s_ok;
-  if (tid == 0) {
-    s_epoch = a.epochs[b] + 1;
-    s_ok = 1;
-  }
-  __syncthreads();
-  const int e = s_epoch;
-  const int parity = e & 1;
-  const long lo = (long)b * AR_ELEMS_PER_BLOCK;
-  const long i0 = lo + tid * 8;
-  const bool mine = i0 < a.n;  // n % 8 == 0 (host-checked)
-  // (3 of the previous use of this half) every peer finished reading it
-  if (tid < a.world && e > 2) {
-    if (!ar_wait_ge(ar_done(a.bufs[a.rank], a.cap, a.max_blocks, tid, b), e - 2, a.timeout)) s_ok = 0;
-  }
-  __syncthreads();
-  // (1) stage, publish
-  bf16* stage = reinterpret_cast<bf16*>(a.bufs[a.rank] + parity * a.cap);
-  if (mine) st16(stage + i0, ld16(a.in + i0));
-  __threadfence_system();
-  __syncthreads();
-  if (tid < a.world)
-    __hip_atomic_store(ar_ready(a.bufs[tid], a.cap, a.max_blocks, a.rank, b), e, __ATOMIC_RELEASE,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
-  // (2) wait for every peer's chunk, reduce
-  if (tid < a.world) {
-    if (!ar_wait_ge(ar_ready(a.bufs[a.rank], a.cap, a.max_blocks, tid, b), e, a.timeout)) s_ok = 0;
-  }
-  __syncthreads();
-  if (mine) {
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int r = 0; r < a.world; ++r) {
-      const int src = (a.rank + r) % a.world;  // stagger the peers each rank hits first
-      float x[8];
-      unpack8(load_sys16(reinterpret_cast<const bf16*>(a.bufs[src] + parity * a.cap) + i0), x);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) acc[k] += x[k];
-    }
-    st16(a.out + i0, pack8(acc));
-  }
-  __syncthreads();
-  // (3) done reading this half
-  if (tid < a.world)
-    __hip_atomic_store(ar_done(a.bufs[tid], a.cap, a.max_blocks, a.rank, b), e, __ATOMIC_RELEASE,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
-  if (tid == 0) {
-    a.epochs[b] = e;
-    if (!s_ok) atomicOr(a.err, 1);
-  }
+  ar_oneshot_chunk(ar_view(a), a.in, a.out, a.n, blockIdx.x);
 }
 
 // X4: one-shot all-gather of `nbytes` per rank (the decode step's top-k candidates, a few KB):
@@ -330,9 +271,33 @@ int mls_ar_create2(int rank, int world, long cap, long cap2, void** ctx_out) {
   c->epochs2 = cap2 ? reinterpret_cast<int*>(c->local + c->off2 + 2 * c->cap2 +
                                              (size_t)3 * AR_MAX_RANKS * c->max_blocks2 * sizeof(int))
                     : nullptr;
+  if (hipMalloc((void**)&c->fuse_cnt, (size_t)c->max_blocks * sizeof(int)) != hipSuccess ||
+      hipMemset(c->fuse_cnt, 0, (size_t)c->max_blocks * sizeof(int)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    hipFree(c->local);
+    delete c;
+    return MLS_UNSUPPORTED;
+  }
   for (int i = 0; i < AR_MAX_RANKS; ++i) c->peers[i] = nullptr;
   c->peers[rank] = c->local;
   *ctx_out = c;
+  return 0;
+}
+
+// The descriptor a GEMM needs to run the one-shot all-reduce of its own n-element output in its
+// epilogue (ar_protocol.h ar_fused_tail); MLS_BAD_ARG when n does not fit the one-shot buffer.
+int mls_ar_fuse_desc(void* ctx, long n, ArFuse* f) {
+  ArCtx* c = (ArCtx*)ctx;
+  if (!c || (!c->opened && c->world > 1) || n <= 0 || n % 8 || (size_t)n * 2 > c->cap) return MLS_BAD_ARG;
+  *f = ArFuse{};
+  for (int r = 0; r < AR_MAX_RANKS; ++r) f->bufs[r] = c->peers[r];
+  f->cap = c->cap;
+  f->rank = c->rank;
+  f->world = c->world;
+  f->max_blocks = c->max_blocks;
+  f->epochs = c->epochs;
+  f->err = c->err;
+  f->cnt = c->fuse_cnt;
+  f->timeout = 1LL << 24;
   return 0;
 }
 
@@ -439,6 +404,7 @@ int mls_ar_reset(void* ctx) {
   const size_t flags = (size_t)2 * AR_MAX_RANKS * c->max_blocks * sizeof(int);
   const size_t bytes = flags + (size_t)c->max_blocks * sizeof(int) + 64;
   if (hipMemset(c->local + 2 * c->cap, 0, bytes) != hipSuccess) return MLS_UNSUPPORTED;
+  if (c->fuse_cnt && hipMemset(c->fuse_cnt, 0, (size_t)c->max_blocks * sizeof(int)) != hipSuccess) return MLS_UNSUPPORTED;
   if (c->cap2) {
     const size_t f2 = (size_t)3 * AR_MAX_RANKS * c->max_blocks2 * sizeof(int) + (size_t)c->max_blocks2 * sizeof(int);
     if (hipMemset(c->local + c->off2 + 2 * c->cap2, 0, f2) != hipSuccess) return MLS_UNSUPPORTED;
@@ -471,6 +437,7 @@ int mls_ar_destroy(void* ctx) {
   for (int r = 0; r < c->world; ++r)
     if (r != c->rank && c->peers[r]) hipIpcCloseMemHandle(c->peers[r]);
   hipFree(c->local);
+  if (c->fuse_cnt) hipFree(c->fuse_cnt);
   delete c;
   return 0;
 }

@@ -18,6 +18,7 @@
 #include <type_traits>
 
 #include "common.h"
+#include "ar_protocol.h"
 
 namespace {
 
@@ -41,6 +42,9 @@ struct SkArgs {
   const int* lens;
   int c_nsplit, c_chunk, c_hq, c_hd;
   const float* wscale;  // fp8 weights: per-output-channel dequantisation scale [N]
+  // fused tensor-parallel all-reduce of `out` (ar_protocol.h; world == 0: none): the row-parallel
+  // decode projections reduce their partial sums across ranks in their own epilogue
+  ArFuse arf;
 };
 
 // fusion modes of the A prologue (template parameter, so the unrolled k loop has no runtime
@@ -558,6 +562,7 @@ __global__ __launch_bounds__(NWV * 64) void skinny_packed_kernel(const SkArgs s)
     if (s.res) o += (float)s.res[(size_t)m * s.N + n];
     s.out[(size_t)m * s.ldo + n] = (bf16)apply_act(o, s.act);
   }
+  if (s.arf.world) ar_fused_tail(s.arf, s.out, s.M, s.N, n0, 16);
 }
 
 // Packed weights, M <= 16 (or A too large for LDS): the A fragments (+ A2) ride beside the weight
@@ -676,7 +681,7 @@ __global__ __launch_bounds__(NWV * 64) void skinny_packed_reg_kernel(const SkArg
     float o = epi(v, n, s);
     if (s.res) o += (float)s.res[(size_t)m * s.N + n];
     s.out[(size_t)m * s.ldo + n] = (bf16)apply_act(o, s.act);
-  }
+  }  if (s.arf.world) ar_fused_tail(s.arf, s.out, s.M, s.N, n0, COLS);
 }
 
 
@@ -907,6 +912,8 @@ int g_skinny_max_split = 0;  // cap on the automatic cross-block K split (0: non
 
 extern "C" {
 
+int mls_ar_fuse_desc(void* ctx, long n, ArFuse* f);  // custom_allreduce.hip
+
 int mls_skinny_set_variant(int no_lds) {
   g_skinny_no_lds = no_lds;
   return 0;
@@ -1038,8 +1045,9 @@ int mls_skinny_pack(const void* W, void* Wp, int N, int K, void* stream) {
 // waves, non-temporal): 0 (8,8,no) 1 (8,8,nt) 2 (8,4,no) 3 (8,4,nt) 4 (16,8,no) 5 (16,8,nt)
 // 6 (16,4,no) 7 (16,4,nt) 8 (8,16,nt) 9 (4,16,nt; the measured default) 10 (4,8,nt); register
 // path only: 11 / 12 = (4,8) over 2 / 4 column tiles per block, 13 = (4,16) over 2.
-int mls_skinny_packed(const void* A, const void* A2, void* A_out, const void* Wp, const float* bias, const void* res,
-                      void* out, int M, int N, int K, int act, int norm, float eps, int variant, void* stream) {
+static int skinny_packed_impl(const void* A, const void* A2, void* A_out, const void* Wp, const float* bias,
+                              const void* res, void* out, int M, int N, int K, int act, int norm, float eps, int variant,
+                              void* stream, const ArFuse* arf) {
   if (M <= 0 || M > 32 || N % 16 || K % 32 || K <= 0) return MLS_BAD_ARG;
   if (A_out && (A_out == A || A_out == A2)) return MLS_BAD_ARG;
   if ((A2 || A_out) && !norm) return MLS_UNSUPPORTED;
@@ -1061,6 +1069,7 @@ int mls_skinny_packed(const void* A, const void* A2, void* A_out, const void* Wp
   s.a_bytes = (uint32_t)ab;
   s.w_bytes = (uint32_t)wb;
   s.nsplit = 1;
+  if (arf) s.arf = *arf;
   const int mode = A2 ? FUSE_ADD_NORM : norm ? FUSE_NORM : FUSE_NONE;
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid(N / 16);
@@ -1140,9 +1149,10 @@ int mls_skinny_packed(const void* A, const void* A2, void* A_out, const void* Wp
 // Packed-weight decode GEMM whose A operand is the split-KV decode attention's output, merged
 // from its partials in the prologue (FUSE_COMBINE; the attention launch then skips its combine
 // kernel).  M <= 4, M * K * 2 <= 64 KiB, K == Hq * D, D % 8 == 0.
-int mls_skinny_packed_combine(const void* A, const float* cws, const float* cml, const int* lens, int nsplit,
-                              int chunk, int Hq, int D, const void* Wp, const float* bias, const void* res, void* out,
-                              int M, int N, int K, int act, int variant, void* stream) {
+static int skinny_packed_combine_impl(const void* A, const float* cws, const float* cml, const int* lens, int nsplit,
+                                      int chunk, int Hq, int D, const void* Wp, const float* bias, const void* res,
+                                      void* out, int M, int N, int K, int act, int variant, void* stream,
+                                      const ArFuse* arf) {
   if (M <= 0 || M > 4 || N % 16 || K % 32 || K != Hq * D || D % 8 || nsplit <= 0 || chunk <= 0) return MLS_BAD_ARG;
   const size_t ab = (size_t)M * K * 2, wb = (size_t)N * K * 2;
   if (wb >= 0x7FFFFFFFull || ab > 65536) return MLS_UNSUPPORTED;
@@ -1165,12 +1175,53 @@ int mls_skinny_packed_combine(const void* A, const float* cws, const float* cml,
   s.c_chunk = chunk;
   s.c_hq = Hq;
   s.c_hd = D;
+  if (arf) s.arf = *arf;
   hipStream_t st = (hipStream_t)stream;
   if (variant == 1)
     hipLaunchKernelGGL((skinny_packed_kernel<8, 8, FUSE_COMBINE, 1>), dim3(N / 16), dim3(512), ab, st, s);
   else
     hipLaunchKernelGGL((skinny_packed_kernel<4, 16, FUSE_COMBINE, 1>), dim3(N / 16), dim3(1024), ab, st, s);
   return (int)hipGetLastError();
+}
+
+int mls_skinny_packed(const void* A, const void* A2, void* A_out, const void* Wp, const float* bias, const void* res,
+                      void* out, int M, int N, int K, int act, int norm, float eps, int variant, void* stream) {
+  return skinny_packed_impl(A, A2, A_out, Wp, bias, res, out, M, N, K, act, norm, eps, variant, stream, nullptr);
+}
+
+int mls_skinny_packed_combine(const void* A, const float* cws, const float* cml, const int* lens, int nsplit,
+                              int chunk, int Hq, int D, const void* Wp, const float* bias, const void* res, void* out,
+                              int M, int N, int K, int act, int variant, void* stream) {
+  return skinny_packed_combine_impl(A, cws, cml, lens, nsplit, chunk, Hq, D, Wp, bias, res, out, M, N, K, act, variant,
+                                    stream, nullptr);
+}
+
+// Row-parallel tensor-parallel projection with its all-reduce FUSED (ar_protocol.h): out = the sum
+// over the ranks of A . Wp^T, reduced in this launch through the one-shot IPC context ar_ctx
+// (custom_allreduce.hip) -- no bias / residual / activation (they would be summed world times).
+// out must be contiguous [M][N] with M * N * 2 <= the context's one-shot cap.
+static int ar_fuse_check(void* ar_ctx, const float* bias, const void* res, int act, int M, int N, ArFuse* f) {
+  if (!ar_ctx || bias || res || act != ACT_NONE) return MLS_BAD_ARG;
+  return mls_ar_fuse_desc(ar_ctx, (long)M * N, f);
+}
+
+int mls_skinny_packed_ar(const void* A, const void* A2, void* A_out, const void* Wp, const void* out_, int M, int N,
+                         int K, int norm, float eps, int variant, void* ar_ctx, void* stream) {
+  ArFuse f;
+  const int rc = ar_fuse_check(ar_ctx, nullptr, nullptr, ACT_NONE, M, N, &f);
+  if (rc) return rc;
+  return skinny_packed_impl(A, A2, A_out, Wp, nullptr, nullptr, const_cast<void*>(out_), M, N, K, ACT_NONE, norm, eps,
+                            variant, stream, &f);
+}
+
+int mls_skinny_packed_combine_ar(const void* A, const float* cws, const float* cml, const int* lens, int nsplit,
+                                 int chunk, int Hq, int D, const void* Wp, void* out, int M, int N, int K, int variant,
+                                 void* ar_ctx, void* stream) {
+  ArFuse f;
+  const int rc = ar_fuse_check(ar_ctx, nullptr, nullptr, ACT_NONE, M, N, &f);
+  if (rc) return rc;
+  return skinny_packed_combine_impl(A, cws, cml, lens, nsplit, chunk, Hq, D, Wp, nullptr, nullptr, out, M, N, K,
+                                    ACT_NONE, variant, stream, &f);
 }
 
 // FP8 (e4m3) decode GEMM (W8A8, see skinny_fp8_kernel): M <= 4, K % 64 == 0, M * K * 2 <= 64 KiB.

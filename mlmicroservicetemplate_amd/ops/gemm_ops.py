@@ -229,6 +229,28 @@ def skinny_packed(x: torch.Tensor, wp: torch.Tensor, N: int, *, delta: Optional[
     return out
 
 
+def skinny_packed_ar(x: torch.Tensor, wp: torch.Tensor, N: int, car, *, variant: int = 9,
+                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Row-parallel TP projection with its all-reduce fused into the GEMM launch: ``sum over ranks of
+    x @ W^T`` (csrc/ar_protocol.h ``ar_fused_tail``: the blocks that complete a 2048-element chunk of
+    the output run that chunk's one-shot IPC all-reduce, no separate collective kernel).  ``car``:
+    the rank's :class:`parallel.custom_ar.CustomAllReduce`; every rank must make the same call."""
+    dev = x.device
+    _need(x, "x", torch.bfloat16, dev)
+    _need(wp, "wp", torch.bfloat16, dev)
+    M, K = x.shape
+    if M > 32 or N % 16 or K % 32 or wp.numel() != N * K:
+        raise ValueError("skinny_packed_ar: M <= 32, N % 16 == 0, K % 32 == 0, wp of N*K elements")
+    if out is None:
+        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    elif tuple(out.shape) != (M, N) or out.dtype != torch.bfloat16 or not out.is_contiguous():
+        raise ValueError(f"out must be contiguous bf16 [M, {N}]")
+    rc = lib().mls_skinny_packed_ar(x.data_ptr(), None, None, wp.data_ptr(), out.data_ptr(), M, N, K, 0, 0.0,
+                                    int(variant), car.ctx_ptr(), stream_ptr(dev))
+    check(rc, "mls_skinny_packed_ar")
+    return out
+
+
 FP8_MAX = 448.0  # OCP e4m3fn
 
 

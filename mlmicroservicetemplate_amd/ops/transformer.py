@@ -235,6 +235,25 @@ def skinny_packed_combine(attn_out: torch.Tensor, parts: DecodePartials, wp: tor
     return out
 
 
+def skinny_packed_combine_ar(attn_out: torch.Tensor, parts: DecodePartials, wp: torch.Tensor, N: int, car, *,
+                             variant: int = 9) -> torch.Tensor:
+    """:func:`skinny_packed_combine` for a row-parallel TP o-projection with its all-reduce fused into
+    the same launch (csrc/ar_protocol.h): the split-KV combine in the prologue, the one-shot IPC
+    all-reduce of the output in the epilogue -- one kernel where there were three."""
+    dev = attn_out.device
+    _need(attn_out, "attn_out", torch.bfloat16, dev)
+    M, K = attn_out.shape
+    if M > 4 or K != parts.n_q_heads * parts.head_dim or wp.numel() != N * K or M * K * 2 > 65536:
+        raise ValueError("skinny_packed_combine_ar: M <= 4, K == Hq * D, M * K * 2 <= 64 KiB, wp of N*K elements")
+    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    rc = lib().mls_skinny_packed_combine_ar(attn_out.data_ptr(), parts.ws.data_ptr(), parts.ws_ml.data_ptr(),
+                                            parts.lens.data_ptr(), parts.nsplit, parts.chunk, parts.n_q_heads,
+                                            parts.head_dim, wp.data_ptr(), out.data_ptr(), M, N, K, int(variant),
+                                            car.ctx_ptr(), stream_ptr(dev))
+    check(rc, "mls_skinny_packed_combine_ar")
+    return out
+
+
 def decode_pick(cand_v: torch.Tensor, cand_i: torch.Tensor, tok: torch.Tensor, pos: torch.Tensor, lens: torch.Tensor,
                 step: torch.Tensor, *, topk: Optional[torch.Tensor] = None, temp: Optional[torch.Tensor] = None,
                 seed: Optional[torch.Tensor] = None, hist: Optional[torch.Tensor] = None,

@@ -128,6 +128,14 @@ class CustomAllReduce:
             raise RuntimeError(f"mls_ar_allreduce2 failed ({rc})")
         return out
 
+    def ctx_ptr(self) -> int:
+        """The native context (for the GEMMs that fuse this all-reduce: ops.skinny_packed_ar)."""
+        return self._ctx.value
+
+    def fusable(self, nelems: int) -> bool:
+        """May a GEMM producing ``nelems`` bf16 outputs fuse the one-shot all-reduce of them?"""
+        return self.enabled and nelems % 8 == 0 and nelems * 2 <= self.cap and nelems * 2 < self.two_shot_min
+
     def errors(self) -> int:
         """Read (and clear) the peer-wait timeout word: non-zero = some one-shot collective since the
         last read completed with a peer missing (its output is partial).  A host sync."""

@@ -67,6 +67,52 @@ def main():
         for i, b in enumerate(bufs):
             want = sum(r + 1 + i + it for r in range(world))
             fails += int(not torch.all(b.float() == want).item())
+    # GEMM-fused all-reduce (ops.skinny_packed_ar): each rank's x_r @ W_r^T summed over the ranks in
+    # the GEMM's own epilogue; interleaved with standalone one-shot calls (shared per-chunk epochs),
+    # eagerly and inside a captured graph
+    from mlmicroservicetemplate_amd import ops
+
+    gw = torch.Generator().manual_seed(100 + rank)
+    for M, N, K in ((1, 4096, 512), (3, 768, 256), (8, 4096, 1792), (4, 2048, 512)):
+        x = (torch.randn(M, K, generator=gw) * 0.5).to(torch.bfloat16)
+        w = (torch.randn(N, K, generator=gw) / K ** 0.5).to(torch.bfloat16)
+        ref = x.float() @ w.float().T
+        dist.all_reduce(ref)
+        wp = ops.pack_skinny(w.to(dev))
+        xd = x.to(dev)
+        for rep in range(2):
+            y = ops.skinny_packed_ar(xd, wp, N, car)
+            torch.cuda.synchronize()
+            err = (y.float().cpu() - ref).abs().max().item() / ref.abs().max().item()
+            fails += err > 2e-2
+            if err > 2e-2:
+                print(f"rank {rank} fused M={M} N={N} K={K} rep={rep} err={err}", flush=True)
+            z = car.all_reduce_(torch.ones(4096, device=dev, dtype=torch.bfloat16))  # standalone in between
+            torch.cuda.synchronize()
+            fails += int(not torch.all(z.float() == world).item())
+    # captured: fused GEMM + standalone one-shot in one graph, replayed
+    x = (torch.randn(2, 512, generator=gw) * 0.5).to(torch.bfloat16)
+    w = (torch.randn(4096, 512, generator=gw) / 512 ** 0.5).to(torch.bfloat16)
+    ref = x.float() @ w.float().T
+    dist.all_reduce(ref)
+    wp, xd = ops.pack_skinny(w.to(dev)), x.to(dev)
+    yo = torch.empty(2, 4096, device=dev, dtype=torch.bfloat16)
+    z = torch.empty(4096, device=dev, dtype=torch.bfloat16)
+    s3 = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s3):
+        g3 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g3, stream=s3):
+            ops.skinny_packed_ar(xd, wp, 4096, car, out=yo)
+            car.all_reduce_(z)
+    for it in range(3):
+        z.fill_(float(rank + it))
+        torch.cuda.synchronize()
+        dist.barrier()
+        g3.replay()
+        torch.cuda.synchronize()
+        err = (yo.float().cpu() - ref).abs().max().item() / ref.abs().max().item()
+        fails += err > 2e-2
+        fails += int(not torch.all(z.float() == sum(r + it for r in range(world))).item())
     fails += car._errors()
     car.close()
     dist.destroy_process_group()

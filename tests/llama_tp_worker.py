@@ -150,7 +150,7 @@ def main():
             tf.append(ci.gather(1, cv.argmax(1, keepdim=True)).squeeze(1))
             cur = cur + 1
     info = torch.tensor([int(m.use_graphs), int(m.comm.car is not None), len(m._graphs) + len(m._dev_graphs),
-                         len(calls)])
+                         len(calls), int(getattr(m, "ar_fused_calls", 0))])
     if m.comm.car is not None:
         info[1] += 10 * m.comm.car.errors()  # peer-wait timeouts would show here
     torch.save({"tokens": out.cpu(), "vals": allv.cpu(), "idx": alli.cpu(), "info": info, "failed": failed,

@@ -31,6 +31,10 @@ CASES = {
     2: (dict(layers=2, hidden=512, heads=8, kv_heads=2, head_dim=128, intermediate=1024), {"MLS_CUSTOM_AR": "0"}),
     8: (dict(layers=2, hidden=512, heads=32, kv_heads=8, head_dim=128, intermediate=2048),
         {"MLS_CUSTOM_AR": "1", "GPU_MAX_HW_QUEUES": "1"}),
+    # the same TP = 8 decode with the row-parallel projections' all-reduce as separate one-shot
+    # kernels (MLS_AR_FUSE=0) instead of fused into the GEMM epilogue
+    "8u": (dict(layers=2, hidden=512, heads=32, kv_heads=8, head_dim=128, intermediate=2048),
+           {"MLS_CUSTOM_AR": "1", "GPU_MAX_HW_QUEUES": "1", "MLS_AR_FUSE": "0"}),
     # fault injection: rank 1 stalls 300 ms with the peer-wait bound at ~a few ms -> every rank's
     # request fails with TPCommError; the next request runs on the RCCL / group fallback.  The tight
     # bound is set only for the stalled request (MLS_AR_TIMEOUT_ITERS_STALL, llama_tp_worker.py):
@@ -41,10 +45,10 @@ CASES = {
               {"MLS_CUSTOM_AR": "1", "GPU_MAX_HW_QUEUES": "1", "STALL_RANK": "1", "STALL_US": "300000",
                "MLS_AR_TIMEOUT_ITERS_STALL": "20000", "MLS_TP_OVERLAP": "0"}),
 }
-WORLD = {2: 2, 8: 8, "stall": 2}
+WORLD = {2: 2, 8: 8, "8u": 8, "stall": 2}
 
 
-@pytest.mark.parametrize("world", [2, 8, "stall"])
+@pytest.mark.parametrize("world", [2, 8, "8u", "stall"])
 def test_fused_tp_matches_tp1(tmp_path, world):
     from mlmicroservicetemplate_amd.models.llama import GenParams, LlamaTP, init_llama_shard, tiny_config
 
@@ -108,7 +112,7 @@ def test_fused_tp_matches_tp1(tmp_path, world):
             got = d["tf_top1"].to(tf_ref.dtype)
             assert sure.sum() >= sure.numel() // 2, "too few decisive steps to test anything"
             assert torch.equal(got[sure], tf_ref[sure]), (r, got, tf_ref, sure)
-        use_graphs, car, graphs, host_trips = d["info"].tolist()
+        use_graphs, car, graphs, host_trips, fused_ar = d["info"].tolist()
         if case == "stall":
             assert d["failed"] == "TPCommError", f"rank {r}: the stalled generation did not fail ({d['failed']!r})"
             assert car == 0, f"rank {r}: the IPC path must be dropped after a peer timeout"
@@ -117,6 +121,11 @@ def test_fused_tp_matches_tp1(tmp_path, world):
             assert use_graphs == 1 and graphs >= 1, f"rank {r}: decode steps were not captured ({d['info']})"
             # X4 on device: the whole decode loop is graph replays; the one host copy is the result
             assert host_trips == 1, f"rank {r}: {host_trips} host round trips in generate()"
+            # the row-parallel o / down projections ran with their all-reduce fused in the GEMM
+            if extra_env.get("MLS_AR_FUSE") == "0":
+                assert fused_ar == 0, f"rank {r}: MLS_AR_FUSE=0 still fused"
+            else:
+                assert fused_ar > 0, f"rank {r}: the GEMM-fused all-reduce never ran"
 
 
 SERVE_CASES = {
