@@ -41,7 +41,7 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def build_model(backend: str, device, batch: int, params):
+def build_model(backend: str, device, batch: int, params, serial: bool = False):
     import torch
 
     from mlmicroservicetemplate_amd.models import resnet
@@ -49,7 +49,9 @@ def build_model(backend: str, device, batch: int, params):
     if backend == "fused":
         from mlmicroservicetemplate_amd.ops import autotune
 
-        tuning = autotune.load_tuning("resnet50", batch)
+        # per-layer kernels measured for the regime the engine runs in: 4 co-running batches
+        # (default) or one batch alone (--serial)
+        tuning = autotune.load_tuning("resnet50", batch, regime="serial" if serial else "concurrent")
         model = resnet.ResNet50Fused(params, device, max_batch=batch, tuning=tuning)
 
         def fwd(x):
@@ -145,7 +147,7 @@ def run_rank(args) -> int:
         torch.cuda.synchronize(device)  # X1 done before any graph capture starts
     t_bcast = time.perf_counter() - t0
 
-    fwd = build_model(args.backend, device, args.batch, params)
+    fwd = build_model(args.backend, device, args.batch, params, serial=args.serial)
     if args.cu_partition and not args.serial:
         from mlmicroservicetemplate_amd import ops
 

@@ -244,16 +244,24 @@ def cache_path(batch: int) -> str:
 SHIPPED_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned")
 
 
-def load_tuning(model: str, batch: int, arch: str = "gfx950") -> Dict[str, Tuple[int, int]]:
+def load_tuning(model: str, batch: int, arch: str = "gfx950", regime: str = "concurrent") -> Dict[str, Tuple[int, int]]:
     """Shipped (measured on MI355X, committed) or cached tuning table; {} -> C++ heuristic.
-    ``MLS_TUNING_FILE`` overrides both (A/B runs of alternative tables)."""
+    ``regime``: "concurrent" -- the table measured under 4 co-running copies (the partitioned
+    serving engine, the throughput bench); "serial" -- one batch alone on the chip (a one-slot engine,
+    ``bench.py --serial``): ``<model>_<arch>_b<batch>_serial.json`` where shipped, where the
+    pipelined 3x3 kernel wins every stride-1 3x3 (ResNet-50 serial forward 905-935 -> 815-820 us,
+    ``profiles/r4_resnet50_serial_kernel_summary_*.txt``), else the concurrent table.
+    ``MLS_TUNING_FILE`` overrides all (A/B runs of alternative tables)."""
     override = os.environ.get("MLS_TUNING_FILE")
     if override:
         with open(override) as f:
             data = json.load(f)
         return {k: (v["best_cfg"], v["best_splitk"]) for k, v in data.items()}
-    for d in (SHIPPED_DIR, CACHE_DIR):
-        path = os.path.join(d, f"{model}_{arch}_b{batch}.json")
+    names = [f"{model}_{arch}_b{batch}.json"]
+    if regime == "serial":
+        names.insert(0, f"{model}_{arch}_b{batch}_serial.json")
+    for d, name in ((d, n) for n in names for d in (SHIPPED_DIR, CACHE_DIR)):
+        path = os.path.join(d, name)
         if os.path.exists(path):
             with open(path) as f:
                 data = json.load(f)

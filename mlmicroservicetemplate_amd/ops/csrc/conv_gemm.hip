@@ -494,24 +494,37 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_kernel(const ConvArgs 
       st16(a.out + (size_t)m * a.ldo + n, pack8(v));
     }
     if (a.pool && a.splitk == 1) {
-      // global average pool: a thread per column walks the pass's rows, one atomic per image segment
+      // global average pool: a thread per column walks the pass's rows in order (a fixed summation
+      // order per image segment: with <= 2 segments per image per column the fp32 atomics commute,
+      // so the pooled sums are bit-identical run to run), one atomic per image segment.  The LDS
+      // reads are issued 8 at a time and the image boundary is tracked instead of divided per row
+      // (the plain per-row walk cost the last conv 3-6 us: profiles/r4_resnet50_serial_head_ab.txt).
       __syncthreads();
       const int n = n0 + tid;
-      if (tid < BN && n < a.N) {
+      const int rows = min(PASS_ROWS, a.M - (m0 + row_lo));
+      if (tid < BN && n < a.N && rows > 0) {
+        int cur = (m0 + row_lo) / a.pool_hw;
+        int next = (cur + 1) * a.pool_hw - (m0 + row_lo);  // first pass row of the next image
         float sum = 0.f;
-        int cur = -1;
-        for (int r = 0; r < PASS_ROWS; ++r) {
-          const int m = m0 + row_lo + r;
-          if (m >= a.M) break;
-          const int b = m / a.pool_hw;
-          if (b != cur) {
-            if (cur >= 0) atomicAdd(a.pool + (size_t)cur * a.N + n, sum * a.pool_scale);
-            sum = 0.f;
-            cur = b;
+        for (int r0 = 0; r0 < rows; r0 += 8) {
+          float x[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) x[j] = Cs[min(r0 + j, PASS_ROWS - 1) * C_LD + tid];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int r = r0 + j;
+            if (r < rows) {
+              if (r == next) {
+                atomicAdd(a.pool + (size_t)cur * a.N + n, sum * a.pool_scale);
+                sum = 0.f;
+                ++cur;
+                next += a.pool_hw;
+              }
+              sum += x[j];
+            }
           }
-          sum += Cs[r * C_LD + tid];
         }
-        if (cur >= 0) atomicAdd(a.pool + (size_t)cur * a.N + n, sum * a.pool_scale);
+        atomicAdd(a.pool + (size_t)cur * a.N + n, sum * a.pool_scale);
       }
     }
   }

@@ -6,12 +6,12 @@
 // to HBM nor read back, and avgpool / FC / softmax-top-k stop being three launches (~31 us serial,
 // round 3's profiles/r3_resnet50_b32_serial_kernel_summary_final.txt).
 //
-// Grid (ceil(N / 16) class groups) x (ceil(B / 16) row groups), 4 waves.  A block computes the
-// 16 x 16 logit tile of its classes x rows on MFMA (D = W_tile . pooled^T, K split over the waves,
+// Grid (ceil(N / 16) class groups) x (ceil(B / 4) row groups), 8 waves.  A block computes the
+// 16-class x 4-row logit tile of its classes x rows on MFMA (D = W_tile . pooled^T, K split over the waves,
 // pooled converted to bf16 on load -- the precision of the unfused bf16 GEMM), reduces the waves
 // through LDS, adds the bias and writes the tile through (sc1) to `logits`.  One ticket per row
 // group: the block that completes a row group (the last of its class groups) runs softmax + top-k
-// for those rows from the written-through logits (sc1 loads, no acquire: guide §6 Guideline 16 R1)
+// for those rows (one row per wave) from the written-through logits (sc1 loads, no acquire: guide §6 Guideline 16 R1)
 // and zeroes the rows' pooled sums for the next launch (the convolution accumulates into them).
 // Counters are this stream's self-resetting split-K counters (conv_gemm.hip).
 #include "common.h"
@@ -38,52 +38,111 @@ struct HeadArgs {
 
 typedef unsigned int head_u32x4 __attribute__((__vector_size__(16)));
 
-__global__ __launch_bounds__(256) void fc_head_kernel(const HeadArgs a) {
-  __shared__ float red[4][HT][HT + 1];
+constexpr int HW = 8;   // waves per block
+constexpr int HR = 4;   // rows per row group: the finisher of a group runs one row per wave, so its
+                        // latency is one write-through load round trip + one top-k, not 16 rows' worth
+
+// softmax + top-k of one row (a whole wave): the row's logits are loaded in one round trip, each
+// lane keeps its MAXV candidates, and k rounds of wave arg-max pick the winners
+template <int MAXV>
+MLS_DEV void head_finish_row(const HeadArgs& a, const rsrc_t& lr, int row, int lane) {
+  float v[MAXV];
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {  // unconditional loads (OOB offset), masked after (see below)
+    const int c = lane + 64 * j;
+    const bool ok = c < a.N;
+    const float x = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(lr, ok ? (row * a.N + c) * 4 : OOB, 0, 16));
+    v[j] = ok ? x : -INFINITY;
+  }
+  float m = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) m = fmaxf(m, v[j]);
+  m = wave_max(m);
+  float s = 0.f;
+  if (a.softmax) {
+#pragma unroll
+    for (int j = 0; j < MAXV; ++j) s += v[j] == -INFINITY ? 0.f : __expf(v[j] - m);
+    s = wave_sum(s);
+  }
+  const bool bad = a.err && a.err[row] != 0;
+  for (int t = 0; t < a.k; ++t) {
+    float bv = -INFINITY;
+    int bj = 0;
+#pragma unroll
+    for (int j = 0; j < MAXV; ++j)
+      if (v[j] > bv) {
+        bv = v[j];
+        bj = j;
+      }
+    int bc = bv == -INFINITY ? 0x7fffffff : lane + 64 * bj;
+    // wave arg-max: larger value wins, ties to the smaller class id
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o, 64);
+      const int oc = __shfl_xor(bc, o, 64);
+      if (ov > bv || (ov == bv && oc < bc)) {
+        bv = ov;
+        bc = oc;
+      }
+    }
+    if (lane == (bc & 63)) {  // the owner removes the winner from its candidates
+#pragma unroll
+      for (int j = 0; j < MAXV; ++j)
+        if (lane + 64 * j == bc) v[j] = -INFINITY;
+    }
+    if (lane == 0) {
+      const float p = a.softmax ? __expf(bv - m) / s : bv;
+      a.vals[row * a.k + t] = bad ? __builtin_nanf("") : p;
+      a.idx[row * a.k + t] = bad ? -1 : (bc < a.N ? bc : -1);
+    }
+  }
+}
+
+__global__ __launch_bounds__(HW * 64) void fc_head_kernel(const HeadArgs a) {
+  __shared__ float red[HW][HT][HT + 1];
   __shared__ int flag;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fq = lane >> 4;
-  const int c0 = blockIdx.x * HT, r0 = blockIdx.y * HT;
+  const int c0 = blockIdx.x * HT, r0 = blockIdx.y * HR;
   const rsrc_t wr = make_rsrc(a.w, a.w_bytes);
   const rsrc_t pr = make_rsrc(a.pooled, a.pooled_bytes);
   const rsrc_t lr = make_rsrc(a.logits, a.logits_bytes);
 
-  // ---- 16 x 16 logit tile: wave w sums k in [w * K/4, (w + 1) * K/4) ----
-  const int kw = a.K / 4;  // host: K % 128 == 0
+  // ---- 16 classes x HR rows (a 16 x 16 MFMA tile, rows past HR read as zero): wave w sums k in
+  //      [w * K/8, (w + 1) * K/8), every load of its range issued before the first MFMA ----
+  const int kw = a.K / HW;  // host: K % 256 == 0, K <= 2048
   const int kb = wid * kw;
   const int cl = c0 + fr, rw = r0 + fr;
   const int woff = cl < a.N ? (cl * a.K + kb + fq * 8) * 2 : OOB;
-  const int poff = rw < a.B ? (rw * a.K + kb + fq * 8) * 4 : OOB;
+  const int poff = fr < HR && rw < a.B ? (rw * a.K + kb + fq * 8) * 4 : OOB;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int k0 = 0; k0 < kw; k0 += 128) {  // 4 k-steps of 32 per trip: 4 x (16 B + 32 B) in flight per lane
-    uint4 wv[4];
-    float4 pv[4][2];
+  uint4 wv[8];
+  float4 pv[8][2];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      wv[s] = bload16(wr, woff == OOB ? OOB : woff + (k0 + 32 * s) * 2);
-      pv[s][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(pr, poff == OOB ? OOB : poff + (k0 + 32 * s) * 4, 0, 0));
-      pv[s][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(pr, poff == OOB ? OOB : poff + (k0 + 32 * s) * 4 + 16, 0, 0));
-    }
+  for (int s = 0; s < 8; ++s) {
+    const bool in = 32 * s < kw;
+    wv[s] = bload16(wr, woff == OOB || !in ? OOB : woff + 32 * s * 2);
+    pv[s][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(pr, poff == OOB || !in ? OOB : poff + 32 * s * 4, 0, 0));
+    pv[s][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(pr, poff == OOB || !in ? OOB : poff + 32 * s * 4 + 16, 0, 0));
+  }
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      bf16x8 b;
-      b[0] = (bf16)pv[s][0].x; b[1] = (bf16)pv[s][0].y; b[2] = (bf16)pv[s][0].z; b[3] = (bf16)pv[s][0].w;
-      b[4] = (bf16)pv[s][1].x; b[5] = (bf16)pv[s][1].y; b[6] = (bf16)pv[s][1].z; b[7] = (bf16)pv[s][1].w;
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wv[s]), b, acc, 0, 0, 0);
-    }
+  for (int s = 0; s < 8; ++s) {
+    bf16x8 b;
+    b[0] = (bf16)pv[s][0].x; b[1] = (bf16)pv[s][0].y; b[2] = (bf16)pv[s][0].z; b[3] = (bf16)pv[s][0].w;
+    b[4] = (bf16)pv[s][1].x; b[5] = (bf16)pv[s][1].y; b[6] = (bf16)pv[s][1].z; b[7] = (bf16)pv[s][1].w;
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wv[s]), b, acc, 0, 0, 0);
   }
   // D[class fq*4 + i][row fr]
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const float v = acc[i];
-    red[wid][fq * 4 + i][fr] = v;
-  }
+  for (int i = 0; i < 4; ++i) red[wid][fq * 4 + i][fr] = acc[i];
   __syncthreads();
-  {
-    const int c = tid >> 4, r = tid & 15;
+  if (tid < HT * HR) {
+    const int c = tid / HR, r = tid % HR;
     const int cg = c0 + c, rg = r0 + r;
-    const float v = red[0][c][r] + red[1][c][r] + red[2][c][r] + red[3][c][r] + (a.bias && cg < a.N ? a.bias[cg] : 0.f);
+    float v = a.bias && cg < a.N ? a.bias[cg] : 0.f;
+#pragma unroll
+    for (int w = 0; w < HW; ++w) v += red[w][c][r];
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), lr, cg < a.N && rg < a.B ? (rg * a.N + cg) * 4 : OOB, 0, 16);
   }
   // publish: every wave's write-through stores drained, then one ticket for this row group
@@ -99,69 +158,21 @@ __global__ __launch_bounds__(256) void fc_head_kernel(const HeadArgs a) {
   __syncthreads();
   if (!flag) return;
 
-  // ---- the row group's finisher: softmax + top-k per row (wave w: rows r0 + 4w .. 4w + 3) ----
-  if (a.k > 0) {
-    const int nv = (a.N + 63) / 64;
-    for (int i = 0; i < 4; ++i) {
-      const int row = r0 + wid * 4 + i;
-      if (row >= a.B) break;  // wave-uniform
-      float v[MAXV];
-#pragma unroll
-      for (int j = 0; j < MAXV; ++j) {
-        const int c = lane + 64 * j;
-        v[j] = j < nv && c < a.N ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(lr, (row * a.N + c) * 4, 0, 16))
-                                 : -INFINITY;
-      }
-      float m = -INFINITY;
-#pragma unroll
-      for (int j = 0; j < MAXV; ++j) m = fmaxf(m, v[j]);
-      m = wave_max(m);
-      float s = 0.f;
-      if (a.softmax) {
-#pragma unroll
-        for (int j = 0; j < MAXV; ++j) s += v[j] == -INFINITY ? 0.f : __expf(v[j] - m);
-        s = wave_sum(s);
-      }
-      const bool bad = a.err && a.err[row] != 0;
-      for (int t = 0; t < a.k; ++t) {
-        float bv = -INFINITY;
-        int bj = 0;
-#pragma unroll
-        for (int j = 0; j < MAXV; ++j)
-          if (v[j] > bv) {
-            bv = v[j];
-            bj = j;
-          }
-        int bc = bv == -INFINITY ? 0x7fffffff : lane + 64 * bj;
-        // wave arg-max: larger value wins, ties to the smaller class id
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-          const float ov = __shfl_xor(bv, o, 64);
-          const int oc = __shfl_xor(bc, o, 64);
-          if (ov > bv || (ov == bv && oc < bc)) {
-            bv = ov;
-            bc = oc;
-          }
-        }
-        if (lane == (bc & 63)) {  // the owner removes the winner from its candidates
-#pragma unroll
-          for (int j = 0; j < MAXV; ++j)
-            if (lane + 64 * j == bc) v[j] = -INFINITY;
-        }
-        if (lane == 0) {
-          const float p = a.softmax ? __expf(bv - m) / s : bv;
-          a.vals[row * a.k + t] = bad ? __builtin_nanf("") : p;
-          a.idx[row * a.k + t] = bad ? -1 : (bc < a.N ? bc : -1);
-        }
-      }
-    }
+  // ---- the row group's finisher: wave w < HR takes row r0 + w.  Every logit load is issued
+  //      unconditionally (out-of-range columns read the OOB offset and are masked to -inf after
+  //      the load): a load behind a per-element condition makes hipcc branch around it and wait
+  //      vmcnt(0) per element -- dependent write-through round trips, ~30 us per group measured ----
+  const int row = r0 + wid;
+  if (a.k > 0 && wid < HR && row < a.B) {
+    if (a.N <= 1024) head_finish_row<16>(a, lr, row, lane);
+    else head_finish_row<MAXV>(a, lr, row, lane);
   }
   // zero the row group's pooled sums for the next launch (every class group has read them: they
   // arrived before this ticket)
-  const int nrows = min(HT, a.B - r0);
+  const int nrows = min(HR, a.B - r0);
   const int n4 = nrows * (a.K / 4);
   float4* pz = reinterpret_cast<float4*>(const_cast<float*>(a.pooled) + (long)r0 * a.K);
-  for (int i = tid; i < n4; i += 256) pz[i] = float4{0.f, 0.f, 0.f, 0.f};
+  for (int i = tid; i < n4; i += HW * 64) pz[i] = float4{0.f, 0.f, 0.f, 0.f};
 }
 
 }  // namespace
@@ -170,14 +181,14 @@ extern "C" {
 
 // pooled [B][K] fp32 (averages, zeroed on return), w [N][K] bf16, bias [N] fp32 or null ->
 // logits [B][N] fp32 (caller's scratch or output) and, for k > 0, vals / idx [B][k] of the
-// (softmax of the) logits' top-k.  err [B] int32 or null.  K % 128 == 0, N <= 2048, k <= 64.
+// (softmax of the) logits' top-k.  err [B] int32 or null.  K % 256 == 0, K <= 2048, N <= 2048, k <= 64.
 int mls_fc_head(const float* pooled, const void* w, const float* bias, float* logits, float* vals, int* idx,
                 const int* err, int B, int N, int K, int k, int softmax, void* stream) {
-  if (B <= 0 || N <= 0 || N > 64 * MAXV || K <= 0 || K % 128 || k < 0 || k > 64 || k > N) return MLS_BAD_ARG;
+  if (B <= 0 || N <= 0 || N > 64 * MAXV || K <= 0 || K % 256 || K > 2048 || k < 0 || k > 64 || k > N) return MLS_BAD_ARG;
   if (k > 0 && (!vals || !idx)) return MLS_BAD_ARG;
   const long pb = (long)B * K * 4, wb = (long)N * K * 2, lb = (long)B * N * 4;
   if (pb >= 0x7fffffffL || wb >= 0x7fffffffL || lb >= 0x7fffffffL) return MLS_UNSUPPORTED;
-  const int nrg = (B + HT - 1) / HT;
+  const int nrg = (B + HR - 1) / HR;
   int* cnt = mls_stream_splitk_counters(stream, nrg);
   if (!cnt) return MLS_UNSUPPORTED;  // counters must exist before graph capture (eager warm-up)
   HeadArgs a;
@@ -193,7 +204,7 @@ int mls_fc_head(const float* pooled, const void* w, const float* bias, float* lo
   a.pooled_bytes = (uint32_t)pb;
   a.w_bytes = (uint32_t)wb;
   a.logits_bytes = (uint32_t)lb;
-  hipLaunchKernelGGL(fc_head_kernel, dim3((N + HT - 1) / HT, nrg), dim3(256), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(fc_head_kernel, dim3((N + HT - 1) / HT, nrg), dim3(HW * 64), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
 

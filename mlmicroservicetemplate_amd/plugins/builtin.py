@@ -152,7 +152,8 @@ class ResNet50Plugin(ModelPlugin):
         buckets = [b for b in s.GRAPH_BUCKETS if b <= s.MAX_BATCH]
         shape = (IMAGE_CONTAINER_BYTES,) if self.containers else (224, 224, 3)
         for dev in devices:
-            fwd = self._build_forward(s.BACKEND, dev, max(buckets), params)
+            serial = not bool(s.CONCURRENT_SLOTS) or int(s.INFLIGHT) <= 1
+            fwd = self._build_forward(s.BACKEND, dev, max(buckets), params, serial=serial)
             if self.containers:
                 from .. import ops
 
@@ -212,7 +213,7 @@ class ResNet50Plugin(ModelPlugin):
         logger.info("auto batch: %d (bound by %s; %.1f MB/image, %.4f ms/image, %.1f GB free)", plan.max_batch,
                     plan.limit, plan.per_sample_bytes / 1e6, plan.per_sample_ms, plan.free_bytes / 1e9)
 
-    def _build_forward(self, backend: str, dev: str, max_batch: int, params):
+    def _build_forward(self, backend: str, dev: str, max_batch: int, params, serial: bool = False):
         import torch
 
         from ..models import resnet
@@ -221,7 +222,7 @@ class ResNet50Plugin(ModelPlugin):
         if backend == "fused":
             from ..ops import autotune
 
-            tuning = autotune.load_tuning("resnet50", max_batch)
+            tuning = autotune.load_tuning("resnet50", max_batch, regime="serial" if serial else "concurrent")
             model = resnet.ResNet50Fused(params, dev, max_batch=max_batch, tuning=tuning)
             self.models.append(model)
             return lambda x: model.classify(x, k)

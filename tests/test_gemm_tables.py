@@ -49,3 +49,18 @@ def test_prefill_row_ranges_route_without_exact_entries(caplog):
             assert ops.tile_route_for(m, n, k)[0] == "blas"
     assert not [r for r in caplog.records if "not in" in r.getMessage()]
     assert ops.tile_route_for(700, 6144, 4096) == ("tile", 0, 1)  # below the range, no exact entry
+
+
+def test_resnet_tuning_regimes():
+    """ResNet-50 per-layer kernel tables per regime: the serial table (one batch alone) takes the
+    pipelined 3x3 kernel on every stride-1 3x3; the concurrent one (4 co-running batches) keeps the
+    halo kernel on layers 1-3; batches without a serial table fall back to the concurrent one."""
+    from mlmicroservicetemplate_amd.ops import autotune
+
+    conc = autotune.load_tuning("resnet50", 32)
+    ser = autotune.load_tuning("resnet50", 32, regime="serial")
+    assert ser["layer1.1.conv2"][0] >= ops.CFG_PIPE and ser["layer3.1.conv2"][0] >= ops.CFG_PIPE
+    assert conc["layer1.1.conv2"][0] < ops.CFG_PIPE
+    assert conc["layer4.1.conv2"][0] >= ops.CFG_PIPE
+    assert set(ser) == set(conc)
+    assert autotune.load_tuning("resnet50", 8, regime="serial") == autotune.load_tuning("resnet50", 8)

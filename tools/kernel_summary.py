@@ -58,10 +58,17 @@ def main():
     ap.add_argument("--window", type=int, default=0, help="only the last N kernels")
     ap.add_argument("--per", type=float, default=1.0, help="divide totals by this many steps")
     ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--last-of", default="", help="start at the --per-th last launch of a kernel whose name "
+                                                   "contains this (e.g. the first kernel of a forward)")
     a = ap.parse_args()
     rows = load(a.path)
     if a.window:
         rows = rows[-a.window:]
+    if a.last_of:
+        starts = [i for i, (_s, _e, n) in enumerate(rows) if a.last_of in n]
+        if len(starts) < int(a.per):
+            raise SystemExit(f"only {len(starts)} launches of {a.last_of!r}")
+        rows = rows[starts[-int(a.per)]:]
     agg = collections.defaultdict(lambda: [0.0, 0])
     for s, e, n in rows:
         agg[short(n)][0] += (e - s) / 1e3

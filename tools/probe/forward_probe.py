@@ -18,12 +18,25 @@ def main():
     batch = int(os.environ.get("BATCH", 32))
     iters = int(os.environ.get("ITERS", 3))
     dev = torch.device("cuda:0")
-    model = ResNet50Fused(init_resnet50(0), dev, max_batch=batch, tuning=autotune.load_tuning("resnet50", batch))
+    model = ResNet50Fused(init_resnet50(0), dev, max_batch=batch, tuning=autotune.load_tuning("resnet50", batch, regime=os.environ.get("REGIME", "concurrent")))
     x = torch.randint(0, 256, (batch, 224, 224, 3), dtype=torch.uint8, device=dev)
     with torch.no_grad():
-        for _ in range(iters):
-            model.classify(x, 5)
+        if os.environ.get("GRAPH") == "1":  # back-to-back replays of the captured forward: serial latency
+            s = torch.cuda.Stream(dev)
+            with torch.cuda.stream(s):  # eager warm-up on the capture stream (per-stream counters)
+                model.classify(x, 5)
             torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(s), torch.cuda.graph(g, stream=s):
+                model.classify(x, 5)
+            torch.cuda.synchronize()
+            for _ in range(iters):
+                g.replay()
+            torch.cuda.synchronize()
+        else:
+            for _ in range(iters):
+                model.classify(x, 5)
+                torch.cuda.synchronize()
     print("forwards", iters, flush=True)
 
 
