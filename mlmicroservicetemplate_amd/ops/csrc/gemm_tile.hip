@@ -832,9 +832,8 @@ struct GtCfg {
 //  10: 256x256 ring (gemm_ring_kernel), 5 x 32, 160 KB      11: 256x256 ring, 4 x 32, 128 KB
 //  12: 256x128 ring, 6 x 32, 144 KB
 //  21: 192x192, 8 waves 4x2, 3 x 64, 144 KB (a 3-deep ring at ~the 256^2 tile's reuse)   22: + PIPE
-//  23: 256x256, 4 waves 2x2 (ONE wave per SIMD, 128x128 wave tile, 256 accumulators), 2 x 64,
-//      128 KB, PIPE: no second wave on the SIMD to contend for the MFMA pipe after each barrier
-//  24: as 23 without the fragment pipeline
+//  (a 4-wave 256x256 tile -- one wave per SIMD, 128x128 wave tile, 256 accumulators -- spills
+//   101-138 VGPRs in the k-loop under hipcc 7.2; not kept: docs/PERF_NOTES.md Round 4)
 GtCfg gt_cfg(int cfg) {
   switch (cfg) {
     case 1: return {256, 256, 512};
@@ -859,8 +858,6 @@ GtCfg gt_cfg(int cfg) {
     case 20: return {256, 256, 512};
     case 21: return {192, 192, 512};
     case 22: return {192, 192, 512};
-    case 23: return {256, 256, 256};
-    case 24: return {256, 256, 256};
     default: return {0, 0, 0};
   }
 }
@@ -917,8 +914,6 @@ int gt_launch(const GemmTileArgs& g0, int cfg, int grid_cap, hipStream_t st) {
     case 20: hipLaunchKernelGGL((gemm_tile_kernel<256, 256, 2, 4, 2, 64, true, false, true>), grid, block, 0, st, g); break;
     case 21: hipLaunchKernelGGL((gemm_tile_kernel<192, 192, 4, 2, 3, 64>), grid, block, 0, st, g); break;
     case 22: hipLaunchKernelGGL((gemm_tile_kernel<192, 192, 4, 2, 3, 64, false, true>), grid, block, 0, st, g); break;
-    case 23: hipLaunchKernelGGL((gemm_tile_kernel<256, 256, 2, 2, 2, 64, false, true>), grid, block, 0, st, g); break;
-    case 24: hipLaunchKernelGGL((gemm_tile_kernel<256, 256, 2, 2, 2, 64, false, true, true>), grid, block, 0, st, g); break;
   }
   return hipGetLastError() == hipSuccess ? MLS_OK : MLS_BAD_ARG;
 }
