@@ -60,6 +60,7 @@ class _Slot:
     outs: Dict[int, Tuple[torch.Tensor, ...]] = field(default_factory=dict)  # bucket -> device outputs
     host_out: Dict[int, Tuple[torch.Tensor, ...]] = field(default_factory=dict)  # bucket -> pinned outputs
     graphs: Dict[int, torch.cuda.CUDAGraph] = field(default_factory=dict)
+    graph_copies: Dict[int, bool] = field(default_factory=dict)  # bucket -> copies inside the graph
     s_comp: Optional[torch.cuda.Stream] = None  # this slot's compute stream (concurrent mode)
     pool: Optional[tuple] = None  # this slot's graph memory pool (concurrent mode)
     ev_h2d: Optional[torch.cuda.Event] = None
@@ -154,6 +155,8 @@ class GpuEngine:
         if copies_on_slot_stream is None:
             copies_on_slot_stream = os.environ.get("MLS_SLOT_COPIES", "1") == "1"
         self.copies_on_slot_stream = bool(copies_on_slot_stream) and self.concurrent
+        self.graph_copies = (self.copies_on_slot_stream and use_graphs
+                             and os.environ.get("MLS_GRAPH_COPIES", "0") == "1")
         # host staging (request arrays -> pinned slot): a persistent native copy pool (GIL released,
         # the submitting thread copies too); one thread's ~5-8 GB/s memcpy is not enough for a
         # 4.8 MB ResNet batch every ~0.6 ms next to the rest of the host loop
@@ -233,14 +236,26 @@ class GpuEngine:
                 for slot in self.slots:
                     for b in self.buckets:
                         g = torch.cuda.CUDAGraph()
+                        # MLS_GRAPH_COPIES=1: the slot's H2D and D2H copies ride inside its graph
+                        # (memcpy nodes from / to its pinned buffers): one replay call per batch,
+                        # 81 -> 45 us of host enqueue -- but the in-graph copies run slower than the
+                        # stream copies (one batch alone +45 us) and the 20-step bench drops
+                        # 48.3-48.6k -> 45.1-45.5k (profiles/r4_engine_graph_copies_ab.jsonl): off
+                        in_graph = self.graph_copies
                         # thread_local: the RCCL watchdog thread (DP ranks keep a process group for
                         # X1 / X6) queries its events concurrently; under the default global mode
                         # that query is an illegal call during capture and aborts the process
                         with torch.cuda.graph(g, pool=slot.pool, stream=slot.s_comp,
                                               capture_error_mode="thread_local"):
+                            if in_graph:
+                                slot.dev_in[:b].copy_(slot.host_in[:b], non_blocking=True)
                             outs = self.forward(slot.dev_in[:b])
+                            if in_graph:
+                                for h, d in zip(slot.host_out[b], outs):
+                                    h.copy_(d, non_blocking=True)
                         slot.graphs[b] = g
                         slot.outs[b] = tuple(outs)
+                        slot.graph_copies[b] = in_graph
                 torch.cuda.synchronize(self.device)
                 logger.info("%s: captured %d hipGraphs (%d slots x buckets %s)", self.name,
                             len(self.slots) * len(self.buckets), len(self.slots), self.buckets)
@@ -319,6 +334,12 @@ class GpuEngine:
             bucket = pick_bucket(n, self.buckets)
             with self._enqueue_lock, torch.cuda.device(self.device):
                 self._pace_launch()
+                if self.use_graphs and slot.graph_copies.get(bucket):
+                    # H2D -> forward -> D2H in one replay on the slot stream
+                    with tracing.range(self._tr_replay), torch.cuda.stream(slot.s_comp):
+                        slot.graphs[bucket].replay()
+                        slot.ev_done.record(slot.s_comp)
+                    return Ticket(self, slot, bucket, n)
                 s_h2d = slot.s_comp if self.copies_on_slot_stream else self.s_h2d
                 s_d2h = slot.s_comp if self.copies_on_slot_stream else self.s_d2h
                 with tracing.range(self._tr_h2d), torch.cuda.stream(s_h2d):

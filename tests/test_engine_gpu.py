@@ -1,5 +1,7 @@
 """GpuEngine on MI355X: concurrent in-flight slots (per-slot streams + graph pools, per-stream
 split-K workspace) must give exactly the results of one-at-a-time execution."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -104,8 +106,27 @@ def test_engine_roctx_ranges():
     finally:
         tracing.set_enabled(False)
     assert s.tolist() == [32.0] * 3
+    assert not eng.graph_copies  # default: the copies are stream operations with their own ranges
     for k in ("stage", "h2d", "replay", "d2h", "d2h_wait"):
         assert f"tr.{k}" in names, (k, names)
+    # MLS_GRAPH_COPIES=1: H2D -> forward -> D2H is one replay
+    os.environ["MLS_GRAPH_COPIES"] = "1"
+    try:
+        eng2 = GpuEngine(lambda x: (x.float().sum(dim=1),), DEV, (16,), torch.uint8, buckets=[4], inflight=2,
+                         concurrent=True, name="tr2")
+    finally:
+        del os.environ["MLS_GRAPH_COPIES"]
+    eng2.warmup(capture=True)
+    tracing.set_enabled(True)
+    try:
+        with tracing.record() as names2:
+            (s2,) = eng2.run([np.full(16, 3, np.uint8)] * 3)
+    finally:
+        tracing.set_enabled(False)
+    assert s2.tolist() == [48.0] * 3 and eng2.graph_copies and eng2.slots[0].graph_copies[4]
+    for k in ("stage", "replay", "d2h_wait"):
+        assert f"tr2.{k}" in names2, (k, names2)
+    assert "tr2.h2d" not in names2
 
 
 def test_cu_partition_masks_select_disjoint_halves():
