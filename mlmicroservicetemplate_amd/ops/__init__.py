@@ -105,6 +105,7 @@ from .transformer import (  # noqa: F401
     decode_attention,
     decode_pick,
     embed_layernorm,
+    embed_layernorm_packed,
     embedding,
     flash_attention,
     kv_append,

@@ -61,6 +61,7 @@ _SIGS = {
     "mls_topk_chunks": [P, P, P, I, I, I, I, I, P],
     "mls_layernorm": [P, P, P, P, P, P, L, I, F, I, P],
     "mls_embed_ln": [P, P, P, P, P, P, P, P, L, I, I, I, F, P],
+    "mls_embed_ln2": [P, P, I, P, P, P, P, P, P, P, P, L, I, I, I, F, P],
     "mls_embedding": [P, P, P, L, I, I, I, P],
     "mls_rope": [P, P, P, P, L, I, I, I, P],
     "mls_ar_create": [I, I, L, P],

@@ -158,17 +158,25 @@ __global__ __launch_bounds__(256) void layernorm_rowblock_kernel(const bf16* __r
 
 // BERT embeddings: out[t] = LN(word[id] + pos[t % S] + type[tt]) ; one wave per token
 template <int CPL>
+// ids / type_ids: token t of sequence t / S at (t / S) * id_stride + t % S -- contiguous [B][S] with
+// id_stride == S, or read in place from the engine's packed request rows [ids | type ids | len]
+// (id_stride = 2S + 1): no unpacking copies.  lens_src / lens_out (optional): sequence b's length at
+// lens_src[b * id_stride] copied to lens_out[b] (contiguous, for the attention kernel).
 __global__ __launch_bounds__(256) void embed_ln_kernel(const int* __restrict__ ids, const int* __restrict__ type_ids,
                                                        const bf16* __restrict__ word, const bf16* __restrict__ pos,
                                                        const bf16* __restrict__ typ, const bf16* __restrict__ gamma,
                                                        const bf16* __restrict__ beta, bf16* __restrict__ out,
-                                                       long rows, int S, int D, int vocab, float eps) {
+                                                       long rows, int S, int D, int vocab, float eps, int id_stride,
+                                                       const int* __restrict__ lens_src, int* __restrict__ lens_out) {
   const int lane = threadIdx.x & 63;
   const long t = (long)blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
   if (t >= rows) return;
-  int id = ids[t];
+  const long seq = t / S;
+  const long at = seq * id_stride + (t - seq * S);
+  if (lens_out && lane == 0 && t == seq * S) lens_out[seq] = lens_src[seq * id_stride];
+  int id = ids[at];
   id = (id < 0 || id >= vocab) ? 0 : id;
-  const int tt = type_ids ? type_ids[t] : 0;
+  const int tt = type_ids ? type_ids[at] : 0;
   const int p = (int)(t % S);
   const int nch = D >> 3;
   float v[CPL][8];
@@ -384,21 +392,42 @@ int mls_layernorm(const void* x, const void* res, const void* gamma, const void*
   return (int)hipGetLastError();
 }
 
-int mls_embed_ln(const int* ids, const int* type_ids, const void* word, const void* pos, const void* typ,
-                 const void* gamma, const void* beta, void* out, long rows, int S, int D, int vocab, float eps,
-                 void* stream) {
-  if (D % 8 || D > 64 * 8 * 4 || rows <= 0 || S <= 0) return MLS_BAD_ARG;
+int mls_embed_ln2(const int* ids, const int* type_ids, int id_stride, const int* lens_src, int* lens_out,
+                  const void* word, const void* pos, const void* typ, const void* gamma, const void* beta, void* out,
+                  long rows, int S, int D, int vocab, float eps, void* stream) {
+  if (D % 8 || D > 64 * 8 * 4 || rows <= 0 || S <= 0 || id_stride < S || (lens_out && !lens_src) || rows % S)
+    return MLS_BAD_ARG;
   const int cpl = (D / 8 + 63) / 64;
   dim3 grid((unsigned)((rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK));
   hipStream_t st = (hipStream_t)stream;
 #define EL_LAUNCH(C)                                                                                                 \
   hipLaunchKernelGGL(embed_ln_kernel<C>, grid, dim3(256), 0, st, ids, type_ids, (const bf16*)word, (const bf16*)pos, \
-                     (const bf16*)typ, (const bf16*)gamma, (const bf16*)beta, (bf16*)out, rows, S, D, vocab, eps)
+                     (const bf16*)typ, (const bf16*)gamma, (const bf16*)beta, (bf16*)out, rows, S, D, vocab, eps, \
+                     id_stride, lens_src, lens_out)
   if (cpl <= 1) EL_LAUNCH(1);
   else if (cpl <= 2) EL_LAUNCH(2);
   else EL_LAUNCH(4);
 #undef EL_LAUNCH
   return (int)hipGetLastError();
+}
+
+int mls_embed_ln(const int* ids, const int* type_ids, const void* word, const void* pos, const void* typ,
+                 const void* gamma, const void* beta, void* out, long rows, int S, int D, int vocab, float eps,
+                 void* stream) {
+  if (S <= 0 || rows % S) {  // a partial last sequence: contiguous ids, plain t % S positions
+    if (D % 8 || D > 64 * 8 * 4 || rows <= 0 || S <= 0) return MLS_BAD_ARG;
+    const long full = rows / S * S;
+    if (full) {
+      const int rc = mls_embed_ln2(ids, type_ids, S, nullptr, nullptr, word, pos, typ, gamma, beta, out, full, S, D,
+                                   vocab, eps, stream);
+      if (rc) return rc;
+    }
+    return mls_embed_ln2(ids + full, type_ids ? type_ids + full : nullptr, (int)(rows - full), nullptr, nullptr, word,
+                         pos, typ, gamma, beta, (bf16*)out + full * D, rows - full, (int)(rows - full), D, vocab, eps,
+                         stream);
+  }
+  return mls_embed_ln2(ids, type_ids, S, nullptr, nullptr, word, pos, typ, gamma, beta, out, rows, S, D, vocab, eps,
+                       stream);
 }
 
 int mls_embedding(const int* ids, const void* table, void* out, long rows, int D, int lo, int hi, void* stream) {

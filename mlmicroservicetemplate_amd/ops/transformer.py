@@ -55,6 +55,28 @@ def embed_layernorm(ids: torch.Tensor, type_ids: Optional[torch.Tensor], word: t
     return out
 
 
+def embed_layernorm_packed(x: torch.Tensor, seq_len: int, word: torch.Tensor, pos: torch.Tensor, typ: torch.Tensor,
+                           gamma: torch.Tensor, beta: torch.Tensor, eps: float = 1e-12):
+    """:func:`embed_layernorm` straight from the engine's packed request rows ``x`` int32
+    ``[B, 2S + 1]`` = ids | type ids | length (``models.bert.pack_requests``): no unpacking copies.
+    Returns ``(out [B*S, D] bf16, lens [B] int32)`` -- the lengths copied out by the same launch."""
+    dev = x.device
+    _need(x, "x", torch.int32, dev)
+    B, W = x.shape
+    S = int(seq_len)
+    if W != 2 * S + 1 or not x.is_contiguous():
+        raise ValueError("x must be contiguous int32 [B, 2*S + 1]")
+    D = word.shape[1]
+    out = torch.empty(B * S, D, device=dev, dtype=torch.bfloat16)
+    lens = torch.empty(B, device=dev, dtype=torch.int32)
+    base = x.data_ptr()
+    rc = lib().mls_embed_ln2(base, base + 4 * S, W, base + 8 * S, lens.data_ptr(), word.data_ptr(), pos.data_ptr(),
+                             typ.data_ptr(), gamma.data_ptr(), beta.data_ptr(), out.data_ptr(), B * S, S, D,
+                             word.shape[0], float(eps), stream_ptr(dev))
+    check(rc, "mls_embed_ln2")
+    return out, lens
+
+
 def embedding(ids: torch.Tensor, table: torch.Tensor, lo: int = 0, hi: Optional[int] = None,
               out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Row gather; with a vocab shard ``[lo, hi)`` out-of-shard ids give zero rows (TP)."""

@@ -53,6 +53,12 @@ def test_bert_b128_s128_engine_vs_fp32():
         sure = (top2[:, 0] - top2[:, 1]) > 2 * (got - ref).abs().max()
         assert torch.equal(got.argmax(-1)[sure], ref.argmax(-1)[sure])
         assert (got.argmax(-1) == ref.argmax(-1)).float().mean() >= 0.9
+    # the serving path: the packed rows read in place by the embedding kernel (lengths copied out by
+    # the same launch) -- bit-identical logits to the unpacked call
+    for packed, _ in batches:
+        x = torch.from_numpy(packed).to(DEV)
+        ids, tt, lens = bert.unpack_requests(x, S)
+        assert torch.equal(model.forward_packed(x, S), model(ids, tt, lens))
 
 
 def test_llama8b_4layer_fused_vs_reference():

@@ -34,9 +34,9 @@ def bench_bert(args):
             packed = bert.pack_requests(toks, S).numpy()
             for name, model in models.items():
                 def fwd(x, model=model, S=S, name=name):
+                    if name == "fused":  # the serving path (plugins/text_classifier.py): packed rows, fused top-k
+                        return model.classify_packed(x, S, 2)
                     ids, tt, lens = bert.unpack_requests(x, S)
-                    if name == "fused":  # the serving head (plugins/text_classifier.py): fused softmax + top-k
-                        return model.classify(ids, tt, lens, 2)
                     logits = model(ids, tt, lens)
                     v, i = torch.topk(torch.softmax(logits.float(), -1), 2, dim=-1)
                     return v, i.to(torch.int32)
