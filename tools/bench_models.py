@@ -41,7 +41,8 @@ def bench_bert(args):
                     v, i = torch.topk(torch.softmax(logits.float(), -1), 2, dim=-1)
                     return v, i.to(torch.int32)
 
-                eng = GpuEngine(fwd, dev, (2 * S + 1,), torch.int32, buckets=[B], inflight=args.inflight, concurrent=True)
+                eng = GpuEngine(fwd, dev, (2 * S + 1,), torch.int32, buckets=[B], inflight=args.inflight, concurrent=True,
+                                cu_partitions=args.cu_partition)
                 eng.warmup(capture=True)
                 for _ in range(5):
                     eng.run(packed)
@@ -157,6 +158,8 @@ def main():
     ap.add_argument("--inflight", type=int, default=5, help="bert: batches in flight (co-running engine slots)")
     ap.add_argument("--backends", nargs="+", default=["fused", "eager"], help="bert: which implementations")
     ap.add_argument("--emulate-tp", type=int, default=1)
+    ap.add_argument("--cu-partition", type=int, default=0,
+                    help="bert: CU-masked partitions for the engine slots (engine/worker.py; 0 = off)")
     ap.add_argument("--skinny-max-split", type=int, default=0)
     ap.add_argument("--kv-pages", type=int, default=0, help="llama: paged KV pool of N 64-row pages (0: per-slot)")
     ap.add_argument("--shuffle-pages", action="store_true", help="llama: hand out pages in random order")

@@ -15,6 +15,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 SHAPES = {  # name: (M, N, K, act)
     "bert32_qkv": (4096, 2304, 768, "none"), "bert32_o": (4096, 768, 768, "none"),
     "bert32_ffn1": (4096, 3072, 768, "gelu"), "bert32_ffn2": (4096, 768, 3072, "none"),
+    "bert64_qkv": (8192, 2304, 768, "none"), "bert64_o": (8192, 768, 768, "none"),
+    "bert64_ffn1": (8192, 3072, 768, "gelu"), "bert64_ffn2": (8192, 768, 3072, "none"),
     "bert128_qkv": (16384, 2304, 768, "none"), "bert128_o": (16384, 768, 768, "none"),
     "bert128_ffn1": (16384, 3072, 768, "gelu"), "bert128_ffn2": (16384, 768, 3072, "none"),
     "llama_qkv": (4096, 6144, 4096, "none"), "llama_o": (4096, 4096, 4096, "none"),
