@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import json
 import os
+import sys
 import time
 from typing import Dict, List, Optional, Tuple
 
@@ -116,7 +117,7 @@ def tune_resnet50(batch: int, device="cuda:0", iters: int = 20, compare_torch: b
     per-batch cost with that many batches co-running (the serving engine's concurrent slots).
     ``layers`` restricts the search to those layer names (probes); the FC is tuned only when
     ``layers`` is None or names it."""
-    from . import CFG_HALO, CFG_HALO_N32, CFG_HALO_XL, conv2d_nhwc, gemm, pack_conv_weight
+    from . import CFG_HALO, CFG_HALO_N32, CFG_HALO_XL, CFG_PIPE, PIPE_VARIANTS, conv2d_nhwc, gemm, pack_conv_weight
     from ..models.resnet import conv_shapes
 
     dev = torch.device(device)
@@ -144,8 +145,12 @@ def tune_resnet50(batch: int, device="cuda:0", iters: int = 20, compare_torch: b
         halo = s.k == 3 and s.stride == 1 and s.cin % 32 == 0 and s.cout % 64 == 0
         halo_cands = [(CFG_HALO, 1), (CFG_HALO, 2), (CFG_HALO, 4), (CFG_HALO_N32, 1), (CFG_HALO_XL, 1),
                       (CFG_HALO_XL, 2), (CFG_HALO_XL, 4)] if halo else []
-        for cfg, sk in [(0, 0)] + cands + halo_cands:
-            if sk > 1 and k // sk < 128:
+        # the pipelined 3x3 kernel: variant x (K splits + 16 x (items per block - 1))
+        pipe_cands = ([(CFG_PIPE + v, ks + 16 * (ipb - 1)) for v in range(PIPE_VARIANTS) for ks in (1, 2)
+                       for ipb in (1, 2) if (s.cin // 32) % ks == 0] if halo and os.environ.get("MLS_TUNE_PIPE", "1") == "1"
+                      else [])
+        for cfg, sk in [(0, 0)] + cands + halo_cands + pipe_cands:
+            if sk > 1 and cfg < CFG_PIPE and k // sk < 128:
                 continue
 
             def mk(o, wsc, cfg=cfg, sk=sk):
@@ -161,6 +166,8 @@ def tune_resnet50(batch: int, device="cuda:0", iters: int = 20, compare_torch: b
             tried[f"{cfg},{sk}"] = round(t * 1e3, 2)
             if (cfg, sk) != (0, 0) and t < best[0]:
                 best = (t, cfg, sk)
+        print(f"autotune: {s.name} best cfg {best[1]} splitk {best[2]} {best[0] * 1e3:.2f} us "
+              f"({len(tried)} tried)", file=sys.stderr, flush=True)  # progress (long GPU jobs)
         entry = {"M": batch * ho * ho, "N": s.cout, "K": k, "best_cfg": best[1], "best_splitk": best[2],
                  "best_us": round(best[0] * 1e3, 2), "heuristic_us": tried.get("0,0"),
                  "tflops": round(flops / (best[0] * 1e-3) / 1e12, 1)}
