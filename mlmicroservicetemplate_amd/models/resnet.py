@@ -334,6 +334,8 @@ class ResNet50Fused:
         self.chain_l3 = os.environ.get("MLS_CHAIN_L3", "0") == "1"
         if os.environ.get("MLS_CHAIN_L2_CW"):  # A/B: layer2 boundaries' chunk width (64 / 32)
             ops.set_chain_l2_cw(int(os.environ["MLS_CHAIN_L2_CW"]))
+        if os.environ.get("MLS_CHAIN_L2_BM"):  # A/B: layer2 boundaries' row tile (128 / 64)
+            ops.lib().mls_chain_set_l2_bm(int(os.environ["MLS_CHAIN_L2_BM"]))
         # normalise + stem + max pool as one kernel (csrc/stem_pool.hip); MLS_FUSED_STEM=0 -> 3 kernels
         self.fuse_stem = image_size == 224 and os.environ.get("MLS_FUSED_STEM", "1") != "0"
         # ... with layer1.0's 1x1 conv on the pooled tiles in the same kernel: tested, measured level

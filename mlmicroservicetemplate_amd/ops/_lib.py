@@ -95,7 +95,8 @@ _SIGS = {
     "mls_stream_destroy": [P],
     "mls_cu_census": [P, I, I, P],
 }
-_OPTIONAL_SIGS: dict = {"mls_set_debug_flags": [I], "mls_chain_set_l2_cw": [I], "mls_skinny_set_variant": [I], "mls_skinny_set_max_split": [I]}
+_OPTIONAL_SIGS: dict = {"mls_set_debug_flags": [I], "mls_chain_set_l2_cw": [I],
+    "mls_chain_set_l2_bm": [I], "mls_skinny_set_variant": [I], "mls_skinny_set_max_split": [I]}
 
 
 class NativeError(RuntimeError):

@@ -400,9 +400,8 @@ __global__ __launch_bounds__(512, OCC) void conv_chain_kernel(const ChainArgs a)
 //   layer2.1 -> 2.2, 2.2 -> 2.3                  2   512  128  64 (or 32: 80 KB, two blocks per CU)
 //   layer2.3 -> layer3.0                         2   512  256  32
 //   layer3.1 -> 3.2 ... layer3.4 -> 3.5          4  1024  256  32
-template <int KS, int N1, int N2, int CW>
+template <int KS, int N1, int N2, int CW, int BM = 128>
 int launch_chain(const ChainArgs& a, hipStream_t st) {
-  constexpr int BM = 128;
   constexpr int LDS = BM * KS * 128 + 2 * (CW * KS * 128 + N2 * CW * 2 + BM * CW * 2);
   constexpr int OCC = LDS <= 80 * 1024 ? 4 : 2;
 #ifdef MLS_CHAIN_SWAP
@@ -416,6 +415,7 @@ int launch_chain(const ChainArgs& a, hipStream_t st) {
 }
 
 int g_chain_cw_l2 = 0;  // layer2 chunk width override (0 = default 64; mls_chain_set_l2_cw for A/B)
+int g_chain_bm_l2 = 128;  // layer2 boundaries' row tile (64: 392 blocks instead of 196 at B = 32)
 
 }  // namespace
 
@@ -465,9 +465,12 @@ int mls_conv_chain(const void* a1, const void* a2, const void* w3, const float* 
   if (ks == 1 && N1 == 256 && N2 == 64) return launch_chain<1, 256, 64, 64>(a, st);
   if (ks == 2 && N1 == 256 && N2 == 64) return launch_chain<2, 256, 64, 64>(a, st);
   if (ks == 1 && N1 == 256 && N2 == 128) return launch_chain<1, 256, 128, 64>(a, st);
-  if (ks == 2 && N1 == 512 && N2 == 128)
+  if (ks == 2 && N1 == 512 && N2 == 128) {
+    if (g_chain_bm_l2 == 64) return launch_chain<2, 512, 128, 64, 64>(a, st);
     return g_chain_cw_l2 == 32 ? launch_chain<2, 512, 128, 32>(a, st) : launch_chain<2, 512, 128, 64>(a, st);
-  if (ks == 2 && N1 == 512 && N2 == 256) return launch_chain<2, 512, 256, 32>(a, st);
+  }
+  if (ks == 2 && N1 == 512 && N2 == 256)
+    return g_chain_bm_l2 == 64 ? launch_chain<2, 512, 256, 64, 64>(a, st) : launch_chain<2, 512, 256, 32>(a, st);
   if (ks == 4 && N1 == 1024 && N2 == 256) return launch_chain<4, 1024, 256, 32>(a, st);
   return MLS_UNSUPPORTED;
 }
@@ -475,6 +478,9 @@ int mls_conv_chain(const void* a1, const void* a2, const void* w3, const float* 
 // A/B switch for the layer2 boundaries' chunk width (64 = 128 KB of LDS, one block per CU; 32 =
 // 80 KB, two per CU).
 void mls_chain_set_l2_cw(int cw) { g_chain_cw_l2 = (cw == 32 || cw == 64) ? cw : 0; }
+
+// A/B switch for the layer2 boundaries' row tile: 128 (default) or 64 (twice the blocks).
+void mls_chain_set_l2_bm(int bm) { g_chain_bm_l2 = bm == 64 ? 64 : 128; }
 
 }  // extern "C"
 

@@ -98,6 +98,27 @@ def test_chain_layer2_chunk_widths(cw):
     assert rel_err(y, y_ref) < 1e-2 and rel_err(t1, t1_ref) < 2e-2
 
 
+@pytest.mark.parametrize("n2", [128, 256])
+def test_chain_layer2_row_tile_64(n2):
+    """The 64-row tile of the layer2 boundaries (twice the blocks of the 128-row default; ragged
+    last tile at B = 3) computes the same y / t1."""
+    from mlmicroservicetemplate_amd import ops
+
+    B, H, K, N1 = 3, 28, 128, 512
+    torch.manual_seed(n2)
+    t2, res = torch.relu(_rand(B, H, H, K)), _rand(B, H, H, N1)
+    w3, w1 = _rand(N1, K, scale=K**-0.5), _rand(n2, N1, scale=N1**-0.5)
+    b3, b1 = torch.randn(N1, device=DEV) * 0.1, torch.randn(n2, device=DEV) * 0.1
+    try:
+        ops.lib().mls_chain_set_l2_bm(64)
+        y, t1 = ops.conv1x1_chain(t2, w3, b3, w1, b1, residual=res)
+    finally:
+        ops.lib().mls_chain_set_l2_bm(128)
+    y_ref = torch.relu(t2.float() @ w3.float().T + b3 + res.float())
+    t1_ref = torch.relu(y_ref.to(torch.bfloat16).float() @ w1.float().T + b1)
+    assert rel_err(y, y_ref) < 1e-2 and rel_err(t1, t1_ref) < 2e-2
+
+
 def test_chain_rejects_unsupported_shapes():
     from mlmicroservicetemplate_amd import ops
 
