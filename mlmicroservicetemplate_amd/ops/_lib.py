@@ -96,7 +96,8 @@ _SIGS = {
     "mls_cu_census": [P, I, I, P],
 }
 _OPTIONAL_SIGS: dict = {"mls_set_debug_flags": [I], "mls_chain_set_l2_cw": [I],
-    "mls_chain_set_l2_bm": [I], "mls_skinny_set_variant": [I], "mls_skinny_set_max_split": [I]}
+    "mls_chain_set_l2_bm": [I],
+    "mls_engine_launch": [P, P, P, _c.c_longlong, P, I, P, P, P, P], "mls_skinny_set_variant": [I], "mls_skinny_set_max_split": [I]}
 
 
 class NativeError(RuntimeError):

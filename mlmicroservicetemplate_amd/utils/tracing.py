@@ -46,6 +46,11 @@ def enabled() -> bool:
     return _ENABLED
 
 
+def active() -> bool:
+    """Are ranges being emitted or recorded (callers may then prefer their instrumented path)?"""
+    return _ENABLED or _sink is not None
+
+
 def set_enabled(flag: bool) -> None:
     global _ENABLED
     _ENABLED = bool(flag)

@@ -1,0 +1,13 @@
+export TMPDIR=/tmp
+OUT=gpurun_out/native3
+mkdir -p $OUT
+for i in 1 2 3 4 5; do
+  MLS_MEASURE_EAGER=0 MLS_BENCH_TICKETS=$OUT/t_on.jsonl timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 >> $OUT/on.jsonl 2>> $OUT/err.log || exit 1
+  MLS_NATIVE_LAUNCH=0 MLS_MEASURE_EAGER=0 MLS_BENCH_TICKETS=$OUT/t_off.jsonl timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 >> $OUT/off.jsonl 2>> $OUT/err.log || exit 1
+done
+python3 -c "
+import json
+for f in ['on','off']:
+    r=[json.loads(l) for l in open('$OUT/'+f+'.jsonl')]
+    print(f, [x['value'] for x in r], [x['p50_latency_ms'] for x in r], [x['host_submit_ms_per_step'] for x in r])
+"
