@@ -796,12 +796,17 @@ class LlamaTP:
         full residual and the last layer's all-reduced delta."""
         ops, cfg, sd = self.ops, self.cfg, self.sd
         D = cfg.head_dim
-        if explicit_slots is None:  # plain cache: the token -> cache row map of rope_kv_'s implicit mode
+        half = B // 2
+        # plain cache: each half runs rope_kv_'s implicit slot mode (token t -> row (t // S) * max_seq
+        # + pos) on a view of the caches starting at its first batch row -- no torch-side slot map
+        # (the head-major layout groups hm_rows slots, so the offset must be a whole group)
+        implicit = explicit_slots is None and (not self.kv_hm_rows or (half * self.max_seq) % self.kv_hm_rows == 0)
+        if explicit_slots is None and not implicit:
             b = torch.arange(B, device=r.device, dtype=torch.int64).repeat_interleave(S)
             pl = pos.long()
             valid = pl < lens.long()[b]
             explicit_slots = torch.where(valid, b * self.max_seq + pl, torch.full_like(pl, -1)).to(torch.int32)
-        half = B // 2
+        slot_elems = sd.hkv * D  # cache elements per slot in either layout
         parts = [(0, half), (half, B)]
         res = [r[b0 * S:b1 * S] for b0, b1 in parts]
         dlt = [None, None]
@@ -813,9 +818,15 @@ class LlamaTP:
                 if pend_d[m] is not None:
                     dlt[m] = pend_d[m].wait()
                 qkv, res[m] = pre_norm(res[m], f"l{i}.qkv", dlt[m])
-                ops.rope_kv_(qkv, pos[lo:hi], self.cos, self.sin, sd.hq, sd.hkv, D, explicit_slots[lo:hi],
-                             self.k_cache[i], self.v_cache[i], lens=lens[b0:b1], seq=S, max_seq=self.max_seq,
-                             hm_rows=self.kv_hm_rows)
+                if implicit:
+                    off = b0 * self.max_seq * slot_elems
+                    ops.rope_kv_(qkv, pos[lo:hi], self.cos, self.sin, sd.hq, sd.hkv, D, None,
+                                 self.k_cache[i].reshape(-1)[off:], self.v_cache[i].reshape(-1)[off:],
+                                 lens=lens[b0:b1], seq=S, max_seq=self.max_seq, hm_rows=self.kv_hm_rows)
+                else:
+                    ops.rope_kv_(qkv, pos[lo:hi], self.cos, self.sin, sd.hq, sd.hkv, D, explicit_slots[lo:hi],
+                                 self.k_cache[i], self.v_cache[i], lens=lens[b0:b1], seq=S, max_seq=self.max_seq,
+                                 hm_rows=self.kv_hm_rows)
                 a = ops.flash_attention(qkv, b1 - b0, S, sd.hq, sd.hkv, D, kv_lens=lens[b0:b1], causal=True)
                 pend_o[m] = self.comm.all_reduce_start(linear(a, f"l{i}.o"))
             for m in range(2):

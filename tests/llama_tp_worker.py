@@ -95,15 +95,26 @@ def main():
     ids = torch.randint(3, cfg.vocab - 1, (3, 24), generator=g)
     lens = torch.tensor([24, 11, 3])
     pos = torch.arange(24, dtype=torch.int32).unsqueeze(0).expand(3, 24).contiguous().cuda()
+    for c in m.k_cache + m.v_cache:
+        c.zero_()
     vals, idx = m.step(ids.cuda(), pos, lens.cuda(), decode=False, k=8)
     allv = m.comm.all_gather(vals)
     alli = m.comm.all_gather(idx)
+    kv_over = [c.clone() for c in m.k_cache + m.v_cache]
     # the overlapped TP prefill (two batch halves, all-reduces started early) vs the plain layer loop
     overlap_on = m.tp_overlap
     m.tp_overlap = False
+    for c in m.k_cache + m.v_cache:
+        c.zero_()
     vals0, idx0 = m.step(ids.cuda(), pos, lens.cuda(), decode=False, k=8)
     m.tp_overlap = overlap_on
     overlap_diff = float((vals0.float() - vals.float()).abs().max())
+    # ... and the KV cache rows each wrote (the halves append through offset cache views): the
+    # same rows, values equal up to the halves' own GEMM tile choices
+    kv_diff = max(float((a.float() - b.float()).abs().max()) for a, b in zip(kv_over, m.k_cache + m.v_cache))
+    kv_nz = [bool((a != 0).any().item()) == bool((b != 0).any().item()) for a, b in zip(kv_over, m.k_cache + m.v_cache)]
+    kv_rows_same = all(torch.equal((a != 0).any(-1), (b != 0).any(-1)) for a, b in zip(kv_over, m.k_cache + m.v_cache))
+    del kv_over
     failed = ""
     stall_rank = int(os.environ.get("STALL_RANK", "-1"))
     if stall_rank >= 0:
@@ -154,7 +165,8 @@ def main():
     if m.comm.car is not None:
         info[1] += 10 * m.comm.car.errors()  # peer-wait timeouts would show here
     torch.save({"tokens": out.cpu(), "vals": allv.cpu(), "idx": alli.cpu(), "info": info, "failed": failed,
-                "overlap_diff": overlap_diff, "tf_top1": torch.stack(tf, 1) if tf else torch.zeros(0)},
+                "overlap_diff": overlap_diff, "kv_diff": kv_diff, "kv_rows_same": bool(kv_rows_same and all(kv_nz)),
+                "tf_top1": torch.stack(tf, 1) if tf else torch.zeros(0)},
                os.environ["OUT"] + f".{rank}.pt")
     dist.destroy_process_group()
 

@@ -105,6 +105,9 @@ def test_fused_tp_matches_tp1(tmp_path, world):
         # overlapped TP prefill (batch halves, early all-reduce starts) == the plain layer loop, up to
         # the GEMM tile choice of the smaller halves (bf16 rounding)
         assert d["overlap_diff"] <= 5e-2 * (v1.abs().max().item() + 1e-6), (r, d["overlap_diff"])
+        # the overlapped prefill's KV appends (per-half offset cache views) land in the same rows
+        assert d["kv_rows_same"], f"rank {r}: overlapped prefill wrote different KV rows"
+        assert d["kv_diff"] <= 0.25, (r, d["kv_diff"])
         # teacher-forced decode (every step fed TP=1's token): exact top-1 on every step whose TP=1
         # margin exceeds 1e-2 of the largest logit -- near-ties excluded, nothing else
         if case != "stall":
