@@ -299,13 +299,14 @@ if __name__ == "__main__":
     ap.add_argument("--no-torch", action="store_true")
     ap.add_argument("--layers", nargs="*", default=None, help="only these layers (probe)")
     ap.add_argument("--cfgs", nargs="*", type=int, default=None, help="only these tile cfgs (with splitk 1/2/4/8)")
+    ap.add_argument("--iters", type=int, default=20, help="graph-replayed calls per timing")
     args = ap.parse_args()
     t0 = time.time()
     cands = None
     if args.cfgs:
         cands = [(c, s) for c in args.cfgs for s in (1, 2, 4, 8)]
     res = tune_resnet50(args.batch, compare_torch=not args.no_torch, concurrency=args.concurrency,
-                        candidates=cands, layers=args.layers)
+                        candidates=cands, layers=args.layers, iters=args.iters)
     tot_best = sum(v["best_us"] for v in res.values())
     tot_heur = sum(v.get("heuristic_us") or v["best_us"] for v in res.values())
     tot_torch = sum(v.get("torch_us", 0) for v in res.values())
