@@ -172,11 +172,23 @@ def run_rank(args) -> int:
     tickets_log = os.environ.get("MLS_BENCH_TICKETS")  # diagnostics: per-batch submit / done times
     events: list = []
 
+    # the next batch is staged into a spare pinned buffer (GpuEngine.prepare) while every slot is
+    # busy, so a freed slot only waits for the enqueue -- how a server stages requests as they
+    # arrive.  Measured level at 20 steps and +0.08 ms p50 (profiles/r4_bench_prestage_ab.jsonl): off
+    # by default (MLS_BENCH_PRESTAGE=1 turns it on)
+    prestage = os.environ.get("MLS_BENCH_PRESTAGE", "0") == "1"
+
     def run_steps(n, lat):
         pending = []
+        nxt = engine.prepare(pool[0]) if prestage and n else None
         for i in range(n):
             t0 = time.perf_counter()
-            pending.append(engine.submit(pool[i % len(pool)]))
+            if prestage:
+                pending.append(engine.launch_prepared(nxt))
+                if i + 1 < n:
+                    nxt = engine.prepare(pool[(i + 1) % len(pool)])
+            else:
+                pending.append(engine.submit(pool[i % len(pool)]))
             host_s[0] += time.perf_counter() - t0
             if len(pending) >= args.inflight:
                 t = pending.pop(0)

@@ -72,20 +72,32 @@ class _Slot:
 class Ticket:
     """Handle for an enqueued batch; :meth:`wait` returns numpy outputs trimmed to ``n`` rows."""
 
-    __slots__ = ("engine", "slot", "bucket", "n", "t_submit", "_result")
+    __slots__ = ("engine", "slot", "bucket", "n", "t_submit", "_result", "staged")
 
-    def __init__(self, engine: "GpuEngine", slot: _Slot, bucket: int, n: int):
+    def __init__(self, engine: "GpuEngine", slot: _Slot, bucket: int, n: int, staged: Optional["Prepared"] = None):
         self.engine = engine
         self.slot = slot
         self.bucket = bucket
         self.n = n
         self.t_submit = time.perf_counter()
         self._result = None
+        self.staged = staged  # a prepared batch's pinned buffer, returned to the pool on completion
 
     def wait(self) -> Tuple[np.ndarray, ...]:
         if self._result is None:
             self._result = self.engine._finish(self)
         return self._result
+
+
+class Prepared:
+    """A batch staged into a spare pinned buffer (:meth:`GpuEngine.prepare`) before any slot is
+    free; :meth:`GpuEngine.launch_prepared` enqueues it (H2D straight from that buffer)."""
+
+    __slots__ = ("buf", "n")
+
+    def __init__(self, buf: torch.Tensor, n: int):
+        self.buf = buf
+        self.n = n
 
 
 class GpuEngine:
@@ -224,6 +236,12 @@ class GpuEngine:
                     slot.pool = self._pool
                 self.slots.append(slot)
                 self._free.put(slot)
+        # spare pinned input buffers for prepare() / launch_prepared(): a batch is staged while every
+        # slot is still busy, so a freed slot only waits for the enqueue (the staging copy of a
+        # 4.8 MB ResNet batch, 80-180 us of host time, moves off the refill path)
+        self._spare: "queue.Queue[torch.Tensor]" = queue.Queue()
+        for _ in range(self.inflight + 1):
+            self._spare.put(torch.zeros((self.max_batch, *self.sample_shape), dtype=sample_dtype, pin_memory=True))
 
     # ------------------------------------------------------------------ capture
     def warmup(self, capture: bool = True) -> None:
@@ -277,6 +295,14 @@ class GpuEngine:
             from .. import ops
 
             lib = ops.lib()
+            # called through a PyDLL handle: the GIL stays held for the ~40 us call.  Through the
+            # CDLL (GIL released per call) 2 of 19 20-step bench runs stalled the host ~6 ms (33.8k
+            # / 35.1k req/s, host submit 0.44 ms/step); with the GIL held, 0 of 8 (median 49.9k
+            # vs 48.9k for the Python enqueue) -- consistent with a GIL hand-off to another thread
+            # held for the 5 ms switch interval (profiles/r4_engine_native_launch_outliers.jsonl)
+            fn = getattr(ctypes.PyDLL(lib._name), "mls_engine_launch")
+            fn.argtypes = lib.mls_engine_launch.argtypes
+            fn.restype = lib.mls_engine_launch.restype
             exec_h = slot.graphs[b].raw_cuda_graph_exec()
             slot.ev_done.record(slot.s_comp)  # torch creates the event lazily: make it exist
             ev = slot.ev_done.cuda_event
@@ -290,7 +316,7 @@ class GpuEngine:
                     h2d.numel() * h2d.element_size(), exec_h, n, dst, src, nb, ev)
             if not exec_h or not ev:
                 raise RuntimeError("graph exec / event handle unavailable")
-            slot.native[b] = (lib.mls_engine_launch, args, (dst, src, nb))  # keep the arrays alive
+            slot.native[b] = (fn, args, (dst, src, nb))  # keep the arrays alive
         except Exception as e:  # noqa: BLE001 - keep the Python enqueue
             logger.warning("%s: native launch unavailable (%s); Python enqueue", self.name, e)
             self.native_launch = False
@@ -325,6 +351,36 @@ class GpuEngine:
             self.last_error = f"{type(e).__name__}: {e}"
             raise
         return self.launch(slot, n)
+
+    def prepare(self, samples) -> Prepared:
+        """Stage a batch into a spare pinned buffer without taking a slot (blocks only while every
+        spare buffer is held by an unfinished prepared batch)."""
+        n = len(samples)
+        if n == 0:
+            raise ValueError("empty batch")
+        pick_bucket(n, self.buckets)
+        buf = self._spare.get()
+        try:
+            with tracing.range(self._tr_stage):
+                dst = buf.numpy() if self.sample_dtype != torch.bfloat16 else None
+                if isinstance(samples, np.ndarray):
+                    dst[:n] = samples
+                elif isinstance(samples, torch.Tensor):
+                    buf[:n].copy_(samples)
+                elif dst is not None:
+                    self._stager.gather(dst, samples)
+                else:
+                    for i, x in enumerate(samples):
+                        dst[i] = x
+        except BaseException:
+            self._spare.put(buf)
+            raise
+        return Prepared(buf, n)
+
+    def launch_prepared(self, prep: Prepared) -> Ticket:
+        """Take a free slot (blocking) and enqueue a :meth:`prepare`-d batch: H2D from its buffer."""
+        slot = self._free.get()
+        return self.launch(slot, prep.n, staged=prep)
 
     # -- zero-copy path: the caller fills the slot's pinned buffer itself (native front end) --
     def acquire(self, timeout: Optional[float] = None) -> Optional[_Slot]:
@@ -363,9 +419,11 @@ class GpuEngine:
         """The slot's pinned host input as a writable numpy view ``[max_batch, *sample_shape]``."""
         return slot.host_in.numpy()
 
-    def launch(self, slot: _Slot, n: int) -> Ticket:
+    def launch(self, slot: _Slot, n: int, staged: Optional[Prepared] = None) -> Ticket:
         """Enqueue H2D -> graph replay -> D2H for the first ``n`` rows already in the slot's pinned
-        buffer.  Consumes the slot (returned to the free list by :meth:`Ticket.wait`)."""
+        buffer (or in ``staged``'s buffer).  Consumes the slot (returned to the free list by
+        :meth:`Ticket.wait`)."""
+        src_host = slot.host_in if staged is None else staged.buf
         try:
             bucket = pick_bucket(n, self.buckets)
             nat = slot.native.get(bucket) if self.native_launch and not tracing.active() else None
@@ -373,22 +431,27 @@ class GpuEngine:
                 with self._enqueue_lock:
                     self._pace_launch()
                     fn, args, _keep = nat
+                    if staged is not None:  # same call, H2D from the prepared buffer
+                        args = args[:2] + (staged.buf.data_ptr(),) + args[3:]
                     rc = fn(*args)
                 if rc != 0:
                     raise RuntimeError(f"mls_engine_launch failed (HIP error {rc})")
-                return Ticket(self, slot, bucket, n)
+                return Ticket(self, slot, bucket, n, staged)
             with self._enqueue_lock, torch.cuda.device(self.device):
                 self._pace_launch()
                 if self.use_graphs and slot.graph_copies.get(bucket):
-                    # H2D -> forward -> D2H in one replay on the slot stream
+                    # H2D -> forward -> D2H in one replay on the slot stream (the graph reads the
+                    # slot's own pinned buffer: a prepared batch is copied into it first)
+                    if staged is not None:
+                        slot.host_in[:n].copy_(staged.buf[:n])
                     with tracing.range(self._tr_replay), torch.cuda.stream(slot.s_comp):
                         slot.graphs[bucket].replay()
                         slot.ev_done.record(slot.s_comp)
-                    return Ticket(self, slot, bucket, n)
+                    return Ticket(self, slot, bucket, n, staged)
                 s_h2d = slot.s_comp if self.copies_on_slot_stream else self.s_h2d
                 s_d2h = slot.s_comp if self.copies_on_slot_stream else self.s_d2h
                 with tracing.range(self._tr_h2d), torch.cuda.stream(s_h2d):
-                    slot.dev_in[:bucket].copy_(slot.host_in[:bucket], non_blocking=True)
+                    slot.dev_in[:bucket].copy_(src_host[:bucket], non_blocking=True)
                     slot.ev_h2d.record(s_h2d)
                 slot.s_comp.wait_event(slot.ev_h2d)
                 with tracing.range(self._tr_replay), torch.cuda.stream(slot.s_comp):
@@ -409,9 +472,11 @@ class GpuEngine:
                     slot.ev_done.record(s_d2h)
         except BaseException as e:
             self._free.put(slot)
+            if staged is not None:
+                self._spare.put(staged.buf)
             self.last_error = f"{type(e).__name__}: {e}"
             raise
-        return Ticket(self, slot, bucket, n)
+        return Ticket(self, slot, bucket, n, staged)
 
     def _pace_launch(self) -> None:
         """Called under the enqueue lock, with this batch's slot already taken."""
@@ -462,6 +527,9 @@ class GpuEngine:
             self.busy_s += time.perf_counter() - t.t_submit
             return tuple(res)
         finally:
+            if t.staged is not None:  # its H2D is done (the batch completed): reusable
+                self._spare.put(t.staged.buf)
+                t.staged = None
             self._free.put(slot)
 
     def run(self, samples) -> Tuple[np.ndarray, ...]:
