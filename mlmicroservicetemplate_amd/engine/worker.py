@@ -297,9 +297,10 @@ class GpuEngine:
             lib = ops.lib()
             # called through a PyDLL handle: the GIL stays held for the ~40 us call.  Through the
             # CDLL (GIL released per call) 2 of 19 20-step bench runs stalled the host ~6 ms (33.8k
-            # / 35.1k req/s, host submit 0.44 ms/step); with the GIL held, 0 of 8 (median 49.9k
-            # vs 48.9k for the Python enqueue) -- consistent with a GIL hand-off to another thread
-            # held for the 5 ms switch interval (profiles/r4_engine_native_launch_outliers.jsonl)
+            # / 35.1k req/s, host submit 0.44 ms/step); with the GIL held 0 of 20 (median 49.9k vs
+            # 48.9-49.3k for the Python enqueue).  The mechanism is not identified -- the bench
+            # process has no other Python thread (tools/probe/threads_probe.py)
+            # (profiles/r4_engine_native_launch_outliers.jsonl)
             fn = getattr(ctypes.PyDLL(lib._name), "mls_engine_launch")
             fn.argtypes = lib.mls_engine_launch.argtypes
             fn.restype = lib.mls_engine_launch.restype

@@ -1,7 +1,7 @@
 export TMPDIR=/tmp
-OUT=gpurun_out/outlier2
+OUT=gpurun_out/outlier3
 mkdir -p $OUT
-for i in 1 2 3 4 5 6 7 8; do
+for i in 1 2 3 4 5 6 7 8 9 10 11 12; do
   MLS_MEASURE_EAGER=0 timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 >> $OUT/on.jsonl 2>> $OUT/err.log || exit 1
   MLS_NATIVE_LAUNCH=0 MLS_MEASURE_EAGER=0 timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 >> $OUT/off.jsonl 2>> $OUT/err.log || exit 1
 done
