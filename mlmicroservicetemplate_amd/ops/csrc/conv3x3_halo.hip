@@ -27,6 +27,7 @@
 // 12 of the 13 stride-1 3x3 layers (13.5 vs 19.1 us on layer1, profiles/r1_halo_vs_table_c4.jsonl)
 // and lifts bench.py from 48.0k to 49.6k req/s.
 #include "common.h"
+#include "fastdiv.h"
 
 #include <cstdlib>
 
@@ -70,6 +71,8 @@ struct HaloArgs {
   int* cnt;          // per-tile arrival counters of this stream (ksplit > 1)
   int B, H, W, Cin, N, th, nb, act, ksplit;
   uint32_t x_bytes, w_bytes, ws_bytes;
+  // runtime divisors (fastdiv.h): ksplit, tiles, H / th, th * W, W, (th + 2) * (W + 2), W + 2
+  FastDiv fd_ks, fd_tiles, fd_tpi, fd_r, fd_w, fd_p2, fd_w2;
 };
 
 // Weight image swizzle: 16-B chunk ch of column n sits at ch ^ h((n >> 2) & 3), h = {0, 2, 3, 1}:
@@ -115,14 +118,16 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_halo_kernel(const HaloArgs a)
   const int P = a.nb * TH2 * W2;    // patch pixels
   const int tiles = (a.B / a.nb) * (a.H / a.th);
   int t = xcd_remap(blockIdx.x, gridDim.x);
-  const int split = t % a.ksplit;  // split-K slices of a tile are neighbours (one XCD's L2)
-  t /= a.ksplit;
-  const int tn = t / tiles, tile = t - tn * tiles;  // column-block-major: neighbours share weights
+  const int tq = fastdiv(t, a.fd_ks);
+  const int split = t - tq * a.ksplit;  // split-K slices of a tile are neighbours (one XCD's L2)
+  t = tq;
+  const int tn = fastdiv(t, a.fd_tiles), tile = t - tn * tiles;  // column-block-major: neighbours share weights
   MLS_CHECK(tn * BN < a.N, 501);
   const int n0 = tn * BN;
   const int tpi = a.H / a.th;  // tiles per image (nb == 1)
-  const int b0 = a.nb > 1 ? tile * a.nb : tile / tpi;
-  const int oh0 = a.nb > 1 ? 0 : (tile - (tile / tpi) * tpi) * a.th;
+  const int ti = fastdiv(tile, a.fd_tpi);
+  const int b0 = a.nb > 1 ? tile * a.nb : ti;
+  const int oh0 = a.nb > 1 ? 0 : (tile - ti * tpi) * a.th;
   const long m_base = (long)tile * R;  // the tile's output pixels are contiguous rows
 
   auto rb_of = [&](int i) { return C::CONTIG ? wid * RBW + i : wid + NW * i; };
@@ -134,9 +139,9 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_halo_kernel(const HaloArgs a)
     const int rb = rb_of(i);
     rb_on[i] = rb * 16 < R;
     const int r = min(rb * 16 + fr, R - 1);  // padded rows read a valid pixel, never stored
-    const int img = r / (a.th * a.W);
+    const int img = fastdiv(r, a.fd_r);
     const int rem = r - img * (a.th * a.W);
-    const int ohl = rem / a.W, ow = rem - (rem / a.W) * a.W;
+    const int ohl = fastdiv(rem, a.fd_w), ow = rem - ohl * a.W;
     pb[i] = (img * TH2 + ohl) * W2 + ow;
   }
 
@@ -149,9 +154,9 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_halo_kernel(const HaloArgs a)
     const int px = j * 16 + (lane >> 2), ch = lane & 3;
     xoff[s] = OOB;
     if (px < P) {
-      const int img = px / (TH2 * W2);
+      const int img = fastdiv(px, a.fd_p2);
       const int rem = px - img * (TH2 * W2);
-      const int pr = rem / W2, pc = rem - (rem / W2) * W2;
+      const int pr = fastdiv(rem, a.fd_w2), pc = rem - pr * W2;
       const int b = b0 + img, ih = oh0 + pr - 1, iw = pc - 1;
       if (b < a.B && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
         xoff[s] = (((b * a.H + ih) * a.W + iw) * a.Cin + ch * 8) * 2;
@@ -442,6 +447,13 @@ int mls_conv3x3_halo(const void* x, const void* w, const float* bias, const void
       a.ws_bytes = (uint32_t)slab;
     }
   }
+  a.fd_ks = fastdiv_make((uint32_t)a.ksplit);
+  a.fd_tiles = fastdiv_make((uint32_t)tiles);
+  a.fd_tpi = fastdiv_make((uint32_t)(H / th));
+  a.fd_r = fastdiv_make((uint32_t)(th * W));
+  a.fd_w = fastdiv_make((uint32_t)W);
+  a.fd_p2 = fastdiv_make((uint32_t)((th + 2) * (W + 2)));
+  a.fd_w2 = fastdiv_make((uint32_t)(W + 2));
   const dim3 grid((unsigned)((long)tiles * (N / bn) * a.ksplit));
   static const bool rs = [] {  // MLS_HALO_RS=0: LDS-DMA staging (A/B)
     const char* e = getenv("MLS_HALO_RS");

@@ -32,6 +32,7 @@
 // Contract as mls_conv3x3_halo (no residual: the ResNet 3x3 convs have none).  Selected per layer
 // through the tuning table (ops.CFG_PIPE + variant).
 #include "common.h"
+#include "fastdiv.h"
 
 int* mls_stream_splitk_counters(void* stream, long ntiles);  // conv_gemm.hip
 
@@ -53,7 +54,12 @@ struct PipeArgs {
   int* cnt;           // per-tile arrival counters of this stream (ksplit > 1)
   int B, H, W, Cin, N, th, nb, act, ksplit;
   int tiles, ntn, nitems, ipb;
+  int nck, tpi;  // input-channel chunks per item, tiles per image (H / th)
   uint32_t x_bytes, w_bytes, ws_bytes, o_bytes;
+  // every runtime divisor of the kernel as a FastDiv: patch pixels per image ((th+2)*(W+2)), patch
+  // row (W+2), output pixels per image-tile (th*W), W, ksplit, ntn, nck, tpi (fastdiv.h: with `/`
+  // the prologue's per-lane geometry was ~500 VALU ops before the first DMA)
+  FastDiv mg_p2, mg_w2, mg_r, mg_w, mg_ks, mg_ntn, mg_nck, mg_tpi;
 };
 
 MLS_DEV void glds16(rsrc_t r, char* lds, int voff, int soff) {
@@ -106,7 +112,7 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_pipe_kernel(const PipeArgs a)
   const int W2 = a.W + 2, TH2 = a.th + 2;
   const int R = a.nb * a.th * a.W;  // output pixels of an item
   const int P = a.nb * TH2 * W2;    // patch pixels of an item
-  const int nck = a.Cin / CK / a.ksplit;
+  const int nck = a.nck;
   const long M = (long)a.B * a.H * a.W;
 
   // items [first, first + mine) of this block, consecutive (the XCD remap keeps neighbouring
@@ -130,9 +136,9 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_pipe_kernel(const PipeArgs a)
     const int px = (wid + NW * s) * 16 + (lane >> 2);
     const int slot = lane & 3;
     const int ch = slot ^ (((px >> 2) & 1) << 1);  // LDS slot `slot` of pixel px holds chunk ch
-    const int img = px / (TH2 * W2);
+    const int img = fastdiv(px, a.mg_p2);
     const int rem = px - img * (TH2 * W2);
-    const int pr = rem / W2, pc = rem - (rem / W2) * W2;
+    const int pr = fastdiv(rem, a.mg_w2), pc = rem - pr * W2;
     pok[s] = px < P && pc >= 1 && pc <= a.W;
     prow[s] = pr;  // ih = oh0 + pr - 1
     prel[s] = (((img * a.H + pr - 1) * a.W + (pc - 1)) * a.Cin + ch * 8) * 2;
@@ -155,10 +161,10 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_pipe_kernel(const PipeArgs a)
 
   // item -> (tile, column block, K slice); items are tile-major
   auto decode = [&](int item, int& tile, int& tn, int& split) {
-    split = item % a.ksplit;
-    const int t2 = item / a.ksplit;
-    tn = t2 % a.ntn;
-    tile = t2 / a.ntn;
+    const int t2 = fastdiv(item, a.mg_ks);
+    split = item - t2 * a.ksplit;
+    tile = fastdiv(t2, a.mg_ntn);
+    tn = t2 - tile * a.ntn;
   };
   // issue cursor: the item whose patch offsets are cached
   int iss_item = -1, iss_wbase = 0, iss_cbase = 0;
@@ -167,14 +173,15 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_pipe_kernel(const PipeArgs a)
   // main loop spread over the 9 taps of the current step (issue cost among the MFMAs, not in a
   // burst at the step start)
   auto prep = [&](int step, char*& st, int& cb) {
-    const int it = first + step / nck, c = step - (step / nck) * nck;
+    const int sq = fastdiv(step, a.mg_nck);
+    const int it = first + sq, c = step - sq * nck;
     if (it != iss_item) {
       iss_item = it;
       int tile, tn, split;
       decode(it, tile, tn, split);
-      const int tpi = a.H / a.th;
-      const int b0 = a.nb > 1 ? tile * a.nb : tile / tpi;
-      const int oh0 = a.nb > 1 ? 0 : (tile - (tile / tpi) * tpi) * a.th;
+      const int ti = fastdiv(tile, a.mg_tpi);
+      const int b0 = a.nb > 1 ? tile * a.nb : ti;
+      const int oh0 = a.nb > 1 ? 0 : (tile - ti * a.tpi) * a.th;
       const int iss_xbase = ((b0 * a.H + oh0) * a.W) * a.Cin * 2;
       iss_wbase = tn * BN * 9 * a.Cin * 2;
       iss_cbase = split * nck;
@@ -203,9 +210,9 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_pipe_kernel(const PipeArgs a)
 #pragma unroll
   for (int i = 0; i < RBW; ++i) {
     const int r = min((wid + NW * i) * 16 + fr, R - 1);
-    const int img = r / (a.th * a.W);
+    const int img = fastdiv(r, a.mg_r);
     const int rem = r - img * (a.th * a.W);
-    const int ohl = rem / a.W, ow = rem - (rem / a.W) * a.W;
+    const int ohl = fastdiv(rem, a.mg_w), ow = rem - ohl * a.W;
     pb[i] = (img * TH2 + ohl) * W2 + ow;
   }
   const int wfo = (fr * 4 + (fq ^ wswz(fr))) * 16;  // this lane's weight-fragment byte offset
@@ -277,11 +284,12 @@ __global__ __launch_bounds__(NW * 64) void conv3x3_pipe_kernel(const PipeArgs a)
       __builtin_amdgcn_sched_barrier(0);
     }
 
-    if ((step + 1) % nck != 0) continue;  // not the item's last chunk
+    const int sq = fastdiv(step, a.mg_nck);
+    if (step - sq * nck != nck - 1) continue;  // not the item's last chunk
 
     // ---- item epilogue: lane = output pixel (rb*16 + fr) x 4 consecutive channels per column block
     int tile, tn, split;
-    decode(first + step / nck, tile, tn, split);
+    decode(first + sq, tile, tn, split);
     const long m_base = (long)tile * R;
     const int n0 = tn * BN;
     if (a.ksplit > 1) {
@@ -454,6 +462,16 @@ int mls_conv3x3_pipe(const void* x, const void* w, const float* bias, void* out,
   }
   a.nitems = a.tiles * a.ntn * a.ksplit;
   a.ipb = ipb;
+  a.nck = Cin / CK / a.ksplit;
+  a.tpi = H / th;
+  a.mg_p2 = fastdiv_make((th + 2) * (W + 2));
+  a.mg_w2 = fastdiv_make(W + 2);
+  a.mg_r = fastdiv_make(th * W);
+  a.mg_w = fastdiv_make(W);
+  a.mg_ks = fastdiv_make(a.ksplit);
+  a.mg_ntn = fastdiv_make(a.ntn);
+  a.mg_nck = fastdiv_make(a.nck);
+  a.mg_tpi = fastdiv_make(a.tpi);
 
   const dim3 grid((unsigned)((a.nitems + ipb - 1) / ipb));
   hipStream_t st = (hipStream_t)stream;

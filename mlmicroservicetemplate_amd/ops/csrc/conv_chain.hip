@@ -26,6 +26,7 @@
 // Numerics: y rounds once exactly as conv_gemm.hip's epilogue (acc + bias + res, ReLU, bf16); t1
 // accumulates the same K order in fp32.
 #include "common.h"
+#include "fastdiv.h"
 
 namespace {
 
@@ -67,6 +68,7 @@ struct ChainArgs {
   bf16* t1;         // [M][N2]
   int M, Ka, Kb, N1, N2;
   int Ho, Wo, H2, W2, stride2;  // dual geometry (M = B * Ho * Wo)
+  FastDiv fd_howo, fd_wo;       // Ho * Wo, Wo (fastdiv.h)
   uint32_t a1_bytes, a2_bytes, w3_bytes, res_bytes, y_bytes, w1_bytes, t1_bytes;
 };
 
@@ -163,9 +165,8 @@ __global__ __launch_bounds__(512, OCC) void conv_chain_kernel(const ChainArgs a)
     } else {  // dual operand: row m of the output grid samples the block input at stride2
       int off = OOB;
       if (m < a.M) {
-        const int hw = a.Ho * a.Wo;
-        const int b = m / hw, rem = m - b * hw;
-        const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
+        const int b = fastdiv(m, a.fd_howo), rem = m - b * (a.Ho * a.Wo);
+        const int oh = fastdiv(rem, a.fd_wo), ow = rem - oh * a.Wo;
         off = (((b * a.H2 + oh * a.stride2) * a.W2 + ow * a.stride2) * a.Kb + (s - KSA) * 64 + lc * 8) * 2;
       }
       glds16(a2r, dst, off, 0);
@@ -448,6 +449,8 @@ int mls_conv_chain(const void* a1, const void* a2, const void* w3, const float* 
   a.N1 = N1;
   a.N2 = N2;
   a.Ho = Ho, a.Wo = Wo, a.H2 = H2, a.W2 = W2, a.stride2 = stride2;
+  a.fd_howo = fastdiv_make((uint32_t)(Ho * Wo));
+  a.fd_wo = fastdiv_make((uint32_t)Wo);
   const long M = a.M;
   const long sizes[7] = {M * Ka * 2, (long)B * H2 * W2 * Kb * 2, (long)N1 * (Ka + Kb) * 2, res ? M * N1 * 2 : 0,
                          M * N1 * 2, (long)N2 * N1 * 2, M * N2 * 2};

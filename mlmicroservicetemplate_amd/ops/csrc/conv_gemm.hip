@@ -24,6 +24,7 @@
 //    reduce-epilogue kernel (deterministic; the launch boundary is captured in the hipGraph).
 //  * XCD-aware bijective block remap so neighbouring tiles share an XCD's L2.
 #include "common.h"
+#include "fastdiv.h"
 
 #include <cstdlib>
 #include <mutex>
@@ -71,7 +72,21 @@ struct ConvArgs {
   float* pool;
   float pool_scale;
   int pool_hw, pool_only;
+  // the kernels' runtime divisors (fastdiv.h; set by set_fastdivs for the launched tile width):
+  // Ho*Wo, Wo, splitk, column tiles, Cin, KW, k-steps per tile (persistent), pool_hw
+  FastDiv fd_howo, fd_wo, fd_split, fd_ntn, fd_cin, fd_kw, fd_nk, fd_pool;
 };
+
+void set_fastdivs(ConvArgs& a, int bn) {
+  a.fd_howo = fastdiv_make((uint32_t)(a.Ho * a.Wo));
+  a.fd_wo = fastdiv_make((uint32_t)a.Wo);
+  a.fd_split = fastdiv_make((uint32_t)(a.splitk > 0 ? a.splitk : 1));
+  a.fd_ntn = fastdiv_make((uint32_t)((a.N + bn - 1) / bn));
+  a.fd_cin = fastdiv_make((uint32_t)a.Cin);
+  a.fd_kw = fastdiv_make((uint32_t)(a.KW > 0 ? a.KW : 1));
+  a.fd_nk = fastdiv_make((uint32_t)((a.K + BK - 1) / BK));
+  a.fd_pool = fastdiv_make((uint32_t)(a.pool_hw > 0 ? a.pool_hw : 1));
+}
 
 int g_dbg_flags = 0;  // set via mls_set_debug_flags (tools/conv_ablate.py); 0 in production
 
@@ -215,9 +230,10 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_kernel(const ConvArgs 
 
   const int ntn = (a.N + BN - 1) / BN;
   int t = xcd_remap(blockIdx.x, gridDim.x);
-  const int split = t % a.splitk;
-  t /= a.splitk;
-  const int tn = t % ntn, tmi = t / ntn;
+  const int tq = fastdiv(t, a.fd_split);
+  const int split = t - tq * a.splitk;
+  t = tq;
+  const int tmi = fastdiv(t, a.fd_ntn), tn = t - tmi * ntn;
   const int m0 = tmi * BM, n0 = tn * BN;
   const int kbeg = split * a.kchunk;
   const int kend = min(a.K, kbeg + a.kchunk);
@@ -239,9 +255,9 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_kernel(const ConvArgs 
     a_v[j] = OOB;
     a_v2[j] = OOB;
     if (m < a.M) {
-      const int b = m / HoWo;
+      const int b = fastdiv(m, a.fd_howo);
       const int rem = m - b * HoWo;
-      const int oh = rem / a.Wo;
+      const int oh = fastdiv(rem, a.fd_wo);
       const int ow = rem - oh * a.Wo;
       if (MODE == MODE_DUAL) {
         a_v[j] = (((b * a.H + oh) * a.W + ow) * a.Cin + lc * 8) * 2;
@@ -296,9 +312,9 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_kernel(const ConvArgs 
 #pragma unroll
       for (int j = 0; j < AI; ++j) glds16(xr, sA + (wid * AI + j) * 1024, a_v[j], soff);
     } else {
-      const int tap = k0 / a.Cin;  // the whole BKT-wide step is inside one tap
+      const int tap = fastdiv(k0, a.fd_cin);  // the whole BKT-wide step is inside one tap
       const int c0 = k0 - tap * a.Cin;
-      const int kh = tap / a.KW;
+      const int kh = fastdiv(tap, a.fd_kw);
       const int kw = tap - kh * a.KW;
       const int uni = ((kh * a.W + kw) * a.Cin + c0) * 2;
 #pragma unroll
@@ -503,7 +519,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_kernel(const ConvArgs 
       const int n = n0 + tid;
       const int rows = min(PASS_ROWS, a.M - (m0 + row_lo));
       if (tid < BN && n < a.N && rows > 0) {
-        int cur = (m0 + row_lo) / a.pool_hw;
+        int cur = fastdiv(m0 + row_lo, a.fd_pool);
         int next = (cur + 1) * a.pool_hw - (m0 + row_lo);  // first pass row of the next image
         float sum = 0.f;
         for (int r0 = 0; r0 < rows; r0 += 8) {
@@ -607,16 +623,17 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_persistent(const ConvA
   uint32_t a_msk[AI];
   auto setup_tile = [&](int k) {  // issue-side per-tile precompute (once per tile)
     const int t = lb + k * G;
-    const int m0 = (t / ntn) * BM, n0 = (t % ntn) * BN;
+    const int tq = fastdiv(t, a.fd_ntn);
+    const int m0 = tq * BM, n0 = (t - tq * ntn) * BN;
 #pragma unroll
     for (int j = 0; j < AI; ++j) {
       const int m = m0 + (wid * AI + j) * 8 + r8;
       a_msk[j] = 0u;
       a_v[j] = OOB;
       if (m < a.M) {
-        const int b = m / HoWo;
+        const int b = fastdiv(m, a.fd_howo);
         const int rem = m - b * HoWo;
-        const int oh = rem / a.Wo;
+        const int oh = fastdiv(rem, a.fd_wo);
         const int ow = rem - oh * a.Wo;
         if (MODE == MODE_1X1) {
           a_v[j] = (((b * a.H + oh * a.stride) * a.W + ow * a.stride) * a.Cin + lc * 8) * 2;
@@ -649,7 +666,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_persistent(const ConvA
   };
 
   auto issue = [&](int sidx, int buf) {
-    const int k = sidx / nk, ks = sidx - k * nk;
+    const int k = fastdiv(sidx, a.fd_nk), ks = sidx - k * nk;
     if (ks == 0) setup_tile(k);
     const int k0 = ks * BK;
     char* sA = smem + buf * STAGE_BYTES;
@@ -665,9 +682,9 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_persistent(const ConvA
 #pragma unroll
       for (int j = 0; j < AI; ++j) glds16(xr, sA + (wid * AI + j) * 1024, a_v[j], soff);
     } else {
-      const int tap = k0 / a.Cin;
+      const int tap = fastdiv(k0, a.fd_cin);
       const int c0 = k0 - tap * a.Cin;
-      const int kh = tap / a.KW;
+      const int kh = fastdiv(tap, a.fd_kw);
       const int kw = tap - kh * a.KW;
       const int uni = ((kh * a.W + kw) * a.Cin + c0) * 2;
 #pragma unroll
@@ -699,7 +716,7 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_persistent(const ConvA
     // exact count of the VMEM ops younger than stage s: stage s+1's DMA (+ its residual pieces)
     // and the previous epilogue's stores
     if (issued > s + 1) {
-      const bool nr = has_res && ((s + 1) % nk == nk - 1);
+      const bool nr = has_res && (s + 1 - fastdiv(s + 1, a.fd_nk) * nk == nk - 1);
       if (nr && prev_epi)
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPS + RI + EPI2) : "memory");
       else if (nr)
@@ -741,9 +758,11 @@ __global__ __launch_bounds__(WM * WN * 64) void conv_gemm_persistent(const ConvA
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
     }
     prev_epi = false;
-    if (s % nk == nk - 1) {
-      const int t = lb + (s / nk) * G;
-      const int m0 = (t / ntn) * BM, n0 = (t % ntn) * BN;
+    const int sq = fastdiv(s, a.fd_nk);
+    if (s - sq * nk == nk - 1) {
+      const int t = lb + sq * G;
+      const int tq = fastdiv(t, a.fd_ntn);
+      const int m0 = tq * BM, n0 = (t - tq * ntn) * BN;
       char* sR = smem + buf * STAGE_BYTES + A_BYTES + B_BYTES;
       // pass 1: in place over the residual tile (each element owned by exactly one lane)
 #pragma unroll
@@ -893,7 +912,8 @@ int num_cus() {
 }
 
 template <int MODE>
-void launch_persistent(int cfg, hipStream_t st, const ConvArgs& a) {
+void launch_persistent(int cfg, hipStream_t st, ConvArgs a) {
+  set_fastdivs(a, cfg == 21 ? 64 : cfg == 22 ? 128 : 64);
   auto grid = [&](int bm, int bn, int per_cu) {
     const long T = (long)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
     const long g = (long)num_cus() * per_cu;
@@ -997,6 +1017,7 @@ int launch_conv(ConvArgs a, int mode, int cfg, int splitk, size_t ws_bytes, hipS
     a.ws_bytes = (uint32_t)((size_t)splitk * a.M * a.N * sizeof(float));
   }
   dim3 grid((unsigned)ntiles);
+  set_fastdivs(a, bn);
   switch (mode) {
     case MODE_1X1: launch_mode<MODE_1X1>(cfg, grid, st, a); break;
     case MODE_GENERIC: launch_mode<MODE_GENERIC>(cfg, grid, st, a); break;

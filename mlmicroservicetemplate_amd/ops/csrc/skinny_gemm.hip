@@ -19,6 +19,7 @@
 
 #include "common.h"
 #include "ar_protocol.h"
+#include "fastdiv.h"
 
 namespace {
 
@@ -45,6 +46,8 @@ struct SkArgs {
   // fused tensor-parallel all-reduce of `out` (ar_protocol.h; world == 0: none): the row-parallel
   // decode projections reduce their partial sums across ranks in their own epilogue
   ArFuse arf;
+  // runtime divisors of the A staging loops (fastdiv.h): K / 8 chunks per row, combine head dim
+  FastDiv fd_kch, fd_hd;
 };
 
 // fusion modes of the A prologue (template parameter, so the unrolled k loop has no runtime
@@ -258,11 +261,11 @@ __global__ __launch_bounds__(NWV * 64) void skinny_lds_kernel(const SkArgs s) {
     for (int mm = 0; mm < 4; ++mm) lens4[mm] = mm < s.M ? __builtin_nontemporal_load(s.lens + mm) : 0;
   }
   for (int q = tid; q < s.M * kch; q += NWV * 64) {
-    const int m = q / kch, c = q - m * kch;
+    const int m = fastdiv(q, s.fd_kch), c = q - m * kch;
     uint4 v;
     if constexpr (FUSE == FUSE_COMBINE) {
       // the decode_combine_kernel arithmetic for this row's 8 dims of one head
-      const int h = (c * 8) / s.c_hd, d0 = (c * 8) % s.c_hd;
+      const int h = fastdiv(c * 8, s.fd_hd), d0 = c * 8 - h * s.c_hd;
       const int L = m == 0 ? lens4[0] : m == 1 ? lens4[1] : m == 2 ? lens4[2] : lens4[3];
       const int ns = min(s.c_nsplit, (L + s.c_chunk - 1) / s.c_chunk);
       if (ns <= 1) {
@@ -427,7 +430,7 @@ __global__ __launch_bounds__(NWV * 64) void skinny_packed_kernel(const SkArgs s)
 #pragma unroll
   for (int j = 0; j < QPT; ++j) {
     const int q = tid + j * T;
-    const int m = q / kch, c = q - m * kch;
+    const int m = fastdiv(q, s.fd_kch), c = q - m * kch;
     const int off = q < nq ? (m * s.lda + c * 8) * 2 : OOB;
     a0[j] = bload16(ar, off);
     if constexpr (FUSE == FUSE_ADD_NORM) a20[j] = bload16(a2r, off);
@@ -447,10 +450,10 @@ __global__ __launch_bounds__(NWV * 64) void skinny_packed_kernel(const SkArgs s)
     for (int mm = 0; mm < 4; ++mm) lens4[mm] = mm < s.M ? __builtin_nontemporal_load(s.lens + mm) : 0;
   }
   auto stage = [&](int q, uint4 v, uint4 v2) {
-    const int m = q / kch, c = q - m * kch;
+    const int m = fastdiv(q, s.fd_kch), c = q - m * kch;
     if constexpr (FUSE == FUSE_COMBINE) {
       // the decode_combine_kernel arithmetic for this row's 8 dims of one head
-      const int h = (c * 8) / s.c_hd, d0 = (c * 8) % s.c_hd;
+      const int h = fastdiv(c * 8, s.fd_hd), d0 = c * 8 - h * s.c_hd;
       const int L = m == 0 ? lens4[0] : m == 1 ? lens4[1] : m == 2 ? lens4[2] : lens4[3];
       const int ns = min(s.c_nsplit, (L + s.c_chunk - 1) / s.c_chunk);
       if (ns > 1) {
@@ -507,7 +510,7 @@ __global__ __launch_bounds__(NWV * 64) void skinny_packed_kernel(const SkArgs s)
   for (int j = 0; j < QPT; ++j)
     if (tid + j * T < nq) stage(tid + j * T, a0[j], a20[j]);
   for (int q = tid + QPT * T; q < nq; q += T) {
-    const int m = q / kch, c = q - m * kch;
+    const int m = fastdiv(q, s.fd_kch), c = q - m * kch;
     stage(q, ld16(s.a + (size_t)m * s.lda + c * 8),
           FUSE == FUSE_ADD_NORM ? ld16(s.a2 + (size_t)m * s.lda + c * 8) : make_uint4(0, 0, 0, 0));
   }
@@ -721,7 +724,7 @@ __global__ __launch_bounds__(NWV * 64) void skinny_fp8_kernel(const SkArgs s) {
 #pragma unroll
   for (int j = 0; j < QPT; ++j) {
     const int q = tid + j * T;
-    const int m = q / kch, c = q - m * kch;
+    const int m = fastdiv(q, s.fd_kch), c = q - m * kch;
     const int off = q < nq ? (m * s.lda + c * 8) * 2 : OOB;
     a0[j] = bload16(ar, off);
     if constexpr (FUSE == FUSE_ADD_NORM) a20[j] = bload16(a2r, off);
@@ -738,7 +741,7 @@ __global__ __launch_bounds__(NWV * 64) void skinny_fp8_kernel(const SkArgs s) {
   float part[4] = {0.f, 0.f, 0.f, 0.f}, amx[4] = {0.f, 0.f, 0.f, 0.f};
   const bool wr_res = FUSE == FUSE_ADD_NORM && s.a_out && blockIdx.x == 0;
   auto stage = [&](int q, uint4 v, uint4 v2) {
-    const int m = q / kch, c = q - m * kch;
+    const int m = fastdiv(q, s.fd_kch), c = q - m * kch;
     if constexpr (FUSE == FUSE_ADD_NORM) {
       v = add_round(v, v2);
       if (wr_res) st16(s.a_out + (size_t)m * s.lda + c * 8, v);
@@ -762,7 +765,7 @@ __global__ __launch_bounds__(NWV * 64) void skinny_fp8_kernel(const SkArgs s) {
   for (int j = 0; j < QPT; ++j)
     if (tid + j * T < nq) stage(tid + j * T, a0[j], a20[j]);
   for (int q = tid + QPT * T; q < nq; q += T) {
-    const int m = q / kch, c = q - m * kch;
+    const int m = fastdiv(q, s.fd_kch), c = q - m * kch;
     stage(q, ld16(s.a + (size_t)m * s.lda + c * 8),
           FUSE == FUSE_ADD_NORM ? ld16(s.a2 + (size_t)m * s.lda + c * 8) : make_uint4(0, 0, 0, 0));
   }
@@ -798,7 +801,7 @@ __global__ __launch_bounds__(NWV * 64) void skinny_fp8_kernel(const SkArgs s) {
   for (int j = 0; j < QMAX; ++j) {
     const int q = tid + j * T;
     if (q < nq) {
-      const int m = q / kch;
+      const int m = fastdiv(q, s.fd_kch);
       const float sc = m == 0 ? inv[0] : m == 1 ? inv[1] : m == 2 ? inv[2] : inv[3];
       float x[8];
       unpack8(hold[j], x);
@@ -943,6 +946,7 @@ int mls_skinny_gemm_norm(const void* A, const void* A2, void* A_out, const void*
   s.out = (bf16*)out;
   s.ws = (float*)ws;
   s.M = M; s.N = N; s.K = K; s.lda = K;
+  s.fd_kch = fastdiv_make((uint32_t)(K >> 3));
   s.act = act;
   s.ldo = act == ACT_SILU_MUL ? N / 2 : N;
   const size_t ab = (size_t)M * K * 2, wb = (size_t)N * K * 2;
@@ -1064,6 +1068,7 @@ static int skinny_packed_impl(const void* A, const void* A2, void* A_out, const 
   s.res = (const bf16*)res;
   s.out = (bf16*)out;
   s.M = M; s.N = N; s.K = K; s.lda = K;
+  s.fd_kch = fastdiv_make((uint32_t)(K >> 3));
   s.act = act;
   s.ldo = act == ACT_SILU_MUL ? N / 2 : N;
   s.a_bytes = (uint32_t)ab;
@@ -1163,6 +1168,7 @@ static int skinny_packed_combine_impl(const void* A, const float* cws, const flo
   s.res = (const bf16*)res;
   s.out = (bf16*)out;
   s.M = M; s.N = N; s.K = K; s.lda = K;
+  s.fd_kch = fastdiv_make((uint32_t)(K >> 3));
   s.act = act;
   s.ldo = act == ACT_SILU_MUL ? N / 2 : N;
   s.a_bytes = (uint32_t)ab;
@@ -1175,6 +1181,7 @@ static int skinny_packed_combine_impl(const void* A, const float* cws, const flo
   s.c_chunk = chunk;
   s.c_hq = Hq;
   s.c_hd = D;
+  s.fd_hd = fastdiv_make((uint32_t)D);
   if (arf) s.arf = *arf;
   hipStream_t st = (hipStream_t)stream;
   if (variant == 1)
@@ -1246,6 +1253,7 @@ int mls_skinny_fp8(const void* A, const void* A2, void* A_out, const void* Wq, c
   s.res = (const bf16*)res;
   s.out = (bf16*)out;
   s.M = M; s.N = N; s.K = K; s.lda = K;
+  s.fd_kch = fastdiv_make((uint32_t)(K >> 3));
   s.act = act;
   s.ldo = act == ACT_SILU_MUL ? N / 2 : N;
   s.a_bytes = (uint32_t)ab;
