@@ -630,16 +630,14 @@ class LlamaTP:
         pos = positions.reshape(-1)
         explicit_slots = None
         if (slot_ids is not None or self.pages is not None) and not decode:
-            # prefill into arbitrary cache rows (continuous batching) / through the page table
-            b = torch.arange(B, device=ids.device, dtype=torch.int64).repeat_interleave(S)
-            pl = pos.long()
-            slot = slot_ids.long()[b] if slot_ids is not None else b
-            valid = pl < lens.long()[b]
+            # prefill into arbitrary cache rows (continuous batching) / through the page table: one
+            # native launch (ops.prefill_slots), -1 past each sequence's length
+            sid = None if slot_ids is None else slot_ids.to(torch.int32)
             if self.pages is not None:
-                row = self.pages.rows(slot, torch.where(valid, pl, torch.zeros_like(pl)))
+                explicit_slots = ops.prefill_slots(pos, lens, B, S, sid, table=self.pages.device_table(),
+                                                   page_rows=self.pages.page_rows)
             else:
-                row = slot * self.max_seq + pl
-            explicit_slots = torch.where(valid, row, torch.full_like(pl, -1)).to(torch.int32)
+                explicit_slots = ops.prefill_slots(pos, lens, B, S, sid, max_seq=self.max_seq)
         # decode split size: 64 rows measured best from batch 1 to 32, at TP = 1 and on an emulated
         # TP = 8 rank (one KV head).  A single 256-row split per KV head (no combine launch) was
         # 1.6 % slower at batch 1, and one 8-wave block walking a whole <= 1024 context in passes
@@ -765,10 +763,11 @@ class LlamaTP:
             o = row_parallel(a, f"l{i}.o")
             gu, r = pre_norm(r, f"l{i}.gate_up", o, act=ops.ACT_SILU_MUL)
             delta = row_parallel(gu, f"l{i}.down")
-        if not decode:
-            last = (torch.arange(B, device=r.device, dtype=torch.int64) * S + lens.long() - 1)
-            r = r.index_select(0, last)
-            delta = None if delta is None else delta.index_select(0, last)
+        if not decode:  # each sequence's last valid token (one native gather of r and delta)
+            if delta is None:
+                r = ops.last_rows(r, lens, B, S)
+            else:
+                r, delta = ops.last_rows(r, lens, B, S, delta)
         if B <= 4 and "lm_head" in self.fp8 and B * r.shape[1] * 2 <= 65536:
             q, sc = self.fp8["lm_head"]
             logits = ops.skinny_fp8(r, q, sc, p["lm_head"].shape[0], delta=delta, norm=True, eps=eps)
@@ -802,10 +801,7 @@ class LlamaTP:
         # (the head-major layout groups hm_rows slots, so the offset must be a whole group)
         implicit = explicit_slots is None and (not self.kv_hm_rows or (half * self.max_seq) % self.kv_hm_rows == 0)
         if explicit_slots is None and not implicit:
-            b = torch.arange(B, device=r.device, dtype=torch.int64).repeat_interleave(S)
-            pl = pos.long()
-            valid = pl < lens.long()[b]
-            explicit_slots = torch.where(valid, b * self.max_seq + pl, torch.full_like(pl, -1)).to(torch.int32)
+            explicit_slots = ops.prefill_slots(pos, lens, B, S, max_seq=self.max_seq)
         slot_elems = sd.hkv * D  # cache elements per slot in either layout
         parts = [(0, half), (half, B)]
         res = [r[b0 * S:b1 * S] for b0, b1 in parts]

@@ -109,7 +109,9 @@ from .transformer import (  # noqa: F401
     embedding,
     flash_attention,
     kv_append,
+    last_rows,
     layernorm,
+    prefill_slots,
     rmsnorm,
     rope_,
     rope_kv_,

@@ -63,6 +63,8 @@ _SIGS = {
     "mls_embed_ln": [P, P, P, P, P, P, P, P, L, I, I, I, F, P],
     "mls_embed_ln2": [P, P, I, P, P, P, P, P, P, P, P, L, I, I, I, F, P],
     "mls_embedding": [P, P, P, L, I, I, I, P],
+    "mls_prefill_slots": [P, P, P, P, I, I, I, I, I, P, P],
+    "mls_last_rows": [P, P, P, I, I, I, P, P, P],
     "mls_rope": [P, P, P, P, L, I, I, I, P],
     "mls_ar_create": [I, I, L, P],
     "mls_ar_create2": [I, I, L, L, P],

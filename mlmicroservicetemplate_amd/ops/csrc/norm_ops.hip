@@ -230,6 +230,43 @@ __global__ __launch_bounds__(256) void embedding_kernel(const int* __restrict__ 
   }
 }
 
+// Prefill KV-cache row of every token (models/llama.py prefill into continuous-batching slots /
+// through the page table; replaces a dozen torch index launches per call): token t = (batch b =
+// t / S, position p = pos[t]) -> -1 unless p < lens[b]; slot = slot_ids ? slot_ids[b] : b; paged:
+// table[slot][p / page_rows] * page_rows + p % page_rows, plain: slot * max_seq + p.
+__global__ __launch_bounds__(256) void prefill_slots_kernel(const int* __restrict__ pos, const int* __restrict__ lens,
+                                                            const int* __restrict__ slot_ids,
+                                                            const int* __restrict__ table, int table_stride,
+                                                            int page_rows, int max_seq, int S, long T,
+                                                            int* __restrict__ out) {
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < T; t += (long)gridDim.x * blockDim.x) {
+    const int b = (int)(t / S), p = pos[t];
+    int row = -1;
+    if (p >= 0 && p < lens[b]) {
+      const int slot = slot_ids ? slot_ids[b] : b;
+      row = table ? table[(long)slot * table_stride + p / page_rows] * page_rows + p % page_rows
+                  : slot * max_seq + p;
+    }
+    out[t] = row;
+  }
+}
+
+// Last valid token row of each sequence: out[b] = src[b * S + lens[b] - 1] (and the same rows of
+// src2 into out2 when given) -- the prefill's hand-off to the LM head.
+__global__ __launch_bounds__(256) void last_rows_kernel(const bf16* __restrict__ src, const bf16* __restrict__ src2,
+                                                        const int* __restrict__ lens, int B, int S, int D,
+                                                        bf16* __restrict__ out, bf16* __restrict__ out2) {
+  const int nch = D >> 3;
+  const long total = (long)B * nch;
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
+    const int b = (int)(q / nch), ch = (int)(q - (long)b * nch);
+    const int l = lens[b];
+    const long row = (long)b * S + (l >= 1 && l <= S ? l - 1 : S - 1);
+    st16(out + (long)b * D + ch * 8, ld16(src + row * D + ch * 8));
+    if (src2) st16(out2 + (long)b * D + ch * 8, ld16(src2 + row * D + ch * 8));
+  }
+}
+
 // Element offset of (cache slot, head, dim chunk) in a KV cache.  hm_rows == 0: row-major
 // [slot][Hkv][D]; hm_rows = R > 0: head-major blocks of R rows, [slot / R][Hkv][R][D] -- a
 // sequence's (R = max_seq) or a page's (R = page rows) rows of one head are contiguous, so the
@@ -434,6 +471,24 @@ int mls_embedding(const int* ids, const void* table, void* out, long rows, int D
   if (D % 8 || rows <= 0) return MLS_BAD_ARG;
   hipLaunchKernelGGL(embedding_kernel, dim3(grid_for(rows * (D / 8), 256)), dim3(256), 0, (hipStream_t)stream, ids,
                      (const bf16*)table, (bf16*)out, rows, D, lo, hi);
+  return (int)hipGetLastError();
+}
+
+int mls_prefill_slots(const int* pos, const int* lens, const int* slot_ids, const int* table, int table_stride,
+                      int page_rows, int max_seq, int B, int S, int* out, void* stream) {
+  if (B <= 0 || S <= 0 || (table && (page_rows <= 0 || table_stride <= 0)) || (!table && max_seq <= 0))
+    return MLS_BAD_ARG;
+  const long T = (long)B * S;
+  hipLaunchKernelGGL(prefill_slots_kernel, dim3(grid_for(T, 256)), dim3(256), 0, (hipStream_t)stream, pos, lens,
+                     slot_ids, table, table_stride, page_rows, max_seq, S, T, out);
+  return (int)hipGetLastError();
+}
+
+int mls_last_rows(const void* src, const void* src2, const int* lens, int B, int S, int D, void* out, void* out2,
+                  void* stream) {
+  if (B <= 0 || S <= 0 || D % 8 || (src2 && !out2)) return MLS_BAD_ARG;
+  hipLaunchKernelGGL(last_rows_kernel, dim3(grid_for((long)B * (D / 8), 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16*)src, (const bf16*)src2, lens, B, S, D, (bf16*)out, (bf16*)out2);
   return (int)hipGetLastError();
 }
 

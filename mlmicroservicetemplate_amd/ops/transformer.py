@@ -77,6 +77,43 @@ def embed_layernorm_packed(x: torch.Tensor, seq_len: int, word: torch.Tensor, po
     return out, lens
 
 
+def prefill_slots(pos: torch.Tensor, lens: torch.Tensor, B: int, S: int, slot_ids: Optional[torch.Tensor] = None,
+                  table: Optional[torch.Tensor] = None, page_rows: int = 0, max_seq: int = 0) -> torch.Tensor:
+    """KV-cache row of every prefill token (int32 ``[B*S]``, -1 = past the sequence's length): batch
+    row b = t // S (or ``slot_ids[b]``), position ``pos[t]``; through the page ``table``
+    ``[slots][pages]`` (``page_rows`` rows each) or ``slot * max_seq + pos``.  One launch."""
+    dev = pos.device
+    _need(pos, "pos", torch.int32, dev)
+    _need(lens, "lens", torch.int32, dev)
+    if slot_ids is not None:
+        _need(slot_ids, "slot_ids", torch.int32, dev)
+    if table is not None:
+        _need(table, "table", torch.int32, dev)
+    out = torch.empty(B * S, device=dev, dtype=torch.int32)
+    rc = lib().mls_prefill_slots(pos.data_ptr(), lens.data_ptr(), _ptr(slot_ids), _ptr(table),
+                                 table.shape[1] if table is not None else 0, page_rows, max_seq, B, S, out.data_ptr(),
+                                 stream_ptr(dev))
+    check(rc, "mls_prefill_slots")
+    return out
+
+
+def last_rows(x: torch.Tensor, lens: torch.Tensor, B: int, S: int, x2: Optional[torch.Tensor] = None):
+    """Row ``b * S + lens[b] - 1`` of ``x`` (and of ``x2``) for every sequence: ``[B, D]`` (pair)."""
+    dev = x.device
+    _need(x, "x", torch.bfloat16, dev)
+    _need(lens, "lens", torch.int32, dev)
+    D = x.shape[-1]
+    out = torch.empty(B, D, device=dev, dtype=torch.bfloat16)
+    out2 = None
+    if x2 is not None:
+        _need(x2, "x2", torch.bfloat16, dev)
+        out2 = torch.empty(B, D, device=dev, dtype=torch.bfloat16)
+    rc = lib().mls_last_rows(x.data_ptr(), _ptr(x2), lens.data_ptr(), B, S, D, out.data_ptr(), _ptr(out2),
+                             stream_ptr(dev))
+    check(rc, "mls_last_rows")
+    return out if x2 is None else (out, out2)
+
+
 def embedding(ids: torch.Tensor, table: torch.Tensor, lo: int = 0, hi: Optional[int] = None,
               out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Row gather; with a vocab shard ``[lo, hi)`` out-of-shard ids give zero rows (TP)."""
