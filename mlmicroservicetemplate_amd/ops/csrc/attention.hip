@@ -90,21 +90,35 @@ __global__ __launch_bounds__(256) void flash_fwd_kernel(const AttnArgs a) {
   if (a.causal) kv_end = min(kv_end, q0 + BQ);
   const int ntiles = (kv_end + BKV - 1) / BKV;
 
-  for (int kt = 0; kt < ntiles; ++kt) {
-    const int kv0 = kt * BKV;
-    // ---- stage K and V tiles (zero rows past L via OOB loads) ----
+  // K / V tiles (zero rows past L via OOB loads) are register double-buffered: tile kt + 1's loads
+  // are issued right after tile kt is in LDS and land while tile kt's MFMAs run (one global
+  // round trip per kernel instead of one per tile: BERT S=128 has 2 tiles, Llama S=512 has 8)
+  constexpr int NI = (BKV * CPR) / 256;
+  uint4 kreg[NI], vreg[NI];
+  auto load_tile = [&](int kt) {
 #pragma unroll
-    for (int i = 0; i < (BKV * CPR) / 256; ++i) {
+    for (int i = 0; i < NI; ++i) {
       const int idx = tid + 256 * i;
       const int row = idx / CPR, ch = idx % CPR;
-      const int kv = kv0 + row;
+      const int kv = kt * BKV + row;
       const bool ok = kv < L;
-      const uint4 kvec = bload16(kr, ok ? (int)(((tok0 + kv) * a.k_stride + (long)hk * D + ch * 8) * 2) : OOB);
-      const uint4 vvec = bload16(vr, ok ? (int)(((tok0 + kv) * a.v_stride + (long)hk * D + ch * 8) * 2) : OOB);
-      *reinterpret_cast<uint4*>(Ks + row * (D * 2) + ((ch ^ (row & (CPR - 1))) * 16)) = kvec;
-      *reinterpret_cast<uint4*>(Vs + row * VST + ch * 16) = vvec;
+      kreg[i] = bload16(kr, ok ? (int)(((tok0 + kv) * a.k_stride + (long)hk * D + ch * 8) * 2) : OOB);
+      vreg[i] = bload16(vr, ok ? (int)(((tok0 + kv) * a.v_stride + (long)hk * D + ch * 8) * 2) : OOB);
+    }
+  };
+  if (ntiles > 0) load_tile(0);
+
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int kv0 = kt * BKV;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int idx = tid + 256 * i;
+      const int row = idx / CPR, ch = idx % CPR;
+      *reinterpret_cast<uint4*>(Ks + row * (D * 2) + ((ch ^ (row & (CPR - 1))) * 16)) = kreg[i];
+      *reinterpret_cast<uint4*>(Vs + row * VST + ch * 16) = vreg[i];
     }
     __syncthreads();
+    if (kt + 1 < ntiles) load_tile(kt + 1);
 
     // ---- S^T = K Q^T : 4 sub-tiles of 16 keys ----
     f32x4 s[4];
