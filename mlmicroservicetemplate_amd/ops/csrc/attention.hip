@@ -196,17 +196,38 @@ __global__ __launch_bounds__(256) void flash_fwd_kernel(const AttnArgs a) {
     __syncthreads();
   }
 
-  // ---- normalise and store: O rows q = qw + 4g + j, cols d = 16dt + fr ----
+  // ---- normalise and store: O rows q = qw + 4g + j, cols d = 16dt + fr
   const float inv_l = l_run > 0.f ? 1.f / l_run : 0.f;
+  if constexpr (D == 64) {  // BERT: 2-B stores straight from the accumulators (the LDS-staged 16-B
+                            // row stores below measured -0.8 % at B=32, level at B=128)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float il = __shfl(inv_l, 4 * g + j, 64);
+      const int q = qw + 4 * g + j;
+      if (q < a.S) {
+        bf16* dst = a.o + (tok0 + q) * a.o_stride + (long)h * D + fr;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) dst[16 * dt] = (bf16)(acc_o[dt][j] * il);
+      }
+    }
+    return;
+  }
+  // D = 128 (Llama prefill, +1-2 % at B=1x512): the wave's [16][D] tile through LDS (the K tile's
+  // space: every wave is past the loop's last barrier), then 16-B row stores
+  bf16* Os = reinterpret_cast<bf16*>(smem) + wid * 16 * D;
+  static_assert(4 * 16 * D * 2 <= K_BYTES, "output tiles fit the K tile");
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const float il = __shfl(inv_l, 4 * g + j, 64);
-    const int q = qw + 4 * g + j;
-    if (q < a.S) {
-      bf16* dst = a.o + (tok0 + q) * a.o_stride + (long)h * D + fr;
 #pragma unroll
-      for (int dt = 0; dt < DT; ++dt) dst[16 * dt] = (bf16)(acc_o[dt][j] * il);
-    }
+    for (int dt = 0; dt < DT; ++dt) Os[(4 * g + j) * D + 16 * dt + fr] = (bf16)(acc_o[dt][j] * il);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = lane; c < 16 * CPR; c += 64) {
+    const int r = c / CPR, ch = c % CPR;
+    const int q = qw + r;
+    if (q < a.S) st16(a.o + (tok0 + q) * a.o_stride + (long)h * D + ch * 8, ld16(Os + r * D + ch * 8));
   }
 }
 
@@ -757,6 +778,7 @@ int mls_flash_attention(const void* q, const void* k, const void* v, void* o, in
                         int causal, float scale, void* stream) {
   if (B <= 0 || S <= 0 || Hq <= 0 || Hkv <= 0 || Hq % Hkv) return MLS_BAD_ARG;
   if (q_stride % 8 || k_stride % 8 || v_stride % 8) return MLS_BAD_ARG;
+  if (o_stride % 8 || (reinterpret_cast<uintptr_t>(o) & 15)) return MLS_BAD_ARG;  // 16-B row stores
   AttnArgs a{};
   a.q = (const bf16*)q;
   a.k = (const bf16*)k;

@@ -1,6 +1,6 @@
 # Flash attention with register double-buffered K/V tiles: numerics, then BERT engine and Llama prefill A/B.
 export TMPDIR=/tmp
-OUT=gpurun_out/attnab
+OUT=gpurun_out/${ATT_OUT:-attnab}
 mkdir -p $OUT
 BASE=$PWD/tools/probe/alt_lib/libmls_base.so
 timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_transformer_ops_gpu.py tests/test_e2e_gpu.py tests/test_models_gpu.py > $OUT/pytest.log 2>&1; rc=$?
