@@ -21,41 +21,58 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const bf16* __restrict__
   if (row >= rows) return;
   const int nch = D >> 3;
   float v[CPL][8];
-  uint4 graw[CPL], braw[CPL];  // gamma / beta issued with x: one memory round trip, not two
+  // Every load of the row is issued before any is consumed, at clamped (always valid) chunk
+  // offsets; the tail lanes' values are dropped below.  With the loads behind per-chunk
+  // `ch < nch` guards hipcc waited vmcnt(0) per chunk: 3 dependent round trips per 16-B chunk.
+  // gamma / beta go with x up to 8 chunks per lane (register budget), after the statistics above.
+  constexpr bool EARLY_GB = CPL <= 8;
+  const bf16* xrow = x + row * D;
+  const bf16* rrow = res ? res + row * D : xrow;
+  const bf16* bsrc = beta ? beta : gamma;
+  uint4 xv[CPL], rv[CPL], graw[CPL], braw[CPL];
 #pragma unroll
   for (int c = 0; c < CPL; ++c) {
-    const int ch = lane + 64 * c;
-    if (ch < nch) {
-      graw[c] = ld16(gamma + ch * 8);
-      braw[c] = beta ? ld16(beta + ch * 8) : make_uint4(0, 0, 0, 0);
+    const int off = min(lane + 64 * c, nch - 1) * 8;
+    xv[c] = ld16(xrow + off);
+    rv[c] = ld16(rrow + off);
+    if constexpr (EARLY_GB) {
+      graw[c] = ld16(gamma + off);
+      braw[c] = ld16(bsrc + off);
     }
   }
   float s = 0.f, ss = 0.f;
 #pragma unroll
   for (int c = 0; c < CPL; ++c) {
     const int ch = lane + 64 * c;
-    if (ch < nch) {
-      unpack8(ld16(x + row * D + ch * 8), v[c]);
-      if (res) {
-        float r[8];
-        unpack8(ld16(res + row * D + ch * 8), r);
+    const bool live = ch < nch;
+    // consumed unconditionally (a tail lane works on a clamped duplicate, zeroed below): a use
+    // under `live` lets hipcc sink the load into the branch and wait for it there
+    unpack8(xv[c], v[c]);
+    if (res) {
+      float r[8];
+      unpack8(rv[c], r);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[c][e] += r[e];
-      }
-      if (res_out) {
-        // the residual stream is carried in bf16; normalise what the next layer will see
-        uint4 p = pack8(v[c]);
-        st16(res_out + row * D + ch * 8, p);
-        unpack8(p, v[c]);
-      }
+      for (int e = 0; e < 8; ++e) v[c][e] += r[e];
+    }
+    if (res_out) {
+      // the residual stream is carried in bf16; normalise what the next layer will see
+      uint4 p = pack8(v[c]);
+      if (live) st16(res_out + row * D + ch * 8, p);
+      unpack8(p, v[c]);
+    }
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        s += v[c][e];
-        ss += v[c][e] * v[c][e];
-      }
-    } else {
+    for (int e = 0; e < 8; ++e) {
+      v[c][e] = live ? v[c][e] : 0.f;
+      s += v[c][e];
+      ss += v[c][e] * v[c][e];
+    }
+  }
+  if constexpr (!EARLY_GB) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[c][e] = 0.f;
+    for (int c = 0; c < CPL; ++c) {
+      const int off = min(lane + 64 * c, nch - 1) * 8;
+      graw[c] = ld16(gamma + off);
+      braw[c] = ld16(bsrc + off);
     }
   }
   s = wave_sum(s);
@@ -77,6 +94,10 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const bf16* __restrict__
       float g[8], b[8], o[8];
       unpack8(graw[c], g);
       unpack8(braw[c], b);
+      if (!beta) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) b[e] = 0.f;
+      }
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = (v[c][e] - mean) * rstd * g[e] + b[e];
       st16(out + row * D + ch * 8, pack8(o));
