@@ -117,23 +117,25 @@ __global__ __launch_bounds__(256) void layernorm_rowblock_kernel(const bf16* __r
   const long row = blockIdx.x;
   const int t = threadIdx.x;
   const int nch = D >> 3;
+  // all loads issued unconditionally at clamped offsets before any use (as layernorm_kernel: the
+  // per-chunk guarded loads made hipcc wait vmcnt(0) per chunk); tail chunks are zeroed below
+  const bf16* xrow = x + row * D;
+  const bf16* rrow = res ? res + row * D : xrow;
   uint4 xraw[CPT], rraw[CPT], graw[CPT], braw[CPT];
 #pragma unroll
   for (int c = 0; c < CPT; ++c) {
-    const int ch = t + 256 * c;
-    xraw[c] = rraw[c] = graw[c] = braw[c] = make_uint4(0, 0, 0, 0);
-    if (ch < nch) {
-      xraw[c] = ld16(x + row * D + ch * 8);
-      if (res) rraw[c] = ld16(res + row * D + ch * 8);
-      graw[c] = ld16(gamma + ch * 8);
-      if (beta) braw[c] = ld16(beta + ch * 8);
-    }
+    const int off = min(t + 256 * c, nch - 1) * 8;
+    xraw[c] = ld16(xrow + off);
+    rraw[c] = ld16(rrow + off);
+    graw[c] = ld16(gamma + off);
+    braw[c] = ld16((beta ? beta : gamma) + off);
   }
   float v[CPT][8];
   float s = 0.f, ss = 0.f;
 #pragma unroll
   for (int c = 0; c < CPT; ++c) {
     const int ch = t + 256 * c;
+    const bool live = ch < nch;
     unpack8(xraw[c], v[c]);
     if (res) {
       float r[8];
@@ -141,13 +143,14 @@ __global__ __launch_bounds__(256) void layernorm_rowblock_kernel(const bf16* __r
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[c][e] += r[e];
     }
-    if (res_out && ch < nch) {
+    if (res_out) {
       const uint4 p = pack8(v[c]);
-      st16(res_out + row * D + ch * 8, p);
+      if (live) st16(res_out + row * D + ch * 8, p);
       unpack8(p, v[c]);
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
+      v[c][e] = live ? v[c][e] : 0.f;
       s += v[c][e];
       ss += v[c][e] * v[c][e];
     }
@@ -171,7 +174,7 @@ __global__ __launch_bounds__(256) void layernorm_rowblock_kernel(const bf16* __r
       unpack8(graw[c], g);
       unpack8(braw[c], b);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = (v[c][e] - mean) * rstd * g[e] + b[e];
+      for (int e = 0; e < 8; ++e) o[e] = (v[c][e] - mean) * rstd * g[e] + (beta ? b[e] : 0.f);
       st16(out + row * D + ch * 8, pack8(o));
     }
   }
