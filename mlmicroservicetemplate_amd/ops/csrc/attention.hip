@@ -729,8 +729,22 @@ __global__ __launch_bounds__(D) void decode_combine_kernel(const DecodeArgs a, i
   const int ns = min(a.nsplit, (L + chunk - 1) / chunk);
   if (ns <= 1) return;  // the split kernel wrote this row directly
   const long rec = (long)bh * a.nsplit;
+  // independent loads first, one round trip: the first 8 splits' partial O (clamped index, used
+  // below only for s < ns) and, when every split has a lane (ns <= D: always at the 64 / 128-row
+  // chunks up to 8k contexts), this lane's (m, l) pair -- kept for the second pass
+  const bool one = ns <= D;  // block-uniform
+  float vpre[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) vpre[j] = a.ws[(rec + min(j, ns - 1)) * D + d];
+  float2 mine = make_float2(-INFINITY, 0.f);
   float mloc = -INFINITY;
-  for (int s = d; s < ns; s += D) mloc = fmaxf(mloc, a.ws_ml[(rec + s) * 2]);
+  if (one) {
+    mine = *reinterpret_cast<const float2*>(a.ws_ml + (rec + min(d, ns - 1)) * 2);
+    if (d >= ns) mine = make_float2(-INFINITY, 0.f);
+    mloc = mine.x;
+  } else {
+    for (int s = d; s < ns; s += D) mloc = fmaxf(mloc, a.ws_ml[(rec + s) * 2]);
+  }
   __shared__ float red[D / 64];
   mloc = wave_max(mloc);
   if ((d & 63) == 0) red[d >> 6] = mloc;
@@ -739,10 +753,16 @@ __global__ __launch_bounds__(D) void decode_combine_kernel(const DecodeArgs a, i
 #pragma unroll
   for (int w = 1; w < D / 64; ++w) M = fmaxf(M, red[w]);
   float lloc = 0.f;
-  for (int s = d; s < ns; s += D) {
-    const float w = M == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(a.ws_ml[(rec + s) * 2] - M);
-    sw[s] = w;
-    lloc += a.ws_ml[(rec + s) * 2 + 1] * w;
+  if (one) {
+    const float w = (M == -INFINITY || d >= ns) ? 0.f : __builtin_amdgcn_exp2f(mine.x - M);
+    if (d < ns) sw[d] = w;
+    lloc = mine.y * w;
+  } else {
+    for (int s = d; s < ns; s += D) {
+      const float w = M == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(a.ws_ml[(rec + s) * 2] - M);
+      sw[s] = w;
+      lloc += a.ws_ml[(rec + s) * 2 + 1] * w;
+    }
   }
   lloc = wave_sum(lloc);
   __syncthreads();
@@ -756,7 +776,11 @@ __global__ __launch_bounds__(D) void decode_combine_kernel(const DecodeArgs a, i
   }
   __syncthreads();
   float O = 0.f;
-  int s = 0;
+  const int nf = min(ns, 8);
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    if (j < nf) O += vpre[j] * sw[j];
+  int s = nf;
   for (; s + 8 <= ns; s += 8) {
     float v[8];
 #pragma unroll

@@ -1,9 +1,9 @@
 # Row-block RMSNorm (decode) with batched loads: numerics, then Llama decode / serving A/B.
 export TMPDIR=/tmp
-OUT=gpurun_out/rbab
+OUT=gpurun_out/${RB_OUT:-rbab}
 mkdir -p $OUT
 BASE=$PWD/tools/probe/alt_lib/libmls_base.so
-timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_transformer_ops_gpu.py tests/test_models_gpu.py tests/test_continuous_device_gpu.py > $OUT/pytest.log 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_transformer_ops_gpu.py tests/test_models_gpu.py tests/test_continuous_device_gpu.py tests/test_kv_pages_gpu.py tests/test_llama_tp_gpu.py > $OUT/pytest.log 2>&1; rc=$?
 tail -3 $OUT/pytest.log
 [ $rc -eq 0 ] || { grep -B5 -A30 "Error\b\|assert" $OUT/pytest.log | head -80; exit $rc; }
 l() {
