@@ -1,6 +1,6 @@
 # End of round: full GPU suite, default bench, smoke, then 5 driver-style 20-step runs.
 export TMPDIR=/tmp
-OUT=gpurun_out/final5
+OUT=gpurun_out/${FIN_OUT:-final5}
 mkdir -p $OUT
 timeout -k 10 1500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1; rc=$?
 tail -3 $OUT/pytest.log
