@@ -194,11 +194,11 @@ def run_rank(args) -> int:
                 t = pending.pop(0)
                 t.wait()
                 lat.append(time.perf_counter() - t.t_submit)
-                events.append((t.t_submit, time.perf_counter()))
+                events.append((t.t_submit, time.perf_counter(), getattr(t, "stamps", None)))
         for t in pending:
             t.wait()
             lat.append(time.perf_counter() - t.t_submit)
-            events.append((t.t_submit, time.perf_counter()))
+            events.append((t.t_submit, time.perf_counter(), getattr(t, "stamps", None)))
 
     phases = os.environ.get("MLS_BENCH_PHASES")  # diagnostics: wall-clock stamps of the phases
 
@@ -231,7 +231,11 @@ def run_rank(args) -> int:
         with open(tickets_log, "a") as f:
             f.write(json.dumps({"steps": args.steps, "elapsed_ms": elapsed * 1e3,
                                 "tickets_ms": [[round((a - t_start) * 1e3, 3), round((b - t_start) * 1e3, 3)]
-                                               for a, b in events]}) + "\n")
+                                               for a, b, _ in events],
+                                # per submit: slot wait, staging, enqueue (ms)
+                                "submit_phases_ms": [None if st is None else
+                                                     [round((st[i + 1] - st[i]) * 1e3, 3) for i in range(3)]
+                                                     for _, _, st in events]}) + "\n")
     elapsed_max = mdist.max_over_ranks(elapsed)
     p50 = float(np.percentile(lat, 50)) * 1e3
     p99 = float(np.percentile(lat, 99)) * 1e3

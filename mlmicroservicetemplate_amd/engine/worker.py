@@ -72,7 +72,7 @@ class _Slot:
 class Ticket:
     """Handle for an enqueued batch; :meth:`wait` returns numpy outputs trimmed to ``n`` rows."""
 
-    __slots__ = ("engine", "slot", "bucket", "n", "t_submit", "_result", "staged")
+    __slots__ = ("engine", "slot", "bucket", "n", "t_submit", "_result", "staged", "stamps")
 
     def __init__(self, engine: "GpuEngine", slot: _Slot, bucket: int, n: int, staged: Optional["Prepared"] = None):
         self.engine = engine
@@ -82,6 +82,7 @@ class Ticket:
         self.t_submit = time.perf_counter()
         self._result = None
         self.staged = staged  # a prepared batch's pinned buffer, returned to the pool on completion
+        self.stamps = None  # submit(): perf_counter at slot wait / staged / enqueued (diagnostics)
 
     def wait(self) -> Tuple[np.ndarray, ...]:
         if self._result is None:
@@ -334,7 +335,9 @@ class GpuEngine:
         if n == 0:
             raise ValueError("empty batch")
         pick_bucket(n, self.buckets)  # validate before taking a slot
+        t0 = time.perf_counter()
         slot = self._free.get()  # blocks while `inflight` batches are outstanding
+        t1 = time.perf_counter()
         try:
             with tracing.range(self._tr_stage):
                 dst = slot.host_in.numpy() if self.sample_dtype != torch.bfloat16 else None
@@ -351,7 +354,12 @@ class GpuEngine:
             self._free.put(slot)
             self.last_error = f"{type(e).__name__}: {e}"
             raise
-        return self.launch(slot, n)
+        t2 = time.perf_counter()
+        tk = self.launch(slot, n)
+        # host phases of this submit (slot wait, staging copy, enqueue): diagnostics for the bench's
+        # ticket log (MLS_BENCH_TICKETS), e.g. to place a multi-ms host stall
+        tk.stamps = (t0, t1, t2, time.perf_counter())
+        return tk
 
     def prepare(self, samples) -> Prepared:
         """Stage a batch into a spare pinned buffer without taking a slot (blocks only while every
