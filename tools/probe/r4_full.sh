@@ -1,5 +1,5 @@
 export TMPDIR=/tmp
-OUT=gpurun_out/full4
+OUT=gpurun_out/full5
 mkdir -p $OUT
 timeout -k 10 1500 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1; rc=$?
 tail -5 $OUT/pytest.log
