@@ -194,11 +194,13 @@ def run_rank(args) -> int:
                 t = pending.pop(0)
                 t.wait()
                 lat.append(time.perf_counter() - t.t_submit)
-                events.append((t.t_submit, time.perf_counter(), getattr(t, "stamps", None)))
+                events.append((t.t_submit, time.perf_counter(), getattr(t, "stamps", None),
+                               getattr(t, "launch_ns", None)))
         for t in pending:
             t.wait()
             lat.append(time.perf_counter() - t.t_submit)
-            events.append((t.t_submit, time.perf_counter(), getattr(t, "stamps", None)))
+            events.append((t.t_submit, time.perf_counter(), getattr(t, "stamps", None),
+                           getattr(t, "launch_ns", None)))
 
     phases = os.environ.get("MLS_BENCH_PHASES")  # diagnostics: wall-clock stamps of the phases
 
@@ -231,11 +233,14 @@ def run_rank(args) -> int:
         with open(tickets_log, "a") as f:
             f.write(json.dumps({"steps": args.steps, "elapsed_ms": elapsed * 1e3,
                                 "tickets_ms": [[round((a - t_start) * 1e3, 3), round((b - t_start) * 1e3, 3)]
-                                               for a, b, _ in events],
+                                               for a, b, _, _ in events],
                                 # per submit: slot wait, staging, enqueue (ms)
                                 "submit_phases_ms": [None if st is None else
                                                      [round((st[i + 1] - st[i]) * 1e3, 3) for i in range(3)]
-                                                     for _, _, st in events]}) + "\n")
+                                                     for _, _, st, _ in events],
+                                # per native enqueue: H2D copy, graph launch, D2H copies, event (us)
+                                "launch_us": [None if ln is None else [round(x / 1e3, 1) for x in ln]
+                                              for _, _, _, ln in events]}) + "\n")
     elapsed_max = mdist.max_over_ranks(elapsed)
     p50 = float(np.percentile(lat, 50)) * 1e3
     p99 = float(np.percentile(lat, 99)) * 1e3

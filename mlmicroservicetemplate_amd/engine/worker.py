@@ -72,7 +72,7 @@ class _Slot:
 class Ticket:
     """Handle for an enqueued batch; :meth:`wait` returns numpy outputs trimmed to ``n`` rows."""
 
-    __slots__ = ("engine", "slot", "bucket", "n", "t_submit", "_result", "staged", "stamps")
+    __slots__ = ("engine", "slot", "bucket", "n", "t_submit", "_result", "staged", "stamps", "launch_ns")
 
     def __init__(self, engine: "GpuEngine", slot: _Slot, bucket: int, n: int, staged: Optional["Prepared"] = None):
         self.engine = engine
@@ -83,6 +83,8 @@ class Ticket:
         self._result = None
         self.staged = staged  # a prepared batch's pinned buffer, returned to the pool on completion
         self.stamps = None  # submit(): perf_counter at slot wait / staged / enqueued (diagnostics)
+        # native enqueue: ns spent in its H2D copy, graph launch, D2H copies and event record
+        self.launch_ns: Optional[Tuple[int, ...]] = None
 
     def wait(self) -> Tuple[np.ndarray, ...]:
         if self._result is None:
@@ -314,11 +316,12 @@ class GpuEngine:
             src = (ctypes.c_void_p * max(n, 1))(*[d.data_ptr() for d in outs])
             nb = (ctypes.c_longlong * max(n, 1))(*[d.numel() * d.element_size() for d in outs])
             h2d = slot.host_in[:b]
+            t_ns = (ctypes.c_longlong * 5)()  # per-call host times of the last enqueue (diagnostics)
             args = (slot.s_comp.cuda_stream, slot.dev_in.data_ptr(), slot.host_in.data_ptr(),
-                    h2d.numel() * h2d.element_size(), exec_h, n, dst, src, nb, ev)
+                    h2d.numel() * h2d.element_size(), exec_h, n, dst, src, nb, ev, t_ns)
             if not exec_h or not ev:
                 raise RuntimeError("graph exec / event handle unavailable")
-            slot.native[b] = (fn, args, (dst, src, nb))  # keep the arrays alive
+            slot.native[b] = (fn, args, (dst, src, nb, t_ns))  # keep the arrays alive
         except Exception as e:  # noqa: BLE001 - keep the Python enqueue
             logger.warning("%s: native launch unavailable (%s); Python enqueue", self.name, e)
             self.native_launch = False
@@ -445,7 +448,10 @@ class GpuEngine:
                     rc = fn(*args)
                 if rc != 0:
                     raise RuntimeError(f"mls_engine_launch failed (HIP error {rc})")
-                return Ticket(self, slot, bucket, n, staged)
+                tk = Ticket(self, slot, bucket, n, staged)
+                t_ns = _keep[3]
+                tk.launch_ns = tuple(t_ns[i + 1] - t_ns[i] for i in range(4))
+                return tk
             with self._enqueue_lock, torch.cuda.device(self.device):
                 self._pace_launch()
                 if self.use_graphs and slot.graph_copies.get(bucket):

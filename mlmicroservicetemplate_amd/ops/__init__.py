@@ -19,18 +19,9 @@ from ._core import (  # noqa: F401
     ACT_SILU_MUL,
     ACT_TANH,
     StreamWorkspace,
-    _ACTS,
-    _act,
-    _need,
-    _ptr,
-    _workspace_args,
     conv_out_hw,
 )
 from .tables import (  # noqa: F401
-    _TABLE_MISSES,
-    _TUNED_DIR,
-    _note_miss,
-    _ops_log,
     gemm_plan,
     gemm_tile_plan,
     load_blas_tuning,
@@ -42,9 +33,6 @@ from .gemm_ops import (  # noqa: F401
     FP8_MAX,
     GEMM_TILE_CFGS,
     SPLIT_COUNTER_ELEMS,
-    _BF16_BIAS,
-    _SPLIT_COUNTERS,
-    _bias_bf16,
     fold_norm,
     fp8_reference,
     gemm,
@@ -64,8 +52,6 @@ from .gemm_ops import (  # noqa: F401
 from .dispatch import (  # noqa: F401
     BLAS_MIN_M,
     TILE_MIN_M,
-    _GEMM_IMPL,
-    _linear_blas,
     linear,
 )
 from .softmax import (  # noqa: F401
@@ -82,7 +68,6 @@ from .vision import (  # noqa: F401
     HALO_CFGS,
     PIPE_CFGS,
     PIPE_VARIANTS,
-    _MEAN_STD_CACHE,
     avgpool_global_nhwc,
     bn_act,
     conv1x1_chain,
@@ -126,11 +111,6 @@ from .image import (  # noqa: F401
 )
 from .partition import (  # noqa: F401
     MASK_WORDS,
-    _MASKED_LOCK,
-    _MASKED_STREAMS,
-    _PARTITION_MASKS,
-    _XCD_MASKS,
-    _partition_masks,
     census_cus,
     cu_census,
     cu_masked_stream,

@@ -74,6 +74,7 @@ _SIGS = {
     "mls_ar_open": [P, P],
     "mls_ar_allreduce": [P, P, P, L, _c.c_longlong, P],
     "mls_ar_error": [P, P],
+    "mls_ar_set_timeout": [P, _c.c_longlong],
     "mls_ar_allgather": [P, P, P, L, _c.c_longlong, P],
     "mls_ar_reset": [P],
     "mls_gpu_sleep": [L, P],
@@ -99,7 +100,7 @@ _SIGS = {
 }
 _OPTIONAL_SIGS: dict = {"mls_set_debug_flags": [I], "mls_chain_set_l2_cw": [I],
     "mls_chain_set_l2_bm": [I],
-    "mls_engine_launch": [P, P, P, _c.c_longlong, P, I, P, P, P, P], "mls_skinny_set_variant": [I], "mls_skinny_set_max_split": [I]}
+    "mls_engine_launch": [P, P, P, _c.c_longlong, P, I, P, P, P, P, P], "mls_skinny_set_variant": [I], "mls_skinny_set_max_split": [I]}
 
 
 class NativeError(RuntimeError):

@@ -53,7 +53,9 @@ struct ArFuse {
 //   wait until every peer finished reading this staging half two epochs ago, stage the chunk,
 //   publish ready everywhere, wait for every peer's ready, sum the chunk over all ranks (fp32, the
 //   same peer order on every rank -> identical bytes everywhere), publish done.
-MLS_DEV void ar_oneshot_chunk(const ArFuse& f, const bf16* in, bf16* out, long n, int c) {
+// `timeout` bounds each peer wait (spin iterations); returns false when one of them ran out (the
+// error word is set too), so a caller running several chunks can stop waiting on a lost peer.
+MLS_DEV bool ar_oneshot_chunk(const ArFuse& f, const bf16* in, bf16* out, long n, int c, long long timeout) {
   __shared__ int s_epoch, s_ok;
   const int tid = threadIdx.x, nt = blockDim.x;
   if (tid == 0) {
@@ -64,7 +66,7 @@ MLS_DEV void ar_oneshot_chunk(const ArFuse& f, const bf16* in, bf16* out, long n
   const int e = s_epoch, parity = e & 1;
   const long lo = (long)c * AR_ELEMS_PER_BLOCK, hi = lo + AR_ELEMS_PER_BLOCK < n ? lo + AR_ELEMS_PER_BLOCK : n;
   if (tid < f.world && e > 2) {
-    if (!ar_wait_ge(ar_done(f.bufs[f.rank], f.cap, f.max_blocks, tid, c), e - 2, f.timeout)) s_ok = 0;
+    if (!ar_wait_ge(ar_done(f.bufs[f.rank], f.cap, f.max_blocks, tid, c), e - 2, timeout)) s_ok = 0;
   }
   __syncthreads();
   bf16* stage = reinterpret_cast<bf16*>(f.bufs[f.rank] + parity * f.cap);
@@ -75,7 +77,7 @@ MLS_DEV void ar_oneshot_chunk(const ArFuse& f, const bf16* in, bf16* out, long n
     __hip_atomic_store(ar_ready(f.bufs[tid], f.cap, f.max_blocks, f.rank, c), e, __ATOMIC_RELEASE,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   if (tid < f.world) {
-    if (!ar_wait_ge(ar_ready(f.bufs[f.rank], f.cap, f.max_blocks, tid, c), e, f.timeout)) s_ok = 0;
+    if (!ar_wait_ge(ar_ready(f.bufs[f.rank], f.cap, f.max_blocks, tid, c), e, timeout)) s_ok = 0;
   }
   __syncthreads();
   for (long i = lo + tid * 8; i < hi; i += (long)nt * 8) {
@@ -93,11 +95,13 @@ MLS_DEV void ar_oneshot_chunk(const ArFuse& f, const bf16* in, bf16* out, long n
   if (tid < f.world)
     __hip_atomic_store(ar_done(f.bufs[tid], f.cap, f.max_blocks, f.rank, c), e, __ATOMIC_RELEASE,
                        __HIP_MEMORY_SCOPE_SYSTEM);
+  const bool ok = s_ok != 0;
   if (tid == 0) {
     f.epochs[c] = e;
-    if (!s_ok) atomicOr(f.err, 1);
+    if (!ok) atomicOr(f.err, 1);
   }
   __syncthreads();  // s_epoch / s_ok are rewritten by the block's next chunk
+  return ok;
 }
 
 // The fused all-reduce tail of a GEMM whose output `out` [M][N] (row stride N, bf16) is this rank's
@@ -111,9 +115,14 @@ MLS_DEV void ar_fused_tail(const ArFuse& f, bf16* out, int M, int N, int c0, int
   __shared__ int s_last[MAXL];
   __shared__ int s_nlast;
   const long n = (long)M * N;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  // publish (MI355X_MICROARCH.md, Valid forms: Producer): every storing wave drains its stores,
+  // the block meets, then ONE lane releases at agent scope and waits for the write-back before
+  // its counter adds (the asm wait: hipcc may drop the fence's own, Guideline 16 Pitfall 12)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     int nl = 0;
     for (int m = 0; m < M; ++m) {
       const long lo = (long)m * N + c0, hi = lo + cols;
@@ -129,10 +138,16 @@ MLS_DEV void ar_fused_tail(const ArFuse& f, bf16* out, int M, int N, int c0, int
         }
       }
     }
-    if (nl) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (nl) {  // Consumer: one agent acquire, its invalidate completed before the barrier
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     s_nlast = nl;
   }
   __syncthreads();
   const int nl = s_nlast;
-  for (int i = 0; i < nl; ++i) ar_oneshot_chunk(f, out, out, n, s_last[i]);
+  // a chunk whose peer wait ran out means a lost peer: the block's later chunks do not spin the
+  // full bound again (each would cost ~timeout); they still publish so the epochs stay in step
+  bool alive = true;
+  for (int i = 0; i < nl; ++i) alive = ar_oneshot_chunk(f, out, out, n, s_last[i], alive ? f.timeout : 1) && alive;
 }

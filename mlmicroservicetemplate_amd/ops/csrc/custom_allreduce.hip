@@ -37,6 +37,7 @@ struct ArCtx {
   int max_blocks2;
   int* epochs2;
   int* fuse_cnt;                 // [max_blocks] arrival counters of the GEMMs that fuse the one-shot
+  long long timeout;             // peer-wait bound (spin iterations) of the GEMM-fused one-shot
 };
 
 // allocation layout: [2][cap] staging | ready[AR_MAX_RANKS][max_blocks] | done[...] | epochs | err
@@ -69,7 +70,7 @@ MLS_DEV ArFuse ar_view(const ArArgs& a) {
 }
 
 __global__ __launch_bounds__(AR_THREADS) void oneshot_allreduce_kernel(const ArArgs a) {
-  ar_oneshot_chunk(ar_view(a), a.in, a.out, a.n, blockIdx.x);
+  ar_oneshot_chunk(ar_view(a), a.in, a.out, a.n, blockIdx.x, a.timeout);
 }
 
 // X4: one-shot all-gather of `nbytes` per rank (the decode step's top-k candidates, a few KB):
@@ -247,6 +248,7 @@ int mls_ar_create2(int rank, int world, long cap, long cap2, void** ctx_out) {
       cap2 % 4096)
     return MLS_BAD_ARG;
   ArCtx* c = new ArCtx{};
+  c->timeout = 1LL << 24;
   c->rank = rank;
   c->world = world;
   c->cap = (size_t)cap;
@@ -297,7 +299,16 @@ int mls_ar_fuse_desc(void* ctx, long n, ArFuse* f) {
   f->epochs = c->epochs;
   f->err = c->err;
   f->cnt = c->fuse_cnt;
-  f->timeout = 1LL << 24;
+  f->timeout = c->timeout;
+  return 0;
+}
+
+// The peer-wait bound the GEMM-fused all-reduce uses (CustomAllReduce.timeout, MLS_AR_TIMEOUT_ITERS):
+// the standalone kernels take theirs per call.
+int mls_ar_set_timeout(void* ctx, long long iters) {
+  ArCtx* c = (ArCtx*)ctx;
+  if (!c || iters <= 0) return MLS_BAD_ARG;
+  c->timeout = iters;
   return 0;
 }
 

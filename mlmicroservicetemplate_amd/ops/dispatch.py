@@ -1,18 +1,14 @@
 """Projection dispatch policy (``linear``): which GEMM kernel a transformer projection runs on."""
 from __future__ import annotations
 
-import ctypes  # noqa: F401
-import functools  # noqa: F401
-import json  # noqa: F401
-import os  # noqa: F401
-from typing import Dict, List, Optional, Sequence, Tuple  # noqa: F401
+import os
+from typing import Optional
 
 import torch
 
-from ._lib import NativeError, available, check, lib, stream_ptr  # noqa: F401
-from ._core import ACT_GELU, ACT_NONE, ACT_SILU_MUL, _act  # noqa: F401
-from .gemm_ops import _bias_bf16, gemm, gemm_tile, silu_mul_interleaved  # noqa: F401
-from .tables import small_m_plan_for, tile_cfg_for, tile_route_for  # noqa: F401
+from ._core import ACT_GELU, ACT_NONE, ACT_SILU_MUL, _act
+from .gemm_ops import _bias_bf16, gemm, gemm_tile, silu_mul_interleaved
+from .tables import small_m_plan_for, tile_cfg_for, tile_route_for
 
 
 # Large-M projections run on the native LDS-DMA MFMA tile kernel (gemm_tile: csrc/gemm_tile.hip),

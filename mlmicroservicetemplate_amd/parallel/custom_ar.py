@@ -48,13 +48,13 @@ class CustomAllReduce:
         self.cap2 = int(cap2_bytes if cap2_bytes is not None else os.environ.get("MLS_AR_TWO_SHOT_CAP", 4 << 20))
         self.two_shot_min = int(two_shot_min if two_shot_min is not None
                                 else os.environ.get("MLS_AR_TWO_SHOT_MIN", 128 << 10))
-        # peer-wait bound in spin iterations (~1 s by default); MLS_AR_TIMEOUT_ITERS shrinks it (tests)
-        self.timeout = int(timeout_iters if timeout_iters is not None
-                           else os.environ.get("MLS_AR_TIMEOUT_ITERS", str(1 << 24)))
         self.enabled = False
         self.reason = ""
         self._lib = _lib.lib()
         self._ctx = ctypes.c_void_p()
+        # peer-wait bound in spin iterations (~1 s by default); MLS_AR_TIMEOUT_ITERS shrinks it (tests)
+        self._timeout = int(timeout_iters if timeout_iters is not None
+                            else os.environ.get("MLS_AR_TIMEOUT_ITERS", str(1 << 24)))
         try:
             self._setup()
             if self_test:
@@ -70,6 +70,7 @@ class CustomAllReduce:
             rc = L.mls_ar_create2(self.rank, self.world, self.cap, self.cap2, ctypes.byref(self._ctx))
             if rc != 0:
                 raise RuntimeError(f"mls_ar_create failed ({rc})")
+            self.timeout = self._timeout  # into the context too (the GEMM-fused all-reduce's bound)
             hs = L.mls_ar_handle_size()
             mine = (ctypes.c_char * hs)()
             if L.mls_ar_handle(self._ctx, ctypes.cast(mine, ctypes.c_void_p)) != 0:
@@ -135,6 +136,18 @@ class CustomAllReduce:
     def fusable(self, nelems: int) -> bool:
         """May a GEMM producing ``nelems`` bf16 outputs fuse the one-shot all-reduce of them?"""
         return self.enabled and nelems % 8 == 0 and nelems * 2 <= self.cap and nelems * 2 < self.two_shot_min
+
+    @property
+    def timeout(self) -> int:
+        """Peer-wait bound (spin iterations) of every one-shot / two-shot wait, the all-reduce
+        fused into the decode GEMMs (``ops.skinny_packed_ar``) included."""
+        return self._timeout
+
+    @timeout.setter
+    def timeout(self, iters: int) -> None:
+        self._timeout = int(iters)
+        if self._ctx and self._lib.mls_ar_set_timeout(self._ctx, self._timeout) != 0:
+            raise RuntimeError("mls_ar_set_timeout failed")
 
     def errors(self) -> int:
         """Read (and clear) the peer-wait timeout word: non-zero = some one-shot collective since the

@@ -114,6 +114,34 @@ def main():
         fails += err > 2e-2
         fails += int(not torch.all(z.float() == sum(r + it for r in range(world))).item())
     fails += car._errors()
+    # a peer lost before a GEMM-fused all-reduce: the fused kernel's peer waits honour
+    # CustomAllReduce.timeout (not a built-in ~1 s per chunk), a block that timed out on one chunk
+    # does not spin the full bound again on its next ones, and the error word reports it
+    import time
+
+    x = (torch.randn(8, 1792, generator=gw) * 0.5).to(torch.bfloat16).to(dev)
+    wp = ops.pack_skinny((torch.randn(4096, 1792, generator=gw) / 1792 ** 0.5).to(torch.bfloat16).to(dev))
+    torch.cuda.synchronize()
+    dist.barrier()
+    car.timeout = 20000
+    t0 = time.perf_counter()
+    if rank == world - 1:
+        ops.gpu_sleep(1500000)  # the "lost" peer arrives 1.5 s late
+    ops.skinny_packed_ar(x, wp, 4096, car)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if rank != world - 1:
+        err = car._errors()
+        print(f"rank {rank} fused stall: {dt * 1e3:.1f} ms, error word {err}", flush=True)
+        fails += int(err == 0) + int(dt > 1.0)
+    dist.barrier()
+    car._errors()
+    car.reset()
+    car.timeout = 1 << 24
+    y = ops.skinny_packed_ar(xd, ops.pack_skinny(w.to(dev)), 4096, car)  # the protocol works again
+    torch.cuda.synchronize()
+    fails += int((y.float().cpu() - ref).abs().max().item() / ref.abs().max().item() > 2e-2)
+    fails += car._errors()
     car.close()
     dist.destroy_process_group()
     print(f"rank {rank} fails {fails}")
