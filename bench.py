@@ -246,6 +246,11 @@ def run_rank(args) -> int:
     p99 = float(np.percentile(lat, 99)) * 1e3
     p50_max = mdist.max_over_ranks(p50)
     p99_max = mdist.max_over_ranks(p99)
+    host_ms = host_s[0] * 1e3 / args.steps
+    host_ms_max = mdist.max_over_ranks(host_ms)  # the slowest rank's host side
+    from mlmicroservicetemplate_amd.parallel.affinity import host_plan_hint
+
+    plan = host_plan_hint()
 
     total_req = world * args.batch * args.steps
     value = total_req / elapsed_max
@@ -290,7 +295,9 @@ def run_rank(args) -> int:
             **({"pytorch_eager_per_gpu_requests_per_s": round(eager, 1),
                 "vs_pytorch_eager_per_gpu": round(value / world / eager, 3)} if eager else {}),
             "weight_broadcast_s": round(t_bcast, 3),
-            "host_submit_ms_per_step": round(host_s[0] * 1e3 / args.steps, 4),
+            "host_submit_ms_per_step": round(host_ms, 4),
+            **({"host_submit_ms_per_step_max_rank": round(host_ms_max, 4),
+                "host_plan_rank0": plan} if world > 1 else {}),
         }
         print(json.dumps(out), flush=True)
     mdist.destroy()

@@ -178,6 +178,13 @@ class GpuEngine:
         # of host time per batch.  The instrumented Python sequence runs while tracing is active.
         self.native_launch = (self.copies_on_slot_stream and use_graphs and not self.graph_copies
                               and os.environ.get("MLS_NATIVE_LAUNCH", "1") == "1")
+        # zero-copy H2D (MLS_PULL_H2D=<workgroups>, 0 = off): the slot's graph starts with a
+        # small copy kernel that pulls the pinned batch over PCIe (ops.h2d_pull) instead of an SDMA
+        # hipMemcpyAsync -- the SDMA path occasionally blocked the enqueue ~6 ms with every queue of
+        # the process stalled (docs/PERF_NOTES.md, round 5)
+        self.pull_h2d = int(os.environ.get("MLS_PULL_H2D", "0")) if (
+            self.copies_on_slot_stream and use_graphs and not self.graph_copies
+            and sample_dtype == torch.uint8) else 0
         # host staging (request arrays -> pinned slot): a persistent native copy pool (GIL released,
         # the submitting thread copies too); one thread's ~5-8 GB/s memcpy is not enough for a
         # 4.8 MB ResNet batch every ~0.6 ms next to the rest of the host loop
@@ -276,6 +283,10 @@ class GpuEngine:
                                               capture_error_mode="thread_local"):
                             if in_graph:
                                 slot.dev_in[:b].copy_(slot.host_in[:b], non_blocking=True)
+                            elif self.pull_h2d:
+                                from .. import ops
+
+                                ops.h2d_pull(slot.host_in[:b], slot.dev_in[:b], self.pull_h2d)
                             outs = self.forward(slot.dev_in[:b])
                             if in_graph:
                                 for h, d in zip(slot.host_out[b], outs):
@@ -288,6 +299,22 @@ class GpuEngine:
                 torch.cuda.synchronize(self.device)
                 logger.info("%s: captured %d hipGraphs (%d slots x buckets %s)", self.name,
                             len(self.slots) * len(self.buckets), len(self.slots), self.buckets)
+            self._prewarm_copies(int(os.environ.get("MLS_COPY_PREWARM", "0")))
+
+    def _prewarm_copies(self, rounds: int) -> None:
+        """``rounds`` x (H2D of every slot's whole input buffer + its D2H copies) on the slot streams
+        (A/B of the copy-engine warm-up, tools/probe/r5_sdma_ab2.sh)."""
+        if rounds <= 0:
+            return
+        with torch.cuda.device(self.device):
+            for _ in range(rounds):
+                for slot in self.slots:
+                    with torch.cuda.stream(slot.s_comp):
+                        slot.dev_in.copy_(slot.host_in, non_blocking=True)
+                        for b in self.buckets:
+                            for h, d in zip(slot.host_out.get(b, ()), slot.outs.get(b, ())):
+                                h.copy_(d, non_blocking=True)
+            torch.cuda.synchronize(self.device)
 
     def _prepare_native(self, slot: _Slot, b: int) -> None:
         """The mls_engine_launch argument tuple of (slot, bucket): raw stream / buffer / graph-exec /
@@ -317,8 +344,9 @@ class GpuEngine:
             nb = (ctypes.c_longlong * max(n, 1))(*[d.numel() * d.element_size() for d in outs])
             h2d = slot.host_in[:b]
             t_ns = (ctypes.c_longlong * 5)()  # per-call host times of the last enqueue (diagnostics)
+            h2d_bytes = 0 if self.pull_h2d else h2d.numel() * h2d.element_size()  # pulled in the graph
             args = (slot.s_comp.cuda_stream, slot.dev_in.data_ptr(), slot.host_in.data_ptr(),
-                    h2d.numel() * h2d.element_size(), exec_h, n, dst, src, nb, ev, t_ns)
+                    h2d_bytes, exec_h, n, dst, src, nb, ev, t_ns)
             if not exec_h or not ev:
                 raise RuntimeError("graph exec / event handle unavailable")
             slot.native[b] = (fn, args, (dst, src, nb, t_ns))  # keep the arrays alive
@@ -443,7 +471,9 @@ class GpuEngine:
                 with self._enqueue_lock:
                     self._pace_launch()
                     fn, args, _keep = nat
-                    if staged is not None:  # same call, H2D from the prepared buffer
+                    if staged is not None and self.pull_h2d:  # the graph pulls from the slot's buffer
+                        slot.host_in.numpy()[:n] = staged.buf.numpy()[:n]
+                    elif staged is not None:  # same call, H2D from the prepared buffer
                         args = args[:2] + (staged.buf.data_ptr(),) + args[3:]
                     rc = fn(*args)
                 if rc != 0:
@@ -465,8 +495,12 @@ class GpuEngine:
                     return Ticket(self, slot, bucket, n, staged)
                 s_h2d = slot.s_comp if self.copies_on_slot_stream else self.s_h2d
                 s_d2h = slot.s_comp if self.copies_on_slot_stream else self.s_d2h
+                pulled = self.pull_h2d and self.use_graphs and bucket in slot.graphs
+                if pulled and staged is not None:  # the graph pulls from the slot's own buffer
+                    slot.host_in[:n].copy_(staged.buf[:n])
                 with tracing.range(self._tr_h2d), torch.cuda.stream(s_h2d):
-                    slot.dev_in[:bucket].copy_(src_host[:bucket], non_blocking=True)
+                    if not pulled:
+                        slot.dev_in[:bucket].copy_(src_host[:bucket], non_blocking=True)
                     slot.ev_h2d.record(s_h2d)
                 slot.s_comp.wait_event(slot.ev_h2d)
                 with tracing.range(self._tr_replay), torch.cuda.stream(slot.s_comp):

@@ -107,6 +107,7 @@ from .image import (  # noqa: F401
     IMAGE_CONTAINER_BYTES,
     IMAGE_SCRATCH_PER_IMAGE,
     gpu_sleep,
+    h2d_pull,
     image_decode,
 )
 from .partition import (  # noqa: F401

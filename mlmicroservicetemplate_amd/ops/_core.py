@@ -1,15 +1,10 @@
 """Shared helpers of the ops wrappers: activation codes, argument checks, per-stream scratch."""
 from __future__ import annotations
 
-import ctypes  # noqa: F401
-import functools  # noqa: F401
-import json  # noqa: F401
-import os  # noqa: F401
-from typing import Dict, List, Optional, Sequence, Tuple  # noqa: F401
+from typing import Optional, Tuple
 
 import torch
 
-from ._lib import NativeError, available, check, lib, stream_ptr  # noqa: F401
 
 ACT_NONE, ACT_RELU, ACT_GELU, ACT_TANH, ACT_SILU, ACT_SILU_MUL = 0, 1, 2, 3, 4, 5
 

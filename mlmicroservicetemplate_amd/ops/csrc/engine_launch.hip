@@ -9,6 +9,8 @@
 
 #include <time.h>
 
+typedef unsigned int u32x4v_e __attribute__((__vector_size__(16)));
+
 namespace {
 inline long long now_ns() {
   timespec ts;
@@ -17,7 +19,43 @@ inline long long now_ns() {
 }
 }  // namespace
 
+// Zero-copy H2D: a few workgroups pull a pinned host buffer (mapped in the GPU's address space)
+// over PCIe into device memory -- a kernel in the slot's own stream (and captured into its graph),
+// so no SDMA copy-engine queue takes part: the SDMA H2D of a 4.8 MB batch occasionally blocked the
+// enqueue ~6 ms with every queue of the process stalled (tools/probe/r5_stall.sh: 4 of ~60 20-step
+// runs; none with HSA_ENABLE_SDMA=0, whose blit kernels cost 7 %).  U 16-B loads in flight per
+// lane; offsets past `bytes` read zero / store nothing (buffer range check), so no tail branch.
+template <int U>
+__global__ __launch_bounds__(256) void h2d_pull_kernel(const void* src, void* dst, uint32_t bytes, int iters) {
+  const rsrc_t s = make_rsrc(src, bytes), d = make_rsrc(dst, bytes);
+  const int stride = (int)gridDim.x * 256 * 16;
+  int off = ((int)blockIdx.x * 256 + (int)threadIdx.x) * 16;
+  for (int it = 0; it < iters; ++it) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      v[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(s, off + u * stride, 0, 2));  // nt
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v_e, v[u]), d, off + u * stride, 0, 0);
+    off += U * stride;
+  }
+}
+
 extern "C" {
+
+// src: pinned host memory (hipHostMalloc / torch pin_memory), dst: device memory, bytes % 16 == 0,
+// < 1 GiB.  blocks: workgroups pulling (each lane keeps 8 x 16 B in flight).
+int mls_h2d_pull(const void* src, void* dst, long long bytes, int blocks, void* stream) {
+  if (!src || !dst || bytes <= 0 || bytes % 16 || bytes >= (1LL << 30) || blocks <= 0 || blocks > 1024)
+    return MLS_BAD_ARG;
+  constexpr int U = 8;
+  const long long step = (long long)blocks * 256 * 16 * U;
+  const int iters = (int)((bytes + step - 1) / step);
+  hipLaunchKernelGGL(h2d_pull_kernel<U>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, src, dst,
+                     (uint32_t)bytes, iters);
+  return (int)hipGetLastError();
+}
 
 // d2h_*: n_d2h (<= 8) destination / source / byte-count triples.  t_ns (optional, 5 entries):
 // CLOCK_MONOTONIC before the H2D, after it, after the graph launch, after the D2H copies and after

@@ -45,7 +45,18 @@ constexpr int POOL_BYTES = NPOOL * COUT * 2;       // 4096: the pooled tile as t
 // output channels of one stem pixel and the epilogue writes 8 B per (row block, column block) --
 // 10 ds_write_b64 per lane per tile instead of 40 single-bf16 writes, one pixel-validity test per
 // row block instead of per element.
-template <int TILES_PER_BLOCK, bool CONV1, bool SWAP = true>
+// LDS-only block barrier: this wave's LDS accesses done, then s_barrier.  __syncthreads() would also
+// drain vmcnt -- the next tile's image bytes (fetched a tile ahead) and the pooled stores would
+// then complete at every barrier, exposing a full memory round trip per tile instead of hiding it.
+MLS_DEV void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// RAWB: the tile loop's barriers as lds_barrier() (default) instead of __syncthreads() (A/B,
+// MLS_STEM_RAWBAR=0).
+template <int TILES_PER_BLOCK, bool CONV1, bool SWAP = true, bool RAWB = true>
 __global__ __launch_bounds__(256, 3) void stem_pool_kernel(const uint8_t* __restrict__ img, const bf16* __restrict__ w,
                                                         const float* __restrict__ bias, bf16* __restrict__ out, int B,
                                                         int H, int W, int Po, float m0, float m1, float m2, float s0,
@@ -144,7 +155,8 @@ __global__ __launch_bounds__(256, 3) void stem_pool_kernel(const uint8_t* __rest
   for (int bx = bx0; bx < bx1; ++bx) {
     const int pw0 = bx * TPW;
     const int sc0 = 2 * pw0 - 1;
-    __syncthreads();  // the previous tile's patch / tile reads are done
+    if constexpr (RAWB) lds_barrier();  // the previous tile's patch / tile reads are done
+    else __syncthreads();
     // patch: normalised bf16 x 4 channels, zero outside the image
 #pragma unroll
     for (int it = 0; it < PIT; ++it) {
@@ -158,7 +170,8 @@ __global__ __launch_bounds__(256, 3) void stem_pool_kernel(const uint8_t* __rest
       *reinterpret_cast<uint2*>(smem + q * 8) = __builtin_bit_cast(uint2, v);
     }
     if (bx + 1 < bx1) fetch(bx + 1);  // next tile's bytes fly during this tile's math
-    __syncthreads();
+    if constexpr (RAWB) lds_barrier();
+    else __syncthreads();
 
     // MFMA over the 7 kernel rows
     f32x4 acc[5][2];
@@ -213,7 +226,8 @@ __global__ __launch_bounds__(256, 3) void stem_pool_kernel(const uint8_t* __rest
               trow[(i * 16 + r) * TSTR + j * 16] = (bf16)(((zero >> k) & 1u) ? 0.f : fmaxf(acc[i][j][r] + bj[j], 0.f));
           }
     }
-    __syncthreads();
+    if constexpr (RAWB) lds_barrier();
+    else __syncthreads();
 
     // 3x3 / 2 max pool: thread = one pooled pixel x 8 channels
     const int pp = tid >> 3, c8 = tid & 7;
@@ -268,9 +282,216 @@ __global__ __launch_bounds__(256, 3) void stem_pool_kernel(const uint8_t* __rest
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// v2 (default; MLS_STEM_V2=0 runs the kernel above).  What the v1 tile loop cost, read from its
+// ISA: the next tile's image bytes were fetched as ubyte / ushort loads that hipcc merges right
+// after issue (s_waitcnt vmcnt(6..1) straight behind the fetch), so every tile paid a full memory
+// round trip before its MFMAs; 448 blocks of 7 tiles left 64 CUs with one block and 192 with two
+// (the kernel lasts two blocks); the pool unpacked 9 x 8 bf16 to fp32 per thread.  v2:
+//  * tile = 7 x 4 pooled outputs (15 x 9 = 135 stem pixels, 9 MFMA row blocks); a block runs 7
+//    tiles along a pooled-row strip, the grid is 32 images x 8 strips x 2 halves = 512 blocks =
+//    exactly 2 per CU, all resident;
+//  * the patch (35 image rows x 28 columns, 4-pixel groups aligned to 4) is fetched as one 12-B
+//    load per thread and kept as raw dwords until the next tile writes it -- the fetch of tile t+1
+//    really flies under tile t's MFMAs;
+//  * waves = 2 row halves (5 / 4 row blocks) x 2 channel halves (2 column blocks): each A
+//    fragment read from LDS feeds two MFMAs;
+//  * 3x3/2 max pool on the raw bf16 bits with v_pk_max_u16 (post-ReLU values are >= 0, so their
+//    bf16 patterns order like unsigned integers), 4 packed maxes per tap instead of 16 fp32 ops.
+namespace v2 {
+constexpr int TPH = 7, TPW = 4;                 // pooled outputs per tile
+constexpr int SR = 2 * TPH + 1, SC = 2 * TPW + 1;  // 15 x 9 stem pixels
+constexpr int SP = SR * SC;                     // 135
+constexpr int RB = 9;                           // 16-row MFMA blocks (144 rows)
+constexpr int PRW = 2 * (SR - 1) + 7;           // patch image rows: 35
+constexpr int PG = 7;                           // 4-pixel column groups: 28 image columns
+constexpr int PSTR = 30;                        // patch row stride in pixels (240 B; col 0 unused)
+constexpr int PATCH_BYTES = (PRW + 2) * PSTR * 8;  // 8880: + 2 dummy rows that threads >= 245 write
+constexpr int TSTR = 72;                        // stem tile row stride (bf16): 144 B
+constexpr int TILE_BYTES = RB * 16 * TSTR * 2;  // 20736
+constexpr int TILES = 7;                        // per block
+constexpr int COUT = 64, KTOT = 7 * 32;
+}  // namespace v2
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4s __attribute__((__vector_size__(16)));
+
+__global__ __launch_bounds__(256, 2) void stem_pool_v2_kernel(const uint8_t* __restrict__ img, const bf16* __restrict__ w,
+                                                           const float* __restrict__ bias, bf16* __restrict__ out,
+                                                           uint32_t img_bytes, int B, float m0, float m1, float m2,
+                                                           float s0, float s1, float s2, long long* stamps) {
+  // stamps (diagnostics, MLS_STEM_STAMPS=1 via mls_stem_set_stamps): s_memtime of lane 0 of every
+  // wave at the kernel start, after the first loads, and at each phase boundary of each tile
+  constexpr int H = 224, W = 224, Po = 56;
+  __shared__ __attribute__((aligned(16))) char smem[v2::PATCH_BYTES + v2::TILE_BYTES];
+  bf16* tile = reinterpret_cast<bf16*>(smem + v2::PATCH_BYTES);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int half = blockIdx.x & 1, strip = (blockIdx.x >> 1) & 7, b = blockIdx.x >> 4;
+  const int ph0 = strip * v2::TPH;
+  const int sr0 = 2 * ph0 - 1;   // first stem row (may be -1)
+  const int ir0 = 2 * sr0 - 3;   // first image row of the patch
+  const rsrc_t ir = make_rsrc(img, img_bytes);
+
+  const int wm = wid >> 1, wn = wid & 1;  // row half (blocks 0-4 / 5-8), channel half
+  const int fr = lane & 15, fq = lane >> 4;
+  bf16x8 bw[2][7];
+  float bq[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = wn * 32 + j * 16 + fr;
+#pragma unroll
+    for (int kh = 0; kh < 7; ++kh)
+      bw[j][kh] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(w + (long)n * v2::KTOT + kh * 32 + fq * 8));
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bq[j][r] = bias[wn * 32 + j * 16 + fq * 4 + r];
+  }
+  // A-fragment offsets of this wave's row blocks: stem pixel p = (r, c) reads patch rows 2r + kh,
+  // columns 4 + 2c + 2fq (+1): the tap pair (2fq, 2fq + 1) of kernel row kh, 4 channels each
+  int abase[5];
+  uint32_t m_pad = 0, m_r0 = 0, m_c0 = 0;  // per row block: padding row, stem row 0, stem column 0
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const int rb = wm * 5 + i;
+    const int p0 = rb * 16 + fr;
+    const int p = p0 < v2::SP ? p0 : v2::SP - 1;
+    const int r = p / v2::SC, c = p - (p / v2::SC) * v2::SC;
+    abase[i] = ((2 * r) * v2::PSTR + 4 + 2 * c + 2 * fq) * 8;
+    m_pad |= (uint32_t)(p0 >= v2::SP) << i;
+    m_r0 |= (uint32_t)(r == 0) << i;
+    m_c0 |= (uint32_t)(c == 0) << i;
+  }
+
+  // patch fetch: thread q -> patch row q / 7, 4-pixel group q % 7 (12 bytes, 4-B aligned); threads
+  // >= 245 land in the two dummy rows (every thread writes: no divergent branch in the loop)
+  const int q = tid;
+  const int prow = q / v2::PG, pgrp = q - (q / v2::PG) * v2::PG;
+  uint32_t raw[3];
+  float valid;  // 1 / 0: a multiplier, not a select (a per-element select made hipcc branch + wait)
+  auto fetch = [&](int t) {
+    const int pc0 = half * (v2::TILES * v2::TPW) + t * v2::TPW;  // first pooled column of tile t
+    const int ix = 4 * pc0 - 8 + 4 * pgrp;           // 16 k - 8 + 4 g: a group is all in or all out
+    const int iy = ir0 + prow;
+    const bool ok = prow < v2::PRW && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+    valid = ok ? 1.f : 0.f;
+    const int off = ok ? ((b * H + iy) * W + ix) * 3 : OOB;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) raw[k] = __builtin_amdgcn_raw_buffer_load_b32(ir, off + 4 * k, 0, 0);
+  };
+  long long* st = stamps ? stamps + ((long)blockIdx.x * 4 + wid) * 64 : nullptr;
+  if (st && lane == 0) st[0] = __builtin_amdgcn_s_memtime();
+  fetch(0);
+  // tile 0's bytes (used at once anyway) and the weight / bias loads complete here: left pending,
+  // hipcc's wait pass merges them into the loop head's state and waits vmcnt(0) there (the
+  // previous tile's pooled store included) instead of vmcnt(1) for the prefetched bytes
+  __builtin_amdgcn_s_waitcnt(0);
+  if (st && lane == 0) st[1] = __builtin_amdgcn_s_memtime();
+  // pool: thread = pooled pixel pp (< 28) x 8-channel chunk; threads >= 224 redo pixel 27 and
+  // store out of range (dropped): every thread stores, so the loop head waits vmcnt(1) for the
+  // prefetched patch bytes, not vmcnt(0) behind a divergent store
+  const int pp = min(tid >> 3, v2::TPH * v2::TPW - 1), c8 = tid & 7;
+  const int pr = pp / v2::TPW, pc = pp - (pp / v2::TPW) * v2::TPW;
+  const rsrc_t orr = make_rsrc(out, (uint32_t)((long)B * Po * Po * v2::COUT * 2));
+
+  for (int t = 0; t < v2::TILES; ++t) {
+    const int pc0 = half * (v2::TILES * v2::TPW) + t * v2::TPW;
+    const int sc0 = 2 * pc0 - 1;
+    lds_barrier();  // the previous tile's patch / tile reads are done
+    if (st && lane == 0) st[2 + 6 * t] = __builtin_amdgcn_s_memtime();
+    {  // normalised bf16 x 4 channels (channel 3 = 0), zero outside the image; the same
+       // arithmetic as v1 ((x - mean) * inv_std, +0 outside), so both kernels give identical bits
+      const float ss[3] = {s0, s1, s2};
+      const float mm[3] = {m0, m1, m2};
+      const bool ok = valid != 0.f;
+      char* dst = smem + (prow * v2::PSTR + 1 + 4 * pgrp) * 8;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bf16x4 v;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const int byte = 3 * j + c;
+          const float x = (float)((raw[byte >> 2] >> (8 * (byte & 3))) & 0xffu);
+          const float nv = (x - mm[c]) * ss[c];
+          v[c] = (bf16)(ok ? nv : 0.f);
+        }
+        v[3] = (bf16)0.f;
+        *reinterpret_cast<uint2*>(dst + j * 8) = __builtin_bit_cast(uint2, v);
+      }
+    }
+    if (t + 1 < v2::TILES) fetch(t + 1);  // lands under this tile's MFMAs
+    if (st && lane == 0) st[3 + 6 * t] = __builtin_amdgcn_s_memtime();
+    lds_barrier();
+    if (st && lane == 0) st[4 + 6 * t] = __builtin_amdgcn_s_memtime();
+
+    f32x4 acc[5][2];
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kh = 0; kh < 7; ++kh) {
+      // every wave runs 5 row blocks (wave row half 1's fifth is padding, dropped by m_pad): no
+      // branch between the fragment reads and the MFMAs, and the critical wave does 5 anyway
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        const bf16x8 av = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(smem + abase[i] + kh * v2::PSTR * 8));
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j][kh], av, acc[i][j], 0, 0, 0);
+      }
+    }
+    if (st && lane == 0) st[5 + 6 * t] = __builtin_amdgcn_s_memtime();
+    // bias + ReLU -> bf16 stem tile; stem pixels outside the image (row / column -1) -> 0
+    const uint32_t zero = (sr0 < 0 ? m_r0 : 0u) | (sc0 < 0 ? m_c0 : 0u);
+    bf16* tp = tile + (wm * 80 + fr) * v2::TSTR + wn * 32 + fq * 4;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      if ((m_pad >> i) & 1u) continue;
+      const bool z = (zero >> i) & 1u;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        bf16x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = acc[i][j][r];  // through a named float (ext-vector element bit-cast hazard)
+          v[r] = (bf16)(z ? 0.f : fmaxf(e + bq[j][r], 0.f));
+        }
+        *reinterpret_cast<uint2*>(tp + i * 16 * v2::TSTR + j * 16) = __builtin_bit_cast(uint2, v);
+      }
+    }
+    if (st && lane == 0) st[6 + 6 * t] = __builtin_amdgcn_s_memtime();
+    lds_barrier();
+
+    {
+      u16x2 mx[4] = {u16x2{0, 0}, u16x2{0, 0}, u16x2{0, 0}, u16x2{0, 0}};
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+          const uint4 v = *reinterpret_cast<const uint4*>(tile + ((2 * pr + dy) * v2::SC + 2 * pc + dx) * v2::TSTR + c8 * 8);
+          mx[0] = __builtin_elementwise_max(mx[0], __builtin_bit_cast(u16x2, v.x));
+          mx[1] = __builtin_elementwise_max(mx[1], __builtin_bit_cast(u16x2, v.y));
+          mx[2] = __builtin_elementwise_max(mx[2], __builtin_bit_cast(u16x2, v.z));
+          mx[3] = __builtin_elementwise_max(mx[3], __builtin_bit_cast(u16x2, v.w));
+        }
+      const uint4 o{__builtin_bit_cast(uint32_t, mx[0]), __builtin_bit_cast(uint32_t, mx[1]),
+                    __builtin_bit_cast(uint32_t, mx[2]), __builtin_bit_cast(uint32_t, mx[3])};
+      const int ooff = tid < v2::TPH * v2::TPW * 8 ? ((((b * Po + ph0 + pr) * Po + pc0 + pc) * v2::COUT + c8 * 8) * 2) : OOB;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4s, o), orr, ooff, 0, 0);
+    }
+    if (st && lane == 0) st[7 + 6 * t] = __builtin_amdgcn_s_memtime();
+  }
+  if (st && lane == 0) st[2 + 6 * v2::TILES] = __builtin_amdgcn_s_memtime();
+}
 }  // namespace
 
 extern "C" {
+
+// diagnostics: v2 writes per-wave phase stamps ([blocks][4 waves][64] int64) here while set
+long long* g_stem_stamps = nullptr;
+int mls_stem_set_stamps(void* buf) {
+  g_stem_stamps = (long long*)buf;
+  return 0;
+}
 
 int mls_stem_pool_conv1(const void* images, const void* w, const float* bias, void* out, int B, int H, int W,
                         const float* mean3, const float* std3, const void* w1, const float* b1, void* t1,
@@ -306,6 +527,17 @@ int mls_stem_pool_conv1(const void* images, const void* w, const float* bias, vo
   const long blocks = (long)B * (Po / TPH) * ((Po / TPW + tpb - 1) / tpb);
   if (blocks > 0x7fffffffL) return MLS_BAD_ARG;
   const bool c1 = w1 != nullptr && t1 != nullptr;
+  static const bool use_v2 = [] {  // MLS_STEM_V2=0: the v1 kernel (A/B)
+    const char* e = getenv("MLS_STEM_V2");
+    return !(e && e[0] == '0');
+  }();
+  const long img_bytes = (long)B * H * W * 3;
+  if (use_v2 && !c1 && img_bytes < 0x7fffffffL) {
+    hipLaunchKernelGGL(stem_pool_v2_kernel, dim3((unsigned)(B * 16)), dim3(256), 0, (hipStream_t)stream,
+                       (const uint8_t*)images, (const bf16*)w, bias, (bf16*)out, (uint32_t)img_bytes, B, mean3[0],
+                       mean3[1], mean3[2], 1.f / std3[0], 1.f / std3[1], 1.f / std3[2], g_stem_stamps);
+    return (int)hipGetLastError();
+  }
   static const bool swap = [] {  // MLS_STEM_SWAP=0: the per-element epilogue (A/B)
     const char* e = getenv("MLS_STEM_SWAP");
     return !(e && e[0] == '0');
@@ -315,6 +547,13 @@ int mls_stem_pool_conv1(const void* images, const void* w, const float* bias, vo
                    : (tpb == 1 ? stem_pool_kernel<1, false> : tpb == 2 ? stem_pool_kernel<2, false>
                                          : tpb == 7 ? stem_pool_kernel<7, false> : stem_pool_kernel<4, false>);
   if (!swap && !c1 && tpb == 7) kernel = stem_pool_kernel<7, false, false>;
+  static const bool rawbar = [] {  // MLS_STEM_RAWBAR=0: __syncthreads() in the tile loop (A/B)
+    const char* e = getenv("MLS_STEM_RAWBAR");
+    return !(e && e[0] == '0');
+  }();
+  if (!rawbar && !c1 && swap)
+    kernel = tpb == 1 ? stem_pool_kernel<1, false, true, false> : tpb == 2 ? stem_pool_kernel<2, false, true, false>
+           : tpb == 7 ? stem_pool_kernel<7, false, true, false> : stem_pool_kernel<4, false, true, false>;
   hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, (const uint8_t*)images,
                      (const bf16*)w, bias, (bf16*)out, B, H, W, Po, mean3[0], mean3[1], mean3[2], 1.f / std3[0],
                      1.f / std3[1], 1.f / std3[2], dbg, (const bf16*)w1, b1, (bf16*)t1);

@@ -1,16 +1,13 @@
 """GEMM kernels: the conv_gemm-based plain GEMM, the persistent large-M tile GEMM, the skinny (decode) GEMMs."""
 from __future__ import annotations
 
-import ctypes  # noqa: F401
-import functools  # noqa: F401
-import json  # noqa: F401
-import os  # noqa: F401
-from typing import Dict, List, Optional, Sequence, Tuple  # noqa: F401
+import ctypes
+from typing import Dict, Optional, Tuple
 
 import torch
 
-from ._lib import NativeError, available, check, lib, stream_ptr  # noqa: F401
-from ._core import ACT_NONE, ACT_SILU_MUL, _act, _need, _ptr, _workspace_args  # noqa: F401
+from ._lib import check, lib, stream_ptr
+from ._core import ACT_NONE, ACT_SILU_MUL, _act, _need, _ptr, _workspace_args
 
 
 def gemm(

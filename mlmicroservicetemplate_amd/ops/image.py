@@ -1,16 +1,12 @@
 """GPU image decode (JPEG coefficient containers -> pixels) and test hooks."""
 from __future__ import annotations
 
-import ctypes  # noqa: F401
-import functools  # noqa: F401
-import json  # noqa: F401
-import os  # noqa: F401
-from typing import Dict, List, Optional, Sequence, Tuple  # noqa: F401
+from typing import Optional
 
 import torch
 
-from ._lib import NativeError, available, check, lib, stream_ptr  # noqa: F401
-from ._core import _need, _ptr  # noqa: F401
+from ._lib import check, lib, stream_ptr
+from ._core import _need, _ptr
 
 
 IMAGE_CONTAINER_BYTES = 64 + 224 * 224 * 3  # frontend/csrc/jpeg_coefs.h CONTAINER_BYTES
@@ -51,3 +47,17 @@ def gpu_sleep(us: int, device=None) -> None:
     """Hold the current stream of ``device`` for ``us`` microseconds (fault injection in tests)."""
     dev = torch.device(device if device is not None else "cuda")
     check(lib().mls_gpu_sleep(int(us), stream_ptr(dev)), "mls_gpu_sleep")
+
+
+def h2d_pull(src: torch.Tensor, dst: torch.Tensor, blocks: int = 32) -> torch.Tensor:
+    """Copy the pinned host tensor ``src`` into the device tensor ``dst`` with a kernel on the current
+    stream (zero-copy reads over PCIe; capturable into a hipGraph).  Same byte size, 16-B multiple."""
+    if src.is_cuda or not src.is_pinned() or not dst.is_cuda:
+        raise ValueError("h2d_pull: src must be pinned host memory and dst a device tensor")
+    if not (src.is_contiguous() and dst.is_contiguous()):
+        raise ValueError("h2d_pull: contiguous tensors only")
+    n = src.numel() * src.element_size()
+    if n != dst.numel() * dst.element_size():
+        raise ValueError("h2d_pull: size mismatch")
+    check(lib().mls_h2d_pull(src.data_ptr(), dst.data_ptr(), n, int(blocks), stream_ptr(dst.device)), "mls_h2d_pull")
+    return dst

@@ -1,15 +1,12 @@
 """CU-masked streams and the spatial partitions of the in-flight batches (census-verified masks)."""
 from __future__ import annotations
 
-import ctypes  # noqa: F401
-import functools  # noqa: F401
-import json  # noqa: F401
-import os  # noqa: F401
-from typing import Dict, List, Optional, Sequence, Tuple  # noqa: F401
+import ctypes
+from typing import Dict, List, Optional, Sequence
 
 import torch
 
-from ._lib import NativeError, available, check, lib, stream_ptr  # noqa: F401
+from ._lib import check, lib
 
 
 MASK_WORDS = 8  # 256 CUs

@@ -1,16 +1,12 @@
 """Row softmax / top-k kernels (classifier heads, attention probabilities, sampling candidates)."""
 from __future__ import annotations
 
-import ctypes  # noqa: F401
-import functools  # noqa: F401
-import json  # noqa: F401
-import os  # noqa: F401
-from typing import Dict, List, Optional, Sequence, Tuple  # noqa: F401
+from typing import Optional, Tuple
 
 import torch
 
-from ._lib import NativeError, available, check, lib, stream_ptr  # noqa: F401
-from ._core import _need, _ptr  # noqa: F401
+from ._lib import check, lib, stream_ptr
+from ._core import _need, _ptr
 
 
 def softmax_topk(

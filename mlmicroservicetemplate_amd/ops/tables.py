@@ -1,15 +1,13 @@
 """Measured per-shape dispatch tables (ops/tuned/*.json) and their lookups -- a served shape that misses a table is logged once per process."""
 from __future__ import annotations
 
-import ctypes  # noqa: F401
-import functools  # noqa: F401
-import json  # noqa: F401
-import os  # noqa: F401
-from typing import Dict, List, Optional, Sequence, Tuple  # noqa: F401
+import functools
+import json
+import os
+from typing import Dict, List, Optional, Tuple
 
 import torch
 
-from ._lib import NativeError, available, check, lib, stream_ptr  # noqa: F401
 
 
 _TUNED_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned")

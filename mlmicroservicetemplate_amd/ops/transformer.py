@@ -1,16 +1,13 @@
 """Transformer ops: norms, embeddings, RoPE, KV cache writes, flash / decode attention, the on-device token pick."""
 from __future__ import annotations
 
-import ctypes  # noqa: F401
-import functools  # noqa: F401
-import json  # noqa: F401
-import os  # noqa: F401
-from typing import Dict, List, Optional, Sequence, Tuple  # noqa: F401
+import os
+from typing import Optional
 
 import torch
 
-from ._lib import NativeError, available, check, lib, stream_ptr  # noqa: F401
-from ._core import ACT_NONE, _need, _ptr  # noqa: F401
+from ._lib import check, lib, stream_ptr
+from ._core import ACT_NONE, _need, _ptr
 
 
 # ------------------------------------------------------------------ transformer ops

@@ -1,16 +1,13 @@
 """ResNet-path ops: implicit-GEMM / halo / pipelined convolutions with fused epilogues, the fused stem, pools, the fused classifier head."""
 from __future__ import annotations
 
-import ctypes  # noqa: F401
-import functools  # noqa: F401
-import json  # noqa: F401
-import os  # noqa: F401
-from typing import Dict, List, Optional, Sequence, Tuple  # noqa: F401
+import ctypes
+from typing import Optional, Tuple
 
 import torch
 
-from ._lib import NativeError, available, check, lib, stream_ptr  # noqa: F401
-from ._core import ACT_NONE, ACT_RELU, _act, _need, _ptr, _workspace_args, conv_out_hw  # noqa: F401
+from ._lib import check, lib, stream_ptr
+from ._core import ACT_NONE, ACT_RELU, _act, _need, _ptr, _workspace_args, conv_out_hw
 
 
 def pack_conv_weight(w_oihw: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor:

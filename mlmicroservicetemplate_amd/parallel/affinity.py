@@ -62,7 +62,12 @@ def gpu_local_cpus(pci_addr: str, sysfs_root: str = "/sys") -> Optional[Set[int]
 
 
 STAGE_THREADS_CAP = 4  # copy threads that saturate one batch's memcpy (docs/PERF_NOTES.md, round 2)
+# a copy thread's memcpy rate into pinned memory with 8 ranks copying at once: the 8-process CPU
+# staging test measured 3.5-8.7 GB/s per instance (profiles/r4_staging_8_rank_processes_cpu.txt);
+# the plan below budgets the low end per thread
+COPY_GBPS_PER_THREAD = 3.5
 _hint: Optional[int] = None
+_plan: Optional[dict] = None
 
 
 def stage_thread_budget(n_cpus: int, ranks_sharing: int, cap: int = STAGE_THREADS_CAP) -> int:
@@ -104,13 +109,33 @@ def stage_threads_hint() -> Optional[int]:
     return _hint
 
 
+def host_plan(n_cpus: int, ranks_sharing: int, bytes_per_sample: int = 224 * 224 * 3,
+              target_samples_per_s: float = 60000.0, numa_bound: bool = False) -> dict:
+    """This rank's host-side budget: staging copy threads from its CPU share, the memcpy rate they
+    give at :data:`COPY_GBPS_PER_THREAD` each (the submitting thread copies too), against what the
+    GPU needs at ``target_samples_per_s`` (ResNet-50 bs=32 on one MI355X: 57k req/s measured x
+    150 KB per image = 8.6 GB/s).  ``headroom`` < 1 means the host, not the GPU, would bound this
+    rank."""
+    threads = stage_thread_budget(n_cpus, ranks_sharing)
+    copy = (threads + 1) * COPY_GBPS_PER_THREAD
+    need = bytes_per_sample * target_samples_per_s / 1e9
+    return {"cpus": int(n_cpus), "ranks_sharing_cpus": int(ranks_sharing), "cpus_per_rank": int(n_cpus) // max(1, int(ranks_sharing)),
+            "stage_threads": threads, "copy_gbps_budget": round(copy, 1), "need_gbps": round(need, 2),
+            "headroom": round(copy / need, 2) if need > 0 else None, "numa_bound": bool(numa_bound)}
+
+
+def host_plan_hint() -> Optional[dict]:
+    """The plan :func:`bind_to_gpu` computed for this process (None: single rank)."""
+    return _plan
+
+
 def bind_to_gpu(device_index: int, world_size: int = 1, sysfs_root: str = "/sys",
                 pci_addr: Optional[str] = None, local_world: Optional[int] = None,
                 pci_of=None) -> Optional[List[int]]:
     """Restrict this process's (calling thread's) CPU affinity to the GPU's local CPUs.
     Returns the CPU list applied, or None when binding is disabled / impossible.  With several
     ranks it also sets :func:`stage_threads_hint` from the CPUs left to this rank."""
-    global _hint
+    global _hint, _plan
     if world_size > 1:
         lw = int(local_world or os.environ.get("LOCAL_WORLD_SIZE", world_size))
         try:
@@ -123,8 +148,9 @@ def bind_to_gpu(device_index: int, world_size: int = 1, sysfs_root: str = "/sys"
         usable = (local0 & allowed0) if local0 and (local0 & allowed0) else allowed0
         sharing = ranks_sharing_cpus(device_index, lw, sysfs_root, pci_of=pci_of) if local0 else lw
         _hint = stage_thread_budget(len(usable), sharing)
-        logger.info("GPU %d: %d usable CPUs shared by %d local ranks -> %d staging threads", device_index,
-                    len(usable), sharing, _hint)
+        _plan = host_plan(len(usable), sharing, numa_bound=bool(local0 and (local0 & allowed0)))
+        logger.info("GPU %d: %d usable CPUs shared by %d local ranks -> %d staging threads (%s)", device_index,
+                    len(usable), sharing, _hint, _plan)
     mode = os.environ.get("MLS_NUMA_BIND", "")
     if mode == "0" or (mode != "1" and world_size <= 1):
         return None

@@ -212,12 +212,21 @@ class LlamaPlugin(ModelPlugin):
         """Ranks > 0: execute rank 0's generate commands until STOP."""
         import torch.distributed as dist
 
+        import time
+
         from ..models.llama import GenParams
 
+        # per-iteration host cost of following (X5): the header broadcast + its host read, and the
+        # iteration itself -- in the worker's info dump (tests/llama_tp_worker.py) and /info
+        st = self.follower_stats = {"iters": 0, "hdr_s": 0.0, "hdr_max_s": 0.0, "iter_s": 0.0}
         while True:
+            t0 = time.perf_counter()
             hdr = torch.zeros(7, dtype=torch.int64, device=self.comm_dev)
             dist.broadcast(hdr, src=0)
             op, B, S, mnt, topk, temp, seed = hdr.tolist()
+            dt = time.perf_counter() - t0
+            st["hdr_s"] += dt
+            st["hdr_max_s"] = max(st["hdr_max_s"], dt)
             if op == OP_STOP:
                 logger.info("rank %d: stop", self.ctx.rank)
                 return 0
@@ -234,7 +243,10 @@ class LlamaPlugin(ModelPlugin):
                         seq = _Seq(ids[j, :n].tolist(), GenParams(mnt_j, topk_j, temp_j / 1000.0, seed_j), None)
                         seq.slot = slot
                         admit.append(seq)
+                t1 = time.perf_counter()
                 self.engine.run_iteration(admit)  # same failure handling / health checks as rank 0
+                st["iter_s"] += time.perf_counter() - t1
+                st["iters"] += 1
                 continue
             ids = torch.zeros(B, S, dtype=torch.int32, device=self.comm_dev)
             lens = torch.zeros(B, dtype=torch.int32, device=self.comm_dev)

@@ -53,10 +53,10 @@ def serve(m, rank, world, cfg):
 
     torch.Tensor.cpu = counting_cpu
     results = []
+    reqs = []
     try:
         if rank == 0:
             g = torch.Generator().manual_seed(11)
-            reqs = []
             for i in range(6):
                 n = int(torch.randint(3, 30, (1,), generator=g))
                 reqs.append((torch.randint(3, cfg.vocab - 1, (n,), generator=g).tolist(),
@@ -74,8 +74,12 @@ def serve(m, rank, world, cfg):
     finally:
         torch.Tensor.cpu = orig
     info = {"iterations": eng.iterations, "host_reads": eng.host_reads, "cpu_calls": len(calls),
-            "dev_mode": int(eng.dev_mode), "failures": eng.failures, "car": int(m.comm.car is not None)}
-    torch.save({"results": json.dumps(results), "info": json.dumps(info)}, os.environ["OUT"] + f".serve.{rank}.pt")
+            "dev_mode": int(eng.dev_mode), "failures": eng.failures, "car": int(m.comm.car is not None),
+            "follower": getattr(plug, "follower_stats", None)}
+    reqs_json = json.dumps([[ids, [gp.max_new_tokens, gp.top_k, gp.temperature, gp.seed]] for ids, gp in reqs]
+                           if rank == 0 else [])
+    torch.save({"results": json.dumps(results), "info": json.dumps(info), "reqs": reqs_json},
+               os.environ["OUT"] + f".serve.{rank}.pt")
 
 
 def main():

@@ -183,7 +183,95 @@ def test_tp_serving_continuous_device_path(tmp_path, case):
         assert all(i["car"] == 0 and i["failures"] >= 1 for i in infos), infos
         return
     assert all(isinstance(x, list) and 1 <= len(x) <= 8 for x in results), results
+    # the served tokens: the same staggered greedy / seeded requests through a TP=1 ContinuousLlama
+    # of the same weights must give the same token lists; a list may differ only from a step where
+    # TP=1's own decision is within rounding of flipping (teacher-forced, as in the test above)
+    reqs = json.loads(torch.load(out + ".serve.0.pt", weights_only=True)["reqs"])
+    ref, robust_steps = _served_tp1_reference(cfg_kw, reqs)
+    same = 0
+    for i, (got, want, (ids, gpl)) in enumerate(zip(results, ref, reqs)):
+        if got == want:
+            same += 1
+            continue
+        t = next((j for j in range(min(len(got), len(want))) if got[j] != want[j]), min(len(got), len(want)))
+        robust = _tp1_decision_robust(cfg_kw, ids, gpl, want, t)
+        assert not robust, f"request {i}: TP=8 {got} vs TP=1 {want} diverge at a decisive step {t}"
+    assert same >= 3 and robust_steps >= 12, (same, robust_steps, results, ref)
+    for r, i in enumerate(infos):
+        if r and i.get("follower"):  # per-iteration host cost of following rank 0 (X5 header)
+            f = i["follower"]
+            print(f"rank {r}: {f['iters']} iterations, header broadcast + read {f['hdr_s'] / max(1, f['iters']) * 1e3:.3f} "
+                  f"ms/iter (max {f['hdr_max_s'] * 1e3:.2f}), iteration {f['iter_s'] / max(1, f['iters']) * 1e3:.3f} ms/iter")
     for i in infos:
         assert i["dev_mode"] == 1 and i["car"] == 1, infos
         # one [2, B] read-back per iteration, no other device -> host copy
         assert i["host_reads"] <= i["iterations"] and i["cpu_calls"] <= i["iterations"], infos
+
+
+_TP1 = {}
+
+
+def _tp1_model(cfg_kw):
+    from mlmicroservicetemplate_amd.models.llama import LlamaTP, init_llama_shard, tiny_config
+
+    key = json.dumps(cfg_kw, sort_keys=True)
+    if key not in _TP1:  # the workers' weights (seed 3) and cache shape, unsharded
+        cfg = tiny_config(**cfg_kw)
+        _TP1[key] = LlamaTP(init_llama_shard(cfg, 1, 0, seed=3, device="cuda"), cfg, backend="fused",
+                            device="cuda", max_batch=4, max_seq=256)
+    return _TP1[key]
+
+
+def _gp(gpl):
+    from mlmicroservicetemplate_amd.models.llama import GenParams
+
+    return GenParams(int(gpl[0]), int(gpl[1]), float(gpl[2]), int(gpl[3]))
+
+
+def _served_tp1_reference(cfg_kw, reqs):
+    """The requests through a TP=1 ContinuousLlama (same submission order and slot count as the
+    TP workers' rank 0); also counts the steps whose decision is robust (decisive)."""
+    from mlmicroservicetemplate_amd.models.llama_serving import ContinuousLlama
+
+    m = _tp1_model(cfg_kw)
+    eng = ContinuousLlama(m).start()
+    try:
+        futs = [eng.submit(ids, _gp(gpl)) for ids, gpl in reqs]
+        out = [f.result(timeout=200) for f in futs]
+    finally:
+        eng.stop()
+    robust = sum(_tp1_decision_robust(cfg_kw, ids, gpl, toks, t) for (ids, gpl), toks in zip(reqs, out)
+                 for t in range(len(toks)))
+    return out, robust
+
+
+def _tp1_decision_robust(cfg_kw, ids, gpl, toks, t) -> bool:
+    """Teacher-forced TP=1 decision at generated step t (prompt + toks[:t] fed): does it survive a
+    rounding-sized change?  Greedy: top-1 margin > 1e-2 of the largest |logit|.  Sampled: the
+    top_k set is decisive (k-th vs (k+1)-th logit) and the seeded draw sits > 5 % of the total
+    weight from every cumulative boundary."""
+    from mlmicroservicetemplate_amd.models.llama import sample_uniform
+
+    m = _tp1_model(cfg_kw)
+    gp = _gp(gpl)
+    n = len(ids)
+    x = torch.tensor([ids], dtype=torch.int64).cuda()
+    pos = torch.arange(n, dtype=torch.int32).unsqueeze(0).cuda()
+    lens = torch.tensor([n], dtype=torch.int32).cuda()
+    vals, idx = m.step(x, pos, lens, decode=False, k=16)
+    cur = lens.clone()
+    for j in range(t):
+        vals, idx = m.decode_step(torch.tensor([toks[j]], dtype=torch.int32).cuda(), cur, 16, max_ctx=n + j + 1)
+        cur = cur + 1
+    cv, _ci = m.gather_candidates(vals, idx)
+    v = torch.sort(cv[0].float(), descending=True).values.cpu()
+    scale = float(v.abs().max()) + 1e-6
+    if gp.top_k <= 1:
+        return float(v[0] - v[1]) / scale > 1e-2
+    k = min(gp.top_k, v.numel() - 1)
+    if float(v[k - 1] - v[k]) / scale <= 1e-2:
+        return False
+    w = torch.exp((v[:k] - v[0]) / max(gp.temperature, 1e-5))
+    cdf = torch.cumsum(w, 0)
+    thr = float(sample_uniform(gp.seed, t)) * float(cdf[-1])
+    return bool(((cdf - thr).abs() / cdf[-1]).min() > 5e-2)
