@@ -158,9 +158,11 @@ def run_rank(args) -> int:
             args.cu_partition = 0
     if args.inflight <= 0:
         args.inflight = 4 if args.cu_partition and not args.serial else 5
+    # the closed-loop client polls its oldest batch's done event (20 ms bound) instead of sleeping
+    # in a blocking sync: s200 56.0k vs 55.2k req/s (profiles/r5_stall_ab_sdma_vs_pull.jsonl)
     engine = GpuEngine(fwd, device, (224, 224, 3), torch.uint8, buckets=[args.batch], inflight=args.inflight,
                        use_graphs=not args.no_graphs, name=f"resnet50.r{info.rank}", concurrent=not args.serial,
-                       cu_partitions=0 if args.serial else args.cu_partition)
+                       cu_partitions=0 if args.serial else args.cu_partition, spin_wait_us=20000.0)
     cu_parts = engine.cu_partitions
     engine.warmup(capture=not args.no_graphs)
 
@@ -259,7 +261,7 @@ def run_rank(args) -> int:
         efwd = build_model("eager", device, args.batch, params)
         eeng = GpuEngine(efwd, device, (224, 224, 3), torch.uint8, buckets=[args.batch], inflight=args.inflight,
                          use_graphs=not args.no_graphs, name=f"eager.r{info.rank}", concurrent=not args.serial,
-                         cu_partitions=0 if args.serial else args.cu_partition)
+                         cu_partitions=0 if args.serial else args.cu_partition, spin_wait_us=20000.0)
         eeng.warmup(capture=not args.no_graphs)
         engine = eeng
         run_steps(min(args.warmup, 5), [])

@@ -61,6 +61,7 @@ class _Slot:
     host_out: Dict[int, Tuple[torch.Tensor, ...]] = field(default_factory=dict)  # bucket -> pinned outputs
     graphs: Dict[int, torch.cuda.CUDAGraph] = field(default_factory=dict)
     graph_copies: Dict[int, bool] = field(default_factory=dict)  # bucket -> copies inside the graph
+    pushed: Dict[int, bool] = field(default_factory=dict)  # bucket -> results pushed to host by the graph
     native: Dict[int, tuple] = field(default_factory=dict)  # bucket -> mls_engine_launch arguments
     s_comp: Optional[torch.cuda.Stream] = None  # this slot's compute stream (concurrent mode)
     pool: Optional[tuple] = None  # this slot's graph memory pool (concurrent mode)
@@ -118,6 +119,7 @@ class GpuEngine:
         stage_workers: Optional[int] = None,
         copies_on_slot_stream: Optional[bool] = None,
         cu_partitions: Optional[int] = None,
+        spin_wait_us: Optional[float] = None,
     ):
         self.forward = forward
         self.device = torch.device(device)
@@ -178,11 +180,13 @@ class GpuEngine:
         # of host time per batch.  The instrumented Python sequence runs while tracing is active.
         self.native_launch = (self.copies_on_slot_stream and use_graphs and not self.graph_copies
                               and os.environ.get("MLS_NATIVE_LAUNCH", "1") == "1")
-        # zero-copy H2D (MLS_PULL_H2D=<workgroups>, 0 = off): the slot's graph starts with a
-        # small copy kernel that pulls the pinned batch over PCIe (ops.h2d_pull) instead of an SDMA
-        # hipMemcpyAsync -- the SDMA path occasionally blocked the enqueue ~6 ms with every queue of
-        # the process stalled (docs/PERF_NOTES.md, round 5)
-        self.pull_h2d = int(os.environ.get("MLS_PULL_H2D", "0")) if (
+        # SDMA-free batch I/O (MLS_PULL_H2D=<workgroups>, default 8; 0 = hipMemcpyAsync copies): the
+        # slot's graph starts with a small copy kernel that pulls the pinned batch over PCIe
+        # (ops.h2d_pull) and ends with one that pushes the results into the pinned output buffers
+        # (ops.d2h_push).  SDMA H2D copies stalled ~6-7 ms in 8 of ~100 20-step bench runs over 6
+        # boxes (hipMemcpyAsync blocked, every in-flight batch waiting on its copy); with both copies
+        # as kernels 0 of 24 on a box where the SDMA arms stalled 6 of 24 (docs/PERF_NOTES.md, round 5)
+        self.pull_h2d = int(os.environ.get("MLS_PULL_H2D", "8")) if (
             self.copies_on_slot_stream and use_graphs and not self.graph_copies
             and sample_dtype == torch.uint8) else 0
         # host staging (request arrays -> pinned slot): a persistent native copy pool (GIL released,
@@ -193,6 +197,12 @@ class GpuEngine:
         self._tr_stage, self._tr_h2d, self._tr_replay, self._tr_d2h, self._tr_wait = (
             f"{name}.{k}" for k in ("stage", "h2d", "replay", "d2h", "d2h_wait"))
         self._enqueue_lock = threading.Lock()
+        # completion wait (Ticket.wait): poll the done event for up to spin_wait_us (MLS_EVENT_SPIN_US)
+        # before the blocking (interrupt) sync -- the refill of a freed slot starts sooner; for a
+        # process whose thread has nothing else to do (bench.py's closed loop), not for servers
+        # whose waiter threads share the GIL with the front end (default 0 = block at once)
+        env_spin = os.environ.get("MLS_EVENT_SPIN_US")
+        self._spin_us = float(env_spin) if env_spin is not None else float(spin_wait_us or 0.0)
         # Launch pacing.  Batches that become ready together (a closed loop, a burst, two slots
         # freed by one clump of completions) otherwise enter the network in lock step: all in the
         # bandwidth-bound early layers at once, then all in the latency-bound late ones, and keep
@@ -288,12 +298,20 @@ class GpuEngine:
 
                                 ops.h2d_pull(slot.host_in[:b], slot.dev_in[:b], self.pull_h2d)
                             outs = self.forward(slot.dev_in[:b])
+                            # ... and the results pushed to the pinned host buffers by a kernel at the
+                            # graph's end (no SDMA D2H either), when every output is a 16-B multiple
+                            push = bool(self.pull_h2d) and all(
+                                d.is_contiguous() and (d.numel() * d.element_size()) % 16 == 0 for d in outs)
+                            if push:
+                                for h, d in zip(slot.host_out[b], outs):
+                                    ops.d2h_push(d, h)
                             if in_graph:
                                 for h, d in zip(slot.host_out[b], outs):
                                     h.copy_(d, non_blocking=True)
                         slot.graphs[b] = g
                         slot.outs[b] = tuple(outs)
                         slot.graph_copies[b] = in_graph
+                        slot.pushed[b] = bool(self.pull_h2d) and not in_graph and push
                         if self.native_launch:
                             self._prepare_native(slot, b)
                 torch.cuda.synchronize(self.device)
@@ -338,10 +356,10 @@ class GpuEngine:
             slot.ev_done.record(slot.s_comp)  # torch creates the event lazily: make it exist
             ev = slot.ev_done.cuda_event
             outs, hosts = slot.outs[b], slot.host_out[b]
-            n = len(outs)
-            dst = (ctypes.c_void_p * max(n, 1))(*[h.data_ptr() for h in hosts])
-            src = (ctypes.c_void_p * max(n, 1))(*[d.data_ptr() for d in outs])
-            nb = (ctypes.c_longlong * max(n, 1))(*[d.numel() * d.element_size() for d in outs])
+            n = 0 if slot.pushed.get(b) else len(outs)  # pushed by the graph itself
+            dst = (ctypes.c_void_p * max(n, 1))(*[h.data_ptr() for h in hosts[:n]])
+            src = (ctypes.c_void_p * max(n, 1))(*[d.data_ptr() for d in outs[:n]])
+            nb = (ctypes.c_longlong * max(n, 1))(*[d.numel() * d.element_size() for d in outs[:n]])
             h2d = slot.host_in[:b]
             t_ns = (ctypes.c_longlong * 5)()  # per-call host times of the last enqueue (diagnostics)
             h2d_bytes = 0 if self.pull_h2d else h2d.numel() * h2d.element_size()  # pulled in the graph
@@ -558,6 +576,10 @@ class GpuEngine:
         try:
             try:
                 with tracing.range(self._tr_wait):
+                    if self._spin_us > 0:  # poll first: a blocking-sync wake-up costs tens of us
+                        end = time.perf_counter() + self._spin_us * 1e-6
+                        while not slot.ev_done.query() and time.perf_counter() < end:
+                            pass
                     slot.ev_done.synchronize()
                 if self._pace > 0 and self.inflight > 1:
                     self._note_done(t)

@@ -106,6 +106,7 @@ from .transformer import (  # noqa: F401
 from .image import (  # noqa: F401
     IMAGE_CONTAINER_BYTES,
     IMAGE_SCRATCH_PER_IMAGE,
+    d2h_push,
     gpu_sleep,
     h2d_pull,
     image_decode,

@@ -79,6 +79,7 @@ _SIGS = {
     "mls_ar_reset": [P],
     "mls_gpu_sleep": [L, P],
     "mls_h2d_pull": [P, P, _c.c_longlong, I, P],
+    "mls_d2h_push": [P, P, _c.c_longlong, I, P],
     "mls_stem_set_stamps": [P],
     "mls_image_decode": [P, P, P, L, I, P, P],
     "mls_decode_pick": [P, P, I, I, I, P, P, P, P, P, P, P, I, P, P, P, P, P],

@@ -44,8 +44,9 @@ __global__ __launch_bounds__(256) void h2d_pull_kernel(const void* src, void* ds
 
 extern "C" {
 
-// src: pinned host memory (hipHostMalloc / torch pin_memory), dst: device memory, bytes % 16 == 0,
-// < 1 GiB.  blocks: workgroups pulling (each lane keeps 8 x 16 B in flight).
+// src: pinned host memory (hipHostMalloc / torch pin_memory), dst: device memory (or the other way
+// round: any two GPU-addressable buffers), bytes % 16 == 0, < 1 GiB.  blocks: workgroups copying
+// (each lane keeps 8 x 16 B in flight).
 int mls_h2d_pull(const void* src, void* dst, long long bytes, int blocks, void* stream) {
   if (!src || !dst || bytes <= 0 || bytes % 16 || bytes >= (1LL << 30) || blocks <= 0 || blocks > 1024)
     return MLS_BAD_ARG;
@@ -55,6 +56,12 @@ int mls_h2d_pull(const void* src, void* dst, long long bytes, int blocks, void* 
   hipLaunchKernelGGL(h2d_pull_kernel<U>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, src, dst,
                      (uint32_t)bytes, iters);
   return (int)hipGetLastError();
+}
+
+// The same copy kernel the other way: device memory -> pinned host memory (the engine's per-batch
+// results, pushed at the end of the slot's graph instead of D2H hipMemcpyAsync on an SDMA queue).
+int mls_d2h_push(const void* src, void* dst, long long bytes, int blocks, void* stream) {
+  return mls_h2d_pull(src, dst, bytes, blocks, stream);
 }
 
 // d2h_*: n_d2h (<= 8) destination / source / byte-count triples.  t_ns (optional, 5 entries):

@@ -16,6 +16,11 @@
 // Counters are this stream's self-resetting split-K counters (conv_gemm.hip).
 #include "common.h"
 
+#include <cstdlib>
+#include <mutex>
+#include <unordered_map>
+#include <utility>
+
 int* mls_stream_splitk_counters(void* stream, long ntiles);  // conv_gemm.hip
 
 namespace {
@@ -175,6 +180,200 @@ __global__ __launch_bounds__(HW * 64) void fc_head_kernel(const HeadArgs a) {
   for (int i = tid; i < n4; i += HW * 64) pz[i] = float4{0.f, 0.f, 0.f, 0.f};
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// v2 (default; MLS_HEAD_V2=0 runs the one-launch kernel above).  That kernel took 20.7 us at B = 32
+// (profiles/r5_head_probe.jsonl): 14.7 us of it the FC alone, because 504 blocks re-read the 4 MB
+// weight 8 times (once per 4-row group) and the fp32 pooled rows 63 times -- ~49 MB for a 0.13
+// GFLOP product -- and then the last block of each row group ran its rows' softmax / top-k.
+// v2 is two launches with no inter-block hand-off inside either:
+//  * head_fc_kernel: grid (class groups of 32) x (K slices of 256) x (row groups of 32); 4 waves,
+//    wave = 16 rows x 16 classes x K 256 = 8 MFMAs with every operand load issued up front; each
+//    weight byte is read by one block per row group; the fp32 partial tile goes to slab
+//    [slice][row][class] (16-B stores: the swapped product gives a lane 4 consecutive classes);
+//  * head_finish_kernel: one block per row sums the slabs in slice order (deterministic), adds the
+//    bias, writes the logits, runs softmax + top-k as block arg-max rounds, and zeroes the row's
+//    pooled sums for the next forward.
+constexpr int HV2_CG = 32, HV2_KS = 256, HV2_RG = 32;
+
+struct HeadV2Args {
+  const float* pooled;
+  const bf16* w;
+  const float* bias;
+  float* slabs;  // [K / HV2_KS][B][N]
+  float* logits;
+  float* vals;
+  int* idx;
+  const int* err;
+  int B, N, K, k, softmax;
+  uint32_t pooled_bytes, w_bytes;
+};
+
+__global__ __launch_bounds__(256) void head_fc_kernel(const HeadV2Args a) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int c0 = blockIdx.x * HV2_CG + (wid & 1) * 16, k0 = blockIdx.y * HV2_KS;
+  const int r0 = blockIdx.z * HV2_RG + (wid >> 1) * 16;
+  const rsrc_t wr = make_rsrc(a.w, a.w_bytes), pr = make_rsrc(a.pooled, a.pooled_bytes);
+  const int cl = c0 + fr, rw = r0 + fr;
+  const int woff = cl < a.N ? (cl * a.K + k0 + fq * 8) * 2 : OOB;
+  const int poff = rw < a.B ? (rw * a.K + k0 + fq * 8) * 4 : OOB;
+  uint4 wv[HV2_KS / 32];
+  float4 pv[HV2_KS / 32][2];
+#pragma unroll
+  for (int s = 0; s < HV2_KS / 32; ++s) {
+    wv[s] = bload16(wr, woff == OOB ? OOB : woff + 64 * s);
+    pv[s][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(pr, poff == OOB ? OOB : poff + 128 * s, 0, 0));
+    pv[s][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(pr, poff == OOB ? OOB : poff + 128 * s + 16, 0, 0));
+  }
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < HV2_KS / 32; ++s) {
+    bf16x8 b;
+    b[0] = (bf16)pv[s][0].x; b[1] = (bf16)pv[s][0].y; b[2] = (bf16)pv[s][0].z; b[3] = (bf16)pv[s][0].w;
+    b[4] = (bf16)pv[s][1].x; b[5] = (bf16)pv[s][1].y; b[6] = (bf16)pv[s][1].z; b[7] = (bf16)pv[s][1].w;
+    // D[class fq*4 + i][row fr]: lane (fr, fq) holds classes c0 + fq*4 .. +3 of row r0 + fr
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wv[s]), b, acc, 0, 0, 0);
+  }
+  const int row = r0 + fr, col = c0 + fq * 4;
+  if (row < a.B && col < a.N) {
+    float* dst = a.slabs + ((long)blockIdx.y * a.B + row) * a.N + col;
+    if (col + 4 <= a.N && (a.N & 3) == 0) {
+      *reinterpret_cast<float4*>(dst) = float4{acc[0], acc[1], acc[2], acc[3]};
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float e = acc[i];  // through a named float (ext-vector element bit-cast hazard)
+        if (col + i < a.N) dst[i] = e;
+      }
+    }
+  }
+}
+
+// block-wide arg-max over (value, class): larger value wins, ties to the smaller class
+MLS_DEV void block_argmax(float& bv, int& bc, float* sv, int* sc) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(bv, o, 64);
+    const int oc = __shfl_xor(bc, o, 64);
+    if (ov > bv || (ov == bv && oc < bc)) {
+      bv = ov;
+      bc = oc;
+    }
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+    sv[wid] = bv;
+    sc[wid] = bc;
+  }
+  __syncthreads();
+  bv = sv[0];
+  bc = sc[0];
+#pragma unroll
+  for (int w = 1; w < 4; ++w)
+    if (sv[w] > bv || (sv[w] == bv && sc[w] < bc)) {
+      bv = sv[w];
+      bc = sc[w];
+    }
+  __syncthreads();  // sv / sc are reused by the next round
+}
+
+constexpr int HV2_PER_T = 4;  // classes per thread in the finisher (N <= 1024)
+constexpr int HV2_MAXS = 8;   // K slices summed with all loads in flight (K <= 2048)
+
+__global__ __launch_bounds__(256) void head_finish_kernel(const HeadV2Args a) {
+  __shared__ float sv[4];
+  __shared__ int sc[4];
+  __shared__ float sred[4];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const int nks = a.K / HV2_KS;
+  const int c = tid * HV2_PER_T;
+  float v[HV2_PER_T];
+  const bool full = c + HV2_PER_T <= a.N && (a.N & 3) == 0;
+#pragma unroll
+  for (int i = 0; i < HV2_PER_T; ++i) v[i] = 0.f;
+  if (full && nks <= HV2_MAXS) {
+    // every slice's 16 B issued before the first is summed (a runtime-count loop waited for each
+    // load in turn: 8 dependent L2 round trips, ~8 of the finisher's 11 us); slices past nks read
+    // zero through the range check; summed in slice order -> the same bits on every launch
+    const rsrc_t sr = make_rsrc(a.slabs, (uint32_t)((size_t)nks * a.B * a.N * 4));
+    float4 x[HV2_MAXS];
+#pragma unroll
+    for (int s = 0; s < HV2_MAXS; ++s)
+      x[s] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            sr, s < nks ? (int)((((size_t)s * a.B + row) * a.N + c) * 4) : OOB, 0, 0));
+#pragma unroll
+    for (int s = 0; s < HV2_MAXS; ++s) {
+      v[0] += x[s].x; v[1] += x[s].y; v[2] += x[s].z; v[3] += x[s].w;
+    }
+  } else {
+    for (int s = 0; s < nks; ++s) {  // slice order: the same sum on every launch
+      const float* src = a.slabs + ((long)s * a.B + row) * a.N + c;
+      for (int i = 0; i < HV2_PER_T; ++i)
+        if (c + i < a.N) v[i] += src[i];
+    }
+  }
+  float m = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < HV2_PER_T; ++i) {
+    if (c + i < a.N) {
+      v[i] += a.bias ? a.bias[c + i] : 0.f;
+      a.logits[(long)row * a.N + c + i] = v[i];
+      m = fmaxf(m, v[i]);
+    } else {
+      v[i] = -INFINITY;
+    }
+  }
+  // zero this row's pooled sums for the next forward (the FC kernel has read them: an earlier launch)
+  float4* pz = reinterpret_cast<float4*>(const_cast<float*>(a.pooled) + (long)row * a.K);
+  for (int i = tid; i < a.K / 4; i += 256) pz[i] = float4{0.f, 0.f, 0.f, 0.f};
+  if (a.k <= 0) return;
+  m = block_max(m, sred);
+  float ssum = 0.f;
+  if (a.softmax) {
+#pragma unroll
+    for (int i = 0; i < HV2_PER_T; ++i) ssum += v[i] == -INFINITY ? 0.f : __expf(v[i] - m);
+    ssum = block_sum(ssum, sred);
+  }
+  const bool bad = a.err && a.err[row] != 0;
+  for (int t = 0; t < a.k; ++t) {
+    float bv = -INFINITY;
+    int bj = 0;
+#pragma unroll
+    for (int i = 0; i < HV2_PER_T; ++i)
+      if (v[i] > bv) {
+        bv = v[i];
+        bj = i;
+      }
+    int bc = bv == -INFINITY ? 0x7fffffff : c + bj;
+    block_argmax(bv, bc, sv, sc);
+    if (bc >= c && bc < c + HV2_PER_T) v[bc - c] = -INFINITY;  // the owner drops the winner
+    if (tid == 0) {
+      const float p = a.softmax ? __expf(bv - m) / ssum : bv;
+      a.vals[row * a.k + t] = bad ? __builtin_nanf("") : p;
+      a.idx[row * a.k + t] = bad ? -1 : (bc < a.N ? bc : -1);
+    }
+  }
+}
+
+float* head_slabs(hipStream_t st, size_t bytes) {
+  static std::mutex mu;
+  static std::unordered_map<hipStream_t, std::pair<float*, size_t>> bufs;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = bufs.find(st);
+  if (it != bufs.end() && it->second.second >= bytes) return it->second.first;
+  if (cs != hipStreamCaptureStatusNone) return nullptr;  // no allocation inside a capture
+  if (it != bufs.end()) (void)hipFree(it->second.first);  // grow (outside any capture)
+  float* p = nullptr;
+  if (hipMalloc(&p, bytes) != hipSuccess) {
+    bufs.erase(st);
+    return nullptr;
+  }
+  bufs[st] = {p, bytes};
+  return p;
+}
 }  // namespace
 
 extern "C" {
@@ -188,6 +387,32 @@ int mls_fc_head(const float* pooled, const void* w, const float* bias, float* lo
   if (k > 0 && (!vals || !idx)) return MLS_BAD_ARG;
   const long pb = (long)B * K * 4, wb = (long)N * K * 2, lb = (long)B * N * 4;
   if (pb >= 0x7fffffffL || wb >= 0x7fffffffL || lb >= 0x7fffffffL) return MLS_UNSUPPORTED;
+  static const bool v2 = [] {  // MLS_HEAD_V2=0: the one-launch kernel (A/B)
+    const char* e = getenv("MLS_HEAD_V2");
+    return !(e && e[0] == '0');
+  }();
+  if (v2 && N <= 256 * HV2_PER_T && K % HV2_KS == 0) {
+    const size_t sb = (size_t)(K / HV2_KS) * B * N * sizeof(float);
+    float* slabs = head_slabs((hipStream_t)stream, sb);
+    if (slabs) {
+      HeadV2Args a2;
+      a2.pooled = pooled;
+      a2.w = (const bf16*)w;
+      a2.bias = bias;
+      a2.slabs = slabs;
+      a2.logits = logits;
+      a2.vals = vals;
+      a2.idx = idx;
+      a2.err = err;
+      a2.B = B, a2.N = N, a2.K = K, a2.k = k, a2.softmax = softmax;
+      a2.pooled_bytes = (uint32_t)pb;
+      a2.w_bytes = (uint32_t)wb;
+      hipLaunchKernelGGL(head_fc_kernel, dim3((N + HV2_CG - 1) / HV2_CG, K / HV2_KS, (B + HV2_RG - 1) / HV2_RG),
+                         dim3(256), 0, (hipStream_t)stream, a2);
+      hipLaunchKernelGGL(head_finish_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, a2);
+      return (int)hipGetLastError();
+    }
+  }
   const int nrg = (B + HR - 1) / HR;
   int* cnt = mls_stream_splitk_counters(stream, nrg);
   if (!cnt) return MLS_UNSUPPORTED;  // counters must exist before graph capture (eager warm-up)

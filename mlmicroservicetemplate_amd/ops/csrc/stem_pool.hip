@@ -320,7 +320,8 @@ typedef unsigned int u32x4s __attribute__((__vector_size__(16)));
 __global__ __launch_bounds__(256, 2) void stem_pool_v2_kernel(const uint8_t* __restrict__ img, const bf16* __restrict__ w,
                                                            const float* __restrict__ bias, bf16* __restrict__ out,
                                                            uint32_t img_bytes, int B, float m0, float m1, float m2,
-                                                           float s0, float s1, float s2, long long* stamps) {
+                                                           float s0, float s1, float s2, long long* stamps,
+                                                           int stagger, int* arrive) {
   // stamps (diagnostics, MLS_STEM_STAMPS=1 via mls_stem_set_stamps): s_memtime of lane 0 of every
   // wave at the kernel start, after the first loads, and at each phase boundary of each tile
   constexpr int H = 224, W = 224, Po = 56;
@@ -378,6 +379,23 @@ __global__ __launch_bounds__(256, 2) void stem_pool_v2_kernel(const uint8_t* __r
 #pragma unroll
     for (int k = 0; k < 3; ++k) raw[k] = __builtin_amdgcn_raw_buffer_load_b32(ir, off + 4 * k, 0, 0);
   };
+  // stagger (MLS_STEM_STAGGER=<cycles>): the second block to arrive on a CU starts that much later,
+  // so the two blocks' MFMA phases do not coincide (arrival parity per CU from a global counter
+  // indexed by the CU's hardware id; never reset, the parity alternates)
+  if (stagger > 0 && arrive) {
+    __shared__ int s_par;
+    if (tid == 0) {
+      const unsigned hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));  // HW_REG_HW_ID
+      const unsigned xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));  // HW_REG_XCC_ID[3:0]
+      const unsigned cu = ((hw >> 8) & 15u) | (((hw >> 12) & 1u) << 4) | (((hw >> 13) & 7u) << 5);
+      s_par = atomicAdd(arrive + ((xcc & 7u) << 8 | (cu & 255u)), 1) & 1;
+    }
+    __syncthreads();
+    if (s_par) {
+      const long long t0 = __builtin_amdgcn_s_memtime();
+      while (__builtin_amdgcn_s_memtime() - t0 < stagger) __builtin_amdgcn_s_sleep(4);
+    }
+  }
   long long* st = stamps ? stamps + ((long)blockIdx.x * 4 + wid) * 64 : nullptr;
   if (st && lane == 0) st[0] = __builtin_amdgcn_s_memtime();
   fetch(0);
@@ -428,16 +446,26 @@ __global__ __launch_bounds__(256, 2) void stem_pool_v2_kernel(const uint8_t* __r
     for (int i = 0; i < 5; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // every wave runs 5 row blocks (wave row half 1's fifth is padding, dropped by m_pad): no
+    // branch between the fragment reads and the MFMAs, and the critical wave does 5 anyway.  The
+    // next kernel row's 5 fragments are read while this row's 10 MFMAs run (register double buffer)
+    bf16x8 av[2][5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+      av[0][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(smem + abase[i]));
 #pragma unroll
     for (int kh = 0; kh < 7; ++kh) {
-      // every wave runs 5 row blocks (wave row half 1's fifth is padding, dropped by m_pad): no
-      // branch between the fragment reads and the MFMAs, and the critical wave does 5 anyway
+      if (kh + 1 < 7) {
 #pragma unroll
-      for (int i = 0; i < 5; ++i) {
-        const bf16x8 av = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(smem + abase[i] + kh * v2::PSTR * 8));
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j][kh], av, acc[i][j], 0, 0, 0);
+        for (int i = 0; i < 5; ++i)
+          av[(kh + 1) & 1][i] = __builtin_bit_cast(
+              bf16x8, *reinterpret_cast<const uint4*>(smem + abase[i] + (kh + 1) * v2::PSTR * 8));
       }
+#pragma unroll
+      for (int i = 0; i < 5; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j][kh], av[kh & 1][i], acc[i][j], 0, 0, 0);
     }
     if (st && lane == 0) st[5 + 6 * t] = __builtin_amdgcn_s_memtime();
     // bias + ReLU -> bf16 stem tile; stem pixels outside the image (row / column -1) -> 0
@@ -486,6 +514,18 @@ __global__ __launch_bounds__(256, 2) void stem_pool_v2_kernel(const uint8_t* __r
 
 extern "C" {
 
+// per-CU arrival counters of the v2 stagger (2048 = 8 XCCs x 256 hardware CU ids), allocated once
+static int* stem_arrivals() {
+  static int* p = [] {
+    int* q = nullptr;
+    if (hipMalloc(&q, 2048 * sizeof(int)) != hipSuccess || hipMemset(q, 0, 2048 * sizeof(int)) != hipSuccess)
+      return (int*)nullptr;
+    (void)hipDeviceSynchronize();
+    return q;
+  }();
+  return p;
+}
+
 // diagnostics: v2 writes per-wave phase stamps ([blocks][4 waves][64] int64) here while set
 long long* g_stem_stamps = nullptr;
 int mls_stem_set_stamps(void* buf) {
@@ -532,10 +572,15 @@ int mls_stem_pool_conv1(const void* images, const void* w, const float* bias, vo
     return !(e && e[0] == '0');
   }();
   const long img_bytes = (long)B * H * W * 3;
+  static const int stagger = [] {
+    const char* e = getenv("MLS_STEM_STAGGER");
+    return e ? atoi(e) : 0;
+  }();
   if (use_v2 && !c1 && img_bytes < 0x7fffffffL) {
     hipLaunchKernelGGL(stem_pool_v2_kernel, dim3((unsigned)(B * 16)), dim3(256), 0, (hipStream_t)stream,
                        (const uint8_t*)images, (const bf16*)w, bias, (bf16*)out, (uint32_t)img_bytes, B, mean3[0],
-                       mean3[1], mean3[2], 1.f / std3[0], 1.f / std3[1], 1.f / std3[2], g_stem_stamps);
+                       mean3[1], mean3[2], 1.f / std3[0], 1.f / std3[1], 1.f / std3[2], g_stem_stamps, stagger,
+                       stagger > 0 ? stem_arrivals() : nullptr);
     return (int)hipGetLastError();
   }
   static const bool swap = [] {  // MLS_STEM_SWAP=0: the per-element epilogue (A/B)

@@ -61,3 +61,17 @@ def h2d_pull(src: torch.Tensor, dst: torch.Tensor, blocks: int = 32) -> torch.Te
         raise ValueError("h2d_pull: size mismatch")
     check(lib().mls_h2d_pull(src.data_ptr(), dst.data_ptr(), n, int(blocks), stream_ptr(dst.device)), "mls_h2d_pull")
     return dst
+
+
+def d2h_push(src: torch.Tensor, dst: torch.Tensor, blocks: int = 1) -> torch.Tensor:
+    """Copy the device tensor ``src`` into the pinned host tensor ``dst`` with a kernel on the current
+    stream (stores over PCIe; capturable).  Same byte size, 16-B multiple."""
+    if not src.is_cuda or dst.is_cuda or not dst.is_pinned():
+        raise ValueError("d2h_push: src must be a device tensor and dst pinned host memory")
+    if not (src.is_contiguous() and dst.is_contiguous()):
+        raise ValueError("d2h_push: contiguous tensors only")
+    n = src.numel() * src.element_size()
+    if n != dst.numel() * dst.element_size() or n % 16:
+        raise ValueError("d2h_push: sizes must match and be a 16-B multiple")
+    check(lib().mls_d2h_push(src.data_ptr(), dst.data_ptr(), n, int(blocks), stream_ptr(src.device)), "mls_d2h_push")
+    return dst
