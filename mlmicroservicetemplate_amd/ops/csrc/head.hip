@@ -70,6 +70,8 @@ MLS_DEV void head_finish_row(const HeadArgs& a, const rsrc_t& lr, int row, int l
     s = wave_sum(s);
   }
   const bool bad = a.err && a.err[row] != 0;
+  float wv = 0.f;
+  int wc = -1;
   for (int t = 0; t < a.k; ++t) {
     float bv = -INFINITY;
     int bj = 0;
@@ -318,16 +320,26 @@ __global__ __launch_bounds__(256) void head_finish_kernel(const HeadV2Args a) {
   for (int i = 0; i < HV2_PER_T; ++i) {
     if (c + i < a.N) {
       v[i] += a.bias ? a.bias[c + i] : 0.f;
-      a.logits[(long)row * a.N + c + i] = v[i];
       m = fmaxf(m, v[i]);
     } else {
       v[i] = -INFINITY;
     }
   }
-  // zero this row's pooled sums for the next forward (the FC kernel has read them: an earlier launch)
-  float4* pz = reinterpret_cast<float4*>(const_cast<float*>(a.pooled) + (long)row * a.K);
-  for (int i = tid; i < a.K / 4; i += 256) pz[i] = float4{0.f, 0.f, 0.f, 0.f};
-  if (a.k <= 0) return;
+  float lg[HV2_PER_T];  // the logits, stored at the end: a store pending at the reductions'
+#pragma unroll          // barriers would make each of them wait for it (vmcnt(0))
+  for (int i = 0; i < HV2_PER_T; ++i) lg[i] = v[i];
+  auto epilogue = [&]() {
+#pragma unroll
+    for (int i = 0; i < HV2_PER_T; ++i)
+      if (c + i < a.N) a.logits[(long)row * a.N + c + i] = lg[i];
+    // zero this row's pooled sums for the next forward (the FC kernel, an earlier launch, read them)
+    float4* pz = reinterpret_cast<float4*>(const_cast<float*>(a.pooled) + (long)row * a.K);
+    for (int i = tid; i < a.K / 4; i += 256) pz[i] = float4{0.f, 0.f, 0.f, 0.f};
+  };
+  if (a.k <= 0) {
+    epilogue();
+    return;
+  }
   m = block_max(m, sred);
   float ssum = 0.f;
   if (a.softmax) {
@@ -336,6 +348,8 @@ __global__ __launch_bounds__(256) void head_finish_kernel(const HeadV2Args a) {
     ssum = block_sum(ssum, sred);
   }
   const bool bad = a.err && a.err[row] != 0;
+  float wv = 0.f;
+  int wc = -1;
   for (int t = 0; t < a.k; ++t) {
     float bv = -INFINITY;
     int bj = 0;
@@ -348,12 +362,16 @@ __global__ __launch_bounds__(256) void head_finish_kernel(const HeadV2Args a) {
     int bc = bv == -INFINITY ? 0x7fffffff : c + bj;
     block_argmax(bv, bc, sv, sc);
     if (bc >= c && bc < c + HV2_PER_T) v[bc - c] = -INFINITY;  // the owner drops the winner
-    if (tid == 0) {
-      const float p = a.softmax ? __expf(bv - m) / ssum : bv;
-      a.vals[row * a.k + t] = bad ? __builtin_nanf("") : p;
-      a.idx[row * a.k + t] = bad ? -1 : (bc < a.N ? bc : -1);
+    if (tid == t) {  // thread t keeps winner t; all k written after the last round
+      wv = a.softmax ? __expf(bv - m) / ssum : bv;
+      wc = bc;
     }
   }
+  if (tid < a.k) {
+    a.vals[row * a.k + tid] = bad ? __builtin_nanf("") : wv;
+    a.idx[row * a.k + tid] = bad ? -1 : (wc < a.N ? wc : -1);
+  }
+  epilogue();
 }
 
 float* head_slabs(hipStream_t st, size_t bytes) {

@@ -40,3 +40,7 @@ def test_custom_allreduce_multiprocess(world):
             raise
         outs.append((p.returncode, out[-2000:]))
     assert all(rc == 0 for rc, _ in outs), outs
+    for _, out in outs:  # the lost-peer case of the GEMM-fused all-reduce: time to fail, error word
+        for line in out.splitlines():
+            if "fused stall" in line:
+                print(line)
