@@ -13,38 +13,41 @@ from .tables import small_m_plan_for, tile_cfg_for, tile_route_for
 
 # Large-M projections run on the native LDS-DMA MFMA tile kernel (gemm_tile: csrc/gemm_tile.hip),
 # the decode-shaped ones (M <= 32, and 33..TILE_MIN_M - 1 rows) on the skinny / conv_gemm kernels with
-# per-shape plans.  hipBLASLt (torch.addmm; a SiLU-mul runs as the native pass after it) runs a
-# default path only where the tile table names it for a projection with no residual epilogue that
-# it measured faster on: the 256-row decode step of 256 serving slots (O / down / LM head,
-# profiles/r4_dec256_gemm_probe.jsonl) and Llama-3-8B TP=1 prefill from 1024 rows, where the
-# library's 1.19-1.58 PFLOP/s beat this kernel's 0.87-1.26 on all four projections
-# (profiles/r4_llama_prefill_gemm_native_vs_blas.jsonl; tuned/gemm_tile_gfx950.json).  Otherwise
-# only on request (impl="blas" or MLS_GEMM_IMPL=blas, the A/B reference).
+# per-shape plans.  hipBLASLt (torch.addmm; a SiLU-mul runs as the native pass after it) runs only
+# the plain projections (no residual epilogue) the tile table routes to it because it measured faster:
+# the Llama-3-8B TP=1 shapes listed in README.md ("impl": "blas" entries of tuned/gemm_tile_gfx950.json:
+# 512-row QKV / O, the 256-row decode step's O / down / LM head, and every projection from 1024 rows;
+# profiles/r4_llama_prefill_gemm_native_vs_blas.jsonl, r4_dec256_gemm_probe.jsonl).  MLS_GEMM_IMPL=native
+# runs those on the tile kernel too; MLS_GEMM_IMPL=blas sends every plain projection to hipBLASLt.
 TILE_MIN_M = int(os.environ.get("MLS_TILE_MIN_M", "256"))
 
 
 BLAS_MIN_M = TILE_MIN_M  # kept for callers that split "large" from "small" token counts
 
 
-_GEMM_IMPL = os.environ.get("MLS_GEMM_IMPL", "native")
+_GEMM_IMPL = os.environ.get("MLS_GEMM_IMPL", "auto")  # auto: the table routes; native; blas
 
 
 def linear(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, act=ACT_NONE,
            residual: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
            impl: str = "auto") -> torch.Tensor:
-    """Transformer projection ``act(a @ w.T + bias) (+ residual)``, all native: M >= TILE_MIN_M on the
-    persistent LDS-DMA tile kernel (:func:`gemm_tile`, bias / GELU / SiLU-mul / residual in its
-    epilogue), smaller M on the skinny / conv_gemm kernels (measured per-shape plans in
-    ``tuned/gemm_plan_gfx950.json``).  ``impl``: "auto" | "native" | "tile" | "blas" (hipBLASLt, the
-    A/B reference only; also ``MLS_GEMM_IMPL=blas``)."""
+    """Transformer projection ``act(a @ w.T + bias) (+ residual)``: M >= TILE_MIN_M on the table's
+    route -- the persistent LDS-DMA tile kernel (:func:`gemm_tile`, bias / GELU / SiLU-mul / residual
+    in its epilogue) or conv_gemm, and hipBLASLt for the plain Llama-3-8B TP=1 shapes the table routes
+    there (module comment) -- smaller M on the skinny / conv_gemm kernels (measured per-shape plans in
+    ``tuned/gemm_plan_gfx950.json``).  ``impl``: "auto" | "native" (never the library) | "tile" |
+    "blas" (hipBLASLt for everything; also ``MLS_GEMM_IMPL=native`` / ``=blas``)."""
     code = _act(act)
     M, K = a.shape
     N = w.shape[0]
     if impl == "blas" or (impl == "auto" and _GEMM_IMPL == "blas"):
         return _linear_blas(a, w, bias, code, residual)
-    if impl == "tile" or (impl == "auto" and M >= TILE_MIN_M and K % 64 == 0 and N % 16 == 0
+    if impl == "tile" or (impl in ("auto", "native") and M >= TILE_MIN_M and K % 64 == 0 and N % 16 == 0
                           and a.device.type == "cuda" and a.is_contiguous() and w.is_contiguous()):
         kind, cfg, sk = tile_route_for(M, N, K) if impl == "auto" else ("tile",) + tile_cfg_for(M, N, K)
+        native_only = impl == "native" or (impl == "auto" and _GEMM_IMPL == "native")
+        if kind == "blas" and native_only:
+            kind, (cfg, sk) = "tile", tile_cfg_for(M, N, K)
         if kind == "blas" and code in (ACT_NONE, ACT_GELU, ACT_SILU_MUL) and residual is None:
             return _linear_blas(a, w, bias, code, residual)
         if kind == "conv":
@@ -52,7 +55,7 @@ def linear(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         if kind != "tile":
             cfg, sk = 0, 1  # a library route for a fused epilogue: the tile kernel's own pick
         return gemm_tile(a, w, bias, act=code, residual=residual, cfg=cfg, splitk=sk, workspace=workspace)
-    plan = small_m_plan_for(M, N, K) if impl == "auto" else None
+    plan = small_m_plan_for(M, N, K) if impl in ("auto", "native") else None
     if plan is not None and plan[0] > 0 and not (code == ACT_SILU_MUL and residual is not None):
         return gemm(a, w, bias, act=code, residual=residual, workspace=workspace, cfg=plan[0], splitk=plan[1])
     return gemm(a, w, bias, act=code, residual=residual, workspace=workspace)

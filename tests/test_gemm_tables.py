@@ -65,3 +65,47 @@ def test_resnet_tuning_regimes():
     assert conc["layer4.1.conv2"][0] >= ops.CFG_PIPE
     assert set(ser) == set(conc)
     assert autotune.load_tuning("resnet50", 8, regime="serial") == autotune.load_tuning("resnet50", 8)
+
+
+def test_readme_lists_every_library_route():
+    """Every shape the tile table routes to hipBLASLt ("impl": "blas") is listed in README.md's
+    library-route table, and the README lists no route the table does not have (VERDICT r4 item 6:
+    the docs name exactly which shapes run which kernel)."""
+    import json
+    import os
+    import re
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "mlmicroservicetemplate_amd", "ops", "tuned", "gemm_tile_gfx950.json")) as f:
+        entries = json.load(f)["entries"]
+    blas = {e["shape"] for e in entries if e.get("impl") == "blas"}
+    with open(os.path.join(root, "README.md")) as f:
+        readme = f.read()
+    listed = set(re.findall(r"^\| `([a-z0-9_]+)` \| ", readme, flags=re.M))
+    assert blas and blas == listed, (sorted(blas), sorted(listed))
+
+
+def test_native_impl_never_routes_to_the_library(monkeypatch):
+    """MLS_GEMM_IMPL=native / impl="native": a shape the table routes to hipBLASLt runs the tile
+    kernel instead (the route is resolved before any GPU call, so this runs on the CPU)."""
+    from mlmicroservicetemplate_amd.ops import dispatch
+
+    calls = []
+    monkeypatch.setattr(dispatch, "_linear_blas", lambda *a, **k: calls.append("blas"))
+    monkeypatch.setattr(dispatch, "gemm_tile", lambda *a, **k: calls.append(("tile", k.get("cfg"), k.get("splitk"))))
+
+    class FakeCuda:  # just enough of a CUDA tensor for the dispatch predicates
+        def __init__(self, *shape):
+            self.shape = shape
+            self.device = type("D", (), {"type": "cuda"})()
+
+        def is_contiguous(self):
+            return True
+
+    a, w = FakeCuda(4096, 4096), FakeCuda(6144, 4096)  # llama_qkv: a "blas" route from 1024 rows
+    assert ops.tile_route_for(4096, 6144, 4096)[0] == "blas"
+    dispatch.linear(a, w)
+    assert calls == ["blas"]
+    calls.clear()
+    dispatch.linear(a, w, impl="native")
+    assert calls and calls[0][0] == "tile", calls
