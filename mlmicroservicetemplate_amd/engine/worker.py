@@ -62,6 +62,7 @@ class _Slot:
     graphs: Dict[int, torch.cuda.CUDAGraph] = field(default_factory=dict)
     graph_copies: Dict[int, bool] = field(default_factory=dict)  # bucket -> copies inside the graph
     pushed: Dict[int, bool] = field(default_factory=dict)  # bucket -> results pushed to host by the graph
+    pulled: Dict[int, bool] = field(default_factory=dict)  # bucket -> input pulled from host by the graph
     native: Dict[int, tuple] = field(default_factory=dict)  # bucket -> mls_engine_launch arguments
     s_comp: Optional[torch.cuda.Stream] = None  # this slot's compute stream (concurrent mode)
     pool: Optional[tuple] = None  # this slot's graph memory pool (concurrent mode)
@@ -258,10 +259,11 @@ class GpuEngine:
                 self._free.put(slot)
         # spare pinned input buffers for prepare() / launch_prepared(): a batch is staged while every
         # slot is still busy, so a freed slot only waits for the enqueue (the staging copy of a
-        # 4.8 MB ResNet batch, 80-180 us of host time, moves off the refill path)
+        # 4.8 MB ResNet batch, 80-180 us of host time, moves off the refill path).  Allocated on the
+        # first prepare(): serving engines that never pre-stage hold no extra pinned memory
         self._spare: "queue.Queue[torch.Tensor]" = queue.Queue()
-        for _ in range(self.inflight + 1):
-            self._spare.put(torch.zeros((self.max_batch, *self.sample_shape), dtype=sample_dtype, pin_memory=True))
+        self._spare_lock = threading.Lock()
+        self._spare_made = False
 
     # ------------------------------------------------------------------ capture
     def warmup(self, capture: bool = True) -> None:
@@ -293,14 +295,17 @@ class GpuEngine:
                                               capture_error_mode="thread_local"):
                             if in_graph:
                                 slot.dev_in[:b].copy_(slot.host_in[:b], non_blocking=True)
-                            elif self.pull_h2d:
+                            # the copy kernel moves whole 16-B units: other input sizes keep the copy
+                            pull = (bool(self.pull_h2d) and not in_graph
+                                    and (slot.host_in[:b].numel() * slot.host_in.element_size()) % 16 == 0)
+                            if pull:
                                 from .. import ops
 
                                 ops.h2d_pull(slot.host_in[:b], slot.dev_in[:b], self.pull_h2d)
                             outs = self.forward(slot.dev_in[:b])
                             # ... and the results pushed to the pinned host buffers by a kernel at the
                             # graph's end (no SDMA D2H either), when every output is a 16-B multiple
-                            push = bool(self.pull_h2d) and all(
+                            push = pull and all(
                                 d.is_contiguous() and (d.numel() * d.element_size()) % 16 == 0 for d in outs)
                             if push:
                                 for h, d in zip(slot.host_out[b], outs):
@@ -311,7 +316,8 @@ class GpuEngine:
                         slot.graphs[b] = g
                         slot.outs[b] = tuple(outs)
                         slot.graph_copies[b] = in_graph
-                        slot.pushed[b] = bool(self.pull_h2d) and not in_graph and push
+                        slot.pulled[b] = pull
+                        slot.pushed[b] = push
                         if self.native_launch:
                             self._prepare_native(slot, b)
                 torch.cuda.synchronize(self.device)
@@ -343,13 +349,13 @@ class GpuEngine:
             from .. import ops
 
             lib = ops.lib()
-            # called through a PyDLL handle: the GIL stays held for the ~40 us call.  Through the
-            # CDLL (GIL released per call) 2 of 19 20-step bench runs stalled the host ~6 ms (33.8k
-            # / 35.1k req/s, host submit 0.44 ms/step); with the GIL held 0 of 20 (median 49.9k vs
-            # 48.9-49.3k for the Python enqueue).  The mechanism is not identified -- the bench
-            # process has no other Python thread (tools/probe/threads_probe.py)
-            # (profiles/r4_engine_native_launch_outliers.jsonl)
-            fn = getattr(ctypes.PyDLL(lib._name), "mls_engine_launch")
+            # called through the CDLL handle: the GIL is released for the call, so a serving
+            # process's front-end / waiter threads run meanwhile.  Round 4 held it (PyDLL) after 2
+            # of 19 20-step runs stalled ~6 ms with it released; round 5 found those stalls in the
+            # SDMA H2D copy itself, with the GIL held as well (docs/PERF_NOTES.md, round 5) -- the
+            # engine no longer uses SDMA (pull_h2d).  MLS_ENQUEUE_HOLD_GIL=1 keeps the PyDLL form.
+            hold = os.environ.get("MLS_ENQUEUE_HOLD_GIL", "0") == "1"
+            fn = getattr(ctypes.PyDLL(lib._name) if hold else lib, "mls_engine_launch")
             fn.argtypes = lib.mls_engine_launch.argtypes
             fn.restype = lib.mls_engine_launch.restype
             exec_h = slot.graphs[b].raw_cuda_graph_exec()
@@ -362,7 +368,7 @@ class GpuEngine:
             nb = (ctypes.c_longlong * max(n, 1))(*[d.numel() * d.element_size() for d in outs[:n]])
             h2d = slot.host_in[:b]
             t_ns = (ctypes.c_longlong * 5)()  # per-call host times of the last enqueue (diagnostics)
-            h2d_bytes = 0 if self.pull_h2d else h2d.numel() * h2d.element_size()  # pulled in the graph
+            h2d_bytes = 0 if slot.pulled.get(b) else h2d.numel() * h2d.element_size()  # pulled in the graph
             args = (slot.s_comp.cuda_stream, slot.dev_in.data_ptr(), slot.host_in.data_ptr(),
                     h2d_bytes, exec_h, n, dst, src, nb, ev, t_ns)
             if not exec_h or not ev:
@@ -417,6 +423,12 @@ class GpuEngine:
         if n == 0:
             raise ValueError("empty batch")
         pick_bucket(n, self.buckets)
+        with self._spare_lock:
+            if not self._spare_made:
+                for _ in range(self.inflight + 1):
+                    self._spare.put(torch.zeros((self.max_batch, *self.sample_shape), dtype=self.sample_dtype,
+                                                pin_memory=True))
+                self._spare_made = True
         buf = self._spare.get()
         try:
             with tracing.range(self._tr_stage):
@@ -489,7 +501,7 @@ class GpuEngine:
                 with self._enqueue_lock:
                     self._pace_launch()
                     fn, args, _keep = nat
-                    if staged is not None and self.pull_h2d:  # the graph pulls from the slot's buffer
+                    if staged is not None and slot.pulled.get(bucket):  # the graph pulls from the slot's buffer
                         slot.host_in.numpy()[:n] = staged.buf.numpy()[:n]
                     elif staged is not None:  # same call, H2D from the prepared buffer
                         args = args[:2] + (staged.buf.data_ptr(),) + args[3:]
@@ -513,7 +525,7 @@ class GpuEngine:
                     return Ticket(self, slot, bucket, n, staged)
                 s_h2d = slot.s_comp if self.copies_on_slot_stream else self.s_h2d
                 s_d2h = slot.s_comp if self.copies_on_slot_stream else self.s_d2h
-                pulled = self.pull_h2d and self.use_graphs and bucket in slot.graphs
+                pulled = self.use_graphs and bucket in slot.graphs and slot.pulled.get(bucket, False)
                 if pulled and staged is not None:  # the graph pulls from the slot's own buffer
                     slot.host_in[:n].copy_(staged.buf[:n])
                 with tracing.range(self._tr_h2d), torch.cuda.stream(s_h2d):

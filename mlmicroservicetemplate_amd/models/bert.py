@@ -262,6 +262,29 @@ class BertFused:
         self.cls_w, self.cls_b = cw, cb
         self._ws = ops.StreamWorkspace(16 << 20, self.device)  # per stream: concurrent engine slots
         self._cls_idx: Dict = {}
+        # LayerNorm folding (csrc/gemm_tile.hip "LayerNorm folding"): LN1 of layer i folds into its
+        # FFN-up projection, LN2 of layer i - 1 into layer i's QKV projection; the residual adds
+        # after them normalize their residual operand in the epilogue.  No LN kernel runs between
+        # the encoder layers' GEMMs (the last layer, which runs on the [CLS] rows only, keeps them).
+        # Folded from the bf16 weights / LN parameters the unfolded path uses; the residual adds that
+        # normalize their residual take that LN's beta in their bias.
+        self.ln_fold = os.environ.get("MLS_BERT_LN_FOLD", "1") != "0"
+        self._fold: Dict[str, torch.Tensor] = {}
+        if self.ln_fold:
+            w, fw = self.w, self._fold
+            for i in range(cfg.layers):
+                g1, b1 = w[f"l{i}.ln1.g"].float(), w[f"l{i}.ln1.b"].float()
+                fw[f"l{i}.ffn1.w"], fw[f"l{i}.ffn1.c"], fw[f"l{i}.ffn1.b"] = \
+                    ops.fold_layernorm(w[f"l{i}.ffn1.w"], w[f"l{i}.ffn1.b"], g1, b1)
+                fw[f"l{i}.ln1.g"] = g1.contiguous()
+                fw[f"l{i}.ffn2.b"] = (w[f"l{i}.ffn2.b"] + b1).contiguous()
+                g2, b2 = w[f"l{i}.ln2.g"].float(), w[f"l{i}.ln2.b"].float()
+                fw[f"l{i}.ln2.g"] = g2.contiguous()
+                if i + 1 < cfg.layers:
+                    j = i + 1
+                    fw[f"l{j}.qkv.w"], fw[f"l{j}.qkv.c"], fw[f"l{j}.qkv.b"] = \
+                        ops.fold_layernorm(w[f"l{j}.qkv.w"], w[f"l{j}.qkv.b"], g2, b2)
+                    fw[f"l{j}.o.b"] = (w[f"l{j}.o.b"] + b2).contiguous()
 
     def forward(self, ids: torch.Tensor, type_ids: Optional[torch.Tensor], lens: torch.Tensor) -> torch.Tensor:
         """ids/type_ids int32 ``[B, S]``, lens int32 ``[B]`` -> bf16 logits ``[B, Cpad]``."""
@@ -295,23 +318,52 @@ class BertFused:
         ws = self._ws.get()
         cls = self._cls_rows(B, S)
         last = cfg.layers - 1
+        H, T, eps, fw = cfg.hidden, B * S, cfg.eps, self._fold
+        fold = self.ln_fold and all(ops.ln_foldable(T, n, k) for n, k in (
+            (3 * H, H), (H, H), (cfg.intermediate, H), (H, cfg.intermediate)))
+        # fold: h = the previous layer's raw pre-LN2 rows (its LN2 output is never formed); part[cur] =
+        # the row statistics (partials) of the rows whose LN the next consumer applies, written by the
+        # residual projection that produced them (two buffers: a producer reads one, writes the other)
+        part = [ops.ln_partials(T, H, x.device) for _ in range(2)] if fold else None
+        cur, h = 0, None
         for i in range(cfg.layers):
             # all four projections native (ops.linear: the LDS-DMA tile kernel from TILE_MIN_M tokens,
             # the conv_gemm tiles below); the residual rides in the o / FFN-down epilogues
-            qkv = ops.linear(x, w[f"l{i}.qkv.w"], w[f"l{i}.qkv.b"], workspace=ws)
+            if h is None:
+                qkv = ops.linear(x, w[f"l{i}.qkv.w"], w[f"l{i}.qkv.b"], workspace=ws)
+            else:
+                qkv = ops.linear_ln(h, fw[f"l{i}.qkv.w"], fw[f"l{i}.qkv.b"], fold_c=fw[f"l{i}.qkv.c"],
+                                    ln_part=part[cur], eps=eps)
             a = ops.flash_attention(qkv, B, S, cfg.heads, cfg.heads, cfg.head_dim, kv_lens=lens)
+            if fold and i < last:
+                if h is None:
+                    h1 = ops.linear_ln(a, w[f"l{i}.o.w"], w[f"l{i}.o.b"], residual=x, stats_part=part[1 - cur])
+                else:
+                    h1 = ops.linear_ln(a, w[f"l{i}.o.w"], fw[f"l{i}.o.b"], residual=h, ln_part=part[cur],
+                                       ln_g=fw[f"l{i - 1}.ln2.g"], stats_part=part[1 - cur], eps=eps)
+                cur = 1 - cur
+                f1 = ops.linear_ln(h1, fw[f"l{i}.ffn1.w"], fw[f"l{i}.ffn1.b"], act=ops.ACT_GELU,
+                                   fold_c=fw[f"l{i}.ffn1.c"], ln_part=part[cur], eps=eps)
+                h = ops.linear_ln(f1, w[f"l{i}.ffn2.w"], fw[f"l{i}.ffn2.b"], residual=h1, ln_part=part[cur],
+                                  ln_g=fw[f"l{i}.ln1.g"], stats_part=part[1 - cur], eps=eps)
+                cur = 1 - cur
+                continue
             if i == last:
                 # the classifier reads only the [CLS] rows of the last layer: its keys / values need
                 # every token (the QKV projection and attention above), but everything after the
                 # attention is per token -- run it on the B [CLS] rows (native row gather) instead
                 # of all B*S (~5 % of the forward's GEMM FLOPs at S = 128; same logits)
                 a = ops.embedding(cls, a)
-                x = ops.embedding(cls, x)
-            h = ops.linear(a, w[f"l{i}.o.w"], w[f"l{i}.o.b"], residual=x, workspace=ws)
-            x = ops.layernorm(h, w[f"l{i}.ln1.g"], w[f"l{i}.ln1.b"], eps=cfg.eps)
+                if h is not None:  # the previous layer's LN2, on the [CLS] rows only
+                    x = ops.layernorm(ops.embedding(cls, h), w[f"l{i - 1}.ln2.g"], w[f"l{i - 1}.ln2.b"], eps=eps)
+                    h = None
+                else:
+                    x = ops.embedding(cls, x)
+            hh = ops.linear(a, w[f"l{i}.o.w"], w[f"l{i}.o.b"], residual=x, workspace=ws)
+            x = ops.layernorm(hh, w[f"l{i}.ln1.g"], w[f"l{i}.ln1.b"], eps=eps)
             f1 = ops.linear(x, w[f"l{i}.ffn1.w"], w[f"l{i}.ffn1.b"], act=ops.ACT_GELU, workspace=ws)
-            h = ops.linear(f1, w[f"l{i}.ffn2.w"], w[f"l{i}.ffn2.b"], residual=x, workspace=ws)
-            x = ops.layernorm(h, w[f"l{i}.ln2.g"], w[f"l{i}.ln2.b"], eps=cfg.eps)
+            hh = ops.linear(f1, w[f"l{i}.ffn2.w"], w[f"l{i}.ffn2.b"], residual=x, workspace=ws)
+            x = ops.layernorm(hh, w[f"l{i}.ln2.g"], w[f"l{i}.ln2.b"], eps=eps)
         pooled = ops.gemm(x, w["pooler.w"], w["pooler.b"], act=ops.ACT_TANH, workspace=ws)  # x: the [CLS] rows
         return ops.gemm(pooled, self.cls_w, self.cls_b, workspace=ws)
 

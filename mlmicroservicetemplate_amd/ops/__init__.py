@@ -33,12 +33,16 @@ from .gemm_ops import (  # noqa: F401
     FP8_MAX,
     GEMM_TILE_CFGS,
     SPLIT_COUNTER_ELEMS,
+    fold_layernorm,
     fold_norm,
     fp8_reference,
     gemm,
     gemm_heuristic,
     gemm_rmsnorm,
     gemm_tile,
+    gemm_tile_ln,
+    layernorm_from_partials,
+    ln_partials,
     interleave_gate_up,
     pack_skinny,
     pack_skinny_fp8,
@@ -53,6 +57,8 @@ from .dispatch import (  # noqa: F401
     BLAS_MIN_M,
     TILE_MIN_M,
     linear,
+    linear_ln,
+    ln_foldable,
 )
 from .softmax import (  # noqa: F401
     softmax_rows,

@@ -39,6 +39,7 @@ _SIGS = {
     "mls_gemm_heuristic": [I, I, I, _c.POINTER(I), _c.POINTER(I)],
     "mls_gemm_tile": [P, P, P, P, P, I, I, I, I, I, I, I, I, I, P, _c.c_longlong, P, I, P],
     "mls_gemm_tile_pick": [I, I],
+    "mls_gemm_tile_ln": [P, P, P, P, P, I, I, I, I, I, P, P, P, P, _c.c_longlong, F, P],
     "mls_gemm_num_cfgs": [],
     "mls_normalize_u8": [P, P, I, I, I, I, FP, FP, P],
     "mls_maxpool2d": [P, P, I, I, I, I, I, I, I, P],

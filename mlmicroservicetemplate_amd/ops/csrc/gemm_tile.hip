@@ -41,6 +41,13 @@ struct GemmTileArgs {
   int splitk;  // K splits per output tile (>= 1); > 1: fp32 slabs in ws + per-tile arrival counters
   float* ws;   // [tiles][splitk][BM * BN] fp32 partial tiles (fragment-linear)
   int* cnt;    // [tiles] arrival counters: zero before the launch, reset to zero by each tile's reducer
+  // LayerNorm folding (see "LayerNorm folding" below)
+  const float* fold_c;    // EPI 4: [N] sum_k W'[n][k] of the gamma-folded weight
+  const float* ln_part;   // EPI 3 / 4: [M][P][2] row partials (sum, sum of squares) of the LN'd operand,
+                          // P = its width / 64 (as a PART epilogue wrote them)
+  const float* ln_g;      // EPI 3: [N] fp32 gamma of the residual's LN (its beta is folded into bias)
+  float* stats_part;      // PART: [M][N / 64][2] partials of the OUTPUT rows, one per 64-column wave tile
+  float eps;
 };
 // ablation flags (tools/gemm_tile_probe.py --ablate; cfg bits 8+ of mls_gemm_tile): timing-only builds
 // of the same instruction stream (cdna_hip_programming.md §7, "price ONE buffer's traffic")
@@ -125,75 +132,193 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 // instruction: half the store instructions of the bf16x4-per-lane layout (the tail is store-ISSUE
 // bound: MI355X_MICROARCH.md, 'attention epilogue store tail').  Bias and residual are loaded in
 // the same layout (16-B range-checked buffer loads, OOB -> 0).
-template <int MT, int NTL, int EPI, int ACT>
-MLS_DEV void gt_epilogue_t(f32x4 (&acc)[MT][NTL], const GemmTileArgs& g, int m0, int n0, int wrow, int wcol) {
+// Row statistics of this lane's MT epilogue rows from the [M][P][2] partials a PART epilogue wrote
+// (P = width / 128 <= 8 partials per row, 128 columns each): lane fq loads partials 2fq and 2fq + 1
+// with one 16-B load (issued first, beside the bias loads), then two lane swaps finish the row in a
+// fixed order -- deterministic.  gt_row_stats_finish returns rmu = -mu * rstd and rrs = rstd.
+template <int MT>
+MLS_DEV void gt_row_stats_issue(const float* part, int width, int m0, int rows, int wrow, uint4 (&t)[MT]) {
+  const int lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4;
+  const int P = width >> 7;
+  const rsrc_t rp = make_rsrc(part + (size_t)m0 * P * 2, (uint32_t)(rows * P * 8));
+#pragma unroll
+  for (int i = 0; i < MT; ++i) t[i] = bload16(rp, 2 * fq < P ? ((wrow + i * 16 + fr) * P + 2 * fq) * 8 : OOB);
+}
+template <int MT>
+MLS_DEV void gt_row_stats_finish(const uint4 (&t)[MT], int width, float eps, float (&rmu)[MT], float (&rrs)[MT]) {
+  const float invn = 1.f / (float)width;
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    float s1 = __uint_as_float(t[i].x) + __uint_as_float(t[i].z);
+    float s2 = __uint_as_float(t[i].y) + __uint_as_float(t[i].w);
+    s1 += xor16_f(s1);
+    s2 += xor16_f(s2);
+    s1 += xor32_f(s1);
+    s2 += xor32_f(s2);
+    const float mu = s1 * invn;
+    const float r = rsqrtf(fmaxf(s2 * invn - mu * mu, 0.f) + eps);
+    rrs[i] = r;
+    rmu[i] = -mu * r;
+  }
+}
+
+// EPI 3: bias + LayerNorm(residual) (row statistics from g.ln_part, fp32 gamma per column; the LN's
+// beta is folded into the bias by the caller);
+// EPI 4: LN-folded A: rstd * (acc - mu * fold_c) + bias (+ act), A-row statistics from g.ln_part.
+// PART: also accumulate each output row's sum / sum of squares over this wave's columns (of the bf16
+// values stored); the two waves of each 128-column block combine theirs through LDS (pscr: [WN][BM]
+// float2 past the ring, one block barrier) and one thread per (row, block) stores the pair to
+// g.stats_part.  Every wave of the block runs the same epilogue, so the barrier is uniform.
+template <int MT, int NTL, int EPI, int ACT, bool PART = false, int BM = 256, int WN = 4>
+MLS_DEV void gt_epilogue_t(f32x4 (&acc)[MT][NTL], const GemmTileArgs& g, int m0, int n0, int wrow, int wcol,
+                           float* pscr = nullptr) {
   static_assert(NTL % 2 == 0, "column tiles pair up");
+  constexpr bool RES = EPI == 1 || EPI == 3;
+  // the LayerNorm forms hold per-row values (stats, partial sums) across the column loop: the 256-row
+  // tile (MT = 8) walks its rows in two halves, each re-reading the (L1-resident) column vectors, so
+  // the per-row arrays stay at 4 entries (the whole tile at once spilled 8-19 VGPRs)
+  constexpr int RH = (EPI >= 3 || PART) && MT >= 8 ? 2 : 1, MH = MT / RH;
   const int lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4;
   const int ldo2 = g.ldo * 2, ldr2 = g.ldr * 2;
   const int rows = g.M - m0 < 256 ? g.M - m0 : 256;  // valid rows of this tile (tiles are <= 256 tall)
   const bool nostore = g.flags & GT_ABL_NOSTORE;
   const rsrc_t ro = make_rsrc(g.out + (size_t)m0 * g.ldo, nostore ? 0u : (uint32_t)(rows * ldo2));
-  const rsrc_t rr = make_rsrc(EPI == 1 ? g.res + (size_t)m0 * g.ldr : g.out, EPI == 1 ? (uint32_t)(rows * ldr2) : 0u);
+  const rsrc_t rr = make_rsrc(RES ? g.res + (size_t)m0 * g.ldr : g.out, RES ? (uint32_t)(rows * ldr2) : 0u);
   const bool use_bias = g.bias && !(g.flags & GT_ABL_NOBIAS);
   const rsrc_t rb = make_rsrc(use_bias ? (const void*)g.bias : (const void*)g.out, use_bias ? (uint32_t)g.N * 4u : 0u);
+  const rsrc_t rg = EPI == 3 || EPI == 4 ? make_rsrc(EPI == 3 ? g.ln_g : g.fold_c, (uint32_t)g.N * 4u) : rb;
   const int sub = (fq & 1) * 16 + (fq >> 1) * 8;  // this lane's 8 columns within the 32-column pair
 #pragma unroll
-  for (int p = 0; p < NTL / 2; ++p) {
-    const int c0 = n0 + wcol + p * 32, c = c0 + sub;
-    const bool col_ok = c < g.N;  // N % 16 == 0: an 8-column run is wholly in or out
-    const f32x4 b_lo = __builtin_bit_cast(f32x4, bload16(rb, col_ok ? c * 4 : OOB));
-    const f32x4 b_hi = __builtin_bit_cast(f32x4, bload16(rb, col_ok ? c * 4 + 16 : OOB));
-    // residual rows two 16-row blocks ahead (a whole column of them live would cost 32 VGPRs and
-    // spill the 256 x 256 tile)
-    const int roff = col_ok ? (wrow + fr) * ldr2 + c * 2 : OOB;
-    uint4 rv0 = {0, 0, 0, 0}, rv1 = {0, 0, 0, 0};
-    if constexpr (EPI == 1) {
-      rv0 = bload16(rr, roff);
-      if (MT > 1) rv1 = bload16(rr, col_ok ? roff + 16 * ldr2 : OOB);
+  for (int h = 0; h < RH; ++h) {
+    const int hrow = wrow + h * MH * 16;  // first row of this half (within the tile)
+    // per-row (-mu * rstd, rstd) of this lane's rows (EPI 3 / 4) and partial sums (PART)
+    float rmu[MH], rrs[MH], ps1[MH], ps2[MH];
+#pragma unroll
+    for (int i = 0; i < MH; ++i) ps1[i] = ps2[i] = 0.f;
+    constexpr bool STATS = EPI == 3 || EPI == 4;
+    const int lnw = EPI == 3 ? g.N : g.K;  // the LN'd rows' width: the residual's (N) or A's (K)
+    uint4 st[MH];
+    if constexpr (STATS) gt_row_stats_issue<MH>(g.ln_part, lnw, m0, rows, hrow, st);
+#pragma unroll
+    for (int p = 0; p < NTL / 2; ++p) {
+      const int c0 = n0 + wcol + p * 32, c = c0 + sub;
+      const bool col_ok = c < g.N;  // N % 16 == 0: an 8-column run is wholly in or out
+      const f32x4 b_lo = __builtin_bit_cast(f32x4, bload16(rb, col_ok ? c * 4 : OOB));
+      const f32x4 b_hi = __builtin_bit_cast(f32x4, bload16(rb, col_ok ? c * 4 + 16 : OOB));
+      f32x4 g_lo = {0.f, 0.f, 0.f, 0.f}, g_hi = g_lo;
+      if constexpr (STATS) {
+        g_lo = __builtin_bit_cast(f32x4, bload16(rg, col_ok ? c * 4 : OOB));
+        g_hi = __builtin_bit_cast(f32x4, bload16(rg, col_ok ? c * 4 + 16 : OOB));
+        if (p == 0) gt_row_stats_finish<MH>(st, lnw, g.eps, rmu, rrs);  // its loads flew beside the bias
+      }
+      // residual rows two 16-row blocks ahead (a whole column of them live would cost 32 VGPRs and
+      // spill the 256 x 256 tile)
+      const int roff = col_ok ? (hrow + fr) * ldr2 + c * 2 : OOB;
+      uint4 rv0 = {0, 0, 0, 0}, rv1 = {0, 0, 0, 0};
+      if constexpr (RES) {
+        rv0 = bload16(rr, roff);
+        if (MH > 1) rv1 = bload16(rr, col_ok ? roff + 16 * ldr2 : OOB);
+      }
+#pragma unroll
+      for (int i = 0; i < MH; ++i) {
+        const int ia = h * MH + i;        // accumulator row block
+        const int r = hrow + i * 16 + fr;  // row within the tile
+        uint4 rcur = rv0;
+        if constexpr (RES) {
+          rv0 = rv1;
+          if (i + 2 < MH) rv1 = bload16(rr, col_ok ? roff + (i + 2) * 16 * ldr2 : OOB);
+        }
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          // __float_as_uint, not __builtin_bit_cast: hipcc (ROCm 7.2) folds a bit_cast of an ext-vector
+          // element feeding this builtin to element 0 -- one swap for all four (checked in the .s)
+          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[ia][2 * p][e]),
+                                                           __float_as_uint(acc[ia][2 * p + 1][e]), false, false);
+          if constexpr (EPI == 4) {  // rstd * (acc - mu * c) + b
+            v[e] = fmaf(rrs[i], __uint_as_float(sw[0]), fmaf(rmu[i], g_lo[e], b_lo[e]));
+            v[4 + e] = fmaf(rrs[i], __uint_as_float(sw[1]), fmaf(rmu[i], g_hi[e], b_hi[e]));
+          } else {
+            v[e] = __uint_as_float(sw[0]) + b_lo[e];
+            v[4 + e] = __uint_as_float(sw[1]) + b_hi[e];
+          }
+        }
+        bf16x8 o;
+        int off;
+        if constexpr (EPI == 2) {
+          // gate lanes fq 0/1 (tile 2p / 2p+1 cols 0-7) pair with their up columns on lanes fq 2/3
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = (bf16)(silu_fast(v[e]) * xor32_f(v[e]));
+          off = fq < 2 && col_ok ? r * ldo2 + ((c0 >> 1) + fq * 8) * 2 : OOB;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float x = v[e];
+            v[e] = ACT == ACT_GELU ? gelu_fast(x) : ACT == ACT_RELU ? fmaxf(x, 0.f) : ACT == ACT_SILU ? silu_fast(x)
+                   : ACT == ACT_TANH ? tanhf(x) : x;
+          }
+          if constexpr (EPI == 1) {
+            const bf16x8 rb8 = __builtin_bit_cast(bf16x8, rcur);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += (float)rb8[e];
+          } else if constexpr (EPI == 3) {
+            const bf16x8 rb8 = __builtin_bit_cast(bf16x8, rcur);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float n = fmaf((float)rb8[e], rrs[i], rmu[i]);  // (r - mu) * rstd
+              v[e] = fmaf(n, e < 4 ? g_lo[e] : g_hi[e - 4], v[e]);
+            }
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[e] = (bf16)v[e];
+          if constexpr (PART) {  // columns >= N read as zero (residual / accumulators) and add nothing
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float q = col_ok ? (float)o[e] : 0.f;
+              ps1[i] += q;
+              ps2[i] = fmaf(q, q, ps2[i]);
+            }
+          }
+          off = col_ok ? r * ldo2 + c * 2 : OOB;
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), ro, off, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);  // keep each row block's live range to itself
+      }
     }
+    if constexpr (PART) {
+      // the 4 lanes fq of a row hold different columns: finish the wave's sums, lanes fq 0 park them
+      static_assert(NTL * 16 == 64, "two 64-column waves per 128-column partial");
+      const int wn = wcol / 64;
 #pragma unroll
-    for (int i = 0; i < MT; ++i) {
-      const int r = wrow + i * 16 + fr;  // row within the tile
-      uint4 rcur = rv0;
-      if constexpr (EPI == 1) {
-        rv0 = rv1;
-        if (i + 2 < MT) rv1 = bload16(rr, col_ok ? roff + (i + 2) * 16 * ldr2 : OOB);
-      }
-      float v[8];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        // __float_as_uint, not __builtin_bit_cast: hipcc (ROCm 7.2) folds a bit_cast of an ext-vector
-        // element feeding this builtin to element 0 -- one swap for all four (checked in the .s)
-        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * p][e]),
-                                                         __float_as_uint(acc[i][2 * p + 1][e]), false, false);
-        v[e] = __uint_as_float(sw[0]) + b_lo[e];
-        v[4 + e] = __uint_as_float(sw[1]) + b_hi[e];
-      }
-      bf16x8 o;
-      int off;
-      if constexpr (EPI == 2) {
-        // gate lanes fq 0/1 (tile 2p / 2p+1 cols 0-7) pair with their up columns on lanes fq 2/3
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = (bf16)(silu_fast(v[e]) * xor32_f(v[e]));
-        off = fq < 2 && col_ok ? r * ldo2 + ((c0 >> 1) + fq * 8) * 2 : OOB;
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float x = v[e];
-          v[e] = ACT == ACT_GELU ? gelu_fast(x) : ACT == ACT_RELU ? fmaxf(x, 0.f) : ACT == ACT_SILU ? silu_fast(x)
-                 : ACT == ACT_TANH ? tanhf(x) : x;
+      for (int i = 0; i < MH; ++i) {
+        float a = ps1[i], b = ps2[i];
+        a += xor16_f(a);
+        b += xor16_f(b);
+        a += xor32_f(a);
+        b += xor32_f(b);
+        if (fq == 0) {
+          float2 v;
+          v.x = a;
+          v.y = b;
+          reinterpret_cast<float2*>(pscr)[wn * BM + hrow + i * 16 + fr] = v;
         }
-        if constexpr (EPI == 1) {
-          const bf16x8 rb8 = __builtin_bit_cast(bf16x8, rcur);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += (float)rb8[e];
-        }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = (bf16)v[e];
-        off = col_ok ? r * ldo2 + c * 2 : OOB;
       }
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), ro, off, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);  // keep each row block's live range to itself
+    }
+  }
+  if constexpr (PART) {
+    // one thread per (row, 128-column block of this tile): add the block's two waves, store the pair
+    constexpr int BN = WN * 64, QB = BN / 128;
+    static_assert(QB >= 1, "tile covers whole 128-column blocks");
+    const int P = g.N >> 7;
+    gt_barrier();
+    const rsrc_t rp = make_rsrc(g.stats_part + (size_t)m0 * P * 2, (uint32_t)(rows * P * 8));
+    for (int t = threadIdx.x; t < BM * QB; t += blockDim.x) {
+      const int r = t % BM, q = t / BM;
+      const float2 a = reinterpret_cast<const float2*>(pscr)[(2 * q) * BM + r];
+      const float2 b = reinterpret_cast<const float2*>(pscr)[(2 * q + 1) * BM + r];
+      const u32x2 v = {__float_as_uint(a.x + b.x), __float_as_uint(a.y + b.y)};
+      const int part = (n0 >> 7) + q;
+      __builtin_amdgcn_raw_buffer_store_b64(v, rp, part < P ? (r * P + part) * 8 : OOB, 0, 0);
     }
   }
 }
@@ -272,10 +397,31 @@ MLS_DEV void gt_epilogue_a(f32x4 (&acc)[MT][NTL], const GemmTileArgs& g, int m0,
   }
 }
 
-// dispatch once per tile, then zero the accumulators for the next tile in one straight run
-template <int MT, int NTL, bool X2 = false>
-MLS_DEV void gt_epilogue(f32x4 (&acc)[MT][NTL], const GemmTileArgs& g, int m0, int n0, int wrow, int wcol) {
-  if (g.act == ACT_SILU_MUL) {
+// dispatch once per tile, then zero the accumulators for the next tile in one straight run.  LN: the
+// LayerNorm-folding epilogues (EPI 3 / 4, + row statistics) -- gemm_tile_kernel instantiations only
+// LNK 1: the folded projection (EPI 4, act none / gelu); LNK 2: the residual projection (EPI 1 / 3,
+// + PART when g.stats_part) -- one instantiation per kind keeps each kernel's register peak to its own
+template <int MT, int NTL, int LNK, int BM, int WN>
+MLS_DEV void gt_epilogue_ln(f32x4 (&acc)[MT][NTL], const GemmTileArgs& g, int m0, int n0, int wrow, int wcol,
+                            float* pscr) {
+  if constexpr (LNK == 1) {
+    if (g.act == ACT_GELU) gt_epilogue_t<MT, NTL, 4, ACT_GELU>(acc, g, m0, n0, wrow, wcol);
+    else gt_epilogue_t<MT, NTL, 4, ACT_NONE>(acc, g, m0, n0, wrow, wcol);
+  } else if (g.stats_part) {
+    if (g.ln_part) gt_epilogue_t<MT, NTL, 3, ACT_NONE, true, BM, WN>(acc, g, m0, n0, wrow, wcol, pscr);
+    else gt_epilogue_t<MT, NTL, 1, ACT_NONE, true, BM, WN>(acc, g, m0, n0, wrow, wcol, pscr);
+  } else {
+    if (g.ln_part) gt_epilogue_t<MT, NTL, 3, ACT_NONE>(acc, g, m0, n0, wrow, wcol);
+    else gt_epilogue_t<MT, NTL, 1, ACT_NONE>(acc, g, m0, n0, wrow, wcol);
+  }
+}
+// LNK != 0: pscr = the LDS scratch past the ring that a PART epilogue combines its waves through
+template <int MT, int NTL, bool X2 = false, int LNK = 0, int BM = 256, int WN = 4>
+MLS_DEV void gt_epilogue(f32x4 (&acc)[MT][NTL], const GemmTileArgs& g, int m0, int n0, int wrow, int wcol,
+                         float* pscr = nullptr) {
+  if constexpr (LNK != 0) {
+    gt_epilogue_ln<MT, NTL, LNK, BM, WN>(acc, g, m0, n0, wrow, wcol, pscr);
+  } else if (g.act == ACT_SILU_MUL) {
     if constexpr (X2) gt_epilogue_x2<MT, NTL, 2, ACT_NONE>(acc, g, m0, n0, wrow, wcol);
     else gt_epilogue_t<MT, NTL, 2, ACT_NONE>(acc, g, m0, n0, wrow, wcol);
   } else if (g.res) {
@@ -370,8 +516,23 @@ MLS_DEV unsigned long long gt_realtime() {
   return t;
 }
 
-template <int BM, int BN, int WM, int WN, int STAGES, int BKS, bool STAMP = false, bool PIPE = false, bool X2 = false>
+// LayerNorm folding (BERT post-LN: x = LN(h) feeds the next projection AND the residual add after
+// it).  No LN kernel runs and x is never formed:
+//  * the producer of h (O / FFN-down projection, residual epilogue) stores h and, per output row and
+//    64-column wave tile, the sum and sum of squares of the bf16 values it stored (PART: [M][N/64][2]);
+//  * the projection that consumes x reads A = h and W' = W . diag(gamma): x . W^T = rstd * (h . W'^T -
+//    mu * c) + beta . W^T with c[n] = sum_k W'[n][k], applied to the accumulator in the epilogue
+//    (EPI 4);
+//  * the residual add after it normalizes its residual operand in the epilogue: (h - mu) * rstd *
+//    gamma + beta (EPI 3);
+//  * both consumers finish each row's (mu, rstd) from the partials themselves (gt_row_stats; the
+//    loads ride beside the bias loads) -- the kernel boundary orders them after the producer, so no
+//    cross-block protocol or extra launch is needed.
+// Removes the LN launch and its T x H read + write per LayerNorm.
+template <int BM, int BN, int WM, int WN, int STAGES, int BKS, bool STAMP = false, bool PIPE = false, bool X2 = false,
+          int LNK = 0>
 __global__ __launch_bounds__(WM * WN * 64) void gemm_tile_kernel(const GemmTileArgs g0) {
+  static_assert(LNK == 0 || (!STAMP && !X2 && BN / WN == 64), "LayerNorm-folding builds: 64-column wave tiles");
   // STAMP: g0.res is the stamp buffer [grid][8] (u64): t0 start, t1 first k-step landed, t2 first
   // tile's last MFMA, t3 its epilogue issued, t4 all stores retired, t5/t6 realtime at t0/t4, t7 tiles
   unsigned long long st[5] = {0, 0, 0, 0, 0}, rt0 = 0;
@@ -391,7 +552,11 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_tile_kernel(const GemmTileA
   static_assert(BKS == 32 || BKS == 64, "stage depth");
   // + 16 B: the split-K "last arriver" flag -- in the SAME __shared__ object as the ring (a second
   // one can make hipcc wait vmcnt(0) before every k-step's first ds_read: §5 item 4(a))
-  __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE_BYTES + 16];
+  // LNK == 2: [WN][BM] float2 scratch past the ring for the PART epilogue's cross-wave combine
+  constexpr int PSCR_BYTES = LNK == 2 ? WN * BM * 8 : 0;
+  static_assert(STAGES * STAGE_BYTES + 16 + PSCR_BYTES <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[STAGES * STAGE_BYTES + 16 + PSCR_BYTES];
+  float* const pscr = reinterpret_cast<float*>(smem + STAGES * STAGE_BYTES + 16);
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid - wm * WN;
@@ -528,9 +693,11 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_tile_kernel(const GemmTileA
       if (c_ti == 0) st[2] = gt_stamp();
     const int cu = bq + c_ti * G;
     tile_mn(c_ti++, m0, n0, k0);
+    // LNK: the LayerNorm-folding epilogues live in their own instantiations (all of them in one
+    // kernel cost ~30 VGPRs + ~60 SGPRs kernel-wide and spilled the 256 x 256 tile)
     const bool reducer = S == 1 || gt_splitk_arrive<BM * BN, MT, NTL>(acc, g, cu / S, cu - (cu / S) * S,
                                                                         (int*)(smem + STAGES * STAGE_BYTES));
-    if (reducer) gt_epilogue<MT, NTL, X2>(acc, g, m0, n0, wm * WTM, wn * WTN);
+    if (reducer) gt_epilogue<MT, NTL, X2, LNK, BM, WN>(acc, g, m0, n0, wm * WTM, wn * WTN, pscr);
     if constexpr (STAMP)
       if (c_ti == 1) st[3] = gt_stamp();
   }
@@ -891,6 +1058,23 @@ int gt_launch(const GemmTileArgs& g0, int cfg, int grid_cap, hipStream_t st) {
   if (g.splitk > 1 && (!sk_ok || (g.K / bks) % g.splitk || !g.ws || !g.cnt)) return MLS_BAD_ARG;
   const int units = ntiles * g.splitk;
   const dim3 grid(units < cap ? units : cap), block(c.threads);
+  if (g.fold_c || g.ln_part || g.stats_part) {  // LayerNorm folding (mls_gemm_tile_ln maps the cfg)
+#define GT_LN_LAUNCH(K)                                                                                              \
+  switch (cfg) {                                                                                                     \
+    case 15: hipLaunchKernelGGL((gemm_tile_kernel<256, 256, 2, 4, 2, 64, false, true, false, K>), grid, block, 0, st, g); break; \
+    case 16: hipLaunchKernelGGL((gemm_tile_kernel<256, 128, 4, 2, 3, 64, false, true, false, K>), grid, block, 0, st, g); break; \
+    case 5: hipLaunchKernelGGL((gemm_tile_kernel<128, 256, 2, 4, 3, 64, false, false, false, K>), grid, block, 0, st, g); break; \
+    case 4: hipLaunchKernelGGL((gemm_tile_kernel<128, 128, 2, 2, 3, 64, false, false, false, K>), grid, block, 0, st, g); break; \
+    default: return MLS_BAD_ARG;                                                                                     \
+  }
+    if (g.fold_c) {
+      GT_LN_LAUNCH(1)
+    } else {
+      GT_LN_LAUNCH(2)
+    }
+#undef GT_LN_LAUNCH
+    return hipGetLastError() == hipSuccess ? MLS_OK : MLS_BAD_ARG;
+  }
   switch (cfg) {
     case 1: hipLaunchKernelGGL((gemm_tile_kernel<256, 256, 2, 4, 2, 64>), grid, block, 0, st, g); break;
     case 2: hipLaunchKernelGGL((gemm_tile_kernel<256, 128, 4, 2, 3, 64>), grid, block, 0, st, g); break;
@@ -970,5 +1154,53 @@ int mls_gemm_tile(const void* A, const void* W, const float* bias, const void* r
 }
 
 int mls_gemm_tile_pick(int M, int N) { return gt_pick(M, N); }
+
+// LayerNorm-folding forms of mls_gemm_tile (module comment "LayerNorm folding"; no split-K, ldo = ldr = N).
+// Row statistics travel as [M][width / 128][2] partials (sum, sum of squares) written by a PART launch.
+//  * fold_c != null: A = the raw pre-LN rows, W = W . diag(gamma), bias = b + W . beta (ops.fold_layernorm);
+//    out = act(rstd * (A . W^T - mu * fold_c) + bias), A-row statistics from ln_part (K / 128 partials).
+//    act: none / gelu;
+//  * res != null: out = A . W^T + bias + res', res' = res, or (res - mu) * rstd * ln_g with ln_part (N / 128
+//    partials) given -- the LN's beta must be folded into bias; stats_part != null: also write the OUTPUT
+//    rows' partials there
+//    (>= M * N / 64 floats; N % 128 == 0).
+// The LN'd widths must be multiples of 128 and at most 1024.  cfg: 0 = by shape; the folding kernels
+// are the 256 x 256 / 256 x 128 PIPE tiles (15 / 16) and the 128 x 256 / 128 x 128 tiles (5 / 4).
+int mls_gemm_tile_ln(const void* A, const void* W, const float* bias, const void* res, void* out, int M, int N,
+                     int K, int act, int cfg, const float* fold_c, const float* ln_part, const float* ln_g,
+                     float* stats_part, long long part_elems, float eps, void* stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || K % 64 || N % 16) return MLS_BAD_ARG;
+  if (fold_c && (res || !ln_part || stats_part || (act != ACT_NONE && act != ACT_GELU) || K % 128 || K > 1024))
+    return MLS_BAD_ARG;
+  if (!fold_c && (!res || act != ACT_NONE)) return MLS_BAD_ARG;
+  if (ln_part && !fold_c && (!ln_g || N % 128 || N > 1024)) return MLS_BAD_ARG;
+  if (stats_part && (N % 128 || (long long)M * (N / 128) * 2 > part_elems)) return MLS_BAD_ARG;
+  const size_t ab = (size_t)M * K * 2, wb = (size_t)N * K * 2;
+  if (ab >= 0x7FFFFFFFull || wb >= 0x7FFFFFFFull || (size_t)M * N >= 0x3FFFFFFFull) return MLS_UNSUPPORTED;
+  int c = (cfg & 0xFF) > 0 ? (cfg & 0xFF) : gt_pick(M, N);
+  switch (c) {
+    case 15: case 16: case 5: case 4: break;
+    case 3: c = 4; break;
+    default: c = gt_cfg(c).bn == 128 ? 16 : 15; break;
+  }
+  GemmTileArgs g{};
+  g.a = (const bf16*)A;
+  g.w = (const bf16*)W;
+  g.bias = bias;
+  g.res = (const bf16*)res;
+  g.out = (bf16*)out;
+  g.M = M; g.N = N; g.K = K; g.act = act;
+  g.ldo = N;
+  g.ldr = N;
+  g.a_bytes = (uint32_t)ab;
+  g.w_bytes = (uint32_t)wb;
+  g.splitk = 1;
+  g.fold_c = fold_c;
+  g.ln_part = ln_part;
+  g.ln_g = ln_g;
+  g.stats_part = stats_part;
+  g.eps = eps;
+  return gt_launch(g, c, 0, (hipStream_t)stream);
+}
 
 }  // extern "C"

@@ -7,7 +7,7 @@ from typing import Optional
 import torch
 
 from ._core import ACT_GELU, ACT_NONE, ACT_SILU_MUL, _act
-from .gemm_ops import _bias_bf16, gemm, gemm_tile, silu_mul_interleaved
+from .gemm_ops import _bias_bf16, gemm, gemm_tile, gemm_tile_ln, silu_mul_interleaved
 from .tables import small_m_plan_for, tile_cfg_for, tile_route_for
 
 
@@ -59,6 +59,26 @@ def linear(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     if plan is not None and plan[0] > 0 and not (code == ACT_SILU_MUL and residual is not None):
         return gemm(a, w, bias, act=code, residual=residual, workspace=workspace, cfg=plan[0], splitk=plan[1])
     return gemm(a, w, bias, act=code, residual=residual, workspace=workspace)
+
+
+def ln_foldable(M: int, N: int, K: int) -> bool:
+    """Whether :func:`linear_ln` runs this shape where :func:`linear` would use the tile kernel too
+    (large M; K and N multiples of the 128-column statistics blocks) -- callers keep an explicit
+    LayerNorm otherwise."""
+    return M >= TILE_MIN_M and K % 128 == 0 and N % 128 == 0 and K <= 4096 and _GEMM_IMPL != "blas"
+
+
+def linear_ln(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, act=ACT_NONE,
+              fold_c: Optional[torch.Tensor] = None, ln_part: Optional[torch.Tensor] = None,
+              residual: Optional[torch.Tensor] = None, ln_g: Optional[torch.Tensor] = None,
+              stats_part: Optional[torch.Tensor] = None, eps: float = 1e-12) -> torch.Tensor:
+    """A projection with LayerNorm folding (:func:`gemm_tile_ln`) on the tile the table picks for the
+    shape (the folding kernels map it to the nearest of theirs)."""
+    M, K = a.shape
+    N = w.shape[0]
+    cfg = tile_cfg_for(M, N, K)[0] if M >= TILE_MIN_M else 0
+    return gemm_tile_ln(a, w, bias, act=act, fold_c=fold_c, ln_part=ln_part, residual=residual, ln_g=ln_g,
+                        stats_part=stats_part, eps=eps, cfg=cfg)
 
 
 def _linear_blas(a, w, bias, code, residual):

@@ -7,7 +7,7 @@ from typing import Dict, Optional, Tuple
 import torch
 
 from ._lib import check, lib, stream_ptr
-from ._core import ACT_NONE, ACT_SILU_MUL, _act, _need, _ptr, _workspace_args
+from ._core import ACT_GELU, ACT_NONE, ACT_SILU_MUL, _act, _need, _ptr, _workspace_args
 
 
 def gemm(
@@ -137,6 +137,91 @@ def gemm_tile(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = N
                              n_out, N, int(cfg), int(grid_cap), sk, ws_ptr, ws_elems, cnt_ptr, SPLIT_COUNTER_ELEMS,
                              stream_ptr(dev))
     check(rc, "mls_gemm_tile")
+    return out
+
+
+def fold_layernorm(w: torch.Tensor, bias: Optional[torch.Tensor], gamma: torch.Tensor, beta: torch.Tensor):
+    """Fold a LayerNorm ``(gamma, beta)`` into the projection after it (csrc/gemm_tile.hip, "LayerNorm
+    folding"): ``LN(h) @ W.T + b = rstd * (h @ W'.T - mu * c) + b'`` with ``W' = W * gamma`` (bf16),
+    ``c = W'.sum(1)`` (fp32 sum of the bf16 ``W'``, so the mean term cancels what the MFMAs add) and
+    ``b' = b + W @ beta``.  Returns ``(W', c, b')``."""
+    wf = w.float()
+    w2 = (wf * gamma.float()[None, :]).to(torch.bfloat16)
+    c = w2.float().sum(1).contiguous()
+    b2 = wf @ beta.float()
+    if bias is not None:
+        b2 = b2 + bias.float()
+    return w2.contiguous(), c, b2.contiguous()
+
+
+def ln_partials(M: int, width: int, device) -> torch.Tensor:
+    """fp32 buffer for the row statistics a residual :func:`gemm_tile_ln` launch writes
+    (``stats_part``) and the next LayerNorm-folding launches read (``ln_part``): per row and 128-column
+    block, the sum and sum of squares of the stored bf16 values."""
+    return torch.empty(M * (width // 128) * 2, device=device, dtype=torch.float32)
+
+
+def layernorm_from_partials(h: torch.Tensor, part: torch.Tensor, eps: float = 1e-12):
+    """(mean, rstd) per row from :func:`ln_partials` -- the host-side oracle of what the kernels do."""
+    M, W = h.shape
+    p = part[: M * (W // 128) * 2].view(M, W // 128, 2).double().sum(1)
+    mu = p[:, 0] / W
+    var = (p[:, 1] / W - mu * mu).clamp_min(0)
+    return mu.float(), torch.rsqrt(var + eps).float()
+
+
+def gemm_tile_ln(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, act=ACT_NONE,
+                 fold_c: Optional[torch.Tensor] = None, ln_part: Optional[torch.Tensor] = None,
+                 residual: Optional[torch.Tensor] = None, ln_g: Optional[torch.Tensor] = None,
+                 stats_part: Optional[torch.Tensor] = None, eps: float = 1e-12, cfg: int = 0,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """The LayerNorm-folding forms of :func:`gemm_tile` (csrc/gemm_tile.hip, "LayerNorm folding").
+    Row statistics travel as :func:`ln_partials` buffers:
+
+    * ``fold_c`` given: ``a`` holds the raw pre-LN rows h, ``ln_part`` their partials (width K);
+      ``w`` / ``bias`` / ``fold_c`` come from :func:`fold_layernorm`; returns ``act(LN(h) @ W.T + b)``
+      (act: none / gelu);
+    * ``residual`` given: ``a @ w.T + bias + r`` with ``r = residual``, or ``(residual - mu) * rstd *
+      ln_g`` when ``ln_part`` (the residual's partials, width N) and ``ln_g`` (fp32 ``[N]``) are
+      given -- that LN's beta must be folded into ``bias``; ``stats_part`` then receives the OUTPUT
+      rows' partials (width N)."""
+    dev = a.device
+    _need(a, "a", torch.bfloat16, dev)
+    _need(w, "w", torch.bfloat16, dev)
+    M, K = a.shape
+    N, K2 = w.shape
+    code = _act(act)
+    if K != K2 or K % 64 or N % 16:
+        raise ValueError("gemm_tile_ln: K % 64 == 0, N % 16 == 0")
+    for name, t, n in (("bias", bias, N), ("fold_c", fold_c, N), ("ln_g", ln_g, N),
+                       ("ln_part", ln_part, M * ((K if fold_c is not None else N) // 128) * 2),
+                       ("stats_part", stats_part, M * (N // 128) * 2)):
+        if t is not None:
+            _need(t, name, torch.float32, dev)
+            if t.numel() < n:
+                raise ValueError(f"{name} needs {n} elements")
+    if fold_c is not None:
+        if ln_part is None or residual is not None or stats_part is not None or code not in (ACT_NONE, ACT_GELU) \
+                or K % 128 or K > 1024:
+            raise ValueError("folded form: ln_part, no residual / stats_part, act none or gelu, K % 128, K <= 1024")
+    else:
+        if residual is None or code != ACT_NONE:
+            raise ValueError("gemm_tile_ln needs fold_c or a residual (and no activation)")
+        _need(residual, "residual", torch.bfloat16, dev)
+        if tuple(residual.shape) != (M, N):
+            raise ValueError("residual must be [M, N]")
+        if ln_part is not None and (ln_g is None or N % 128 or N > 1024):
+            raise ValueError("a LayerNorm'd residual needs ln_g and N % 128 == 0, N <= 1024")
+        if stats_part is not None and N % 128:
+            raise ValueError("stats_part needs N % 128 == 0")
+    if out is None:
+        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    else:
+        _need(out, "out", torch.bfloat16, dev)
+    rc = lib().mls_gemm_tile_ln(a.data_ptr(), w.data_ptr(), _ptr(bias), _ptr(residual), out.data_ptr(), M, N, K,
+                                code, int(cfg), _ptr(fold_c), _ptr(ln_part), _ptr(ln_g), _ptr(stats_part),
+                                stats_part.numel() if stats_part is not None else 0, float(eps), stream_ptr(dev))
+    check(rc, "mls_gemm_tile_ln")
     return out
 
 

@@ -237,3 +237,31 @@ def test_prepared_batches_match_submit():
         for a, b in zip(ref, outs):
             np.testing.assert_array_equal(a[0], b[0])
     assert eng._spare.qsize() == eng.inflight + 1
+
+
+def test_sdma_free_io_and_fallback():
+    """Round 5: a concurrent uint8 engine pulls its input and pushes its results with copy kernels
+    inside the slot graph (no SDMA copies); a bucket whose input is not a 16-B multiple keeps the
+    stream copies.  Both give the eager results."""
+    from mlmicroservicetemplate_amd.engine.worker import GpuEngine
+
+    w = torch.randn(16, 48, device=DEV)
+    eng = GpuEngine(lambda x: ((x.float() @ w.T).to(torch.bfloat16),), DEV, (48,), torch.uint8, buckets=[4, 8],
+                    inflight=2, concurrent=True, name="pull")
+    eng.warmup(capture=True)
+    assert eng.pull_h2d > 0
+    assert all(sl.pulled[b] and sl.pushed[b] for sl in eng.slots for b in (4, 8))
+    rng = np.random.default_rng(3)
+    for n in (3, 8, 1):
+        x = rng.integers(0, 256, (n, 48), dtype=np.uint8)
+        got = eng.run(x)[0]
+        ref = (torch.from_numpy(x).to(DEV).float() @ w.T).to(torch.bfloat16).float().cpu().numpy()
+        np.testing.assert_allclose(got, ref, rtol=1e-2, atol=1e-2 * np.abs(ref).max())
+    w5 = torch.randn(16, 5, device=DEV)
+    eng5 = GpuEngine(lambda x: ((x.float() @ w5.T).to(torch.bfloat16),), DEV, (5,), torch.uint8, buckets=[3],
+                     inflight=2, concurrent=True, name="odd")
+    eng5.warmup(capture=True)
+    assert not any(sl.pulled[3] for sl in eng5.slots)  # 15 bytes: the copy path
+    x = rng.integers(0, 256, (3, 5), dtype=np.uint8)
+    ref = (torch.from_numpy(x).to(DEV).float() @ w5.T).to(torch.bfloat16).float().cpu().numpy()
+    np.testing.assert_allclose(eng5.run(x)[0], ref, rtol=1e-2, atol=1e-2 * np.abs(ref).max())
