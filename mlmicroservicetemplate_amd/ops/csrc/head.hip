@@ -280,7 +280,40 @@ MLS_DEV void block_argmax(float& bv, int& bc, float* sv, int* sc) {
   __syncthreads();  // sv / sc are reused by the next round
 }
 
+// DPP / lane-swap wave reductions (no LDS traffic: the ds_bpermute form costs ~12 dependent LDS
+// round trips per arg-max)
+MLS_DEV float hv2_wave_max(float v) {
+  v = fmaxf(v, dpp_f<0xB1>(v));   // lane ^ 1
+  v = fmaxf(v, dpp_f<0x4E>(v));   // lane ^ 2
+  v = fmaxf(v, dpp_f<0x141>(v));  // row_half_mirror: the other quad of the 8
+  v = fmaxf(v, dpp_f<0x140>(v));  // row_mirror: the other half of the 16
+  v = fmaxf(v, xor16_f(v));
+  return fmaxf(v, xor32_f(v));
+}
+MLS_DEV float hv2_wave_sum(float v) {
+  v = group_sum<16>(v);
+  v += xor16_f(v);
+  return v + xor32_f(v);
+}
+MLS_DEV int hv2_wave_min(int c) {
+  float v = __int_as_float(c);  // moved as bits; compared as ints
+  auto mn = [](float a, float b) { return __int_as_float(min(__float_as_int(a), __float_as_int(b))); };
+  v = mn(v, dpp_f<0xB1>(v));
+  v = mn(v, dpp_f<0x4E>(v));
+  v = mn(v, dpp_f<0x141>(v));
+  v = mn(v, dpp_f<0x140>(v));
+  v = mn(v, xor16_f(v));
+  return __float_as_int(mn(v, xor32_f(v)));
+}
+// wave arg-max of (v, c): larger v wins, ties to the smaller class; every lane gets the winner
+MLS_DEV void hv2_wave_argmax(float& v, int& c) {
+  const float m = hv2_wave_max(v);
+  c = hv2_wave_min(v == m ? c : 0x7fffffff);
+  v = m;
+}
+
 constexpr int HV2_PER_T = 4;  // classes per thread in the finisher (N <= 1024)
+constexpr int HV2_FAST_K = 16;  // top-k up to this: wave-local top-k + one barrier + a one-wave merge
 constexpr int HV2_MAXS = 8;   // K slices summed with all loads in flight (K <= 2048)
 
 __global__ __launch_bounds__(256) void head_finish_kernel(const HeadV2Args a) {
@@ -340,6 +373,71 @@ __global__ __launch_bounds__(256) void head_finish_kernel(const HeadV2Args a) {
     epilogue();
     return;
   }
+  const bool bad = a.err && a.err[row] != 0;
+  if (a.k <= HV2_FAST_K) {
+    // each wave: its max / exp-sum and its own top-k (k rounds of DPP arg-max, no barrier); one
+    // barrier hands the 4 waves' candidates to wave 0, which merges them with k more rounds.  The
+    // softmax sum combines the waves' sums rescaled to the global max.
+    __shared__ float cv[4 * HV2_FAST_K], wm[4], ws[4];
+    __shared__ int cc[4 * HV2_FAST_K];
+    const int lane = tid & 63, wid = tid >> 6;
+    const float mw = hv2_wave_max(m);
+    float sw = 0.f;
+    if (a.softmax) {
+#pragma unroll
+      for (int i = 0; i < HV2_PER_T; ++i) sw += v[i] == -INFINITY ? 0.f : __expf(v[i] - mw);
+      sw = hv2_wave_sum(sw);
+    }
+    for (int t = 0; t < a.k; ++t) {
+      float bv = -INFINITY;
+      int bj = 0;
+#pragma unroll
+      for (int i = 0; i < HV2_PER_T; ++i)
+        if (v[i] > bv) {
+          bv = v[i];
+          bj = i;
+        }
+      int bc = bv == -INFINITY ? 0x7fffffff : c + bj;
+      hv2_wave_argmax(bv, bc);
+      if (bc >= c && bc < c + HV2_PER_T) v[bc - c] = -INFINITY;  // the owner drops the winner
+      if (lane == t) {
+        cv[wid * a.k + t] = bv;
+        cc[wid * a.k + t] = bc;
+      }
+    }
+    if (lane == 0) {
+      wm[wid] = mw;
+      ws[wid] = sw;
+    }
+    __syncthreads();
+    if (wid == 0) {
+      const int nc = 4 * a.k;
+      float bv0 = lane < nc ? cv[lane] : -INFINITY;
+      int bc0 = lane < nc ? cc[lane] : 0x7fffffff;
+      const float gm = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
+      float gs = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) gs += ws[w] * __expf(wm[w] - gm);
+      float ov = 0.f;
+      int oc = -1;
+      for (int t = 0; t < a.k; ++t) {
+        float bv = bv0;
+        int bc = bc0;
+        hv2_wave_argmax(bv, bc);
+        if (bc0 == bc && bv0 == bv) bv0 = -INFINITY, bc0 = 0x7fffffff;  // the holder drops it
+        if (lane == t) {
+          ov = a.softmax ? __expf(bv - gm) / gs : bv;
+          oc = bc;
+        }
+      }
+      if (lane < a.k) {
+        a.vals[row * a.k + lane] = bad ? __builtin_nanf("") : ov;
+        a.idx[row * a.k + lane] = bad ? -1 : (oc < a.N ? oc : -1);
+      }
+    }
+    epilogue();
+    return;
+  }
   m = block_max(m, sred);
   float ssum = 0.f;
   if (a.softmax) {
@@ -347,7 +445,6 @@ __global__ __launch_bounds__(256) void head_finish_kernel(const HeadV2Args a) {
     for (int i = 0; i < HV2_PER_T; ++i) ssum += v[i] == -INFINITY ? 0.f : __expf(v[i] - m);
     ssum = block_sum(ssum, sred);
   }
-  const bool bad = a.err && a.err[row] != 0;
   float wv = 0.f;
   int wc = -1;
   for (int t = 0; t < a.k; ++t) {

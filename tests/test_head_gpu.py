@@ -38,6 +38,28 @@ def test_fc_head_matches_fp32(B):
     assert torch.equal(lg, logits)
 
 
+@pytest.mark.parametrize("N,k", [(1000, 1), (1000, 5), (1000, 16), (1000, 17), (1000, 40), (10, 5), (300, 16)])
+def test_fc_head_topk_against_torch(N, k):
+    """The finisher's top-k (k <= 16: wave-local top-k + one-wave merge; larger k: block rounds)
+    against torch.topk of the softmax of the logits the same launch returned."""
+    from mlmicroservicetemplate_amd import ops
+
+    B = 8
+    g = torch.Generator(device="cpu").manual_seed(N + k)
+    pooled = (torch.rand(B, 2048, generator=g) * 2).to(DEV)
+    w = (torch.randn(N, 2048, generator=g) * 0.03).to(torch.bfloat16).to(DEV)
+    b = (torch.randn(N, generator=g) * 0.1).to(DEV)
+    vals, idx, logits = ops.fc_head(pooled, w, b, k)
+    torch.cuda.synchronize()
+    rv, ri = torch.softmax(logits.float(), -1).topk(k, -1)
+    assert torch.allclose(vals.float(), rv, rtol=1e-4, atol=1e-7)
+    distinct = torch.ones_like(rv, dtype=torch.bool)
+    distinct[:, 1:] &= rv[:, 1:] != rv[:, :-1]
+    distinct[:, :-1] &= rv[:, :-1] != rv[:, 1:]
+    assert torch.equal(idx.long()[distinct], ri[distinct])
+    assert (idx >= 0).all() and (idx < N).all()
+
+
 def test_fc_head_error_rows_and_repeat():
     from mlmicroservicetemplate_amd import ops
 
