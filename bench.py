@@ -290,7 +290,11 @@ def run_rank(args) -> int:
             "config": {"model": "resnet50-v1.5", "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "seq_len": None, "image_size": 224, "parallelism": f"dp{world}",
                        "backend": args.backend, "hipgraph": not args.no_graphs, "inflight": args.inflight,
-                       "concurrent_slots": not args.serial, "cu_partitions": cu_parts},
+                       "concurrent_slots": not args.serial, "cu_partitions": cu_parts,
+                       # which slot layout ran: CU-masked partitions (census-verified masks, 4 slots)
+                       # or the unpartitioned 5-slot fallback
+                       "partition_mode": (os.environ.get("MLS_CU_PARTITION_MODE", "intra") if cu_parts
+                                          else "unpartitioned")},
             "p50_latency_ms": round(p50_max, 3),
             "p99_latency_ms": round(p99_max, 3),
             "per_gpu_requests_per_s": round(value / world, 1),
