@@ -269,6 +269,9 @@ class GpuEngine:
     def warmup(self, capture: bool = True) -> None:
         """Run every bucket eagerly once (kernel load / autotune caches), then capture graphs."""
         with torch.cuda.device(self.device), torch.no_grad():
+            # the model's construction (weight packing, folding) ran on the default stream; the
+            # slot streams do not wait for it on their own
+            torch.cuda.synchronize(self.device)
             for slot in self.slots:
                 for b in self.buckets:
                     with torch.cuda.stream(slot.s_comp):

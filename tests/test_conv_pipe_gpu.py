@@ -74,6 +74,7 @@ def test_pipe_through_conv2d_cfg_and_graph():
     ref = _ref(x, w, b)
     ws = torch.empty(2 * 32 * 14 * 14 * 256, device=DEV, dtype=torch.float32)
     s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())  # the inputs were made on the default stream
     with torch.cuda.stream(s):
         y = ops.conv2d_nhwc(x, wp, b, kernel=3, stride=1, pad=1, act=ops.ACT_RELU, workspace=ws,
                             cfg=ops.CFG_PIPE + 1, splitk=2 + 16)  # warm: counters allocated

@@ -119,6 +119,9 @@ def test_resnet_fused_head_vs_unfused_and_graph():
     imgs = torch.randint(0, 256, (32, 224, 224, 3), dtype=torch.uint8, device=DEV)
     ref = resnet50_reference({k: v.to(DEV) for k, v in params.items()}, imgs).float()
     s = torch.cuda.Stream()
+    # the model's weight packing, the images and the reference ran on the default stream: order
+    # the side stream after them (without this the first forward raced the packing kernels)
+    s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
         lg = m(imgs).float()
         v1, i1 = m.classify(imgs, 5)

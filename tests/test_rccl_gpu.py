@@ -68,6 +68,7 @@ SCRIPT = textwrap.dedent("""
     # RCCL inside a captured hipGraph (thread_local capture mode: the watchdog thread polls)
     s = torch.cuda.Stream()
     buf = torch.ones(8192, device=dev)
+    s.wait_stream(torch.cuda.current_stream())  # buf was filled on the default stream
     with torch.cuda.stream(s):
         dist.all_reduce(buf)
     torch.cuda.synchronize()
