@@ -319,7 +319,8 @@ class BertFused:
         cls = self._cls_rows(B, S)
         last = cfg.layers - 1
         H, T, eps, fw = cfg.hidden, B * S, cfg.eps, self._fold
-        fold = self.ln_fold and all(ops.ln_foldable(T, n, k) for n, k in (
+        # the LN'd width (hidden) travels as 128-column partials read two per lane: H % 256, H <= 1024
+        fold = self.ln_fold and H % 256 == 0 and H <= 1024 and all(ops.ln_foldable(T, n, k) for n, k in (
             (3 * H, H), (H, H), (cfg.intermediate, H), (H, cfg.intermediate)))
         # fold: h = the previous layer's raw pre-LN2 rows (its LN2 output is never formed); part[cur] =
         # the row statistics (partials) of the rows whose LN the next consumer applies, written by the

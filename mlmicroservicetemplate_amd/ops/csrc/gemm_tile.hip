@@ -133,7 +133,7 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 // bound: MI355X_MICROARCH.md, 'attention epilogue store tail').  Bias and residual are loaded in
 // the same layout (16-B range-checked buffer loads, OOB -> 0).
 // Row statistics of this lane's MT epilogue rows from the [M][P][2] partials a PART epilogue wrote
-// (P = width / 128 <= 8 partials per row, 128 columns each): lane fq loads partials 2fq and 2fq + 1
+// (P = width / 128 <= 8 partials per row, 128 columns each, P even): lane fq loads partials 2fq and 2fq + 1
 // with one 16-B load (issued first, beside the bias loads), then two lane swaps finish the row in a
 // fixed order -- deterministic.  gt_row_stats_finish returns rmu = -mu * rstd and rrs = rstd.
 template <int MT>
@@ -1164,16 +1164,18 @@ int mls_gemm_tile_pick(int M, int N) { return gt_pick(M, N); }
 //    partials) given -- the LN's beta must be folded into bias; stats_part != null: also write the OUTPUT
 //    rows' partials there
 //    (>= M * N / 64 floats; N % 128 == 0).
-// The LN'd widths must be multiples of 128 and at most 1024.  cfg: 0 = by shape; the folding kernels
+// The LN'd widths must be multiples of 256 and at most 1024.  cfg: 0 = by shape; the folding kernels
 // are the 256 x 256 / 256 x 128 PIPE tiles (15 / 16) and the 128 x 256 / 128 x 128 tiles (5 / 4).
 int mls_gemm_tile_ln(const void* A, const void* W, const float* bias, const void* res, void* out, int M, int N,
                      int K, int act, int cfg, const float* fold_c, const float* ln_part, const float* ln_g,
                      float* stats_part, long long part_elems, float eps, void* stream) {
   if (M <= 0 || N <= 0 || K <= 0 || K % 64 || N % 16) return MLS_BAD_ARG;
-  if (fold_c && (res || !ln_part || stats_part || (act != ACT_NONE && act != ACT_GELU) || K % 128 || K > 1024))
+  // the LN'd rows' partials are read two per lane with 16-B loads (gt_row_stats_issue): their width
+  // must be a multiple of 256 (an even partial count) and at most 1024
+  if (fold_c && (res || !ln_part || stats_part || (act != ACT_NONE && act != ACT_GELU) || K % 256 || K > 1024))
     return MLS_BAD_ARG;
   if (!fold_c && (!res || act != ACT_NONE)) return MLS_BAD_ARG;
-  if (ln_part && !fold_c && (!ln_g || N % 128 || N > 1024)) return MLS_BAD_ARG;
+  if (ln_part && !fold_c && (!ln_g || N % 256 || N > 1024)) return MLS_BAD_ARG;
   if (stats_part && (N % 128 || (long long)M * (N / 128) * 2 > part_elems)) return MLS_BAD_ARG;
   const size_t ab = (size_t)M * K * 2, wb = (size_t)N * K * 2;
   if (ab >= 0x7FFFFFFFull || wb >= 0x7FFFFFFFull || (size_t)M * N >= 0x3FFFFFFFull) return MLS_UNSUPPORTED;

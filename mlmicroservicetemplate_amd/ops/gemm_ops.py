@@ -202,16 +202,16 @@ def gemm_tile_ln(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] 
                 raise ValueError(f"{name} needs {n} elements")
     if fold_c is not None:
         if ln_part is None or residual is not None or stats_part is not None or code not in (ACT_NONE, ACT_GELU) \
-                or K % 128 or K > 1024:
-            raise ValueError("folded form: ln_part, no residual / stats_part, act none or gelu, K % 128, K <= 1024")
+                or K % 256 or K > 1024:
+            raise ValueError("folded form: ln_part, no residual / stats_part, act none or gelu, K % 256, K <= 1024")
     else:
         if residual is None or code != ACT_NONE:
             raise ValueError("gemm_tile_ln needs fold_c or a residual (and no activation)")
         _need(residual, "residual", torch.bfloat16, dev)
         if tuple(residual.shape) != (M, N):
             raise ValueError("residual must be [M, N]")
-        if ln_part is not None and (ln_g is None or N % 128 or N > 1024):
-            raise ValueError("a LayerNorm'd residual needs ln_g and N % 128 == 0, N <= 1024")
+        if ln_part is not None and (ln_g is None or N % 256 or N > 1024):
+            raise ValueError("a LayerNorm'd residual needs ln_g and N % 256 == 0, N <= 1024")
         if stats_part is not None and N % 128:
             raise ValueError("stats_part needs N % 128 == 0")
     if out is None:

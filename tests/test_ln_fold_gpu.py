@@ -104,6 +104,15 @@ def test_gemm_tile_ln_rejects_bad_args():
         ops.gemm_tile_ln(a, w, residual=a, ln_part=part)  # no gamma
     with pytest.raises(ValueError):
         ops.gemm_tile_ln(a, w, residual=a, stats_part=part[:10])  # too small
+    # an odd count of 128-column partials (width 640) cannot be read two per lane
+    w640 = torch.zeros(640, 768, device=DEV, dtype=torch.bfloat16)
+    r640 = torch.zeros(256, 640, device=DEV, dtype=torch.bfloat16)
+    with pytest.raises(ValueError):
+        ops.gemm_tile_ln(a, w640, residual=r640, ln_part=ops.ln_partials(256, 640, DEV), ln_g=torch.ones(640, device=DEV))
+    a640 = torch.zeros(256, 640, device=DEV, dtype=torch.bfloat16)
+    with pytest.raises(ValueError):
+        ops.gemm_tile_ln(a640, torch.zeros(768, 640, device=DEV, dtype=torch.bfloat16), fold_c=c,
+                         ln_part=ops.ln_partials(256, 640, DEV))
 
 
 @pytest.mark.parametrize("B,S", [(8, 128), (32, 128)])
