@@ -211,16 +211,19 @@ def run_rank(args) -> int:
             with open(phases, "a") as f:
                 f.write(f"{what} {time.time():.3f}\n")
 
+    # no cyclic-GC pass inside the ~13 ms window (a full collection over torch's object graph is
+    # milliseconds of host time the submit loop would stall for; the servers gc.freeze() their
+    # start-up objects once the model is ready: api/app.py, frontend/native.py).  The collection
+    # runs BEFORE the warmup steps: collected between them and the window, its idle gap left the
+    # window's first submit cold (staging 0.16 vs 0.09 ms, graph launch 67-94 vs 28-53 us) and the
+    # 20-step value 2.6 % lower (5 of 5 interleaved pairs, profiles/r5_s20_gc_before_warmup_ab.jsonl)
+    gc.collect()
+    gc.disable()
     stamp("warmup")
     run_steps(args.warmup, [])
     host_s[0] = 0.0
     events.clear()
     lat: list = []
-    # no cyclic-GC pass inside the ~13 ms window (a full collection over torch's object graph is
-    # milliseconds of host time the submit loop would stall for; the servers gc.freeze() their
-    # start-up objects once the model is ready: api/app.py, frontend/native.py)
-    gc.collect()
-    gc.disable()
     mdist.barrier()
     torch.cuda.synchronize(device)
     stamp("timed")
