@@ -1,7 +1,7 @@
 # Item-2 check on the final tree: 10 consecutive driver-style 20-step runs on one box, then the
 # default 200-step bench and the 8-rank gloo rehearsal (8 ranks sharing this box's one GPU)
 export TMPDIR=/tmp
-OUT=gpurun_out/r5final
+OUT=gpurun_out/${R5F_OUT:-r5final}
 mkdir -p $OUT
 for r in 1 2 3 4 5 6 7 8 9 10; do
   MLS_MEASURE_EAGER=0 timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/s20_$r.json 2>> $OUT/err.log || { tail -20 $OUT/err.log; exit 1; }
