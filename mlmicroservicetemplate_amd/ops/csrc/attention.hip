@@ -5,7 +5,9 @@
 //     valid length), Hq == Hkv, D = 64.  Llama: causal, GQA (Hq / Hkv query heads share a KV
 //     head), D = 128.  Q/K/V are read in place from the fused QKV projection output (strided).
 //
-//     Block = 4 waves = 64 query rows (16 per wave), K/V tiles of 64 keys staged in LDS.
+//     Block = NW waves = 16 NW query rows (16 per wave), K/V tiles of 64 keys staged in LDS.  NW = 4
+//     in general; BERT (D = 64, 64 < S <= 128) uses NW = 8 so one block holds a whole
+//     (sequence, head) and its K/V rows are fetched once (-8 % kernel time at B=128).
 //     Per wave and tile, with v_mfma_f32_16x16x32_bf16:
 //       S^T = K . Q^T   (A = K rows from LDS, B = Q^T fragments kept in registers): the key is
 //                       on the accumulator row, the query on the lane -> softmax statistics of
@@ -21,6 +23,8 @@
 //     ("flash-decoding"): grid (splits, Hkv, B); each wave walks keys with 16-B loads, one key
 //     row per D/8 lanes, all G = Hq/Hkv query heads of the KV head at once (GQA: every K/V byte
 //     is read once for the G heads); partial (m, l, O) per split, then a combine kernel.
+#include <cstdlib>
+
 #include "common.h"
 
 typedef short short4v __attribute__((ext_vector_type(4)));
@@ -43,9 +47,10 @@ struct AttnArgs {
 
 MLS_DEV float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
-template <int D>
-__global__ __launch_bounds__(256) void flash_fwd_kernel(const AttnArgs a) {
-  constexpr int BQ = 64, BKV = 64;
+template <int D, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void flash_fwd_kernel(const AttnArgs a) {
+  constexpr int NT = 64 * NW;            // threads; NW waves x 16 query rows
+  constexpr int BQ = 16 * NW, BKV = 64;
   constexpr int CPR = D / 8;             // 16-B chunks per row
   constexpr int KK = D / 32;             // k-steps of the S^T MFMA
   constexpr int DT = D / 16;             // 16-wide d tiles of O
@@ -93,12 +98,13 @@ __global__ __launch_bounds__(256) void flash_fwd_kernel(const AttnArgs a) {
   // K / V tiles (zero rows past L via OOB loads) are register double-buffered: tile kt + 1's loads
   // are issued right after tile kt is in LDS and land while tile kt's MFMAs run (one global
   // round trip per kernel instead of one per tile: BERT S=128 has 2 tiles, Llama S=512 has 8)
-  constexpr int NI = (BKV * CPR) / 256;
+  constexpr int NI = (BKV * CPR) / NT;
+  static_assert(NI * NT == BKV * CPR, "tile chunks split evenly over the block");
   uint4 kreg[NI], vreg[NI];
   auto load_tile = [&](int kt) {
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int idx = tid + 256 * i;
+      const int idx = tid + NT * i;
       const int row = idx / CPR, ch = idx % CPR;
       const int kv = kt * BKV + row;
       const bool ok = kv < L;
@@ -112,7 +118,7 @@ __global__ __launch_bounds__(256) void flash_fwd_kernel(const AttnArgs a) {
     const int kv0 = kt * BKV;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int idx = tid + 256 * i;
+      const int idx = tid + NT * i;
       const int row = idx / CPR, ch = idx % CPR;
       *reinterpret_cast<uint4*>(Ks + row * (D * 2) + ((ch ^ (row & (CPR - 1))) * 16)) = kreg[i];
       *reinterpret_cast<uint4*>(Vs + row * VST + ch * 16) = vreg[i];
@@ -210,24 +216,24 @@ __global__ __launch_bounds__(256) void flash_fwd_kernel(const AttnArgs a) {
         for (int dt = 0; dt < DT; ++dt) dst[16 * dt] = (bf16)(acc_o[dt][j] * il);
       }
     }
-    return;
-  }
-  // D = 128 (Llama prefill, +1-2 % at B=1x512): the wave's [16][D] tile through LDS (the K tile's
-  // space: every wave is past the loop's last barrier), then 16-B row stores
-  bf16* Os = reinterpret_cast<bf16*>(smem) + wid * 16 * D;
-  static_assert(4 * 16 * D * 2 <= K_BYTES, "output tiles fit the K tile");
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float il = __shfl(inv_l, 4 * g + j, 64);
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) Os[(4 * g + j) * D + 16 * dt + fr] = (bf16)(acc_o[dt][j] * il);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int c = lane; c < 16 * CPR; c += 64) {
-    const int r = c / CPR, ch = c % CPR;
-    const int q = qw + r;
-    if (q < a.S) st16(a.o + (tok0 + q) * a.o_stride + (long)h * D + ch * 8, ld16(Os + r * D + ch * 8));
+  } else {
+    // D = 128 (Llama prefill, +1-2 % at B=1x512): the wave's [16][D] tile through LDS (the K tile's
+    // space: every wave is past the loop's last barrier), then 16-B row stores
+    bf16* Os = reinterpret_cast<bf16*>(smem) + wid * 16 * D;
+    static_assert(NW * 16 * D * 2 <= K_BYTES, "output tiles fit the K tile");
+  #pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float il = __shfl(inv_l, 4 * g + j, 64);
+  #pragma unroll
+      for (int dt = 0; dt < DT; ++dt) Os[(4 * g + j) * D + 16 * dt + fr] = (bf16)(acc_o[dt][j] * il);
+    }
+    __syncthreads();
+  #pragma unroll
+    for (int c = lane; c < 16 * CPR; c += 64) {
+      const int r = c / CPR, ch = c % CPR;
+      const int q = qw + r;
+      if (q < a.S) st16(a.o + (tok0 + q) * a.o_stride + (long)h * D + ch * 8, ld16(Os + r * D + ch * 8));
+    }
   }
 }
 
@@ -819,6 +825,18 @@ int mls_flash_attention(const void* q, const void* k, const void* v, void* o, in
   const size_t vb = ((size_t)(T - 1) * v_stride + (size_t)Hkv * D) * 2;
   if (qb >= 0x7FFFFFFFull || kb >= 0x7FFFFFFFull || vb >= 0x7FFFFFFFull) return MLS_UNSUPPORTED;
   a.q_bytes = (uint32_t)qb; a.k_bytes = (uint32_t)kb; a.v_bytes = (uint32_t)vb;
+  // BERT (D = 64, S <= 128): one 8-wave block holds all 128 queries of a (sequence, head), so the
+  // head's K/V rows are fetched once instead of once per 64-query tile (MLS_FLASH_NW=4 restores
+  // the 4-wave tiling for A/B)
+  static const int nw_env = [] {
+    const char* e = getenv("MLS_FLASH_NW");
+    return e ? atoi(e) : 8;
+  }();
+  if (D == 64 && S > 64 && S <= 128 && nw_env == 8) {
+    dim3 grid(1, Hq, B);
+    hipLaunchKernelGGL((flash_fwd_kernel<64, 8>), grid, dim3(512), 0, (hipStream_t)stream, a);
+    return (int)hipGetLastError();
+  }
   dim3 grid((S + 63) / 64, Hq, B);
   if (D == 64)
     hipLaunchKernelGGL(flash_fwd_kernel<64>, grid, dim3(256), 0, (hipStream_t)stream, a);

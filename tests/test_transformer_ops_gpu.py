@@ -106,6 +106,8 @@ def test_rope_and_kv_append(ops):
     # B, S, Hq, Hkv, D, causal, lens
     (3, 128, 12, 12, 64, False, [128, 77, 1]),
     (2, 77, 12, 12, 64, False, None),
+    (4, 128, 12, 12, 64, False, [1, 64, 65, 127]),  # 8-wave BERT block: lens at the tile edges
+    (2, 100, 4, 2, 64, True, None),                  # 8-wave block, causal + GQA
     (2, 200, 8, 2, 128, True, None),
     (1, 333, 4, 1, 128, True, None),
     (2, 64, 4, 1, 128, False, [64, 5]),
@@ -120,13 +122,14 @@ def test_flash_attention(ops, cfg):
     assert rel(out, ref) < 2e-2
 
 
-def test_flash_attention_spike_rescale(ops):
+@pytest.mark.parametrize("S,spike", [(256, 200), (128, 100)])  # 4-wave and 8-wave blocks
+def test_flash_attention_spike_rescale(ops, S, spike):
     """Force the online-softmax rescale branch: one key row is a huge spike for every query,
     placed in a late tile so the running max jumps (guide §5.4 rule 26)."""
-    B, S, H, D = 1, 256, 2, 64
+    B, H, D = 1, 2, 64
     torch.manual_seed(4)
     qkv = torch.randn(B * S, 3 * H * D, device=DEV)
-    qkv[200, H * D: 2 * H * D] = qkv[:, : H * D].mean(0) * 40  # key 200 aligned with all queries
+    qkv[spike, H * D: 2 * H * D] = qkv[:, : H * D].mean(0) * 40  # key aligned with all queries
     qkv = qkv.to(torch.bfloat16)
     out = ops.flash_attention(qkv, B, S, H, H, D)
     ref = R.attention(qkv, B, S, H, H, D)
