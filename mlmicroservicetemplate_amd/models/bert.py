@@ -269,6 +269,8 @@ class BertFused:
         # Folded from the bf16 weights / LN parameters the unfolded path uses; the residual adds that
         # normalize their residual take that LN's beta in their bias.
         self.ln_fold = os.environ.get("MLS_BERT_LN_FOLD", "1") != "0"
+        # last layer: Q and attention of the [CLS] rows only (MLS_BERT_CLS_Q=0: all rows, then gather)
+        self.cls_q = os.environ.get("MLS_BERT_CLS_Q", "1") != "0"
         self._fold: Dict[str, torch.Tensor] = {}
         if self.ln_fold:
             w, fw = self.w, self._fold
@@ -330,12 +332,40 @@ class BertFused:
         for i in range(cfg.layers):
             # all four projections native (ops.linear: the LDS-DMA tile kernel from TILE_MIN_M tokens,
             # the conv_gemm tiles below); the residual rides in the o / FFN-down epilogues
-            if h is None:
-                qkv = ops.linear(x, w[f"l{i}.qkv.w"], w[f"l{i}.qkv.b"], workspace=ws)
+            if i == last and not self.cls_q:  # A/B arm: full QKV + attention, then the [CLS] rows
+                if h is None:
+                    qkv = ops.linear(x, w[f"l{i}.qkv.w"], w[f"l{i}.qkv.b"], workspace=ws)
+                    x = ops.embedding(cls, x)
+                else:
+                    qkv = ops.linear_ln(h, fw[f"l{i}.qkv.w"], fw[f"l{i}.qkv.b"], fold_c=fw[f"l{i}.qkv.c"],
+                                        ln_part=part[cur], eps=eps)
+                    x = ops.layernorm(ops.embedding(cls, h), w[f"l{i - 1}.ln2.g"], w[f"l{i - 1}.ln2.b"], eps=eps)
+                    h = None
+                a = ops.embedding(cls, ops.flash_attention(qkv, B, S, cfg.heads, cfg.heads, cfg.head_dim,
+                                                           kv_lens=lens))
+            elif i == last:
+                # the classifier reads only the [CLS] rows of the last layer: the keys / values need
+                # every token, but the queries and everything after the attention are per token --
+                # K / V of all B*S rows (the K / V rows of the QKV projection), Q, attention (one
+                # query per sequence) and the rest of the layer on the B [CLS] rows (native row
+                # gather) instead of all B*S (~1/12 of the attention and ~6 % of the GEMM FLOPs)
+                if h is not None:  # the previous layer's LN2: folded into K / V, explicit on [CLS]
+                    x = ops.layernorm(ops.embedding(cls, h), w[f"l{i - 1}.ln2.g"], w[f"l{i - 1}.ln2.b"], eps=eps)
+                    kv = ops.linear_ln(h, fw[f"l{i}.qkv.w"][H:], fw[f"l{i}.qkv.b"][H:],
+                                       fold_c=fw[f"l{i}.qkv.c"][H:], ln_part=part[cur], eps=eps)
+                    h = None
+                else:
+                    kv = ops.linear(x, w[f"l{i}.qkv.w"][H:], w[f"l{i}.qkv.b"][H:], workspace=ws)
+                    x = ops.embedding(cls, x)
+                q = ops.linear(x, w[f"l{i}.qkv.w"][:H], w[f"l{i}.qkv.b"][:H], workspace=ws)
+                a = ops.flash_attention_rows(q, kv, B, S, 1, cfg.heads, cfg.heads, cfg.head_dim, kv_lens=lens)
             else:
-                qkv = ops.linear_ln(h, fw[f"l{i}.qkv.w"], fw[f"l{i}.qkv.b"], fold_c=fw[f"l{i}.qkv.c"],
-                                    ln_part=part[cur], eps=eps)
-            a = ops.flash_attention(qkv, B, S, cfg.heads, cfg.heads, cfg.head_dim, kv_lens=lens)
+                if h is None:
+                    qkv = ops.linear(x, w[f"l{i}.qkv.w"], w[f"l{i}.qkv.b"], workspace=ws)
+                else:
+                    qkv = ops.linear_ln(h, fw[f"l{i}.qkv.w"], fw[f"l{i}.qkv.b"], fold_c=fw[f"l{i}.qkv.c"],
+                                        ln_part=part[cur], eps=eps)
+                a = ops.flash_attention(qkv, B, S, cfg.heads, cfg.heads, cfg.head_dim, kv_lens=lens)
             if fold and i < last:
                 if h is None:
                     h1 = ops.linear_ln(a, w[f"l{i}.o.w"], w[f"l{i}.o.b"], residual=x, stats_part=part[1 - cur])
@@ -349,17 +379,6 @@ class BertFused:
                                   ln_g=fw[f"l{i}.ln1.g"], stats_part=part[1 - cur], eps=eps)
                 cur = 1 - cur
                 continue
-            if i == last:
-                # the classifier reads only the [CLS] rows of the last layer: its keys / values need
-                # every token (the QKV projection and attention above), but everything after the
-                # attention is per token -- run it on the B [CLS] rows (native row gather) instead
-                # of all B*S (~5 % of the forward's GEMM FLOPs at S = 128; same logits)
-                a = ops.embedding(cls, a)
-                if h is not None:  # the previous layer's LN2, on the [CLS] rows only
-                    x = ops.layernorm(ops.embedding(cls, h), w[f"l{i - 1}.ln2.g"], w[f"l{i - 1}.ln2.b"], eps=eps)
-                    h = None
-                else:
-                    x = ops.embedding(cls, x)
             hh = ops.linear(a, w[f"l{i}.o.w"], w[f"l{i}.o.b"], residual=x, workspace=ws)
             x = ops.layernorm(hh, w[f"l{i}.ln1.g"], w[f"l{i}.ln1.b"], eps=eps)
             f1 = ops.linear(x, w[f"l{i}.ffn1.w"], w[f"l{i}.ffn1.b"], act=ops.ACT_GELU, workspace=ws)

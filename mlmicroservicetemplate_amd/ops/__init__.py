@@ -99,6 +99,7 @@ from .transformer import (  # noqa: F401
     embed_layernorm_packed,
     embedding,
     flash_attention,
+    flash_attention_rows,
     kv_append,
     last_rows,
     layernorm,

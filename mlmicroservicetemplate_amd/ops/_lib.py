@@ -88,6 +88,7 @@ _SIGS = {
     "mls_rope_kv": [P, P, P, P, L, I, I, I, I, P, P, P, P, I, I, L, I, I, P],
     "mls_kv_append": [P, I, I, I, P, P, P, L, I, I, I, P],
     "mls_flash_attention": [P, P, P, P, I, I, I, I, I, I, I, I, I, P, I, F, P],
+    "mls_flash_attention_rows": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, P, I, F, P],
     "mls_skinny_gemm": [P, P, P, P, P, P, SZ, I, I, I, I, I, P],
     "mls_skinny_gemm_norm": [P, P, P, P, P, P, P, P, SZ, I, I, I, I, I, I, F, P],
     "mls_skinny_pack": [P, P, I, I, P],

@@ -39,6 +39,7 @@ struct AttnArgs {
   bf16* o;
   int q_stride, k_stride, v_stride, o_stride;  // token-row strides (elements)
   int B, S, Hq, Hkv;
+  int q_rows;          // query rows per sequence (positions 0 .. q_rows - 1; == S for full attention)
   const int* kv_lens;  // [B] valid keys per sequence (nullptr -> S)
   int causal;
   float scale_log2;  // softmax scale * log2(e)
@@ -69,7 +70,7 @@ __global__ __launch_bounds__(64 * NW) void flash_fwd_kernel(const AttnArgs a) {
   const int qw = q0 + wid * 16;
   MLS_CHECK(!a.kv_lens || a.kv_lens[b] <= a.S, 301);
   const int L = a.kv_lens ? min(a.kv_lens[b], a.S) : a.S;
-  const long tok0 = (long)b * a.S;
+  const long tok0 = (long)b * a.S, tokq = (long)b * a.q_rows;  // first K/V row, first Q / O row
 
   const rsrc_t qr = make_rsrc(a.q, a.q_bytes);
   const rsrc_t kr = make_rsrc(a.k, a.k_bytes);
@@ -81,7 +82,7 @@ __global__ __launch_bounds__(64 * NW) void flash_fwd_kernel(const AttnArgs a) {
     const int q = qw + fr;
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
-      const int off = q < a.S ? (int)(((tok0 + q) * a.q_stride + (long)h * D + 32 * kk + 8 * g) * 2) : OOB;
+      const int off = q < a.q_rows ? (int)(((tokq + q) * a.q_stride + (long)h * D + 32 * kk + 8 * g) * 2) : OOB;
       qf[kk] = __builtin_bit_cast(bf16x8, bload16(qr, off));
     }
   }
@@ -210,8 +211,8 @@ __global__ __launch_bounds__(64 * NW) void flash_fwd_kernel(const AttnArgs a) {
     for (int j = 0; j < 4; ++j) {
       const float il = __shfl(inv_l, 4 * g + j, 64);
       const int q = qw + 4 * g + j;
-      if (q < a.S) {
-        bf16* dst = a.o + (tok0 + q) * a.o_stride + (long)h * D + fr;
+      if (q < a.q_rows) {
+        bf16* dst = a.o + (tokq + q) * a.o_stride + (long)h * D + fr;
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) dst[16 * dt] = (bf16)(acc_o[dt][j] * il);
       }
@@ -232,7 +233,7 @@ __global__ __launch_bounds__(64 * NW) void flash_fwd_kernel(const AttnArgs a) {
     for (int c = lane; c < 16 * CPR; c += 64) {
       const int r = c / CPR, ch = c % CPR;
       const int q = qw + r;
-      if (q < a.S) st16(a.o + (tok0 + q) * a.o_stride + (long)h * D + ch * 8, ld16(Os + r * D + ch * 8));
+      if (q < a.q_rows) st16(a.o + (tokq + q) * a.o_stride + (long)h * D + ch * 8, ld16(Os + r * D + ch * 8));
     }
   }
 }
@@ -802,11 +803,14 @@ __global__ __launch_bounds__(D) void decode_combine_kernel(const DecodeArgs a, i
 
 extern "C" {
 
-// q/k/v point at the first element of head 0 of token 0; strides are token-row strides.
-int mls_flash_attention(const void* q, const void* k, const void* v, void* o, int q_stride, int k_stride,
-                        int v_stride, int o_stride, int B, int S, int Hq, int Hkv, int D, const int* kv_lens,
-                        int causal, float scale, void* stream) {
-  if (B <= 0 || S <= 0 || Hq <= 0 || Hkv <= 0 || Hq % Hkv) return MLS_BAD_ARG;
+// q/k/v point at the first element of head 0 of token 0; strides are token-row strides.  q_rows:
+// query (and output) rows per sequence -- S for full attention; fewer = the first q_rows positions
+// of each sequence only, against all of its keys (BERT's last layer: the [CLS] row), q / o then
+// hold B * q_rows rows.
+int mls_flash_attention_rows(const void* q, const void* k, const void* v, void* o, int q_stride, int k_stride,
+                             int v_stride, int o_stride, int B, int S, int q_rows, int Hq, int Hkv, int D,
+                             const int* kv_lens, int causal, float scale, void* stream) {
+  if (B <= 0 || S <= 0 || Hq <= 0 || Hkv <= 0 || Hq % Hkv || q_rows <= 0 || q_rows > S) return MLS_BAD_ARG;
   if (q_stride % 8 || k_stride % 8 || v_stride % 8) return MLS_BAD_ARG;
   if (o_stride % 8 || (reinterpret_cast<uintptr_t>(o) & 15)) return MLS_BAD_ARG;  // 16-B row stores
   AttnArgs a{};
@@ -816,15 +820,20 @@ int mls_flash_attention(const void* q, const void* k, const void* v, void* o, in
   a.o = (bf16*)o;
   a.q_stride = q_stride; a.k_stride = k_stride; a.v_stride = v_stride; a.o_stride = o_stride;
   a.B = B; a.S = S; a.Hq = Hq; a.Hkv = Hkv;
+  a.q_rows = q_rows;
   a.kv_lens = kv_lens;
   a.causal = causal;
   a.scale_log2 = scale * 1.4426950408889634f;
-  const long T = (long)B * S;
-  const size_t qb = ((size_t)(T - 1) * q_stride + (size_t)Hq * D) * 2;
+  const long T = (long)B * S, TQ = (long)B * q_rows;
+  const size_t qb = ((size_t)(TQ - 1) * q_stride + (size_t)Hq * D) * 2;
   const size_t kb = ((size_t)(T - 1) * k_stride + (size_t)Hkv * D) * 2;
   const size_t vb = ((size_t)(T - 1) * v_stride + (size_t)Hkv * D) * 2;
   if (qb >= 0x7FFFFFFFull || kb >= 0x7FFFFFFFull || vb >= 0x7FFFFFFFull) return MLS_UNSUPPORTED;
   a.q_bytes = (uint32_t)qb; a.k_bytes = (uint32_t)kb; a.v_bytes = (uint32_t)vb;
+  if (D == 64 && q_rows <= 16) {  // a few rows per sequence: one wave per (sequence, head)
+    hipLaunchKernelGGL((flash_fwd_kernel<64, 1>), dim3(1, Hq, B), dim3(64), 0, (hipStream_t)stream, a);
+    return (int)hipGetLastError();
+  }
   // BERT (D = 64, S <= 128): one 8-wave block holds all 128 queries of a (sequence, head), so the
   // head's K/V rows are fetched once instead of once per 64-query tile (MLS_FLASH_NW=4 restores
   // the 4-wave tiling for A/B)
@@ -832,12 +841,11 @@ int mls_flash_attention(const void* q, const void* k, const void* v, void* o, in
     const char* e = getenv("MLS_FLASH_NW");
     return e ? atoi(e) : 8;
   }();
-  if (D == 64 && S > 64 && S <= 128 && nw_env == 8) {
-    dim3 grid(1, Hq, B);
-    hipLaunchKernelGGL((flash_fwd_kernel<64, 8>), grid, dim3(512), 0, (hipStream_t)stream, a);
+  if (D == 64 && q_rows > 64 && q_rows <= 128 && nw_env == 8) {
+    hipLaunchKernelGGL((flash_fwd_kernel<64, 8>), dim3(1, Hq, B), dim3(512), 0, (hipStream_t)stream, a);
     return (int)hipGetLastError();
   }
-  dim3 grid((S + 63) / 64, Hq, B);
+  dim3 grid((q_rows + 63) / 64, Hq, B);
   if (D == 64)
     hipLaunchKernelGGL(flash_fwd_kernel<64>, grid, dim3(256), 0, (hipStream_t)stream, a);
   else if (D == 128)
@@ -845,6 +853,13 @@ int mls_flash_attention(const void* q, const void* k, const void* v, void* o, in
   else
     return MLS_UNSUPPORTED;
   return (int)hipGetLastError();
+}
+
+int mls_flash_attention(const void* q, const void* k, const void* v, void* o, int q_stride, int k_stride,
+                        int v_stride, int o_stride, int B, int S, int Hq, int Hkv, int D, const int* kv_lens,
+                        int causal, float scale, void* stream) {
+  return mls_flash_attention_rows(q, k, v, o, q_stride, k_stride, v_stride, o_stride, B, S, S, Hq, Hkv, D, kv_lens,
+                                  causal, scale, stream);
 }
 
 // workspace: ws >= B*Hq*nsplit*D floats, ws_ml >= B*Hq*nsplit*2 floats, nsplit = ceil(max_len/chunk);

@@ -193,6 +193,38 @@ def flash_attention(qkv: torch.Tensor, batch: int, seq: int, n_q_heads: int, n_k
     return out
 
 
+def flash_attention_rows(q: torch.Tensor, kv: torch.Tensor, batch: int, seq: int, q_rows: int, n_q_heads: int,
+                         n_kv_heads: int, head_dim: int, *, kv_lens: Optional[torch.Tensor] = None,
+                         causal: bool = False, scale: Optional[float] = None,
+                         out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Attention of the first ``q_rows`` positions of every sequence against all of its keys:
+    ``q [B*q_rows, >= Hq*D]`` (row-strided), ``kv [B*S, 2*Hkv*D]`` (K then V, e.g. a fused K/V
+    projection).  Returns ``[B*q_rows, Hq*D]``.  BERT's last layer runs its [CLS] rows this way
+    (``q_rows = 1``: one wave per (sequence, head))."""
+    dev = q.device
+    if q.dtype != torch.bfloat16:  # row-strided: not _need's contiguity check
+        raise TypeError(f"q: expected torch.bfloat16, got {q.dtype}")
+    _need(kv, "kv", torch.bfloat16, dev)
+    HD, KD = n_q_heads * head_dim, n_kv_heads * head_dim
+    if q.dim() != 2 or q.shape[0] != batch * q_rows or q.shape[1] < HD or q.stride(1) != 1:
+        raise ValueError("q must be [batch * q_rows, >= Hq*D] with unit column stride")
+    if tuple(kv.shape) != (batch * seq, 2 * KD) or not kv.is_contiguous():
+        raise ValueError("kv must be a contiguous [batch * seq, 2 * Hkv * D]")
+    if not 0 < q_rows <= seq:
+        raise ValueError("q_rows must be in 1..seq")
+    if kv_lens is not None:
+        _need(kv_lens, "kv_lens", torch.int32, dev)
+    out = torch.empty(batch * q_rows, HD, device=dev, dtype=torch.bfloat16) if out is None else out
+    scale = head_dim ** -0.5 if scale is None else scale
+    es = kv.element_size()
+    rc = lib().mls_flash_attention_rows(q.data_ptr(), kv.data_ptr(), kv.data_ptr() + KD * es, out.data_ptr(),
+                                        q.stride(0), 2 * KD, 2 * KD, out.stride(0), batch, seq, q_rows, n_q_heads,
+                                        n_kv_heads, head_dim, _ptr(kv_lens), int(causal), float(scale),
+                                        stream_ptr(dev))
+    check(rc, "mls_flash_attention_rows")
+    return out
+
+
 def decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, lens: torch.Tensor,
                      n_q_heads: int, n_kv_heads: int, head_dim: int, *, chunk: int = 64,
                      scale: Optional[float] = None, workspace: Optional[torch.Tensor] = None,

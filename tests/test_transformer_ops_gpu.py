@@ -122,6 +122,23 @@ def test_flash_attention(ops, cfg):
     assert rel(out, ref) < 2e-2
 
 
+@pytest.mark.parametrize("q_rows", [1, 3, 16, 77, 128])  # 1-wave, 4-wave and 8-wave launches
+def test_flash_attention_rows(ops, q_rows):
+    """The first q_rows positions of each sequence (q from a strided [CLS]-style view, K/V from a
+    fused [T, 2*Hkv*D] projection) vs the full reference attention's rows."""
+    B, S, H, D = 4, 128, 12, 64
+    torch.manual_seed(5)
+    qkv = torch.randn(B * S, 3 * H * D, device=DEV).to(torch.bfloat16)
+    lens = torch.tensor([128, 90, 17, 1], device=DEV, dtype=torch.int32)
+    ref = R.attention(qkv, B, S, H, H, D, kv_lens=lens).view(B, S, H * D)[:, :q_rows].reshape(B * q_rows, -1)
+    rows = (torch.arange(B, device=DEV)[:, None] * S + torch.arange(q_rows, device=DEV)[None]).reshape(-1)
+    wide = qkv[rows]  # [B*q_rows, 3HD]: q is its first H*D columns (row stride 3HD)
+    kv = qkv[:, H * D:].contiguous()
+    out = ops.flash_attention_rows(wide[:, : H * D], kv, B, S, q_rows, H, H, D, kv_lens=lens)
+    assert out.shape == (B * q_rows, H * D)
+    assert rel(out, ref) < 2e-2
+
+
 @pytest.mark.parametrize("S,spike", [(256, 200), (128, 100)])  # 4-wave and 8-wave blocks
 def test_flash_attention_spike_rescale(ops, S, spike):
     """Force the online-softmax rescale branch: one key row is a huge spike for every query,

@@ -16,7 +16,8 @@ SHAPES = {  # name: (M, N, K)
     "bert_ffn2": (4096, 768, 3072), "dec16_qkv": (16, 6144, 4096), "dec16_gateup": (16, 28672, 4096),
     "dec1_down": (1, 4096, 14336), "dec8_down": (8, 4096, 14336), "dec32_gateup": (32, 28672, 4096),
     "bert128_qkv": (128, 2304, 768), "bert128_ffn1": (128, 3072, 768), "bert128_ffn2": (128, 768, 3072),
-    "bert128_o": (128, 768, 768), "bert1024_qkv": (1024, 2304, 768), "bert1024_ffn2": (1024, 768, 3072),
+    "bert128_o": (128, 768, 768), "bert32_o": (32, 768, 768), "bert32_ffn1": (32, 3072, 768),
+    "bert32_ffn2": (32, 768, 3072), "bert1024_qkv": (1024, 2304, 768), "bert1024_ffn2": (1024, 768, 3072),
     "m64_qkv": (64, 6144, 4096), "m256_gateup": (256, 28672, 4096),
     "dec256_qkv": (256, 6144, 4096), "dec256_o": (256, 4096, 4096), "dec256_down": (256, 4096, 14336),
     "dec256_lm": (256, 128256, 4096),
