@@ -1,4 +1,5 @@
 # 20-step window: second stream of each CU partition on a thinned mask (MLS_SLOT_THIN=k drops every
+# (the MLS_SLOT_THIN option was measured slower and removed from engine/worker.py; kept as the record)
 # k-th CU) so the two batches of a half desynchronize -- interleaved A/B
 export TMPDIR=/tmp
 OUT=gpurun_out/r5thin
