@@ -21,10 +21,35 @@ GEMM_CFGS = list(range(1, 20)) + list(range(23, 32))  # conv_gemm.hip kCfgs (20.
 CANDIDATES: List[Tuple[int, int]] = [(c, s) for c in GEMM_CFGS for s in (1, 2, 4, 8)] + [(20, 1), (21, 1), (22, 1)]
 
 
+def _flush_mb() -> int:
+    """``MLS_TUNE_FLUSH_MB`` (default 0): after every timed call, a fill of that many MB (split over
+    the co-running streams) evicts the L2s, so each call reads its operands from the MALL / HBM as a
+    layer inside the forward does (its input was written by the previous kernel, often on other
+    XCDs) instead of from an L2 warmed by the previous identical call; the fill's own time, measured
+    alone, is subtracted."""
+    return int(os.environ.get("MLS_TUNE_FLUSH_MB", "0"))
+
+
+def _with_flush(fn, buf):
+    def run():
+        fn()
+        buf.fill_(1)
+    return run
+
+
 def _time(fn, iters: int = 20, warmup: int = 3) -> float:
     """ms per call of ``fn`` measured on the GPU timeline: the ``iters`` calls are captured into
     one hipGraph and replayed, so host-side launch cost (Python + ctypes, ~10 us/call) cannot
     hide kernels shorter than it (timing eager launches would floor every kernel at that cost)."""
+    mb = _flush_mb()
+    if mb > 0:
+        buf = torch.empty(mb << 20, dtype=torch.uint8, device=torch.cuda.current_device())
+        t_fill = _time_plain(lambda: buf.fill_(1), iters, warmup)
+        return max(_time_plain(_with_flush(fn, buf), iters, warmup) - t_fill, 0.0)
+    return _time_plain(fn, iters, warmup)
+
+
+def _time_plain(fn, iters: int = 20, warmup: int = 3) -> float:
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
@@ -57,6 +82,16 @@ def _time_multi(fns, iters: int = 20, warmup: int = 3) -> float:
     where a throughput-efficient tile beats a latency-optimal one."""
     if len(fns) == 1:
         return _time(fns[0], iters, warmup)
+    mb = _flush_mb()
+    if mb > 0:
+        bufs = [torch.empty((mb << 20) // len(fns), dtype=torch.uint8, device=torch.cuda.current_device())
+                for _ in fns]
+        t_fill = _time_multi_plain([(lambda b=b: b.fill_(1)) for b in bufs], iters, warmup)
+        return max(_time_multi_plain([_with_flush(f, b) for f, b in zip(fns, bufs)], iters, warmup) - t_fill, 0.0)
+    return _time_multi_plain(fns, iters, warmup)
+
+
+def _time_multi_plain(fns, iters: int = 20, warmup: int = 3) -> float:
     main = torch.cuda.current_stream()
     # MLS_TUNE_PARTITIONS=P: the copies run on CU-masked streams, copy i in partition i % P -- how a
     # partitioned serving engine (engine/worker.py, cu_partitions) co-runs its batches
