@@ -16,6 +16,25 @@ _MASKED_STREAMS: Dict[tuple, torch.cuda.ExternalStream] = {}
 
 
 _MASKED_LOCK = __import__("threading").Lock()
+_ATEXIT_SET = False
+
+
+def release_masked_streams(key=None) -> None:
+    """Synchronize and destroy the pooled CU-masked streams (all of them, or those created with
+    ``key``); registered with ``atexit`` when the first one is created: the HIP runtime otherwise
+    tears them down in its static destructors, after a profiler's tool library has finalized --
+    ``rocprofv3`` runs of the partitioned bench segfaulted in ``__cxa_finalize`` after writing their
+    output (rc 0 with this; ``tools/probe/r5_exit.sh``).  Engines still holding a released stream
+    must not run again."""
+    with _MASKED_LOCK:
+        ks = [k for k in _MASKED_STREAMS if key is None or k[2] == key]
+        streams = [_MASKED_STREAMS.pop(k) for k in ks]
+    for st in streams:
+        try:
+            st.synchronize()
+            lib().mls_stream_destroy(st.cuda_stream)
+        except Exception:  # noqa: BLE001 -- best effort at interpreter exit
+            pass
 
 
 def cu_masked_stream(mask: Sequence[int], device=None, key=0) -> torch.cuda.ExternalStream:
@@ -39,6 +58,12 @@ def cu_masked_stream(mask: Sequence[int], device=None, key=0) -> torch.cuda.Exte
                 check(lib().mls_stream_create_cumask(ctypes.cast(words, ctypes.c_void_p), len(mask),
                                                      ctypes.byref(out)), "mls_stream_create_cumask")
             st = _MASKED_STREAMS[ck] = torch.cuda.ExternalStream(out.value, device=dev)
+            global _ATEXIT_SET
+            if not _ATEXIT_SET:
+                import atexit
+
+                atexit.register(release_masked_streams)
+                _ATEXIT_SET = True
         return st
 
 

@@ -150,6 +150,22 @@ def test_cu_partition_masks_select_disjoint_halves():
         assert seen == full
 
 
+def test_release_masked_streams():
+    """ops.partition.release_masked_streams destroys the pooled masked streams of one key (what the
+    atexit hook does for all of them); a later request for that key creates a working stream again."""
+    from mlmicroservicetemplate_amd import ops
+    from mlmicroservicetemplate_amd.ops import partition
+
+    m = ops.partition_masks(2, DEV, mode="intra")[0]
+    st = ops.cu_masked_stream(m, DEV, key="release-test")
+    n0 = len(ops.census_cus(ops.cu_census(st, blocks=1024)))
+    partition.release_masked_streams("release-test")
+    assert not any(k[2] == "release-test" for k in partition._MASKED_STREAMS)
+    st2 = ops.cu_masked_stream(m, DEV, key="release-test")
+    assert len(ops.census_cus(ops.cu_census(st2, blocks=1024))) == n0
+    partition.release_masked_streams("release-test")
+
+
 def test_partitioned_engine_matches_serial():
     """Slots on CU-masked streams (2 partitions) give exactly the results of one-at-a-time execution."""
     from mlmicroservicetemplate_amd.engine.worker import GpuEngine
