@@ -65,7 +65,11 @@ def main():
     # a masked side stream of the same half pulls the next batch into the other buffer (what an engine
     # fed by more batches than slots could do); the compute stream waits on the pull's event
     xs2 = [torch.empty_like(x) for x in xs]
-    sides = [ops.cu_masked_stream(masks[i % 2], dev, key=2 + i // 2) for i in range(4)]
+    # SIDE=masked: the side streams on the same half's mask; SIDE=plain: ordinary (unmasked) streams
+    if os.environ.get("SIDE", "masked") == "plain":
+        sides = [torch.cuda.Stream(dev) for _ in range(4)]
+    else:
+        sides = [ops.cu_masked_stream(masks[i % 2], dev, key=2 + i // 2) for i in range(4)]
 
     def build_fwd(bufs):
         gs = []
