@@ -70,6 +70,26 @@ def build_model(backend: str, device, batch: int, params, serial: bool = False):
     return fwd
 
 
+def agree_partitions(requested: int, local_ok: bool) -> int:
+    """The CU-partition count every rank runs with: ``requested`` only if every rank's masks
+    verified, else 0 on ALL ranks -- so one rank's fallback cannot leave the ranks running (and the
+    JSON describing) different slot layouts."""
+    from mlmicroservicetemplate_amd.parallel import dist as mdist
+
+    return requested if mdist.all_ranks_true(bool(requested) and local_ok) else 0
+
+
+def rank_config(local: dict) -> dict:
+    """The per-rank engine settings (``local``) gathered over the process group and merged: agreed
+    keys keep their value, disagreeing ones read ``"mixed"`` (``ranks_consistent`` false), plus the
+    backend / world size the process group actually formed."""
+    from mlmicroservicetemplate_amd.parallel import dist as mdist
+
+    merged = mdist.merge_rank_configs(mdist.gather_objects(dict(local)))
+    merged.update(mdist.group_description())
+    return merged
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -148,23 +168,48 @@ def run_rank(args) -> int:
     t_bcast = time.perf_counter() - t0
 
     fwd = build_model(args.backend, device, args.batch, params, serial=args.serial)
-    if args.cu_partition and not args.serial:
+    if args.serial:
+        args.cu_partition = 0
+    if args.cu_partition:
         from mlmicroservicetemplate_amd import ops
 
         # the census-verified masks (cached for the engine); a device whose mask layout does not
         # verify runs unpartitioned -- and then with the 5 slots of that mode
-        if ops.partition_masks(args.cu_partition, device, mode=os.environ.get("MLS_CU_PARTITION_MODE", "intra")) is None:
+        local_ok = ops.partition_masks(args.cu_partition, device,
+                                       mode=os.environ.get("MLS_CU_PARTITION_MODE", "intra")) is not None
+        if not local_ok:
             print(f"bench: CU partitions unavailable on {device}; unpartitioned", file=sys.stderr)
-            args.cu_partition = 0
+    else:
+        local_ok = False
+    # every rank runs the same layout: one rank without verified masks takes all ranks unpartitioned
+    agreed = agree_partitions(args.cu_partition, local_ok) if world > 1 else (args.cu_partition if local_ok else 0)
+    if agreed != args.cu_partition and local_ok:
+        print(f"bench: rank {info.rank}: another rank cannot partition its CUs; all ranks unpartitioned",
+              file=sys.stderr)
+    args.cu_partition = agreed
     if args.inflight <= 0:
         args.inflight = 4 if args.cu_partition and not args.serial else 5
     # the closed-loop client polls its oldest batch's done event (20 ms bound) instead of sleeping
     # in a blocking sync: s200 56.0k vs 55.2k req/s (profiles/r5_stall_ab_sdma_vs_pull.jsonl)
+    # the next batch is staged into a spare pinned buffer (GpuEngine.prepare) while every slot is
+    # busy, so a freed slot only waits for the enqueue -- how a server stages requests as they
+    # arrive; the slot's graph pulls it straight from that buffer (ops.h2d_pull_cell).  Request
+    # latency then runs from the start of its staging (Ticket.t_arrive), not from the launch.
+    prestage = os.environ.get("MLS_BENCH_PRESTAGE", "0") == "1"
     engine = GpuEngine(fwd, device, (224, 224, 3), torch.uint8, buckets=[args.batch], inflight=args.inflight,
                        use_graphs=not args.no_graphs, name=f"resnet50.r{info.rank}", concurrent=not args.serial,
                        cu_partitions=0 if args.serial else args.cu_partition, spin_wait_us=20000.0)
     cu_parts = engine.cu_partitions
     engine.warmup(capture=not args.no_graphs)
+    # what every rank actually runs (the engine itself can still fall back, e.g. no hardware queue
+    # left for a masked stream): merged over the ranks, "mixed" where they disagree
+    ranks_cfg = rank_config({
+        "backend": args.backend, "hipgraph": not args.no_graphs, "inflight": args.inflight,
+        "concurrent_slots": not args.serial, "cu_partitions": cu_parts,
+        "partition_mode": (os.environ.get("MLS_CU_PARTITION_MODE", "intra") if cu_parts else "unpartitioned"),
+        "prestage": prestage, "batch": args.batch})
+    if not ranks_cfg["ranks_consistent"]:
+        print(f"bench: ranks disagree on the engine layout: {ranks_cfg}", file=sys.stderr)
 
     rng = np.random.default_rng(1234 + info.rank)
     pool = [[rng.integers(0, 256, (224, 224, 3), dtype=np.uint8) for _ in range(args.batch)] for _ in range(4)]
@@ -174,11 +219,6 @@ def run_rank(args) -> int:
     tickets_log = os.environ.get("MLS_BENCH_TICKETS")  # diagnostics: per-batch submit / done times
     events: list = []
 
-    # the next batch is staged into a spare pinned buffer (GpuEngine.prepare) while every slot is
-    # busy, so a freed slot only waits for the enqueue -- how a server stages requests as they
-    # arrive.  Measured level at 20 steps and +0.08 ms p50 (profiles/r4_bench_prestage_ab.jsonl): off
-    # by default (MLS_BENCH_PRESTAGE=1 turns it on)
-    prestage = os.environ.get("MLS_BENCH_PRESTAGE", "0") == "1"
 
     def run_steps(n, lat):
         pending = []
@@ -195,13 +235,13 @@ def run_rank(args) -> int:
             if len(pending) >= args.inflight:
                 t = pending.pop(0)
                 t.wait()
-                lat.append(time.perf_counter() - t.t_submit)
-                events.append((t.t_submit, time.perf_counter(), getattr(t, "stamps", None),
+                lat.append(time.perf_counter() - t.t_arrive)
+                events.append((t.t_arrive, time.perf_counter(), getattr(t, "stamps", None),
                                getattr(t, "launch_ns", None)))
         for t in pending:
             t.wait()
-            lat.append(time.perf_counter() - t.t_submit)
-            events.append((t.t_submit, time.perf_counter(), getattr(t, "stamps", None),
+            lat.append(time.perf_counter() - t.t_arrive)
+            events.append((t.t_arrive, time.perf_counter(), getattr(t, "stamps", None),
                            getattr(t, "launch_ns", None)))
 
     phases = os.environ.get("MLS_BENCH_PHASES")  # diagnostics: wall-clock stamps of the phases
@@ -251,6 +291,8 @@ def run_rank(args) -> int:
     p99 = float(np.percentile(lat, 99)) * 1e3
     p50_max = mdist.max_over_ranks(p50)
     p99_max = mdist.max_over_ranks(p99)
+    # per-rank req/s and p50 (each rank's own clock), in rank order
+    per_rank = mdist.gather_objects((round(args.batch * args.steps / elapsed, 1), round(p50, 3)))
     host_ms = host_s[0] * 1e3 / args.steps
     host_ms_max = mdist.max_over_ranks(host_ms)  # the slowest rank's host side
     from mlmicroservicetemplate_amd.parallel.affinity import host_plan_hint
@@ -290,17 +332,16 @@ def run_rank(args) -> int:
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic uint8 224x224x3 images, random-init weights",
+            # the slot layout every rank ran (CU-masked partitions with 4 slots, or the unpartitioned
+            # 5-slot fallback), merged over the ranks: "mixed" + ranks_consistent false if they differ
             "config": {"model": "resnet50-v1.5", "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "seq_len": None, "image_size": 224, "parallelism": f"dp{world}",
-                       "backend": args.backend, "hipgraph": not args.no_graphs, "inflight": args.inflight,
-                       "concurrent_slots": not args.serial, "cu_partitions": cu_parts,
-                       # which slot layout ran: CU-masked partitions (census-verified masks, 4 slots)
-                       # or the unpartitioned 5-slot fallback
-                       "partition_mode": (os.environ.get("MLS_CU_PARTITION_MODE", "intra") if cu_parts
-                                          else "unpartitioned")},
+                       **{k: v for k, v in ranks_cfg.items() if k != "batch"}},
             "p50_latency_ms": round(p50_max, 3),
             "p99_latency_ms": round(p99_max, 3),
             "per_gpu_requests_per_s": round(value / world, 1),
+            "per_rank_requests_per_s": [v for v, _ in per_rank],
+            "per_rank_p50_latency_ms": [p for _, p in per_rank],
             **({"pytorch_eager_per_gpu_requests_per_s": round(eager, 1),
                 "vs_pytorch_eager_per_gpu": round(value / world / eager, 3)} if eager else {}),
             "weight_broadcast_s": round(t_bcast, 3),

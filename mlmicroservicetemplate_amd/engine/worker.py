@@ -57,6 +57,10 @@ class _Slot:
     idx: int
     host_in: torch.Tensor  # pinned [max_b, *sample_shape]
     dev_in: torch.Tensor  # device [max_b, *sample_shape]
+    # pinned int64 cell holding the address the graph's input pull reads from (ops.h2d_pull_cell):
+    # host_in's by default, a pre-staged batch's own pinned buffer for launch_prepared()
+    src_cell: Optional[torch.Tensor] = None
+    cell_np: Optional[np.ndarray] = None  # numpy view of src_cell (cheap host writes)
     outs: Dict[int, Tuple[torch.Tensor, ...]] = field(default_factory=dict)  # bucket -> device outputs
     host_out: Dict[int, Tuple[torch.Tensor, ...]] = field(default_factory=dict)  # bucket -> pinned outputs
     graphs: Dict[int, torch.cuda.CUDAGraph] = field(default_factory=dict)
@@ -74,14 +78,17 @@ class _Slot:
 class Ticket:
     """Handle for an enqueued batch; :meth:`wait` returns numpy outputs trimmed to ``n`` rows."""
 
-    __slots__ = ("engine", "slot", "bucket", "n", "t_submit", "_result", "staged", "stamps", "launch_ns")
+    __slots__ = ("engine", "slot", "bucket", "n", "t_submit", "t_arrive", "_result", "staged", "stamps", "launch_ns")
 
     def __init__(self, engine: "GpuEngine", slot: _Slot, bucket: int, n: int, staged: Optional["Prepared"] = None):
         self.engine = engine
         self.slot = slot
         self.bucket = bucket
         self.n = n
-        self.t_submit = time.perf_counter()
+        self.t_submit = time.perf_counter()  # enqueue time (launch -> done: the pacing estimate)
+        # when the batch's requests were handed to the engine: its staging start for a prepared
+        # batch (request latency = t_arrive -> result)
+        self.t_arrive = staged.t0 if staged is not None else self.t_submit
         self._result = None
         self.staged = staged  # a prepared batch's pinned buffer, returned to the pool on completion
         self.stamps = None  # submit(): perf_counter at slot wait / staged / enqueued (diagnostics)
@@ -98,11 +105,12 @@ class Prepared:
     """A batch staged into a spare pinned buffer (:meth:`GpuEngine.prepare`) before any slot is
     free; :meth:`GpuEngine.launch_prepared` enqueues it (H2D straight from that buffer)."""
 
-    __slots__ = ("buf", "n")
+    __slots__ = ("buf", "n", "t0")
 
-    def __init__(self, buf: torch.Tensor, n: int):
+    def __init__(self, buf: torch.Tensor, n: int, t0: Optional[float] = None):
         self.buf = buf
         self.n = n
+        self.t0 = time.perf_counter() if t0 is None else t0  # prepare() start
 
 
 class GpuEngine:
@@ -243,7 +251,10 @@ class GpuEngine:
                     ev_h2d=torch.cuda.Event(),
                     ev_comp=torch.cuda.Event(),
                     ev_done=torch.cuda.Event(blocking=True),
+                    src_cell=torch.zeros(2, dtype=torch.int64, pin_memory=True),
                 )
+                slot.cell_np = slot.src_cell.numpy()
+                slot.cell_np[0] = slot.host_in.data_ptr()
                 if self.concurrent:
                     if part_masks is not None:
                         # pooled per (mask, slot-in-partition): engines built one after another in a
@@ -304,7 +315,10 @@ class GpuEngine:
                             if pull:
                                 from .. import ops
 
-                                ops.h2d_pull(slot.host_in[:b], slot.dev_in[:b], self.pull_h2d)
+                                # the source address comes from the slot's pinned cell at run time,
+                                # so a pre-staged batch is pulled straight from its own buffer
+                                ops.h2d_pull_cell(slot.src_cell, slot.host_in[:b].numel() * slot.host_in.element_size(),
+                                                  slot.dev_in[:b], self.pull_h2d)
                             outs = self.forward(slot.dev_in[:b])
                             # ... and the results pushed to the pinned host buffers by a kernel at the
                             # graph's end (no SDMA D2H either), when every output is a 16-B multiple
@@ -426,6 +440,7 @@ class GpuEngine:
         if n == 0:
             raise ValueError("empty batch")
         pick_bucket(n, self.buckets)
+        t0 = time.perf_counter()
         with self._spare_lock:
             if not self._spare_made:
                 for _ in range(self.inflight + 1):
@@ -448,7 +463,7 @@ class GpuEngine:
         except BaseException:
             self._spare.put(buf)
             raise
-        return Prepared(buf, n)
+        return Prepared(buf, n, t0)
 
     def launch_prepared(self, prep: Prepared) -> Ticket:
         """Take a free slot (blocking) and enqueue a :meth:`prepare`-d batch: H2D from its buffer."""
@@ -501,12 +516,13 @@ class GpuEngine:
             bucket = pick_bucket(n, self.buckets)
             nat = slot.native.get(bucket) if self.native_launch and not tracing.active() else None
             if nat is not None:
+                pulled = slot.pulled.get(bucket)
+                if pulled:  # the graph pulls from the address in the slot's cell: no host copy
+                    slot.cell_np[0] = src_host.data_ptr()
                 with self._enqueue_lock:
                     self._pace_launch()
                     fn, args, _keep = nat
-                    if staged is not None and slot.pulled.get(bucket):  # the graph pulls from the slot's buffer
-                        slot.host_in.numpy()[:n] = staged.buf.numpy()[:n]
-                    elif staged is not None:  # same call, H2D from the prepared buffer
+                    if staged is not None and not pulled:  # same call, H2D from the prepared buffer
                         args = args[:2] + (staged.buf.data_ptr(),) + args[3:]
                     rc = fn(*args)
                 if rc != 0:
@@ -529,8 +545,8 @@ class GpuEngine:
                 s_h2d = slot.s_comp if self.copies_on_slot_stream else self.s_h2d
                 s_d2h = slot.s_comp if self.copies_on_slot_stream else self.s_d2h
                 pulled = self.use_graphs and bucket in slot.graphs and slot.pulled.get(bucket, False)
-                if pulled and staged is not None:  # the graph pulls from the slot's own buffer
-                    slot.host_in[:n].copy_(staged.buf[:n])
+                if pulled:  # the graph pulls from the address in the slot's cell
+                    slot.cell_np[0] = src_host.data_ptr()
                 with tracing.range(self._tr_h2d), torch.cuda.stream(s_h2d):
                     if not pulled:
                         slot.dev_in[:bucket].copy_(src_host[:bucket], non_blocking=True)
@@ -548,9 +564,11 @@ class GpuEngine:
                             self._alloc_host_out(slot, bucket, outs)
                     slot.ev_comp.record(slot.s_comp)
                 s_d2h.wait_event(slot.ev_comp)
+                pushed = self.use_graphs and bucket in slot.graphs and slot.pushed.get(bucket, False)
                 with tracing.range(self._tr_d2h), torch.cuda.stream(s_d2h):
-                    for h, d in zip(slot.host_out[bucket], outs):
-                        h.copy_(d, non_blocking=True)
+                    if not pushed:  # a pushing graph already wrote its results to the pinned buffers
+                        for h, d in zip(slot.host_out[bucket], outs):
+                            h.copy_(d, non_blocking=True)
                     slot.ev_done.record(s_d2h)
         except BaseException as e:
             self._free.put(slot)

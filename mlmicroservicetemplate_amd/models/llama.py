@@ -36,6 +36,10 @@ import torch.nn.functional as F
 from ..ops import reference as R
 from ..utils import tracing
 
+# int32 words of the serving loop's control row (op, admissions, longest prompt, iteration check):
+# rank 0's next-iteration header, carried by the decode step's X4 gather (serve_graph)
+CTL_WORDS = 4
+
 
 @dataclass
 class LlamaConfig:
@@ -1002,21 +1006,32 @@ class LlamaTP:
         if self.tp == 1 or getattr(self.comm, "graph_safe", False):
             return True
         car = getattr(self.comm, "car", None)
-        if car is not None:
-            return B * (2 * k + self._gather_pad(k)) * 4 <= car.cap
+        if car is not None:  # + the serving step's control row (serve_graph)
+            return (B + 1) * (2 * k + self._gather_pad(k)) * 4 <= car.cap
         return self._rccl_graphs and not getattr(self.comm, "host_staged", False)
 
-    def _gather_dev(self, vals: torch.Tensor, idx: torch.Tensor):
+    def _gather_dev(self, vals: torch.Tensor, idx: torch.Tensor, ctl: Optional[torch.Tensor] = None):
         """X4 on device: every rank's [B, k] candidates -> ([tp, B, k] f32, [tp, B, k] i32), one
-        collective (values and ids packed in one fp32 row); graph-capturable."""
+        collective (values and ids packed in one fp32 row); graph-capturable.  ``ctl`` (int32
+        [CTL_WORDS], optional): one more row rides the same collective, and the call returns a third
+        value, RANK 0's ctl words (int32 [CTL_WORDS]) -- the serving loop's next-iteration header
+        (models/llama_serving.py), with no collective of its own."""
         if self.tp == 1:
+            if ctl is not None:
+                return vals.unsqueeze(0), idx.unsqueeze(0), ctl.clone()
             return vals.unsqueeze(0), idx.unsqueeze(0)
         B, k = vals.shape
         pad = self._gather_pad(k)
         parts = [vals.float(), idx.view(torch.float32)]
         if pad:
             parts.append(torch.zeros(B, pad, device=vals.device, dtype=torch.float32))
-        pack = torch.cat(parts, dim=1).contiguous()
+        pack = torch.cat(parts, dim=1)
+        if ctl is not None:  # W = 2k + pad >= 4 >= CTL_WORDS fp32 columns
+            W = pack.shape[1]
+            row = torch.zeros(1, W, device=vals.device, dtype=torch.float32)
+            row[0, : ctl.numel()] = ctl.view(torch.float32)
+            pack = torch.cat([pack, row], dim=0)
+        pack = pack.contiguous()
         car = getattr(self.comm, "car", None)
         if car is not None and car.gather_eligible(pack):
             with tracing.range("tp.all_gather"):
@@ -1027,6 +1042,10 @@ class LlamaTP:
             g = torch.empty((self.tp, *pack.shape), device=pack.device, dtype=pack.dtype)
             with tracing.range("tp.all_gather"):
                 dist.all_gather_into_tensor(g, pack, group=self.comm.group)
+        if ctl is not None:
+            c0 = g[0, B, : ctl.numel()].contiguous().view(torch.int32)
+            g = g[:, :B]
+            return g[..., :k].contiguous(), g[..., k: 2 * k].contiguous().view(torch.int32), c0
         return g[..., :k].contiguous(), g[..., k: 2 * k].contiguous().view(torch.int32)
 
     def _dev_buffers(self, B: int):
@@ -1080,13 +1099,19 @@ class LlamaTP:
         ``E`` int32 [2, B] is the one per-iteration read-back -- row 0 the prefill picks of the
         iteration's new sequences, row 1 (= ``tok``, the decode graph's input and output token) the
         decode picks; ``active`` masks idle slots out of the pick (they decode a dummy token into
-        their own cache row / the scratch page and keep pos 0)."""
+        their own cache row / the scratch page and keep pos 0).  ``E_all`` = ``E`` followed by
+        ``ctl_out`` (int32 [CTL_WORDS]): rank 0's ``ctl_in`` as the decode step's gather carried it
+        (the next iteration's header at TP > 1), and ``err_out`` (int32 [1]): this rank's one-shot
+        collectives' sticky peer-timeout word after the step -- all read back in the same copy."""
         st = self._serve.get(B)
         if st is None:
             dev = self.device
             z = lambda dt: torch.zeros(B, device=dev, dtype=dt)  # noqa: E731
-            E = torch.zeros(2, B, device=dev, dtype=torch.int32)
-            st = {"E": E, "tok": E[1], "pos": z(torch.int32), "lens": torch.ones(B, device=dev, dtype=torch.int32),
+            E_all = torch.zeros(2 * B + CTL_WORDS + 1, device=dev, dtype=torch.int32)
+            E = E_all[: 2 * B].view(2, B)
+            st = {"E": E, "E_all": E_all, "ctl_out": E_all[2 * B: 2 * B + CTL_WORDS], "err_out": E_all[2 * B + CTL_WORDS:],
+                  "ctl_in": torch.zeros(CTL_WORDS, device=dev, dtype=torch.int32),
+                  "tok": E[1], "pos": z(torch.int32), "lens": torch.ones(B, device=dev, dtype=torch.int32),
                   "step": z(torch.int32), "topk": torch.ones(B, device=dev, dtype=torch.int32),
                   "temp": torch.ones(B, device=dev, dtype=torch.float32), "seed": z(torch.int64),
                   "active": z(torch.int32)}
@@ -1118,7 +1143,11 @@ class LlamaTP:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 v, i = self.step(st["tok"].view(B, 1), st["pos"].view(B, 1), st["lens"], decode=True, k=k)
-                cv, ci = self._gather_dev(v, i)
+                cv, ci, c0 = self._gather_dev(v, i, ctl=st["ctl_in"])
+                st["ctl_out"].copy_(c0)
+                car = getattr(self.comm, "car", None)
+                if car is not None:  # did a peer wait of this step (or an earlier one) time out?
+                    car.error_peek(st["err_out"])
                 self.ops.decode_pick(cv, ci, st["tok"], st["pos"], st["lens"], st["step"], topk=st["topk"],
                                      temp=st["temp"], seed=st["seed"], active=st["active"])
         finally:

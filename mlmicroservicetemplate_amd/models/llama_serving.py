@@ -18,9 +18,17 @@ than being overtaken), and its pages return to the pool when it retires.
 Each sequence samples with its own parameters and the same seeded rule as a batch-of-one
 ``LlamaTP.generate`` (``pick_token``), so results do not depend on what else is in flight.
 
-Tensor parallelism: rank 0 runs the scheduler and broadcasts each iteration's admissions; every
+Tensor parallelism: rank 0 runs the scheduler and publishes each iteration's admissions; every
 rank then executes the identical iteration (same prefills, same decode steps, the same sampled
-tokens from the all-gathered candidates), so followers need no other coordination.
+tokens from the all-gathered candidates), so followers need no other coordination.  What a
+follower must learn per iteration is rank 0's header (stop? how many admissions, longest prompt).
+With the device-resident iterations at TP > 1 that header rides the decode step's X4 gather: before
+replaying iteration i's decode graph rank 0 already takes iteration i+1's admissions (from the slots
+free at that point -- a slot freed by iteration i is refilled one iteration later) and writes the
+header into its control row (``LlamaTP.serve_state`` ``ctl_in``); every rank reads it back with the
+iteration's one ``E`` copy.  A follower then issues a collective only when there is something to
+receive: the admissions' metadata / prompt ids, or an explicit header when no decode step ran (the
+engine was idle).  ``MLS_TP_CARRY_HEADER=0`` restores one header broadcast per iteration.
 
 Device-resident iterations (default whenever ``LlamaTP._device_loop_ok`` holds -- the fused
 backend on a GPU with graph-capturable collectives; ``MLS_SERVE_DEVICE_PICK=0`` forces the host
@@ -50,13 +58,28 @@ from typing import Callable, Deque, List, Optional
 
 import torch
 
-from .llama import GenParams, LlamaTP
+from .llama import CTL_WORDS, GenParams, LlamaTP, TPCommError
 
 logger = logging.getLogger("mlsamd.llama_serving")
+
+OP_STOP, OP_GENERATE, OP_ITER = 0, 1, 2  # TP control header ops (plugins/llm.py)
 
 
 class EngineFull(Exception):
     pass
+
+
+class HeaderLost(RuntimeError):
+    """A follower read a carried header that fails its check: the decode step's exchange with
+    rank 0 is broken, so this rank cannot know what rank 0 does next -- it stops following (the
+    process exits non-zero) rather than guess."""
+
+
+def ctl_check(iteration: int, op: int, n: int, S: int) -> int:
+    """Check word of a carried header: ties it to the iteration all ranks are in (a stale or torn
+    control row from a timed-out exchange fails it)."""
+    h = (iteration * 2654435761 + op * 40503 + n * 9973 + S * 131 + 0x4D4C5331) & 0x7FFFFFFF
+    return int(h)
 
 
 @dataclass
@@ -72,11 +95,27 @@ class _Seq:
 
 class ContinuousLlama:
     def __init__(self, model: LlamaTP, max_queue: int = 4096,
-                 broadcast: Optional[Callable[[Optional[List[_Seq]]], Optional[List[_Seq]]]] = None):
+                 broadcast: Optional[Callable[[Optional[List[_Seq]]], Optional[List[_Seq]]]] = None,
+                 channel=None):
         self.m = model
         self.B = model.max_batch
         self.max_queue = max_queue
-        self.broadcast = broadcast  # TP: rank 0 publishes each iteration's admissions
+        self.broadcast = broadcast  # TP (legacy hook): rank 0 publishes each iteration's admissions
+        # TP: the control channel (plugins/llm.py LlamaPlugin: send_header / send_admissions on rank
+        # 0, recv_header / recv_admissions on the followers); headers ride the decode gather when
+        # they can (module docstring)
+        self.channel = channel
+        self.leader = int(getattr(model, "rank", 0)) == 0
+        self._carry = (channel is not None and model.tp > 1
+                       and os.environ.get("MLS_TP_CARRY_HEADER", "1") != "0")
+        self._next_hdr = None  # (op, n, S) of the next iteration, read back from this one's decode step
+        self._planned: Optional[List[_Seq]] = None  # rank 0: the admissions that header announced
+        self._ctl_host = None  # rank 0: pinned int32 [CTL_WORDS] staging of the header
+        self._carry_check = False  # this iteration's carried header needs the health all-reduce
+        self._ctl_bad = None  # the control row read back failed its check (its words)
+        # how iteration headers reached the followers (diagnostics; tests/llama_tp_worker.py)
+        self.proto = {"explicit_headers": 0, "carried_headers": 0, "admission_broadcasts": 0,
+                      "iters_no_admit_bcast": 0}
         self.slots: List[Optional[_Seq]] = [None] * self.B
         self._pending: Deque[_Seq] = collections.deque()
         self._lock = threading.Lock()
@@ -136,9 +175,11 @@ class ContinuousLlama:
         return d
 
     # ---------------------------------------------------------------- scheduler (rank 0)
-    def _take_admissions(self) -> Optional[List[_Seq]]:
+    def _take_admissions(self, block: bool = True) -> Optional[List[_Seq]]:
+        """Queued requests for the free slots (None = stop).  ``block``: wait while there is
+        nothing to do at all."""
         with self._wake:
-            while not self._stop and not self._pending and all(s is None for s in self.slots):
+            while block and not self._stop and not self._pending and all(s is None for s in self.slots):
                 self._wake.wait(0.05)
             if self._stop:
                 return None
@@ -163,12 +204,105 @@ class ContinuousLlama:
 
     def _loop(self) -> None:
         while True:
-            admit = self._take_admissions()
-            if self.broadcast is not None:
-                self.broadcast(admit)  # None = stop, announced to the followers too
+            admit = self._leader_admissions()
             if admit is None:
                 break
             self.run_iteration(admit)
+
+    def _leader_admissions(self) -> Optional[List[_Seq]]:
+        """Rank 0: this iteration's admissions (None = stop), announced to the followers -- by
+        nothing more when the last decode step already carried the header, else explicitly."""
+        hdr, self._next_hdr = self._next_hdr, None
+        if hdr is not None:
+            admit, self._planned = self._planned, None
+            self.proto["carried_headers"] += 1
+            if hdr[0] == OP_STOP:
+                return None
+            if admit:
+                self.channel.send_admissions(admit)
+                self.proto["admission_broadcasts"] += 1
+            return admit or []
+        admit = self._take_admissions()
+        if self.channel is not None:
+            self.channel.send_header(admit)  # None = stop; admissions follow the header when any
+            self.proto["explicit_headers"] += 1
+            if admit:
+                self.proto["admission_broadcasts"] += 1
+        elif self.broadcast is not None:
+            self.broadcast(admit)  # None = stop, announced to the followers too
+        return admit
+
+    def follow(self) -> int:
+        """Ranks > 0 (TP): replay rank 0's iterations until it stops.  Each header comes from the
+        previous decode step's read-back when it carried one, else from the channel; admissions
+        are received only when the header announces some."""
+        st = self.follower_stats = {"iters": 0, "hdr_s": 0.0, "hdr_max_s": 0.0, "iter_s": 0.0}
+        while True:
+            t0 = time.perf_counter()
+            hdr, self._next_hdr = self._next_hdr, None
+            bcast = hdr is None
+            if hdr is None:
+                hdr = self.channel.recv_header()
+                self.proto["explicit_headers"] += 1
+            else:
+                self.proto["carried_headers"] += 1
+            op, n, S = hdr
+            if op == OP_STOP:
+                logger.info("follower: stop")
+                return 0
+            admit: List[_Seq] = []
+            if n:
+                admit = self.channel.recv_admissions(n, S)
+                self.proto["admission_broadcasts"] += 1
+                bcast = True
+            elif bcast:
+                self.proto["iters_no_admit_bcast"] += 1
+            dt = time.perf_counter() - t0
+            st["hdr_s"] += dt
+            st["hdr_max_s"] = max(st["hdr_max_s"], dt)
+            t1 = time.perf_counter()
+            try:
+                self.run_iteration(admit)  # same failure handling / health checks as rank 0
+            except HeaderLost:
+                logger.error("follower: carried header lost; leaving the TP group")
+                return 3
+            st["iter_s"] += time.perf_counter() - t1
+            st["iters"] += 1
+
+    def _plan_next(self, st) -> None:
+        """Rank 0, before the decode replay: take the next iteration's admissions now and write
+        their header into the control row the decode step's gather carries to every rank."""
+        planned = self._take_admissions(block=False)
+        self._planned = planned
+        if planned is None:
+            hdr = (OP_STOP, 0, 0)
+        else:
+            hdr = (OP_ITER, len(planned), max((len(q.ids) for q in planned), default=0))
+        if self._ctl_host is None:
+            self._ctl_host = torch.zeros(CTL_WORDS, dtype=torch.int32, pin_memory=True)
+        self._ctl_host.numpy()[:] = [*hdr, ctl_check(self.iterations, *hdr)]
+        st["ctl_in"].copy_(self._ctl_host, non_blocking=True)
+
+    def _sync_iterations(self) -> None:
+        """Collective (after a TPCommError, which every rank raises from the same all-reduce):
+        every rank continues from the largest iteration count."""
+        import torch.distributed as dist
+
+        group = getattr(self.m.comm, "group", None)
+        dev = self.m.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+        t = torch.tensor([self.iterations], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        self.iterations = int(t.item())
+
+    def _unplan(self) -> None:
+        """Rank 0 after a failed iteration: the planned admissions go back to the queue head."""
+        planned, self._planned = self._planned, None
+        self._next_hdr = None
+        if planned:
+            with self._wake:
+                for q in reversed(planned):
+                    q.slot = -1
+                    self._pending.appendleft(q)
 
     def run_iteration(self, admit: List[_Seq]) -> None:
         """One iteration + the periodic comm-health check; on any failure every in-flight request
@@ -178,13 +312,26 @@ class ContinuousLlama:
             finished = self.iteration(admit)
             # a result leaves only after a health check that covers the steps which produced it (a
             # peer that missed a one-shot all-reduce leaves partial sums behind): every iteration
-            # that retires a sequence, and every health_every-th one (all ranks: same decisions)
-            if self.m.tp > 1 and (finished or (self.health_every and self.iterations % self.health_every == 0)):
+            # that retires a sequence, and every health_every-th one (all ranks: same decisions);
+            # also every iteration whose carried header is in doubt or announces admissions
+            doubt, self._carry_check = self._carry_check, False
+            if self.m.tp > 1 and (doubt or finished or (self.health_every and self.iterations % self.health_every == 0)):
                 self.m.check_comm_health()
+            bad, self._ctl_bad = self._ctl_bad, None
+            if bad is not None:  # torn control row, yet no rank saw a timeout: cannot resynchronise
+                raise HeaderLost(f"iteration {self.iterations - 1}: control row {bad} fails its check")
             for q in finished:
                 if q.future is not None and not q.future.done():
                     q.future.set_result(list(q.out))
+        except HeaderLost:
+            raise
         except BaseException as e:  # fail everything in flight, keep serving
+            self._unplan()  # the next header goes out explicitly (every rank resets alike)
+            self._carry_check, self._ctl_bad = False, None
+            if isinstance(e, TPCommError) and self._carry:
+                # raised on every rank by the same all-reduce; with carried headers a rank in doubt
+                # may have reached it one iteration before its peers: agree on the count again
+                self._sync_iterations()
             logger.exception("generate iteration failed")
             self.failures += 1
             for q in finished:
@@ -259,17 +406,31 @@ class ContinuousLlama:
             for s in admit:
                 s.cur = len(s.ids)
         active = [s for s in self.slots if s is not None]
+        carry = self._carry and m.tp > 1
         if active:
             k = max(1, min(max(s.gp.top_k for s in active), m.top_k_max))
             max_ctx = max(s.cur for s in active) + 1
             g = m.serve_graph(self.B, k, m.ctx_bucket(max_ctx))
             if m.pages is not None:
                 m.pages.device_table()  # the graph reads the table buffer in place
+            if carry and self.leader:
+                self._plan_next(st)  # the next iteration's header rides this step's gather
             g.replay()
         if admit or active:
-            E = st["E"].cpu()  # the iteration's one device -> host copy
+            E_all = st["E_all"].cpu()  # the iteration's one device -> host copy
             self.host_reads += 1
+            E = E_all[: 2 * self.B].view(2, self.B)
             e0, e1 = E[0].tolist(), E[1].tolist()
+            if active and carry:
+                c = E_all[2 * self.B:].tolist()
+                ok = c[3] == ctl_check(self.iterations, c[0], c[1], c[2]) and c[0] in (OP_STOP, OP_ITER)
+                # a carried header is trusted only with no peer timeout on this rank; any doubt, and
+                # any header that announces admissions (the process group is about to be used), goes
+                # through the comm-health all-reduce first -- a rank in doubt stops taking part in
+                # the one-shot collectives, so its peers time out too and join that all-reduce
+                self._carry_check = (not ok) or c[4] != 0 or c[1] > 0
+                self._ctl_bad = None if ok else c[:4]
+                self._next_hdr = (c[0], c[1], c[2]) if ok else None
             new = {id(s) for s in admit}
             for s in admit:
                 s.out.append(int(e0[s.slot]))

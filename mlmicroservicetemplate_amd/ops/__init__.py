@@ -116,6 +116,7 @@ from .image import (  # noqa: F401
     d2h_push,
     gpu_sleep,
     h2d_pull,
+    h2d_pull_cell,
     image_decode,
 )
 from .partition import (  # noqa: F401

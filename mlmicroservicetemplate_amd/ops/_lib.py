@@ -49,7 +49,7 @@ _SIGS = {
     "mls_conv3x3_halo_geometry": [I, I, I, _c.POINTER(I), _c.POINTER(I)],
     "mls_conv3x3_halo_geometry_v": [I, I, I, I, _c.POINTER(I), _c.POINTER(I)],
     "mls_conv2d_pool": [P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, I, I, I, P],
-    "mls_fc_head": [P, P, P, P, P, P, P, I, I, I, I, I, P],
+    "mls_fc_head": [P, P, P, P, P, P, P, I, I, I, I, I, P, _c.c_longlong, P],
     "mls_conv3x3_pipe": [P, P, P, P, P, SZ, I, I, I, I, I, I, I, I, I, P],
     "mls_conv3x3_pipe_geometry": [I, I, I, I, _c.POINTER(I), _c.POINTER(I)],
     "mls_conv3x3_pipe_num_variants": [],
@@ -75,11 +75,13 @@ _SIGS = {
     "mls_ar_open": [P, P],
     "mls_ar_allreduce": [P, P, P, L, _c.c_longlong, P],
     "mls_ar_error": [P, P],
+    "mls_ar_error_peek": [P, P, P],
     "mls_ar_set_timeout": [P, _c.c_longlong],
     "mls_ar_allgather": [P, P, P, L, _c.c_longlong, P],
     "mls_ar_reset": [P],
     "mls_gpu_sleep": [L, P],
     "mls_h2d_pull": [P, P, _c.c_longlong, I, P],
+    "mls_h2d_pull_cell": [P, P, _c.c_longlong, I, P],
     "mls_d2h_push": [P, P, _c.c_longlong, I, P],
     "mls_stem_set_stamps": [P],
     "mls_image_decode": [P, P, P, L, I, P, P],

@@ -29,6 +29,8 @@ LIB_NAME = "libmls_kernels.so"
 DEBUG_LIB_NAME = "libmls_kernels_debug.so"  # -DMLS_DEBUG: bounds-checked variant (MLS_DEBUG=1)
 ARCH = os.environ.get("MLS_OFFLOAD_ARCH", "gfx950")
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
+if os.environ.get("MLS_GELU_ERF", "0") == "1":  # exact erf GELU in every GEMM epilogue (common.h gelu_fast)
+    CXXFLAGS.append("-DMLS_GELU_ERF")
 
 
 def hipcc() -> str:

@@ -180,11 +180,17 @@ MLS_DEV float erf_fast(float x) {
 // instructions (one v_exp, one v_rcp) -- half the issue cost of 0.5 x (1 + erf_fast(x / sqrt 2)),
 // which made the FFN-up epilogue VALU-bound (12k vs 5.5k cycles per 256 x 256 tile).  It differs from
 // the erf form by <= 4.7e-4 (at x = 2.70, where a bf16 ulp is 7.8e-3).
+// Built with -DMLS_GELU_ERF (MLS_GELU_ERF=1 at ops.build time) every epilogue computes the exact erf
+// form instead (the reference BERT's GELU; tests/test_gelu_epilogue_gpu.py bounds the difference).
 MLS_DEV float gelu_fast(float x) {
+#ifdef MLS_GELU_ERF
+  return 0.5f * x * (1.f + erf_fast(x * 0.70710678118654752f));
+#else
   constexpr float k0 = -2.f * 0.7978845608028654f * 1.4426950408889634f;  // -2 sqrt(2/pi) log2(e)
   constexpr float k1 = k0 * 0.044715f;
   const float z = fmaf(x * x, k1, k0) * x;  // -2u log2(e)
   return x * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(z));
+#endif
 }
 MLS_DEV float silu_fast(float x) { return x * __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 

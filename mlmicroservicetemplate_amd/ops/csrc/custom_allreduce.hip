@@ -227,6 +227,12 @@ __global__ void gpu_sleep_kernel(long long ticks) {
   while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
 }
 
+// copy the (sticky) error word into a device int32 -- capturable, so a serving decode graph
+// reports its collectives' peer timeouts in the iteration's one read-back (models/llama_serving.py)
+__global__ void ar_error_peek_kernel(const int* err, int* dst) {
+  if (threadIdx.x == 0) dst[0] = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace
 
 extern "C" {
@@ -439,6 +445,14 @@ int mls_ar_error(void* ctx, int* out) {
   if (hipMemcpy(out, c->err, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return MLS_UNSUPPORTED;
   const int zero = 0;
   return (int)hipMemcpy(c->err, &zero, sizeof(int), hipMemcpyHostToDevice);
+}
+
+// dst (device int32) <- the error word, on `stream`, without resetting it (mls_ar_error resets)
+int mls_ar_error_peek(void* ctx, int* dst, void* stream) {
+  ArCtx* c = (ArCtx*)ctx;
+  if (!c || !dst) return MLS_BAD_ARG;
+  hipLaunchKernelGGL(ar_error_peek_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (const int*)c->err, dst);
+  return (int)hipGetLastError();
 }
 
 int mls_ar_destroy(void* ctx) {

@@ -42,7 +42,46 @@ __global__ __launch_bounds__(256) void h2d_pull_kernel(const void* src, void* ds
   }
 }
 
+// The same pull with the source address read at run time from a pinned host cell (`src_cell`,
+// one 8-B word the host writes before the graph launch): a captured graph pulls whichever pinned
+// buffer a batch was staged in (GpuEngine.prepare), so a pre-staged batch needs no host memcpy into
+// the slot's own buffer.  The cell is read with a system-scope load (no cache may hold a stale
+// address from the previous launch) and made wave-uniform for the buffer descriptor.
+template <int U>
+__global__ __launch_bounds__(256) void h2d_pull_cell_kernel(const unsigned long long* src_cell, void* dst,
+                                                            uint32_t bytes, int iters) {
+  const unsigned long long a = __hip_atomic_load(src_cell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  const void* src = (const void*)(((unsigned long long)hi << 32) | lo);
+  const rsrc_t s = make_rsrc(src, bytes), d = make_rsrc(dst, bytes);
+  const int stride = (int)gridDim.x * 256 * 16;
+  int off = ((int)blockIdx.x * 256 + (int)threadIdx.x) * 16;
+  for (int it = 0; it < iters; ++it) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      v[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(s, off + u * stride, 0, 2));  // nt
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v_e, v[u]), d, off + u * stride, 0, 0);
+    off += U * stride;
+  }
+}
+
 extern "C" {
+
+// src_cell: pinned host word holding the source address (pinned host memory, `bytes` readable).
+int mls_h2d_pull_cell(const void* src_cell, void* dst, long long bytes, int blocks, void* stream) {
+  if (!src_cell || !dst || bytes <= 0 || bytes % 16 || bytes >= (1LL << 30) || blocks <= 0 || blocks > 1024)
+    return MLS_BAD_ARG;
+  constexpr int U = 8;
+  const long long step = (long long)blocks * 256 * 16 * U;
+  const int iters = (int)((bytes + step - 1) / step);
+  hipLaunchKernelGGL(h2d_pull_cell_kernel<U>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                     (const unsigned long long*)src_cell, dst, (uint32_t)bytes, iters);
+  return (int)hipGetLastError();
+}
 
 // src: pinned host memory (hipHostMalloc / torch pin_memory), dst: device memory (or the other way
 // round: any two GPU-addressable buffers), bytes % 16 == 0, < 1 GiB.  blocks: workgroups copying

@@ -44,9 +44,10 @@ struct GemmTileArgs {
   // LayerNorm folding (see "LayerNorm folding" below)
   const float* fold_c;    // EPI 4: [N] sum_k W'[n][k] of the gamma-folded weight
   const float* ln_part;   // EPI 3 / 4: [M][P][2] row partials (sum, sum of squares) of the LN'd operand,
-                          // P = its width / 64 (as a PART epilogue wrote them)
+                          // P = its width / 128 (as a PART epilogue wrote them)
   const float* ln_g;      // EPI 3: [N] fp32 gamma of the residual's LN (its beta is folded into bias)
-  float* stats_part;      // PART: [M][N / 64][2] partials of the OUTPUT rows, one per 64-column wave tile
+  float* stats_part;      // PART: [M][N / 128][2] partials of the OUTPUT rows, one per 128-column block
+                          // (its two 64-column waves combined through LDS): M * N / 64 floats
   float eps;
 };
 // ablation flags (tools/gemm_tile_probe.py --ablate; cfg bits 8+ of mls_gemm_tile): timing-only builds
@@ -519,7 +520,8 @@ MLS_DEV unsigned long long gt_realtime() {
 // LayerNorm folding (BERT post-LN: x = LN(h) feeds the next projection AND the residual add after
 // it).  No LN kernel runs and x is never formed:
 //  * the producer of h (O / FFN-down projection, residual epilogue) stores h and, per output row and
-//    64-column wave tile, the sum and sum of squares of the bf16 values it stored (PART: [M][N/64][2]);
+//    128-column block, the sum and sum of squares of the bf16 values it stored (PART: [M][N/128][2],
+//    the block's two 64-column waves combined through LDS);
 //  * the projection that consumes x reads A = h and W' = W . diag(gamma): x . W^T = rstd * (h . W'^T -
 //    mu * c) + beta . W^T with c[n] = sum_k W'[n][k], applied to the accumulator in the epilogue
 //    (EPI 4);
@@ -1360,7 +1362,7 @@ int mls_gemm_tile_pick(int M, int N) { return gt_pick(M, N); }
 //  * res != null: out = A . W^T + bias + res', res' = res, or (res - mu) * rstd * ln_g with ln_part (N / 128
 //    partials) given -- the LN's beta must be folded into bias; stats_part != null: also write the OUTPUT
 //    rows' partials there
-//    (>= M * N / 64 floats; N % 128 == 0).
+//    ([M][N / 128][2]: >= M * N / 64 floats in total; N % 128 == 0).
 // The LN'd widths must be multiples of 256 and at most 1024.  cfg: 0 = by shape; the folding kernels
 // are the 256 x 256 / 256 x 128 PIPE tiles (15 / 16) and the 128 x 256 / 128 x 128 tiles (5 / 4).
 int mls_gemm_tile_ln(const void* A, const void* W, const float* bias, const void* res, void* out, int M, int N,

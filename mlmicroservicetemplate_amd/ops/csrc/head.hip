@@ -19,6 +19,7 @@
 #include <cstdlib>
 #include <mutex>
 #include <unordered_map>
+#include <vector>
 #include <utility>
 
 int* mls_stream_splitk_counters(void* stream, long ntiles);  // conv_gemm.hip
@@ -471,21 +472,24 @@ __global__ __launch_bounds__(256) void head_finish_kernel(const HeadV2Args a) {
   epilogue();
 }
 
+// Fallback slab store for callers that pass no workspace: one slab per stream, grown outside any
+// capture.  A replaced slab is never freed -- a graph captured earlier on the stream (engines share
+// the pooled CU-masked streams) keeps writing to it, and hipFree would synchronize the device while
+// other slots run -- it is retired and stays allocated.  ops.fc_head passes a workspace from the
+// torch allocator (in a capture: the graph's pool), so this store is only for raw-ABI callers.
 float* head_slabs(hipStream_t st, size_t bytes) {
   static std::mutex mu;
   static std::unordered_map<hipStream_t, std::pair<float*, size_t>> bufs;
+  static std::vector<float*> retired;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(st, &cs) != hipSuccess) return nullptr;
   std::lock_guard<std::mutex> g(mu);
   auto it = bufs.find(st);
   if (it != bufs.end() && it->second.second >= bytes) return it->second.first;
   if (cs != hipStreamCaptureStatusNone) return nullptr;  // no allocation inside a capture
-  if (it != bufs.end()) (void)hipFree(it->second.first);  // grow (outside any capture)
   float* p = nullptr;
-  if (hipMalloc(&p, bytes) != hipSuccess) {
-    bufs.erase(st);
-    return nullptr;
-  }
+  if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;  // the old slab (if any) stays valid
+  if (it != bufs.end()) retired.push_back(it->second.first);
   bufs[st] = {p, bytes};
   return p;
 }
@@ -496,8 +500,11 @@ extern "C" {
 // pooled [B][K] fp32 (averages, zeroed on return), w [N][K] bf16, bias [N] fp32 or null ->
 // logits [B][N] fp32 (caller's scratch or output) and, for k > 0, vals / idx [B][k] of the
 // (softmax of the) logits' top-k.  err [B] int32 or null.  K % 256 == 0, K <= 2048, N <= 2048, k <= 64.
+// ws: fp32 workspace of ws_bytes >= (K / 256) * B * N * 4 for the v2 kernels' partial slabs (the
+// caller's allocator: in a capture, the graph's pool), or null for the per-stream fallback store.
 int mls_fc_head(const float* pooled, const void* w, const float* bias, float* logits, float* vals, int* idx,
-                const int* err, int B, int N, int K, int k, int softmax, void* stream) {
+                const int* err, int B, int N, int K, int k, int softmax, float* ws, long long ws_bytes,
+                void* stream) {
   if (B <= 0 || N <= 0 || N > 64 * MAXV || K <= 0 || K % 256 || K > 2048 || k < 0 || k > 64 || k > N) return MLS_BAD_ARG;
   if (k > 0 && (!vals || !idx)) return MLS_BAD_ARG;
   const long pb = (long)B * K * 4, wb = (long)N * K * 2, lb = (long)B * N * 4;
@@ -508,7 +515,8 @@ int mls_fc_head(const float* pooled, const void* w, const float* bias, float* lo
   }();
   if (v2 && N <= 256 * HV2_PER_T && K % HV2_KS == 0) {
     const size_t sb = (size_t)(K / HV2_KS) * B * N * sizeof(float);
-    float* slabs = head_slabs((hipStream_t)stream, sb);
+    if (ws && ws_bytes < (long long)sb) return MLS_BAD_ARG;
+    float* slabs = ws ? ws : head_slabs((hipStream_t)stream, sb);
     if (slabs) {
       HeadV2Args a2;
       a2.pooled = pooled;

@@ -63,6 +63,20 @@ def h2d_pull(src: torch.Tensor, dst: torch.Tensor, blocks: int = 32) -> torch.Te
     return dst
 
 
+def h2d_pull_cell(cell: torch.Tensor, nbytes: int, dst: torch.Tensor, blocks: int = 32) -> torch.Tensor:
+    """Like :func:`h2d_pull`, but the source address is read when the kernel runs from ``cell`` (a
+    pinned host int64 tensor of >= 1 element whose element 0 holds a pinned-buffer address with
+    ``nbytes`` readable bytes).  Captured once, a graph then pulls from whichever pinned buffer the
+    host wrote into the cell before the replay (engine/worker.py pre-staged batches)."""
+    if cell.is_cuda or not cell.is_pinned() or cell.dtype != torch.int64 or not dst.is_cuda:
+        raise ValueError("h2d_pull_cell: cell must be a pinned host int64 tensor and dst a device tensor")
+    if not dst.is_contiguous() or nbytes != dst.numel() * dst.element_size():
+        raise ValueError("h2d_pull_cell: dst must be contiguous and nbytes its byte size")
+    check(lib().mls_h2d_pull_cell(cell.data_ptr(), dst.data_ptr(), int(nbytes), int(blocks), stream_ptr(dst.device)),
+          "mls_h2d_pull_cell")
+    return dst
+
+
 def d2h_push(src: torch.Tensor, dst: torch.Tensor, blocks: int = 1) -> torch.Tensor:
     """Copy the device tensor ``src`` into the pinned host tensor ``dst`` with a kernel on the current
     stream (stores over PCIe; capturable).  Same byte size, 16-B multiple."""

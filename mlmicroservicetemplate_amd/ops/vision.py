@@ -364,8 +364,12 @@ def fc_head(pooled: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor],
             vals = torch.empty(B, k, device=dev, dtype=torch.float32)
         if idx is None:
             idx = torch.empty(B, k, device=dev, dtype=torch.int32)
+    # the v2 kernels' per-K-slice partial slabs come from the torch allocator (inside a capture:
+    # the graph's own pool, alive as long as the graph), never from a buffer the library frees
+    ws = torch.empty((K // 256) * B * N if K % 256 == 0 else 0, device=dev, dtype=torch.float32)
     check(lib().mls_fc_head(pooled.data_ptr(), w.data_ptr(), _ptr(bias), logits.data_ptr(), _ptr(vals), _ptr(idx),
-                            _ptr(err), B, N, K, int(k), int(softmax), stream_ptr(dev)), "mls_fc_head")
+                            _ptr(err), B, N, K, int(k), int(softmax), ws.data_ptr() if ws.numel() else None,
+                            ws.numel() * 4, stream_ptr(dev)), "mls_fc_head")
     return vals, idx, logits
 
 

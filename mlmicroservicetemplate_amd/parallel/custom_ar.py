@@ -154,6 +154,16 @@ class CustomAllReduce:
         last read completed with a peer missing (its output is partial).  A host sync."""
         return self._errors() if self.enabled or self._ctx else 0
 
+    def error_peek(self, dst: torch.Tensor) -> None:
+        """``dst`` (device int32, >= 1 element) <- the error word on the current stream, without
+        clearing it: capturable, so a graph reports its collectives' peer timeouts in a read-back
+        it makes anyway (the continuous engine's carried-header check)."""
+        if dst.dtype != torch.int32 or not dst.is_cuda or dst.numel() < 1:
+            raise ValueError("error_peek: dst must be a device int32 tensor")
+        rc = self._lib.mls_ar_error_peek(self._ctx, dst.data_ptr(), torch.cuda.current_stream(self.device).cuda_stream)
+        if rc != 0:
+            raise RuntimeError(f"mls_ar_error_peek failed ({rc})")
+
     def reset(self) -> None:
         """Restart the device protocol after a timeout (per-block epochs may disagree between ranks):
         collective -- every rank calls it; process-group barriers on both sides guarantee no

@@ -171,3 +171,44 @@ def max_over_ranks(value: float, group=None) -> float:
     with tracing.range("dist.max"):
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return float(t.item())
+
+
+def gather_objects(obj, group=None) -> list:
+    """Every rank's ``obj`` (picklable), in rank order, on every rank; ``[obj]`` without a group."""
+    if not dist.is_initialized():
+        return [obj]
+    out = [None] * dist.get_world_size(group)
+    with tracing.range("dist.gather_objects"):
+        dist.all_gather_object(out, obj, group=group)
+    return out
+
+
+def all_ranks_true(flag: bool, group=None) -> bool:
+    """True only if ``flag`` holds on every rank (a capability every rank must agree on)."""
+    return all(bool(x) for x in gather_objects(bool(flag), group))
+
+
+def group_description(group=None) -> dict:
+    """The process group as it was formed: backend and world size (``none`` / 1 without one)."""
+    if not dist.is_initialized():
+        return {"dist_backend": "none", "dist_world": 1}
+    return {"dist_backend": str(dist.get_backend(group)), "dist_world": int(dist.get_world_size(group))}
+
+
+def merge_rank_configs(per_rank: List[dict]) -> dict:
+    """Fold per-rank config dicts into one: a key every rank agrees on keeps its value, a key the
+    ranks disagree on becomes ``"mixed"`` with the per-rank values under ``<key>_per_rank``;
+    ``ranks_consistent`` says whether all agreed."""
+    merged: dict = {}
+    consistent = True
+    keys = sorted({k for d in per_rank for k in d})
+    for k in keys:
+        vals = [d.get(k) for d in per_rank]
+        if all(v == vals[0] for v in vals):
+            merged[k] = vals[0]
+        else:
+            consistent = False
+            merged[k] = "mixed"
+            merged[f"{k}_per_rank"] = vals
+    merged["ranks_consistent"] = consistent
+    return merged

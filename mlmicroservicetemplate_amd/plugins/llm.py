@@ -19,11 +19,10 @@ from typing import Any, Dict, List, Tuple
 
 import torch
 
+from ..models.llama_serving import OP_GENERATE, OP_ITER, OP_STOP
 from .base import ModelPlugin, PluginContext, register
 
 logger = logging.getLogger("mlsamd.plugin")
-
-OP_STOP, OP_GENERATE, OP_ITER = 0, 1, 2
 
 
 @register("llama")
@@ -71,8 +70,7 @@ class LlamaPlugin(ModelPlugin):
         if bool(getattr(s, "CONTINUOUS_BATCHING", True)):
             from ..models.llama_serving import ContinuousLlama
 
-            self.engine = ContinuousLlama(self.model, max_queue=int(s.MAX_QUEUE),
-                                          broadcast=self._broadcast_iter if tp > 1 else None)
+            self.engine = ContinuousLlama(self.model, max_queue=int(s.MAX_QUEUE), channel=self if tp > 1 else None)
             if ctx.rank == 0:
                 self.engine.start()
         logger.info("llama ready: tp=%d rank=%d backend=%s device=%s", tp, ctx.rank, backend, dev)
@@ -187,8 +185,10 @@ class LlamaPlugin(ModelPlugin):
             out = self.model.generate(ids, lens, gp)
         return out.cpu().tolist()
 
-    def _broadcast_iter(self, admit) -> None:
-        """Rank 0, continuous mode: publish one iteration's admissions (None = stop)."""
+    # ---- the continuous engine's TP control channel (models/llama_serving.py ContinuousLlama):
+    # explicit headers only when no decode step carried one; admissions only when there are any
+    def send_header(self, admit) -> None:
+        """Rank 0: one iteration's header (None = stop), then its admissions when it has any."""
         import torch.distributed as dist
 
         hdr = torch.zeros(7, dtype=torch.int64, device=self.comm_dev)
@@ -200,13 +200,53 @@ class LlamaPlugin(ModelPlugin):
         hdr[:3] = torch.tensor([OP_ITER, n, S])
         dist.broadcast(hdr, src=0)
         if n:
-            meta = torch.tensor([[a.slot, len(a.ids), a.gp.max_new_tokens, a.gp.top_k, round(a.gp.temperature * 1000),
-                                  a.gp.seed] for a in admit], dtype=torch.int64, device=self.comm_dev)
-            ids = torch.zeros(n, S, dtype=torch.int64, device=self.comm_dev)
-            for j, a in enumerate(admit):
-                ids[j, : len(a.ids)] = torch.tensor(a.ids, dtype=torch.int64)
-            dist.broadcast(meta, src=0)
-            dist.broadcast(ids, src=0)
+            self.send_admissions(admit)
+
+    def send_admissions(self, admit) -> None:
+        """Rank 0: the admitted sequences' slot / length / sampling parameters and prompt ids."""
+        import torch.distributed as dist
+
+        n = len(admit)
+        S = max(len(a.ids) for a in admit)
+        meta = torch.tensor([[a.slot, len(a.ids), a.gp.max_new_tokens, a.gp.top_k, round(a.gp.temperature * 1000),
+                              a.gp.seed] for a in admit], dtype=torch.int64, device=self.comm_dev)
+        ids = torch.zeros(n, S, dtype=torch.int64, device=self.comm_dev)
+        for j, a in enumerate(admit):
+            ids[j, : len(a.ids)] = torch.tensor(a.ids, dtype=torch.int64)
+        dist.broadcast(meta, src=0)
+        dist.broadcast(ids, src=0)
+
+    def recv_header(self):
+        """Followers: (op, admissions, longest prompt) of rank 0's explicit header."""
+        import torch.distributed as dist
+
+        hdr = torch.zeros(7, dtype=torch.int64, device=self.comm_dev)
+        dist.broadcast(hdr, src=0)
+        op, n, S = hdr[:3].tolist()
+        return op, n, S
+
+    def recv_admissions(self, n: int, S: int):
+        """Followers: the ``n`` sequences rank 0 admits this iteration (prompts padded to ``S``)."""
+        import torch.distributed as dist
+
+        from ..models.llama import GenParams
+        from ..models.llama_serving import _Seq
+
+        meta = torch.zeros(n, 6, dtype=torch.int64, device=self.comm_dev)
+        ids = torch.zeros(n, S, dtype=torch.int64, device=self.comm_dev)
+        dist.broadcast(meta, src=0)
+        dist.broadcast(ids, src=0)
+        admit = []
+        ids_l = ids.tolist()
+        for j, (slot, ln, mnt_j, topk_j, temp_j, seed_j) in enumerate(meta.tolist()):
+            seq = _Seq(ids_l[j][:ln], GenParams(mnt_j, topk_j, temp_j / 1000.0, seed_j), None)
+            seq.slot = slot
+            admit.append(seq)
+        return admit
+
+    def _broadcast_iter(self, admit) -> None:
+        """Rank 0, continuous mode, one header per iteration (the legacy hook form)."""
+        self.send_header(admit)
 
     def follower_loop(self) -> int:
         """Ranks > 0: execute rank 0's generate commands until STOP."""
@@ -216,6 +256,11 @@ class LlamaPlugin(ModelPlugin):
 
         from ..models.llama import GenParams
 
+        if self.engine is not None:  # continuous batching: the engine's own follow loop (headers
+            try:                     # carried by the decode steps where possible)
+                return self.engine.follow()
+            finally:
+                self.follower_stats = dict(self.engine.follower_stats, **self.engine.proto)
         # per-iteration host cost of following (X5): the header broadcast + its host read, and the
         # iteration itself -- in the worker's info dump (tests/llama_tp_worker.py) and /info
         st = self.follower_stats = {"iters": 0, "hdr_s": 0.0, "hdr_max_s": 0.0, "iter_s": 0.0}

@@ -10,7 +10,7 @@ import torch.distributed as dist
 
 def serve(m, rank, world, cfg):
     """MODE=serve: the /generate serving path -- ContinuousLlama on every rank, rank 0 scheduling
-    and broadcasting admissions (plugins/llm.py _broadcast_iter / follower_loop), the device-
+    and publishing admissions (plugins/llm.py control channel / follower_loop), the device-
     resident iterations; counts the device -> host copies the iterations make.  STALL_RANK: that
     rank's stream stalls before its first decode step (the peers' one-shot waits time out): every
     in-flight request must fail with TPCommError, none may return tokens."""
@@ -25,7 +25,7 @@ def serve(m, rank, world, cfg):
     plug.model = m
     plug.comm_dev = torch.device("cpu")  # gloo
     plug.ctx = types.SimpleNamespace(rank=rank)
-    eng = ContinuousLlama(m, broadcast=plug._broadcast_iter if rank == 0 else None)
+    eng = ContinuousLlama(m, channel=plug)
     plug.engine = eng
     stall_rank = int(os.environ.get("STALL_RANK", "-1"))
     if rank == stall_rank:
@@ -75,7 +75,7 @@ def serve(m, rank, world, cfg):
         torch.Tensor.cpu = orig
     info = {"iterations": eng.iterations, "host_reads": eng.host_reads, "cpu_calls": len(calls),
             "dev_mode": int(eng.dev_mode), "failures": eng.failures, "car": int(m.comm.car is not None),
-            "follower": getattr(plug, "follower_stats", None)}
+            "follower": getattr(plug, "follower_stats", None), "proto": eng.proto}
     reqs_json = json.dumps([[ids, [gp.max_new_tokens, gp.top_k, gp.temperature, gp.seed]] for ids, gp in reqs]
                            if rank == 0 else [])
     torch.save({"results": json.dumps(results), "info": json.dumps(info), "reqs": reqs_json},

@@ -240,6 +240,8 @@ def test_prepared_batches_match_submit():
     ref = [eng.run(b) for b in batches]
     for active in (False, True):
         ctx = tracing.record() if active else contextlib.nullcontext()
+        for sl in eng.slots:  # the graphs pull a prepared batch from its own buffer, not host_in
+            sl.host_in.zero_()
         with ctx:
             pending, outs = [], []
             nxt = eng.prepare(batches[0])
@@ -252,7 +254,12 @@ def test_prepared_batches_match_submit():
             outs += [t.wait() for t in pending]
         for a, b in zip(ref, outs):
             np.testing.assert_array_equal(a[0], b[0])
+        assert not any(bool(sl.host_in.any()) for sl in eng.slots), "a prepared batch was copied into host_in"
     assert eng._spare.qsize() == eng.inflight + 1
+    # plain submits after prepared launches pull from host_in again (the cell is re-pointed)
+    for i in range(4):
+        np.testing.assert_array_equal(eng.run(batches[i])[0], ref[i][0])
+        assert any(int(sl.src_cell[0]) == sl.host_in.data_ptr() for sl in eng.slots)
 
 
 def test_sdma_free_io_and_fallback():

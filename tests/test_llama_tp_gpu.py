@@ -200,8 +200,15 @@ def test_tp_serving_continuous_device_path(tmp_path, case):
     for r, i in enumerate(infos):
         if r and i.get("follower"):  # per-iteration host cost of following rank 0 (X5 header)
             f = i["follower"]
-            print(f"rank {r}: {f['iters']} iterations, header broadcast + read {f['hdr_s'] / max(1, f['iters']) * 1e3:.3f} "
-                  f"ms/iter (max {f['hdr_max_s'] * 1e3:.2f}), iteration {f['iter_s'] / max(1, f['iters']) * 1e3:.3f} ms/iter")
+            print(f"rank {r}: {f['iters']} iterations, header receive {f['hdr_s'] / max(1, f['iters']) * 1e3:.3f} "
+                  f"ms/iter (max {f['hdr_max_s'] * 1e3:.2f}), iteration {f['iter_s'] / max(1, f['iters']) * 1e3:.3f} ms/iter, "
+                  f"headers carried {f['carried_headers']} / explicit {f['explicit_headers']}, "
+                  f"admission broadcasts {f['admission_broadcasts']}")
+            # the headers ride the decode steps' gather: an iteration without admissions issues no
+            # collective of its own, and most headers never touch the process group
+            assert f["iters_no_admit_bcast"] == 0, f
+            assert f["carried_headers"] > f["explicit_headers"], f
+            assert f["explicit_headers"] + f["carried_headers"] == f["iters"] + 1, f  # + the STOP
     for i in infos:
         assert i["dev_mode"] == 1 and i["car"] == 1, infos
         # one [2, B] read-back per iteration, no other device -> host copy
