@@ -105,12 +105,13 @@ class Prepared:
     """A batch staged into a spare pinned buffer (:meth:`GpuEngine.prepare`) before any slot is
     free; :meth:`GpuEngine.launch_prepared` enqueues it (H2D straight from that buffer)."""
 
-    __slots__ = ("buf", "n", "t0")
+    __slots__ = ("buf", "n", "t0", "dev")
 
     def __init__(self, buf: torch.Tensor, n: int, t0: Optional[float] = None):
         self.buf = buf
         self.n = n
         self.t0 = time.perf_counter() if t0 is None else t0  # prepare() start
+        self.dev = None  # prepull: (device buffer, event after its pull) -- the batch already on the GPU
 
 
 class GpuEngine:
@@ -198,6 +199,14 @@ class GpuEngine:
         self.pull_h2d = int(os.environ.get("MLS_PULL_H2D", "8")) if (
             self.copies_on_slot_stream and use_graphs and not self.graph_copies
             and sample_dtype == torch.uint8) else 0
+        # Early pull of pre-staged batches (MLS_PREPULL=1): prepare() stages a batch into a spare
+        # pinned buffer while every slot is busy AND pulls it at once, on the engine's I/O stream,
+        # into a spare device buffer; the slot's graph later starts with a device-to-device copy
+        # (the same cell-addressed copy kernel with all MLS_PREPULL_WG workgroups, ~2-3 us) instead
+        # of the ~90 us PCIe pull -- the pull leaves the batch's critical path.
+        self.prepull = bool(self.pull_h2d) and os.environ.get("MLS_PREPULL", "0") == "1"
+        self.pull_grid = max(self.pull_h2d, int(os.environ.get("MLS_PREPULL_WG", "64"))) if self.prepull \
+            else self.pull_h2d
         # host staging (request arrays -> pinned slot): a persistent native copy pool (GIL released,
         # the submitting thread copies too); one thread's ~5-8 GB/s memcpy is not enough for a
         # 4.8 MB ResNet batch every ~0.6 ms next to the rest of the host loop
@@ -238,6 +247,7 @@ class GpuEngine:
         self.healthy = True
         self.last_error: Optional[str] = None
         with torch.cuda.device(self.device):
+            self.s_io = torch.cuda.Stream(self.device) if self.prepull else None  # early pulls
             self.s_h2d = torch.cuda.Stream(self.device)
             self.s_comp = torch.cuda.Stream(self.device)
             self.s_d2h = torch.cuda.Stream(self.device)
@@ -255,6 +265,7 @@ class GpuEngine:
                 )
                 slot.cell_np = slot.src_cell.numpy()
                 slot.cell_np[0] = slot.host_in.data_ptr()
+                slot.cell_np[1] = self.pull_h2d  # workgroups that copy from host memory
                 if self.concurrent:
                     if part_masks is not None:
                         # pooled per (mask, slot-in-partition): engines built one after another in a
@@ -275,6 +286,7 @@ class GpuEngine:
         self._spare: "queue.Queue[torch.Tensor]" = queue.Queue()
         self._spare_lock = threading.Lock()
         self._spare_made = False
+        self._dev_spare: "queue.Queue[tuple]" = queue.Queue()  # prepull: (device buffer, event)
 
     # ------------------------------------------------------------------ capture
     def warmup(self, capture: bool = True) -> None:
@@ -318,7 +330,7 @@ class GpuEngine:
                                 # the source address comes from the slot's pinned cell at run time,
                                 # so a pre-staged batch is pulled straight from its own buffer
                                 ops.h2d_pull_cell(slot.src_cell, slot.host_in[:b].numel() * slot.host_in.element_size(),
-                                                  slot.dev_in[:b], self.pull_h2d)
+                                                  slot.dev_in[:b], self.pull_grid)
                             outs = self.forward(slot.dev_in[:b])
                             # ... and the results pushed to the pinned host buffers by a kernel at the
                             # graph's end (no SDMA D2H either), when every output is a 16-B multiple
@@ -372,9 +384,9 @@ class GpuEngine:
             # SDMA H2D copy itself, with the GIL held as well (docs/PERF_NOTES.md, round 5) -- the
             # engine no longer uses SDMA (pull_h2d).  MLS_ENQUEUE_HOLD_GIL=1 keeps the PyDLL form.
             hold = os.environ.get("MLS_ENQUEUE_HOLD_GIL", "0") == "1"
-            fn = getattr(ctypes.PyDLL(lib._name) if hold else lib, "mls_engine_launch")
-            fn.argtypes = lib.mls_engine_launch.argtypes
-            fn.restype = lib.mls_engine_launch.restype
+            fn = getattr(ctypes.PyDLL(lib._name) if hold else lib, "mls_engine_launch_after")
+            fn.argtypes = lib.mls_engine_launch_after.argtypes
+            fn.restype = lib.mls_engine_launch_after.restype
             exec_h = slot.graphs[b].raw_cuda_graph_exec()
             slot.ev_done.record(slot.s_comp)  # torch creates the event lazily: make it exist
             ev = slot.ev_done.cuda_event
@@ -386,7 +398,8 @@ class GpuEngine:
             h2d = slot.host_in[:b]
             t_ns = (ctypes.c_longlong * 5)()  # per-call host times of the last enqueue (diagnostics)
             h2d_bytes = 0 if slot.pulled.get(b) else h2d.numel() * h2d.element_size()  # pulled in the graph
-            args = (slot.s_comp.cuda_stream, slot.dev_in.data_ptr(), slot.host_in.data_ptr(),
+            # (the first argument: an event the slot's stream waits for first -- a prepulled batch's pull)
+            args = (None, slot.s_comp.cuda_stream, slot.dev_in.data_ptr(), slot.host_in.data_ptr(),
                     h2d_bytes, exec_h, n, dst, src, nb, ev, t_ns)
             if not exec_h or not ev:
                 raise RuntimeError("graph exec / event handle unavailable")
@@ -446,6 +459,10 @@ class GpuEngine:
                 for _ in range(self.inflight + 1):
                     self._spare.put(torch.zeros((self.max_batch, *self.sample_shape), dtype=self.sample_dtype,
                                                 pin_memory=True))
+                if self.prepull:
+                    for _ in range(self.inflight + 2):
+                        self._dev_spare.put((torch.empty((self.max_batch, *self.sample_shape), dtype=self.sample_dtype,
+                                                         device=self.device), torch.cuda.Event()))
                 self._spare_made = True
         buf = self._spare.get()
         try:
@@ -463,7 +480,26 @@ class GpuEngine:
         except BaseException:
             self._spare.put(buf)
             raise
-        return Prepared(buf, n, t0)
+        prep = Prepared(buf, n, t0)
+        if self.prepull:
+            self._pull_early(prep)
+        return prep
+
+    def _pull_early(self, prep: Prepared) -> None:
+        """prepull: the staged batch goes to a spare device buffer now, on the I/O stream (the
+        bucket's rows: the graph copies exactly those); its event orders the slot's graph after it."""
+        from .. import ops
+
+        b = pick_bucket(prep.n, self.buckets)
+        d = self._dev_spare.get()
+        try:
+            with torch.cuda.device(self.device), torch.cuda.stream(self.s_io):
+                ops.h2d_pull(prep.buf[:b], d[0][:b], self.pull_h2d)
+                d[1].record(self.s_io)
+        except BaseException:
+            self._dev_spare.put(d)
+            raise
+        prep.dev = d
 
     def launch_prepared(self, prep: Prepared) -> Ticket:
         """Take a free slot (blocking) and enqueue a :meth:`prepare`-d batch: H2D from its buffer."""
@@ -517,13 +553,20 @@ class GpuEngine:
             nat = slot.native.get(bucket) if self.native_launch and not tracing.active() else None
             if nat is not None:
                 pulled = slot.pulled.get(bucket)
-                if pulled:  # the graph pulls from the address in the slot's cell: no host copy
+                early = pulled and staged is not None and staged.dev is not None
+                if early:  # already on the device: the graph's copy reads it there, all workgroups
+                    slot.cell_np[0] = staged.dev[0].data_ptr()
+                    slot.cell_np[1] = 0
+                elif pulled:  # the graph pulls from the address in the slot's cell: no host copy
                     slot.cell_np[0] = src_host.data_ptr()
+                    slot.cell_np[1] = self.pull_h2d
                 with self._enqueue_lock:
                     self._pace_launch()
                     fn, args, _keep = nat
-                    if staged is not None and not pulled:  # same call, H2D from the prepared buffer
-                        args = args[:2] + (staged.buf.data_ptr(),) + args[3:]
+                    if early:  # the slot's stream first waits for the early pull
+                        args = (staged.dev[1].cuda_event,) + args[1:]
+                    elif staged is not None and not pulled:  # same call, H2D from the prepared buffer
+                        args = args[:3] + (staged.buf.data_ptr(),) + args[4:]
                     rc = fn(*args)
                 if rc != 0:
                     raise RuntimeError(f"mls_engine_launch failed (HIP error {rc})")
@@ -545,8 +588,14 @@ class GpuEngine:
                 s_h2d = slot.s_comp if self.copies_on_slot_stream else self.s_h2d
                 s_d2h = slot.s_comp if self.copies_on_slot_stream else self.s_d2h
                 pulled = self.use_graphs and bucket in slot.graphs and slot.pulled.get(bucket, False)
-                if pulled:  # the graph pulls from the address in the slot's cell
+                early = pulled and staged is not None and staged.dev is not None
+                if early:  # pulled to the device already: the graph copies it from there
+                    slot.cell_np[0] = staged.dev[0].data_ptr()
+                    slot.cell_np[1] = 0
+                    slot.s_comp.wait_event(staged.dev[1])
+                elif pulled:  # the graph pulls from the address in the slot's cell
                     slot.cell_np[0] = src_host.data_ptr()
+                    slot.cell_np[1] = self.pull_h2d
                 with tracing.range(self._tr_h2d), torch.cuda.stream(s_h2d):
                     if not pulled:
                         slot.dev_in[:bucket].copy_(src_host[:bucket], non_blocking=True)
@@ -574,6 +623,8 @@ class GpuEngine:
             self._free.put(slot)
             if staged is not None:
                 self._spare.put(staged.buf)
+                if staged.dev is not None:
+                    self._dev_spare.put(staged.dev)
             self.last_error = f"{type(e).__name__}: {e}"
             raise
         return Ticket(self, slot, bucket, n, staged)
@@ -633,6 +684,8 @@ class GpuEngine:
         finally:
             if t.staged is not None:  # its H2D is done (the batch completed): reusable
                 self._spare.put(t.staged.buf)
+                if t.staged.dev is not None:
+                    self._dev_spare.put(t.staged.dev)
                 t.staged = None
             self._free.put(slot)
 
@@ -642,7 +695,7 @@ class GpuEngine:
     def stats(self) -> dict:
         return {"name": self.name, "device": str(self.device), "batches": self.batches, "samples": self.samples,
                 "inflight": self.inflight, "buckets": self.buckets, "graphs": self.use_graphs,
-                "concurrent": self.concurrent, "cu_partitions": self.cu_partitions,
+                "concurrent": self.concurrent, "cu_partitions": self.cu_partitions, "prepull": self.prepull,
                 "native_staging": self._stager.native,
                 "pace_gap_us": round(self._pace * self._lat_s / max(1, self.inflight) * 1e6, 1),
                 "healthy": self.healthy, "last_error": self.last_error,

@@ -236,7 +236,10 @@ class ContinuousLlama:
         """Ranks > 0 (TP): replay rank 0's iterations until it stops.  Each header comes from the
         previous decode step's read-back when it carried one, else from the channel; admissions
         are received only when the header announces some."""
-        st = self.follower_stats = {"iters": 0, "hdr_s": 0.0, "hdr_max_s": 0.0, "iter_s": 0.0}
+        # hdr_s: time spent learning each iteration's header (+ receiving its admissions); first_hdr_s:
+        # the first of them, which also waits out rank 0's start-up (weights, graph capture)
+        st = self.follower_stats = {"iters": 0, "hdr_s": 0.0, "hdr_max_s": 0.0, "iter_s": 0.0, "first_hdr_s": None,
+                                    "explicit_s": 0.0, "carried_s": 0.0}
         while True:
             t0 = time.perf_counter()
             hdr, self._next_hdr = self._next_hdr, None
@@ -258,8 +261,12 @@ class ContinuousLlama:
             elif bcast:
                 self.proto["iters_no_admit_bcast"] += 1
             dt = time.perf_counter() - t0
-            st["hdr_s"] += dt
-            st["hdr_max_s"] = max(st["hdr_max_s"], dt)
+            if st["first_hdr_s"] is None:
+                st["first_hdr_s"] = dt
+            else:
+                st["hdr_s"] += dt
+                st["hdr_max_s"] = max(st["hdr_max_s"], dt)
+                st["explicit_s" if bcast else "carried_s"] += dt
             t1 = time.perf_counter()
             try:
                 self.run_iteration(admit)  # same failure handling / health checks as rank 0

@@ -107,7 +107,7 @@ _SIGS = {
 }
 _OPTIONAL_SIGS: dict = {"mls_set_debug_flags": [I], "mls_chain_set_l2_cw": [I],
     "mls_chain_set_l2_bm": [I],
-    "mls_engine_launch": [P, P, P, _c.c_longlong, P, I, P, P, P, P, P], "mls_skinny_set_variant": [I], "mls_skinny_set_max_split": [I]}
+    "mls_engine_launch": [P, P, P, _c.c_longlong, P, I, P, P, P, P, P], "mls_engine_launch_after": [P, P, P, P, _c.c_longlong, P, I, P, P, P, P, P], "mls_skinny_set_variant": [I], "mls_skinny_set_max_split": [I]}
 
 
 class NativeError(RuntimeError):

@@ -42,20 +42,28 @@ __global__ __launch_bounds__(256) void h2d_pull_kernel(const void* src, void* ds
   }
 }
 
-// The same pull with the source address read at run time from a pinned host cell (`src_cell`,
-// one 8-B word the host writes before the graph launch): a captured graph pulls whichever pinned
-// buffer a batch was staged in (GpuEngine.prepare), so a pre-staged batch needs no host memcpy into
-// the slot's own buffer.  The cell is read with a system-scope load (no cache may hold a stale
-// address from the previous launch) and made wave-uniform for the buffer descriptor.
+// The same pull with the source read at run time from a pinned host cell the host writes before
+// the graph launch: cell[0] = source address (pinned host memory, or device memory), cell[1] = how
+// many of the launch's workgroups copy (0 = all).  A captured graph thus pulls whichever buffer a
+// batch was staged in (GpuEngine.prepare): a pre-staged batch needs no host memcpy into the slot's
+// own buffer, and a batch already pulled to the device ahead of its launch (GpuEngine prepull) is
+// a device-to-device copy by all of the workgroups -- PCIe sets the host pull's ~90 us with 8 of
+// them, HBM wants more.  The cell is read with system-scope loads (no cache may hold the previous
+// launch's words) and made wave-uniform for the buffer descriptor.
 template <int U>
 __global__ __launch_bounds__(256) void h2d_pull_cell_kernel(const unsigned long long* src_cell, void* dst,
-                                                            uint32_t bytes, int iters) {
+                                                            uint32_t bytes) {
   const unsigned long long a = __hip_atomic_load(src_cell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const unsigned long long nb = __hip_atomic_load(src_cell + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
   const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  const int nblk_req = (int)__builtin_amdgcn_readfirstlane((unsigned)nb);
+  const int nblk = nblk_req > 0 && nblk_req < (int)gridDim.x ? nblk_req : (int)gridDim.x;
+  if ((int)blockIdx.x >= nblk) return;
   const void* src = (const void*)(((unsigned long long)hi << 32) | lo);
   const rsrc_t s = make_rsrc(src, bytes), d = make_rsrc(dst, bytes);
-  const int stride = (int)gridDim.x * 256 * 16;
+  const int stride = nblk * 256 * 16;
+  const int iters = (int)((bytes + (uint32_t)(stride * U) - 1) / (uint32_t)(stride * U));
   int off = ((int)blockIdx.x * 256 + (int)threadIdx.x) * 16;
   for (int it = 0; it < iters; ++it) {
     uint4 v[U];
@@ -70,16 +78,18 @@ __global__ __launch_bounds__(256) void h2d_pull_cell_kernel(const unsigned long 
 }
 
 extern "C" {
+int mls_engine_launch_after(void* wait_event, void* stream, void* h2d_dst, const void* h2d_src, long long h2d_bytes,
+                            void* graph_exec, int n_d2h, void* const* d2h_dst, void* const* d2h_src,
+                            const long long* d2h_bytes, void* event, long long* t_ns);
 
-// src_cell: pinned host word holding the source address (pinned host memory, `bytes` readable).
+// src_cell: pinned host words {source address (`bytes` readable), workgroups to copy with (0 = all
+// `blocks`)}.
 int mls_h2d_pull_cell(const void* src_cell, void* dst, long long bytes, int blocks, void* stream) {
   if (!src_cell || !dst || bytes <= 0 || bytes % 16 || bytes >= (1LL << 30) || blocks <= 0 || blocks > 1024)
     return MLS_BAD_ARG;
   constexpr int U = 8;
-  const long long step = (long long)blocks * 256 * 16 * U;
-  const int iters = (int)((bytes + step - 1) / step);
   hipLaunchKernelGGL(h2d_pull_cell_kernel<U>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
-                     (const unsigned long long*)src_cell, dst, (uint32_t)bytes, iters);
+                     (const unsigned long long*)src_cell, dst, (uint32_t)bytes);
   return (int)hipGetLastError();
 }
 
@@ -110,11 +120,21 @@ int mls_d2h_push(const void* src, void* dst, long long bytes, int blocks, void* 
 int mls_engine_launch(void* stream, void* h2d_dst, const void* h2d_src, long long h2d_bytes, void* graph_exec,
                       int n_d2h, void* const* d2h_dst, void* const* d2h_src, const long long* d2h_bytes,
                       void* event, long long* t_ns) {
+  return mls_engine_launch_after(nullptr, stream, h2d_dst, h2d_src, h2d_bytes, graph_exec, n_d2h, d2h_dst, d2h_src,
+                                 d2h_bytes, event, t_ns);
+}
+
+// the same, the slot's stream first waiting for `wait_event` (recorded on another stream: the
+// early pull of a pre-staged batch, GpuEngine prepull), or no wait when it is null
+int mls_engine_launch_after(void* wait_event, void* stream, void* h2d_dst, const void* h2d_src, long long h2d_bytes,
+                            void* graph_exec, int n_d2h, void* const* d2h_dst, void* const* d2h_src,
+                            const long long* d2h_bytes, void* event, long long* t_ns) {
   if (!graph_exec || n_d2h < 0 || n_d2h > 8) return MLS_BAD_ARG;
   hipStream_t st = (hipStream_t)stream;
   hipError_t e = hipSuccess;
+  if (wait_event) e = hipStreamWaitEvent(st, (hipEvent_t)wait_event, 0);
   if (t_ns) t_ns[0] = now_ns();
-  if (h2d_bytes > 0) e = hipMemcpyAsync(h2d_dst, h2d_src, (size_t)h2d_bytes, hipMemcpyHostToDevice, st);
+  if (h2d_bytes > 0 && e == hipSuccess) e = hipMemcpyAsync(h2d_dst, h2d_src, (size_t)h2d_bytes, hipMemcpyHostToDevice, st);
   if (t_ns) t_ns[1] = now_ns();
   if (e == hipSuccess) e = hipGraphLaunch((hipGraphExec_t)graph_exec, st);
   if (t_ns) t_ns[2] = now_ns();

@@ -288,3 +288,55 @@ def test_sdma_free_io_and_fallback():
     x = rng.integers(0, 256, (3, 5), dtype=np.uint8)
     ref = (torch.from_numpy(x).to(DEV).float() @ w5.T).to(torch.bfloat16).float().cpu().numpy()
     np.testing.assert_allclose(eng5.run(x)[0], ref, rtol=1e-2, atol=1e-2 * np.abs(ref).max())
+
+
+@pytest.mark.parametrize("model", ["linear", "resnet50"])
+def test_prepull_batches_match_serial(monkeypatch, model):
+    """MLS_PREPULL=1: prepare() stages a batch AND pulls it to a spare device buffer on the I/O
+    stream; the slot's graph then copies it device-to-device.  Back-to-back prepared batches (more of
+    them than device buffers, slots reused while earlier batches are still in flight) give exactly
+    the outputs of one-at-a-time serial runs: no buffer is overwritten before its graph read it."""
+    from mlmicroservicetemplate_amd.engine.worker import GpuEngine
+
+    monkeypatch.setenv("MLS_PREPULL", "1")
+    rng = np.random.default_rng(21)
+    if model == "linear":
+        w = torch.randn(16, 48, device=DEV)
+        fwd = lambda x: ((x.float() @ w.T).to(torch.bfloat16), x.float().sum(dim=1))  # noqa: E731
+        shape, sizes, buckets = (48,), (3, 8, 5, 8, 2, 7, 8, 1, 8, 8, 4, 6), [4, 8]
+    else:
+        from mlmicroservicetemplate_amd.models import resnet
+        from mlmicroservicetemplate_amd.ops.autotune import load_tuning
+
+        m = resnet.ResNet50Fused(resnet.init_resnet50(2), DEV, max_batch=8, tuning=load_tuning("resnet50", 8))
+        fwd = lambda x: m.classify(x, 5)  # noqa: E731
+        shape, sizes, buckets = (224, 224, 3), (8, 8, 5, 8, 8, 8, 3, 8), [8]
+    batches = [rng.integers(0, 256, (n, *shape), dtype=np.uint8) for n in sizes]
+    serial = GpuEngine(fwd, DEV, shape, torch.uint8, buckets=buckets, inflight=1, name="ser")
+    serial.warmup()
+    ref = [serial.run(b) for b in batches]
+    eng = GpuEngine(fwd, DEV, shape, torch.uint8, buckets=buckets, inflight=3, concurrent=True, name="prepull",
+                    cu_partitions=0)
+    eng.warmup(capture=True)
+    assert eng.prepull and eng.pull_grid >= eng.pull_h2d and eng.s_io is not None
+    for sl in eng.slots:
+        sl.host_in.zero_()
+    pending, outs = [], []
+    nxt = eng.prepare(batches[0])
+    assert nxt.dev is not None
+    for i in range(len(batches)):
+        pending.append(eng.launch_prepared(nxt))
+        if i + 1 < len(batches):
+            nxt = eng.prepare(batches[i + 1])
+        if len(pending) >= eng.inflight:
+            outs.append(pending.pop(0).wait())
+    outs += [t.wait() for t in pending]
+    for a, b in zip(ref, outs):
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
+    assert not any(bool(sl.host_in.any()) for sl in eng.slots)
+    assert eng._dev_spare.qsize() == eng.inflight + 2 and eng._spare.qsize() == eng.inflight + 1
+    # a plain submit (pulled from the slot's pinned buffer over PCIe) still works after them
+    for i in range(3):
+        for x, y in zip(eng.run(batches[i]), ref[i]):
+            np.testing.assert_array_equal(x, y)
