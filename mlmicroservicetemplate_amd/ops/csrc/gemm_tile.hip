@@ -718,199 +718,6 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_tile_kernel(const GemmTileA
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// 8-phase variant (cfg 23; cdna_hip_programming.md §5 "The 256^2 8-phase template" / T3+T4): the
-// 256 x 256 tile of cfg 15 (8 waves 2 x 4, wave tile 128 x 64, same LDS image, swizzle, epilogues
-// and persistent tile walk), with each K-step split into 4 phases of 16 MFMAs -- one 64 x 32 quadrant
-// of the wave tile -- and the two wave groups (wm = 0: waves 0-3, wm = 1: waves 4-7; one wave of each
-// per SIMD) one barrier apart, so in every barrier interval one wave per SIMD multiplies while the
-// other reads its next quadrant's fragments and issues DMA.
-//  * half-tiles: A-ht h = A rows {wm * 128 + h * 64 + 0..63}, W-ht h = W rows {wn * 64 + h * 32 + 0..31}
-//    (16 KB each, 2 x 16-B DMAs per thread); quadrant (qm, qn) reads A-ht qm and W-ht qn only;
-//  * phases of K-step j (buffer j & 1): (0,0) reads A-ht0 + W-ht0, (0,1) W-ht1, (1,1) A-ht1, (1,0)
-//    nothing (all fragments kept: 64 VGPRs);
-//  * DMA, one half-tile per phase: phase 0 W-ht1 of step j+1, 1 A-ht1 of j+1, 2 A-ht0 of j+2, 3 W-ht0
-//    of j+2 -- every restage >= 2 phases after the last read of that region (WAR), 5-6 phases of lead;
-//  * RAW: before the first barrier of phase s, vmcnt(8) (the 4 half-tiles issued after the one the
-//    next phase reads may fly) in phases 0, 1, 3; each reader passes a barrier after every wave's
-//    wait (the lagging group waits one barrier later, before the barrier the leading group reads after).
-// LNK 2 (the PART epilogue's block barrier): the groups re-align for the epilogue (one extra barrier
-// each side).  No split-K.
-template <int LNK>
-__global__ __launch_bounds__(512) void gemm_8p_kernel(const GemmTileArgs g) {
-  constexpr int BM = 256, BN = 256, WM = 2, WN = 4, NT = 512;
-  constexpr int WTM = 128, WTN = 64, MT = 8, NTL = 4;
-  constexpr int ROWB = 128, A_BYTES = BM * ROWB, STAGE_BYTES = A_BYTES + BN * ROWB;
-  constexpr int PSCR_BYTES = LNK == 2 ? WN * BM * 8 : 0;
-  static_assert(2 * STAGE_BYTES + PSCR_BYTES <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES + 16 + PSCR_BYTES];
-  float* const pscr = reinterpret_cast<float*>(smem + 2 * STAGE_BYTES + 16);
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid / WN, wn = wid - wm * WN;
-  const int tiles_m = (g.M + BM - 1) / BM, ntiles = tiles_m * g.tiles_n;
-  const int G = gridDim.x, bq = xcd_remap(blockIdx.x, G);
-  const int my_tiles = bq < ntiles ? (ntiles - 1 - bq) / G + 1 : 0;
-  const int nk = g.K / 64, nsteps = my_tiles * nk;
-  const rsrc_t ra = make_rsrc(g.a, g.a_bytes), rw = make_rsrc(g.w, g.w_bytes);
-  const int K2 = g.K * 2;
-
-  // DMA pieces: thread row rr = tid / 8 (0..63) of a 64-row piece, lane-linear source chunk
-  // (tid & 7) ^ swz(row) (swz depends on row & 15; every piece origin is 16-aligned)
-  const int rr = tid >> 3;
-  const int src_col = ((tid & 7) ^ ((rr >> 1) & 7)) * 16;
-  // A-ht h, piece p (= wm of the rows): rows p * 128 + h * 64 + rr.  W-ht h, piece p: rows
-  // wn' * 64 + h * 32 + (rr & 31), wn' = 2p + rr / 32 -- a wave's 8 rows stay inside one wn' block,
-  // so its 1 KB LDS image is contiguous at row wn' * 64 + h * 32 + (wid & 3) * 8
-  auto issue = [&](char* buf, int h, bool isA, int m0, int n0, int kt) {
-    const int koff = kt * ROWB;
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      if (isA) {
-        const int row = p * 128 + h * 64 + rr;
-        gt_glds16(ra, buf + (p * 128 + h * 64 + wid * 8) * ROWB, m0 + row < g.M ? row * K2 + src_col : OOB,
-                  m0 * K2 + koff);
-      } else {
-        const int wnp = 2 * p + (rr >> 5);
-        const int row = wnp * 64 + h * 32 + (rr & 31);
-        gt_glds16(rw, buf + A_BYTES + ((2 * p + (wid >> 2)) * 64 + h * 32 + (wid & 3) * 8) * ROWB,
-                  n0 + row < g.N ? row * K2 + src_col : OOB, n0 * K2 + koff);
-      }
-    }
-  };
-  auto tile_mn = [&](int ti, int& m0, int& n0) {
-    int tm, tn;
-    gt_tile(bq + ti * G, tiles_m, g.tiles_n, tm, tn);
-    m0 = tm * BM;
-    n0 = tn * BN;
-  };
-  // loader cursors: K-step j + 1 (c1) and j + 2 (c2) as (tile, k-step) -> (m0, n0, kt)
-  struct Cur { int ti, kt, m0, n0; };
-  Cur c1{0, 0, 0, 0}, c2{0, 0, 0, 0};
-  auto advance = [&](Cur& c) {
-    if (++c.kt == nk) {
-      c.kt = 0;
-      if (++c.ti < my_tiles) tile_mn(c.ti, c.m0, c.n0);
-    }
-  };
-
-  f32x4 acc[MT][NTL];
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int j = 0; j < NTL; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int fr = lane & 15, fq = lane >> 4;
-  const int sw = (fr >> 1) & 7;
-  const int coff0 = (fq ^ sw) << 4, coff1 = ((4 + fq) ^ sw) << 4;
-  const int a_rd = (wm * WTM + fr) * ROWB, w_rd = A_BYTES + (wn * WTN + fr) * ROWB;
-  bf16x8 af[4][2], w0[2][2], w1[2][2];
-  auto rdA = [&](const char* base, int qm) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      af[i][0] = *reinterpret_cast<const bf16x8*>(base + a_rd + (4 * qm + i) * 16 * ROWB + coff0);
-      af[i][1] = *reinterpret_cast<const bf16x8*>(base + a_rd + (4 * qm + i) * 16 * ROWB + coff1);
-    }
-  };
-  auto rdW = [&](const char* base, int qn, bf16x8 (&w)[2][2]) {
-#pragma unroll
-    for (int jn = 0; jn < 2; ++jn) {
-      w[jn][0] = *reinterpret_cast<const bf16x8*>(base + w_rd + (2 * qn + jn) * 16 * ROWB + coff0);
-      w[jn][1] = *reinterpret_cast<const bf16x8*>(base + w_rd + (2 * qn + jn) * 16 * ROWB + coff1);
-    }
-  };
-  // k-half outermost: the two MFMAs into one accumulator sit 8 apart (a dependent back-to-back pair
-  // would wait for the first's result); the same per-element k order as cfg 15 (bit-identical)
-  auto mm = [&](int qm, int qn, const bf16x8 (&w)[2][2]) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kh = 0; kh < 2; ++kh)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int jn = 0; jn < 2; ++jn)
-          acc[4 * qm + i][2 * qn + jn] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[jn][kh], af[i][kh], acc[4 * qm + i][2 * qn + jn], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  auto bar = []() {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-
-  if (nsteps > 0) {
-    // prologue: K-step 0 whole, K-step 1's A-ht0 + W-ht0 (the steady state's in-flight set at (0, 0))
-    int m0, n0;
-    tile_mn(0, m0, n0);
-    c1 = Cur{0, 0, m0, n0};
-    issue(smem, 0, true, m0, n0, 0);
-    issue(smem, 0, false, m0, n0, 0);
-    issue(smem, 1, false, m0, n0, 0);
-    issue(smem, 1, true, m0, n0, 0);
-    advance(c1);  // -> step 1
-    c2 = c1;
-    if (nsteps > 1) {
-      issue(smem + STAGE_BYTES, 0, true, c1.m0, c1.n0, c1.kt);
-      issue(smem + STAGE_BYTES, 0, false, c1.m0, c1.n0, c1.kt);
-      gt_wait_vmcnt<8>();  // step 0's A-ht0 / W-ht0 landed (4 half-tiles after them may fly)
-    } else {
-      gt_wait_vmcnt<4>();
-    }
-    advance(c2);  // -> step 2
-    bar();        // B0: every wave's wait above passed
-    if (wm == 1) bar();  // the lagging group
-  }
-
-  int c_kt = 0, c_ti = 0;
-  for (int j = 0; j < nsteps; ++j) {
-    const char* base = smem + (j & 1) * STAGE_BYTES;
-    char* nxt = smem + ((j + 1) & 1) * STAGE_BYTES;  // step j + 1's buffer (= step j + 2's is base)
-    const bool has1 = j + 1 < nsteps, has2 = j + 2 < nsteps;
-    // phase 0: quadrant (0, 0)
-    rdA(base, 0);
-    rdW(base, 0, w0);
-    if (has1) issue(nxt, 1, false, c1.m0, c1.n0, c1.kt);
-    if (has1) gt_wait_vmcnt<8>(); else gt_wait_vmcnt<0>();  // step j's W-ht1 (phase 1)
-    bar();
-    mm(0, 0, w0);
-    bar();
-    // phase 1: quadrant (0, 1)
-    rdW(base, 1, w1);
-    if (has1) issue(nxt, 1, true, c1.m0, c1.n0, c1.kt);
-    if (has1) gt_wait_vmcnt<8>(); else gt_wait_vmcnt<0>();  // step j's A-ht1 (phase 2)
-    bar();
-    mm(0, 1, w1);
-    bar();
-    // phase 2: quadrant (1, 1)
-    rdA(base, 1);
-    if (has2) issue(const_cast<char*>(base), 0, true, c2.m0, c2.n0, c2.kt);
-    bar();
-    mm(1, 1, w1);
-    bar();
-    // phase 3: quadrant (1, 0)
-    if (has2) issue(const_cast<char*>(base), 0, false, c2.m0, c2.n0, c2.kt);
-    if (has2) gt_wait_vmcnt<8>();         // step j + 1's A-ht0 / W-ht0 (next phase 0)
-    else if (has1) gt_wait_vmcnt<4>();
-    bar();
-    mm(1, 0, w0);
-    bar();
-    c1 = c2;
-    advance(c2);
-    if (++c_kt < nk) continue;
-    c_kt = 0;
-    int m0, n0;
-    tile_mn(c_ti++, m0, n0);
-    if constexpr (LNK == 2) {
-      if (wm == 0) bar();  // re-align: the PART epilogue combines waves through LDS behind a barrier
-      gt_epilogue<MT, NTL, false, LNK, BM, WN>(acc, g, m0, n0, wm * WTM, wn * WTN, pscr);
-      if (wm == 1) bar();
-    } else {
-      gt_epilogue<MT, NTL, false, LNK, BM, WN>(acc, g, m0, n0, wm * WTM, wn * WTN, pscr);
-    }
-  }
-  if (nsteps > 0 && wm == 0) bar();  // matches the lagging group's extra barrier
-}
 
 // ---------------------------------------------------------------------------------------------
 // Ping-pong variant (cfg 8 / 9): the 8 waves are two groups of 4 -- group 0 = waves 0-3, group 1 =
@@ -1221,7 +1028,6 @@ GtCfg gt_cfg(int cfg) {
     case 20: return {256, 256, 512};
     case 21: return {192, 192, 512};
     case 22: return {192, 192, 512};
-    case 23: return {256, 256, 512};
     default: return {0, 0, 0};
   }
 }
@@ -1249,7 +1055,7 @@ int gt_launch(const GemmTileArgs& g0, int cfg, int grid_cap, hipStream_t st) {
   int cap = grid_cap > 0 ? grid_cap : gt_num_cus() * per_cu;
   const int ntiles = tiles_m * g.tiles_n;
   // split-K: tile-kernel cfgs only; whole k-steps per split, room for every slab and counter
-  const bool sk_ok = cfg <= 7 || (cfg >= 13 && cfg != 23);
+  const bool sk_ok = cfg <= 7 || cfg >= 13;
   const int bks = cfg == 6 || cfg == 7 ? 32 : 64;
   if (g.splitk < 1) g.splitk = 1;
   if (g.splitk > 1 && (!sk_ok || (g.K / bks) % g.splitk || !g.ws || !g.cnt)) return MLS_BAD_ARG;
@@ -1262,7 +1068,6 @@ int gt_launch(const GemmTileArgs& g0, int cfg, int grid_cap, hipStream_t st) {
     case 16: hipLaunchKernelGGL((gemm_tile_kernel<256, 128, 4, 2, 3, 64, false, true, false, K>), grid, block, 0, st, g); break; \
     case 5: hipLaunchKernelGGL((gemm_tile_kernel<128, 256, 2, 4, 3, 64, false, false, false, K>), grid, block, 0, st, g); break; \
     case 4: hipLaunchKernelGGL((gemm_tile_kernel<128, 128, 2, 2, 3, 64, false, false, false, K>), grid, block, 0, st, g); break; \
-    case 23: hipLaunchKernelGGL((gemm_8p_kernel<K>), grid, block, 0, st, g); break;                                 \
     default: return MLS_BAD_ARG;                                                                                     \
   }
     if (g.fold_c) {
@@ -1296,7 +1101,6 @@ int gt_launch(const GemmTileArgs& g0, int cfg, int grid_cap, hipStream_t st) {
     case 20: hipLaunchKernelGGL((gemm_tile_kernel<256, 256, 2, 4, 2, 64, true, false, true>), grid, block, 0, st, g); break;
     case 21: hipLaunchKernelGGL((gemm_tile_kernel<192, 192, 4, 2, 3, 64>), grid, block, 0, st, g); break;
     case 22: hipLaunchKernelGGL((gemm_tile_kernel<192, 192, 4, 2, 3, 64, false, true>), grid, block, 0, st, g); break;
-    case 23: hipLaunchKernelGGL((gemm_8p_kernel<0>), grid, block, 0, st, g); break;
   }
   return hipGetLastError() == hipSuccess ? MLS_OK : MLS_BAD_ARG;
 }
@@ -1380,7 +1184,7 @@ int mls_gemm_tile_ln(const void* A, const void* W, const float* bias, const void
   if (ab >= 0x7FFFFFFFull || wb >= 0x7FFFFFFFull || (size_t)M * N >= 0x3FFFFFFFull) return MLS_UNSUPPORTED;
   int c = (cfg & 0xFF) > 0 ? (cfg & 0xFF) : gt_pick(M, N);
   switch (c) {
-    case 15: case 16: case 5: case 4: case 23: break;
+    case 15: case 16: case 5: case 4: break;
     case 3: c = 4; break;
     default: c = gt_cfg(c).bn == 128 ? 16 : 15; break;
   }

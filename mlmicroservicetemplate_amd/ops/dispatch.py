@@ -11,14 +11,13 @@ from .gemm_ops import _bias_bf16, gemm, gemm_tile, gemm_tile_ln, silu_mul_interl
 from .tables import small_m_plan_for, tile_cfg_for, tile_route_for
 
 
-# Large-M projections run on the native LDS-DMA MFMA tile kernel (gemm_tile: csrc/gemm_tile.hip),
-# the decode-shaped ones (M <= 32, and 33..TILE_MIN_M - 1 rows) on the skinny / conv_gemm kernels with
-# per-shape plans.  hipBLASLt (torch.addmm; a SiLU-mul runs as the native pass after it) runs only
-# the plain projections (no residual epilogue) the tile table routes to it because it measured faster:
-# the Llama-3-8B TP=1 shapes listed in README.md ("impl": "blas" entries of tuned/gemm_tile_gfx950.json:
-# 512-row QKV / O, the 256-row decode step's O / down / LM head, and every projection from 1024 rows;
-# profiles/r4_llama_prefill_gemm_native_vs_blas.jsonl, r4_dec256_gemm_probe.jsonl).  MLS_GEMM_IMPL=native
-# runs those on the tile kernel too; MLS_GEMM_IMPL=blas sends every plain projection to hipBLASLt.
+# Every projection runs on our own kernels: large M on the LDS-DMA MFMA tile kernel (gemm_tile:
+# csrc/gemm_tile.hip) or, for short-M shapes whose tiles cannot fill the chip, the conv_gemm kernel
+# with in-launch split-K -- per shape as tuned/gemm_tile_gfx950.json measured -- and the decode-shaped
+# ones (M <= 32, and 33..TILE_MIN_M - 1 rows) on the skinny / conv_gemm kernels with per-shape plans.
+# No default path calls a library GEMM (round 6 routed the last nine Llama-3-8B TP=1 shapes that still
+# went to hipBLASLt to their best native config: profiles/r6_gemm_native_routes_probe.jsonl).
+# hipBLASLt (torch.addmm) is reachable only as the explicit A/B arm: MLS_GEMM_IMPL=blas, impl="blas".
 TILE_MIN_M = int(os.environ.get("MLS_TILE_MIN_M", "256"))
 
 
@@ -33,10 +32,9 @@ def linear(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
            impl: str = "auto") -> torch.Tensor:
     """Transformer projection ``act(a @ w.T + bias) (+ residual)``: M >= TILE_MIN_M on the table's
     route -- the persistent LDS-DMA tile kernel (:func:`gemm_tile`, bias / GELU / SiLU-mul / residual
-    in its epilogue) or conv_gemm, and hipBLASLt for the plain Llama-3-8B TP=1 shapes the table routes
-    there (module comment) -- smaller M on the skinny / conv_gemm kernels (measured per-shape plans in
-    ``tuned/gemm_plan_gfx950.json``).  ``impl``: "auto" | "native" (never the library) | "tile" |
-    "blas" (hipBLASLt for everything; also ``MLS_GEMM_IMPL=native`` / ``=blas``)."""
+    in its epilogue) or conv_gemm -- smaller M on the skinny / conv_gemm kernels (measured per-shape
+    plans in ``tuned/gemm_plan_gfx950.json``).  ``impl``: "auto" / "native" (the same: our kernels) |
+    "tile" | "blas" (hipBLASLt, the A/B arm only; also ``MLS_GEMM_IMPL=blas``)."""
     code = _act(act)
     M, K = a.shape
     N = w.shape[0]
@@ -44,16 +42,11 @@ def linear(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         return _linear_blas(a, w, bias, code, residual)
     if impl == "tile" or (impl in ("auto", "native") and M >= TILE_MIN_M and K % 64 == 0 and N % 16 == 0
                           and a.device.type == "cuda" and a.is_contiguous() and w.is_contiguous()):
-        kind, cfg, sk = tile_route_for(M, N, K) if impl == "auto" else ("tile",) + tile_cfg_for(M, N, K)
-        native_only = impl == "native" or (impl == "auto" and _GEMM_IMPL == "native")
-        if kind == "blas" and native_only:
-            kind, (cfg, sk) = "tile", tile_cfg_for(M, N, K)
-        if kind == "blas" and code in (ACT_NONE, ACT_GELU, ACT_SILU_MUL) and residual is None:
-            return _linear_blas(a, w, bias, code, residual)
+        kind, cfg, sk = tile_route_for(M, N, K) if impl in ("auto", "native") else ("tile",) + tile_cfg_for(M, N, K)
         if kind == "conv":
             return gemm(a, w, bias, act=code, residual=residual, workspace=workspace, cfg=cfg, splitk=sk)
         if kind != "tile":
-            cfg, sk = 0, 1  # a library route for a fused epilogue: the tile kernel's own pick
+            cfg, sk = 0, 1  # an unknown route kind (e.g. an old table's "blas"): the tile kernel's own pick
         return gemm_tile(a, w, bias, act=code, residual=residual, cfg=cfg, splitk=sk, workspace=workspace)
     plan = small_m_plan_for(M, N, K) if impl in ("auto", "native") else None
     if plan is not None and plan[0] > 0 and not (code == ACT_SILU_MUL and residual is not None):

@@ -70,7 +70,7 @@ def gemm(
 
 GEMM_TILE_CFGS = {1: (256, 256), 2: (256, 128), 3: (128, 128), 4: (128, 128), 5: (128, 256), 6: (256, 256),
                   7: (256, 128), 8: (256, 256), 9: (256, 128), 10: (256, 256), 11: (256, 256), 12: (256, 128),
-                  15: (256, 256), 16: (256, 128), 21: (192, 192), 22: (192, 192), 23: (256, 256)}
+                  15: (256, 256), 16: (256, 128), 21: (192, 192), 22: (192, 192)}
 
 
 _SPLIT_COUNTERS: Dict[Tuple[int, int], torch.Tensor] = {}
@@ -125,7 +125,7 @@ def gemm_tile(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = N
         if tuple(out.shape) != (M, n_out):
             raise ValueError(f"out must be [M, {n_out}]")
     sk, ws_ptr, ws_elems, cnt_ptr = 1, None, 0, None
-    if splitk > 1 and workspace is not None and (cfg & 0xFF) in GEMM_TILE_CFGS and (cfg & 0xFF) != 23:
+    if splitk > 1 and workspace is not None and (cfg & 0xFF) in GEMM_TILE_CFGS:
         bm, bn = GEMM_TILE_CFGS[cfg & 0xFF]
         bks = 32 if (cfg & 0xFF) in (6, 7) else 64
         tiles = -(-M // bm) * -(-N // bn)

@@ -35,7 +35,7 @@ def load_blas_tuning(path: Optional[str] = None) -> bool:
 @functools.lru_cache(maxsize=None)
 def gemm_plan() -> Dict[Tuple[int, int, int], Tuple[int, int]]:
     """Measured per-shape choices for :func:`linear` (``tuned/gemm_plan_gfx950.json``): exact
-    ``(M, N, K)`` -> ``(cfg, splitk)`` of the native kernel, cfg 0 = hipBLASLt.  ``MLS_GEMM_PLAN=0``
+    ``(M, N, K)`` -> ``(cfg, splitk)`` of the native kernel, cfg 0 = its own heuristic pick.  ``MLS_GEMM_PLAN=0``
     disables it."""
     if os.environ.get("MLS_GEMM_PLAN", "1") == "0":
         return {}
@@ -71,10 +71,10 @@ def tile_cfg_for(M: int, N: int, K: int) -> Tuple[int, int]:
 
 
 def tile_route_for(M: int, N: int, K: int) -> Tuple[str, int, int]:
-    """``(impl, cfg, splitk)`` of a large-M projection: impl "tile" (gemm_tile), "conv" (the conv_gemm
-    kernel, for short-M shapes whose tiles cannot fill the chip) or "blas" (hipBLASLt, a plain GEMM
-    the library measured faster on) -- the table's per-shape winner; a miss runs the tile kernel's
-    own pick (logged once)."""
+    """``(impl, cfg, splitk)`` of a large-M projection: impl "tile" (gemm_tile) or "conv" (the conv_gemm
+    kernel, for short-M shapes whose tiles cannot fill the chip) -- the table's per-shape winner; a
+    miss runs the tile kernel's own pick (logged once).  The shipped table has no library route
+    (tests/test_gemm_tables.py); :func:`ops.linear` runs any other kind on the tile kernel."""
     e = gemm_tile_plan().get((M, N, K))
     if e is not None:
         return e
