@@ -189,13 +189,15 @@ def run_rank(args) -> int:
     args.cu_partition = agreed
     if args.inflight <= 0:
         args.inflight = 4 if args.cu_partition and not args.serial else 5
+    # MLS_BENCH_PRESTAGE=1: the next batch is staged into a spare pinned buffer (GpuEngine.prepare)
+    # while every slot is busy, so a freed slot only waits for the enqueue -- how a server stages
+    # requests as they arrive; the slot's graph pulls it straight from that buffer
+    # (ops.h2d_pull_cell).  Request latency then runs from the start of its staging
+    # (Ticket.t_arrive), not from the launch.  Level at 20 steps, -1 % at 200, p50 +0.27 ms
+    # (profiles/r6_bench_prestage_prepull_ab.jsonl): off by default
+    prestage = os.environ.get("MLS_BENCH_PRESTAGE", "0") == "1"
     # the closed-loop client polls its oldest batch's done event (20 ms bound) instead of sleeping
     # in a blocking sync: s200 56.0k vs 55.2k req/s (profiles/r5_stall_ab_sdma_vs_pull.jsonl)
-    # the next batch is staged into a spare pinned buffer (GpuEngine.prepare) while every slot is
-    # busy, so a freed slot only waits for the enqueue -- how a server stages requests as they
-    # arrive; the slot's graph pulls it straight from that buffer (ops.h2d_pull_cell).  Request
-    # latency then runs from the start of its staging (Ticket.t_arrive), not from the launch.
-    prestage = os.environ.get("MLS_BENCH_PRESTAGE", "0") == "1"
     engine = GpuEngine(fwd, device, (224, 224, 3), torch.uint8, buckets=[args.batch], inflight=args.inflight,
                        use_graphs=not args.no_graphs, name=f"resnet50.r{info.rank}", concurrent=not args.serial,
                        cu_partitions=0 if args.serial else args.cu_partition, spin_wait_us=20000.0)
