@@ -286,7 +286,7 @@ class ContinuousLlama:
         else:
             hdr = (OP_ITER, len(planned), max((len(q.ids) for q in planned), default=0))
         if self._ctl_host is None:
-            self._ctl_host = torch.zeros(CTL_WORDS, dtype=torch.int32, pin_memory=True)
+            self._ctl_host = torch.zeros(CTL_WORDS, dtype=torch.int32, pin_memory=torch.cuda.is_available())
         self._ctl_host.numpy()[:] = [*hdr, ctl_check(self.iterations, *hdr)]
         st["ctl_in"].copy_(self._ctl_host, non_blocking=True)
 
