@@ -153,7 +153,7 @@ def run_rank(args) -> int:
     torch.cuda.set_device(device)
     from mlmicroservicetemplate_amd.parallel.affinity import bind_to_gpu
 
-    bind_to_gpu(device.index, world)  # host staging on the GPU's NUMA node (multi-rank runs)
+    numa_cpus = bind_to_gpu(device.index, world)  # host staging on the GPU's NUMA node
 
     from mlmicroservicetemplate_amd.engine.worker import GpuEngine
     from mlmicroservicetemplate_amd.models import resnet
@@ -209,7 +209,7 @@ def run_rank(args) -> int:
         "backend": args.backend, "hipgraph": not args.no_graphs, "inflight": args.inflight,
         "concurrent_slots": not args.serial, "cu_partitions": cu_parts,
         "partition_mode": (os.environ.get("MLS_CU_PARTITION_MODE", "intra") if cu_parts else "unpartitioned"),
-        "prestage": prestage, "batch": args.batch})
+        "prestage": prestage, "batch": args.batch, "numa_bound": bool(numa_cpus)})
     if not ranks_cfg["ranks_consistent"]:
         print(f"bench: ranks disagree on the engine layout: {ranks_cfg}", file=sys.stderr)
 

@@ -8,8 +8,11 @@ runtime, the node's CPU list from sysfs, and restricts the calling thread (threa
 -- the engine's staging pool -- inherit it) to that list intersected with the CPUs the process
 may use.  Call before allocating pinned memory so first-touch places it on the local node.
 
-``MLS_NUMA_BIND=0`` disables; ``=1`` forces it for single-process runs (default: only with
-several ranks, where it matters).
+``MLS_NUMA_BIND=0`` disables, ``=1`` forces it.  By default every rank binds -- a single-rank
+run too, provided the GPU-local CPUs it may use number at least :data:`SINGLE_RANK_MIN_CPUS` (or
+all it may use), so a small CPU share on the far socket is not shrunk further.  Single-rank A/B
+on one MI355X (profiles/r6_numa_bind_single_rank_ab.jsonl): bound 53.1k vs 52.7k req/s mean over
+5 paired 20-step runs (4 of 5 pairs ahead), 57.1k vs 56.8k at 200 steps.
 
 Host-thread budget: on an 8-GPU node four ranks share each socket's CPUs, and every rank's
 engine would otherwise start 4 staging copy threads regardless (plus the submitting thread, the
@@ -61,6 +64,7 @@ def gpu_local_cpus(pci_addr: str, sysfs_root: str = "/sys") -> Optional[Set[int]
     return cpus or None
 
 
+SINGLE_RANK_MIN_CPUS = 8  # a default single-rank bind keeps at least this many CPUs (or all allowed)
 STAGE_THREADS_CAP = 4  # copy threads that saturate one batch's memcpy (docs/PERF_NOTES.md, round 2)
 # a copy thread's memcpy rate into pinned memory with 8 ranks copying at once: the 8-process CPU
 # staging test measured 3.5-8.7 GB/s per instance (profiles/r4_staging_8_rank_processes_cpu.txt);
@@ -152,7 +156,7 @@ def bind_to_gpu(device_index: int, world_size: int = 1, sysfs_root: str = "/sys"
         logger.info("GPU %d: %d usable CPUs shared by %d local ranks -> %d staging threads (%s)", device_index,
                     len(usable), sharing, _hint, _plan)
     mode = os.environ.get("MLS_NUMA_BIND", "")
-    if mode == "0" or (mode != "1" and world_size <= 1):
+    if mode == "0":
         return None
     addr = pci_addr or (pci_of or pci_address)(device_index)
     if addr is None:
@@ -166,6 +170,10 @@ def bind_to_gpu(device_index: int, world_size: int = 1, sysfs_root: str = "/sys"
         return None
     cpus = sorted(local & allowed)
     if not cpus or set(cpus) == allowed:
+        return None
+    if mode != "1" and world_size <= 1 and len(cpus) < min(SINGLE_RANK_MIN_CPUS, len(allowed)):
+        logger.info("GPU %d: only %d of %d allowed CPUs are local; not binding a single rank", device_index,
+                    len(cpus), len(allowed))
         return None
     try:
         os.sched_setaffinity(0, cpus)

@@ -30,13 +30,38 @@ def test_bind_to_gpu_restricts_and_respects_switches(tmp_path, monkeypatch):
     allowed = sorted(os.sched_getaffinity(0))
     root = _fake_sysfs(tmp_path, "0000:05:00.0", str(allowed[0]))
     monkeypatch.delenv("MLS_NUMA_BIND", raising=False)
-    assert bind_to_gpu(0, world_size=1, sysfs_root=root, pci_addr="0000:05:00.0") is None  # single rank: off
+    # single rank by default: binds only when it keeps enough CPUs (one local CPU of several: no)
+    assert bind_to_gpu(0, world_size=1, sysfs_root=root, pci_addr="0000:05:00.0") is None
     monkeypatch.setenv("MLS_NUMA_BIND", "0")
     assert bind_to_gpu(0, world_size=8, sysfs_root=root, pci_addr="0000:05:00.0") is None
     monkeypatch.delenv("MLS_NUMA_BIND")
     try:
         got = bind_to_gpu(0, world_size=8, sysfs_root=root, pci_addr="0000:05:00.0")
         assert got == [allowed[0]] and sorted(os.sched_getaffinity(0)) == [allowed[0]]
+    finally:
+        os.sched_setaffinity(0, allowed)
+
+
+@pytest.mark.skipif(not hasattr(os, "sched_getaffinity") or len(os.sched_getaffinity(0)) < 2,
+                    reason="needs >= 2 usable CPUs")
+def test_single_rank_binds_by_default_when_enough_cpus_are_local(tmp_path, monkeypatch):
+    from mlmicroservicetemplate_amd.parallel import affinity
+
+    allowed = sorted(os.sched_getaffinity(0))
+    half = allowed[: max(1, len(allowed) // 2)]
+    root = _fake_sysfs(tmp_path, "0000:05:00.0", ",".join(map(str, half)))
+    monkeypatch.delenv("MLS_NUMA_BIND", raising=False)
+    monkeypatch.setattr(affinity, "SINGLE_RANK_MIN_CPUS", len(half))
+    try:
+        assert bind_to_gpu(0, world_size=1, sysfs_root=root, pci_addr="0000:05:00.0") == half
+        assert sorted(os.sched_getaffinity(0)) == half
+    finally:
+        os.sched_setaffinity(0, allowed)
+    monkeypatch.setattr(affinity, "SINGLE_RANK_MIN_CPUS", len(half) + 1)
+    assert bind_to_gpu(0, world_size=1, sysfs_root=root, pci_addr="0000:05:00.0") is None  # too few local
+    monkeypatch.setenv("MLS_NUMA_BIND", "1")  # forced: binds regardless
+    try:
+        assert bind_to_gpu(0, world_size=1, sysfs_root=root, pci_addr="0000:05:00.0") == half
     finally:
         os.sched_setaffinity(0, allowed)
 
