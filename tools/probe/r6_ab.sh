@@ -16,7 +16,7 @@ run_arm() {  # $1 = arm spec, $2 = steps, $3 = warmup
   python3 -c "import json; d=json.load(open('$OUT/b.json')); d['arm']='$name'; print(json.dumps(d))" >> $OUT/bench.jsonl
 }
 for i in $(seq 1 ${ROUNDS:-3}); do
-  for arm in $ARMS; do run_arm "$arm" 20 5 || exit 1; done
+  for arm in $ARMS; do run_arm "$arm" 20 ${WARM:-5} || exit 1; done
 done
 for arm in $ARMS; do run_arm "$arm" 200 20 || exit 1; done
 python3 -c "
