@@ -18,6 +18,25 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def _warm(step, ms):
+    """Run ``step`` until ``ms`` of load have passed (the GPU's clocks ramp up over tens of ms of
+    load after idling: bench.py's warmup floor, docs/PERF_NOTES.md round 6)."""
+    t = time.perf_counter()
+    while (time.perf_counter() - t) * 1e3 < ms:
+        step()
+    torch.cuda.synchronize()
+
+
+def _closed_loop(eng, x, n):
+    pend = []
+    for _ in range(n):
+        pend.append(eng.submit(x))
+        if len(pend) >= eng.inflight:
+            pend.pop(0).wait()
+    for t in pend:
+        t.wait()
+
+
 def bench_bert(args):
     from mlmicroservicetemplate_amd.engine.worker import GpuEngine
     from mlmicroservicetemplate_amd.models import bert
@@ -46,6 +65,7 @@ def bench_bert(args):
                 eng.warmup(capture=True)
                 for _ in range(5):
                     eng.run(packed)
+                _warm(lambda: _closed_loop(eng, packed, 2 * eng.inflight), args.warm_ms)
                 n = args.steps
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
@@ -94,7 +114,7 @@ def bench_llama(args):
         pos = torch.arange(S, device=dev, dtype=torch.int32).unsqueeze(0).expand(B, S).contiguous()
         for _ in range(2):
             m.step(ids, pos, lens, decode=False, k=1)
-        torch.cuda.synchronize()
+        _warm(lambda: (m.step(ids, pos, lens, decode=False, k=1), torch.cuda.synchronize()), args.warm_ms)
         t1 = time.perf_counter()
         for _ in range(3):
             m.step(ids, pos, lens, decode=False, k=1)
@@ -104,7 +124,7 @@ def bench_llama(args):
         cur = lens.view(B, 1).clone()
         for _ in range(3):
             m.decode_step(tok, cur, 1, max_ctx=S + 1)
-        torch.cuda.synchronize()
+        _warm(lambda: (m.decode_step(tok, cur, 1, max_ctx=S + 1), torch.cuda.synchronize()), args.warm_ms)
         t2 = time.perf_counter()
         n = args.steps
         for _ in range(n):
@@ -155,6 +175,7 @@ def main():
     ap.add_argument("--seqs", type=int, nargs="+", default=[128])
     ap.add_argument("--prompt", type=int, default=512)
     ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warm-ms", type=float, default=200.0, help="untimed load before each timed window (0 = off)")
     ap.add_argument("--inflight", type=int, default=5, help="bert: batches in flight (co-running engine slots)")
     ap.add_argument("--backends", nargs="+", default=["fused", "eager"], help="bert: which implementations")
     ap.add_argument("--emulate-tp", type=int, default=1)
