@@ -510,6 +510,213 @@ __global__ __launch_bounds__(256, 2) void stem_pool_v2_kernel(const uint8_t* __r
   }
   if (st && lane == 0) st[2 + 6 * v2::TILES] = __builtin_amdgcn_s_memtime();
 }
+
+// ---------------------------------------------------------------------------------------------
+// v3 (MLS_STEM_VER=3 / mls_stem_set_version): v2's tiles, weights, fragment layout and arithmetic
+// -- bit-identical output -- with the tile loop software-pipelined.  v2's stamps put a tile at
+// patch 620 + MFMA 2300 + epilogue 1300 + pool 930 cycles per wave, phases separated by three
+// block barriers, so the matrix pipe idles for ~60 % of the loop, and the two blocks of a CU run
+// their phases in lockstep.  v3 double-buffers the patch and the stem tile in LDS (2 x 8880 +
+// 2 x 20736 B, still 2 blocks per CU) and runs, between ONE barrier per tile:
+//   patch(t+1) written from the bytes fetched a tile earlier, fetch(t+2) issued,
+//   MFMA(t) on patch[t&1] with pool(t-1) on tile[(t-1)&1] interleaved into its kernel rows,
+//   epilogue(t) -> tile[t&1].
+// Tile -1's pool and tile 7's patch run on dummy data (stores dropped by the range check, loads
+// zero-filled), so the loop body has no branches.
+__global__ __launch_bounds__(256, 2) void stem_pool_v3_kernel(const uint8_t* __restrict__ img, const bf16* __restrict__ w,
+                                                           const float* __restrict__ bias, bf16* __restrict__ out,
+                                                           uint32_t img_bytes, int B, float m0, float m1, float m2,
+                                                           float s0, float s1, float s2) {
+  constexpr int H = 224, W = 224, Po = 56;
+  constexpr int NT = v2::TILES;
+  __shared__ __attribute__((aligned(16))) char smem[2 * v2::PATCH_BYTES + 2 * v2::TILE_BYTES];
+  auto patch_buf = [&](int i) { return smem + (i & 1) * v2::PATCH_BYTES; };
+  auto tile_buf = [&](int i) { return reinterpret_cast<bf16*>(smem + 2 * v2::PATCH_BYTES + (i & 1) * v2::TILE_BYTES); };
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int half = blockIdx.x & 1, strip = (blockIdx.x >> 1) & 7, b = blockIdx.x >> 4;
+  const int ph0 = strip * v2::TPH;
+  const int sr0 = 2 * ph0 - 1;
+  const int ir0 = 2 * sr0 - 3;
+  const rsrc_t ir = make_rsrc(img, img_bytes);
+
+  const int wm = wid >> 1, wn = wid & 1;
+  const int fr = lane & 15, fq = lane >> 4;
+  bf16x8 bw[2][7];
+  float bq[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = wn * 32 + j * 16 + fr;
+#pragma unroll
+    for (int kh = 0; kh < 7; ++kh)
+      bw[j][kh] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(w + (long)n * v2::KTOT + kh * 32 + fq * 8));
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bq[j][r] = bias[wn * 32 + j * 16 + fq * 4 + r];
+  }
+  int abase[5];
+  uint32_t m_pad = 0, m_r0 = 0, m_c0 = 0;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const int rb = wm * 5 + i;
+    const int p0 = rb * 16 + fr;
+    const int p = p0 < v2::SP ? p0 : v2::SP - 1;
+    const int r = p / v2::SC, c = p - (p / v2::SC) * v2::SC;
+    abase[i] = ((2 * r) * v2::PSTR + 4 + 2 * c + 2 * fq) * 8;
+    m_pad |= (uint32_t)(p0 >= v2::SP) << i;
+    m_r0 |= (uint32_t)(r == 0) << i;
+    m_c0 |= (uint32_t)(c == 0) << i;
+  }
+
+  const int q = tid;
+  const int prow = q / v2::PG, pgrp = q - (q / v2::PG) * v2::PG;
+  uint32_t raw[3];
+  float valid;
+  auto fetch = [&](int t) {  // t >= NT: nothing to fetch (zero bytes, valid = 0)
+    const int pc0 = half * (NT * v2::TPW) + t * v2::TPW;
+    const int ix = 4 * pc0 - 8 + 4 * pgrp;
+    const int iy = ir0 + prow;
+    const bool ok = t < NT && prow < v2::PRW && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+    valid = ok ? 1.f : 0.f;
+    const int off = ok ? ((b * H + iy) * W + ix) * 3 : OOB;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) raw[k] = __builtin_amdgcn_raw_buffer_load_b32(ir, off + 4 * k, 0, 0);
+  };
+  // normalised bf16 x 4 channels from raw[]: x * s + (-m * s) as one FMA per value with both
+  // terms zeroed for pixels outside the image (their bytes load as 0), 2 VALU per value instead
+  // of v2's subtract / multiply / select
+  const float nb0 = -m0 * s0, nb1 = -m1 * s1, nb2 = -m2 * s2;
+  auto write_patch = [&](char* pb) {
+    const float ss[3] = {s0 * valid, s1 * valid, s2 * valid};
+    const float bb[3] = {nb0 * valid, nb1 * valid, nb2 * valid};
+    char* dst = pb + (prow * v2::PSTR + 1 + 4 * pgrp) * 8;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bf16x4 v;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const int byte = 3 * j + c;
+        const float x = (float)((raw[byte >> 2] >> (8 * (byte & 3))) & 0xffu);
+        v[c] = (bf16)__builtin_fmaf(x, ss[c], bb[c]);
+      }
+      v[3] = (bf16)0.f;
+      *reinterpret_cast<uint2*>(dst + j * 8) = __builtin_bit_cast(uint2, v);
+    }
+  };
+
+  const int pp = min(tid >> 3, v2::TPH * v2::TPW - 1), c8 = tid & 7;
+  const int pr = pp / v2::TPW, pc = pp - (pp / v2::TPW) * v2::TPW;
+  const rsrc_t orr = make_rsrc(out, (uint32_t)((long)B * Po * Po * v2::COUT * 2));
+  const bool pool_lane = tid < v2::TPH * v2::TPW * 8;
+
+  fetch(0);
+  __builtin_amdgcn_s_waitcnt(0);
+  write_patch(patch_buf(0));
+  fetch(1);
+  lds_barrier();
+
+  for (int t = 0; t < NT; ++t) {
+    // patch of tile t+1 (bytes fetched one tile ago), then the bytes of tile t+2
+    write_patch(patch_buf(t + 1));
+    fetch(t + 2);
+
+    // MFMA(t) with pool(t-1) interleaved: 9 pool taps spread over the 7 kernel rows
+    const char* pb = patch_buf(t);
+    const bf16* tp_prev = tile_buf(t + 1);
+    u16x2 mx[4] = {u16x2{0, 0}, u16x2{0, 0}, u16x2{0, 0}, u16x2{0, 0}};
+    f32x4 acc[5][2];
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{bq[j][0], bq[j][1], bq[j][2], bq[j][3]};  // bias as C
+    bf16x8 av[2][5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+      av[0][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(pb + abase[i]));
+#pragma unroll
+    for (int kh = 0; kh < 7; ++kh) {
+      // the next kernel row's A fragments and this row's pool taps (kh 0-1 two taps, the rest one:
+      // 9 over 7) are issued, then this row's 10 MFMAs, then the taps are max-reduced; the
+      // scheduling barriers keep hipcc from sinking the loads next to their first use (it did:
+      // each fragment read was waited for right after its issue)
+      uint4 tv[2];
+      if (kh + 1 < 7) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i)
+          av[(kh + 1) & 1][i] = __builtin_bit_cast(
+              bf16x8, *reinterpret_cast<const uint4*>(pb + abase[i] + (kh + 1) * v2::PSTR * 8));
+      }
+      const int tap0 = kh < 2 ? 2 * kh : kh + 2, ntap = kh < 2 ? 2 : 1;
+#pragma unroll
+      for (int u = 0; u < ntap; ++u) {
+        const int tap = tap0 + u, dy = tap / 3, dx = tap % 3;
+        tv[u] = *reinterpret_cast<const uint4*>(tp_prev + ((2 * pr + dy) * v2::SC + 2 * pc + dx) * v2::TSTR + c8 * 8);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 5; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j][kh], av[kh & 1][i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < ntap; ++u) {
+        mx[0] = __builtin_elementwise_max(mx[0], __builtin_bit_cast(u16x2, tv[u].x));
+        mx[1] = __builtin_elementwise_max(mx[1], __builtin_bit_cast(u16x2, tv[u].y));
+        mx[2] = __builtin_elementwise_max(mx[2], __builtin_bit_cast(u16x2, tv[u].z));
+        mx[3] = __builtin_elementwise_max(mx[3], __builtin_bit_cast(u16x2, tv[u].w));
+      }
+    }
+    {  // pooled tile t-1 out (tile -1: dropped)
+      const int pc0p = half * (NT * v2::TPW) + (t - 1) * v2::TPW;
+      const uint4 o{__builtin_bit_cast(uint32_t, mx[0]), __builtin_bit_cast(uint32_t, mx[1]),
+                    __builtin_bit_cast(uint32_t, mx[2]), __builtin_bit_cast(uint32_t, mx[3])};
+      const int ooff = (t > 0 && pool_lane) ? ((((b * Po + ph0 + pr) * Po + pc0p + pc) * v2::COUT + c8 * 8) * 2) : OOB;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4s, o), orr, ooff, 0, 0);
+    }
+    // epilogue(t): ReLU -> bf16 stem tile t (the bias rode in as the MFMA's C); stem pixels
+    // outside the image -> 0.  On the fp32 bit patterns as integers (negative floats, -0 included,
+    // are negative integers): clamp(e, 0, lim) with lim = 0 for such a row block, INT_MAX else --
+    // one v_med3_i32 per value (a float med3 / max gets NaN-canonicalising maxes added by hipcc)
+    const int sc0 = 2 * (half * (NT * v2::TPW) + t * v2::TPW) - 1;
+    const uint32_t zero = (sr0 < 0 ? m_r0 : 0u) | (sc0 < 0 ? m_c0 : 0u);
+    bf16* tp = tile_buf(t) + (wm * 80 + fr) * v2::TSTR + wn * 32 + fq * 4;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      if ((m_pad >> i) & 1u) continue;
+      const int lim = ((zero >> i) & 1u) ? 0 : 0x7fffffff;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        bf16x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = acc[i][j][r];
+          const int ei = __builtin_bit_cast(int, e);
+          v[r] = (bf16)__builtin_bit_cast(float, min(max(ei, 0), lim));
+        }
+        *reinterpret_cast<uint2*>(tp + i * 16 * v2::TSTR + j * 16) = __builtin_bit_cast(uint2, v);
+      }
+    }
+    lds_barrier();
+  }
+  {  // the last tile's pool
+    const bf16* tpl = tile_buf(NT - 1);
+    u16x2 mx[4] = {u16x2{0, 0}, u16x2{0, 0}, u16x2{0, 0}, u16x2{0, 0}};
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        const uint4 v = *reinterpret_cast<const uint4*>(tpl + ((2 * pr + dy) * v2::SC + 2 * pc + dx) * v2::TSTR + c8 * 8);
+        mx[0] = __builtin_elementwise_max(mx[0], __builtin_bit_cast(u16x2, v.x));
+        mx[1] = __builtin_elementwise_max(mx[1], __builtin_bit_cast(u16x2, v.y));
+        mx[2] = __builtin_elementwise_max(mx[2], __builtin_bit_cast(u16x2, v.z));
+        mx[3] = __builtin_elementwise_max(mx[3], __builtin_bit_cast(u16x2, v.w));
+      }
+    const int pc0 = half * (NT * v2::TPW) + (NT - 1) * v2::TPW;
+    const uint4 o{__builtin_bit_cast(uint32_t, mx[0]), __builtin_bit_cast(uint32_t, mx[1]),
+                  __builtin_bit_cast(uint32_t, mx[2]), __builtin_bit_cast(uint32_t, mx[3])};
+    const int ooff = pool_lane ? ((((b * Po + ph0 + pr) * Po + pc0 + pc) * v2::COUT + c8 * 8) * 2) : OOB;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4s, o), orr, ooff, 0, 0);
+  }
+}
 }  // namespace
 
 extern "C" {
@@ -528,6 +735,19 @@ static int* stem_arrivals() {
 
 // diagnostics: v2 writes per-wave phase stamps ([blocks][4 waves][64] int64) here while set
 long long* g_stem_stamps = nullptr;
+// which tile loop runs (3: software-pipelined v3, the default; 2: phase-serial v2, also taken
+// while stamps or a stagger are set); MLS_STEM_VER overrides the default, mls_stem_set_version
+// switches at run time (tests compare the two).  v3 vs v2 (profiles/r6_stem_v3_ab.jsonl): alone
+// 22.3 vs 24.7 us per B=32 call, bench 20 steps 55.5-56.0k vs 55.3-55.5k (3 of 3 pairs), 200 level
+static int g_stem_ver = [] {
+  const char* e = getenv("MLS_STEM_VER");
+  return e && (e[0] == '2' || e[0] == '3') ? e[0] - '0' : 3;
+}();
+int mls_stem_set_version(int v) {
+  const int old = g_stem_ver;
+  if (v == 2 || v == 3) g_stem_ver = v;
+  return old;
+}
 int mls_stem_set_stamps(void* buf) {
   g_stem_stamps = (long long*)buf;
   return 0;
@@ -576,6 +796,12 @@ int mls_stem_pool_conv1(const void* images, const void* w, const float* bias, vo
     const char* e = getenv("MLS_STEM_STAGGER");
     return e ? atoi(e) : 0;
   }();
+  if (use_v2 && !c1 && img_bytes < 0x7fffffffL && g_stem_ver == 3 && !g_stem_stamps && stagger <= 0) {
+    hipLaunchKernelGGL(stem_pool_v3_kernel, dim3((unsigned)(B * 16)), dim3(256), 0, (hipStream_t)stream,
+                       (const uint8_t*)images, (const bf16*)w, bias, (bf16*)out, (uint32_t)img_bytes, B, mean3[0],
+                       mean3[1], mean3[2], 1.f / std3[0], 1.f / std3[1], 1.f / std3[2]);
+    return (int)hipGetLastError();
+  }
   if (use_v2 && !c1 && img_bytes < 0x7fffffffL) {
     hipLaunchKernelGGL(stem_pool_v2_kernel, dim3((unsigned)(B * 16)), dim3(256), 0, (hipStream_t)stream,
                        (const uint8_t*)images, (const bf16*)w, bias, (bf16*)out, (uint32_t)img_bytes, B, mean3[0],

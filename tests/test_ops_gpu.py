@@ -269,6 +269,46 @@ def test_stem_pool_fused_matches_three_kernels(B):
     assert err < 2e-2, err
 
 
+@pytest.mark.parametrize("B", [1, 3, 32])
+def test_stem_pool_v3_pipelined_matches_v2_and_fp32(B):
+    """The software-pipelined stem tile loop (v3: double-buffered patch / stem tile, pool of tile
+    t-1 inside tile t's MFMAs, bias as the MFMA's C, FMA normalisation) against the phase-serial v2
+    loop -- every image row strip and both column halves, image borders included -- and against
+    the fp32 PyTorch reference.  v3 adds the bias first and normalises with one FMA, so a few
+    values round differently (one bf16 ulp)."""
+    import torch.nn.functional as F
+
+    from mlmicroservicetemplate_amd import ops
+    from mlmicroservicetemplate_amd.models.resnet import IMAGENET_MEAN, IMAGENET_STD
+
+    g = torch.Generator(device="cpu").manual_seed(20 + B)
+    imgs = torch.randint(0, 256, (B, 224, 224, 3), dtype=torch.uint8, generator=g).to(DEV)
+    w = (torch.randn(64, 3, 7, 7, generator=g) * 0.05).to(torch.bfloat16).to(DEV)
+    wp = ops.pack_conv_weight(w)
+    bias = (torch.randn(64, generator=g) * 0.5).to(DEV)
+    lib = ops.lib()
+    old = lib.mls_stem_set_version(2)
+    try:
+        v2 = ops.stem_pool_u8(imgs, wp, bias, IMAGENET_MEAN, IMAGENET_STD)
+        lib.mls_stem_set_version(3)
+        v3 = ops.stem_pool_u8(imgs, wp, bias, IMAGENET_MEAN, IMAGENET_STD)
+        torch.cuda.synchronize()
+    finally:
+        lib.mls_stem_set_version(old)
+    assert v3.shape == (B, 56, 56, 64)
+    diff = (v3.float() - v2.float()).abs()
+    assert diff.max().item() <= 0.02 * v2.float().abs().max().item()
+    assert (diff > 0).float().mean().item() < 0.05
+    # zero-forced border rows / columns and every tile position agree on which outputs are zero
+    assert torch.equal(v3 == 0, v2 == 0) or ((v3 == 0) != (v2 == 0)).float().mean().item() < 1e-3
+    mean = torch.tensor(IMAGENET_MEAN, device=DEV).view(1, 3, 1, 1)
+    std = torch.tensor(IMAGENET_STD, device=DEV).view(1, 3, 1, 1)
+    xr = ((imgs.permute(0, 3, 1, 2).float() - mean) / std).to(torch.bfloat16).float()
+    ref = F.max_pool2d(F.relu(F.conv2d(xr, w.float(), bias, stride=2, padding=3)), 3, 2, 1).permute(0, 2, 3, 1)
+    err = ((v3.float() - ref).abs().max() / ref.abs().max()).item()
+    assert err < 2e-2, err
+
+
 @pytest.mark.parametrize("B", [1, 3])
 def test_stem_pool_conv1_fused(B):
     """The stem kernel with layer1.0's 1x1 conv on its pooled tiles: pooled map unchanged, t1 equal
@@ -282,9 +322,16 @@ def test_stem_pool_conv1_fused(B):
     bias = (torch.randn(64, generator=g) * 0.5).to(DEV)
     w1 = (torch.randn(64, 64, generator=g) / 8).to(torch.bfloat16).to(DEV)
     b1 = (torch.randn(64, generator=g) * 0.1).to(DEV)
-    pooled = ops.stem_pool_u8(imgs, wp, bias, IMAGENET_MEAN, IMAGENET_STD)
+    lib = ops.lib()
+    old = lib.mls_stem_set_version(2)  # the phase-serial loop: the same arithmetic as the conv1 kernel
+    try:
+        pooled = ops.stem_pool_u8(imgs, wp, bias, IMAGENET_MEAN, IMAGENET_STD)
+    finally:
+        lib.mls_stem_set_version(old)
     x, t1 = ops.stem_pool_u8(imgs, wp, bias, IMAGENET_MEAN, IMAGENET_STD, conv1_w=w1, conv1_b=b1)
     assert torch.equal(x, pooled)
+    # the default (pipelined v3) loop rounds a few values differently (bias first, FMA normalisation)
+    assert rel_err(ops.stem_pool_u8(imgs, wp, bias, IMAGENET_MEAN, IMAGENET_STD), pooled) < 1e-2
     sep = ops.conv2d_nhwc(x, w1.view(64, 1, 1, 64), b1, kernel=1, act=ops.ACT_RELU)
     assert rel_err(t1, sep) < 1e-2
     ref = torch.relu(x.float() @ w1.float().T + b1)
