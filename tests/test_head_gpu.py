@@ -82,6 +82,38 @@ def test_fc_head_error_rows_and_repeat():
         assert torch.isfinite(vals[ok]).all()
 
 
+def test_fc_head_graph_survives_larger_eager_call_on_its_stream():
+    """A graph captured with a small head (engine A) keeps working after a larger head runs eagerly
+    on the SAME stream (engine B warming up on a pooled masked stream): the partial slabs come
+    from each call's own workspace tensor (the graph's from its pool), so nothing the graph
+    captured is freed or re-sized under it (round-5 advisor finding on head_slabs)."""
+    from mlmicroservicetemplate_amd import ops
+
+    g = torch.Generator(device="cpu").manual_seed(7)
+    w = (torch.randn(1000, 2048, generator=g) * 0.03).to(torch.bfloat16).to(DEV)
+    b = (torch.randn(1000, generator=g) * 0.1).to(DEV)
+    small = (torch.rand(8, 2048, generator=g) * 2).to(DEV)
+    src = small.clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        vals0, idx0, lg0 = ops.fc_head(small, w, b, 5)  # eager reference (zeroes `small`)
+        small.copy_(src)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=s):
+            gv, gi, glg = ops.fc_head(small, w, b, 5)
+        small.copy_(src)
+        big = (torch.rand(64, 2048, generator=g) * 2).to(DEV)
+        ops.fc_head(big, w, b, 5)  # a larger eager call on the same stream
+        junk = torch.full((64 * 8 * 1000,), 7.0, device=DEV)  # reuse pressure on freed memory
+        for _ in range(2):
+            small.copy_(src)
+            graph.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(gi, idx0) and torch.equal(glg, lg0)
+        del junk
+
+
 def test_conv2d_pool_matches_fp32():
     from mlmicroservicetemplate_amd import ops
 
