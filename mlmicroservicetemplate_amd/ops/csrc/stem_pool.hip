@@ -315,6 +315,7 @@ constexpr int COUT = 64, KTOT = 7 * 32;
 }  // namespace v2
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef short i16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4s __attribute__((__vector_size__(16)));
 
 __global__ __launch_bounds__(256, 2) void stem_pool_v2_kernel(const uint8_t* __restrict__ img, const bf16* __restrict__ w,
@@ -621,7 +622,7 @@ __global__ __launch_bounds__(256, 2) void stem_pool_v3_kernel(const uint8_t* __r
     // MFMA(t) with pool(t-1) interleaved: 9 pool taps spread over the 7 kernel rows
     const char* pb = patch_buf(t);
     const bf16* tp_prev = tile_buf(t + 1);
-    u16x2 mx[4] = {u16x2{0, 0}, u16x2{0, 0}, u16x2{0, 0}, u16x2{0, 0}};
+    i16x2 mx[4] = {i16x2{0, 0}, i16x2{0, 0}, i16x2{0, 0}, i16x2{0, 0}};
     f32x4 acc[5][2];
 #pragma unroll
     for (int i = 0; i < 5; ++i)
@@ -659,10 +660,10 @@ __global__ __launch_bounds__(256, 2) void stem_pool_v3_kernel(const uint8_t* __r
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int u = 0; u < ntap; ++u) {
-        mx[0] = __builtin_elementwise_max(mx[0], __builtin_bit_cast(u16x2, tv[u].x));
-        mx[1] = __builtin_elementwise_max(mx[1], __builtin_bit_cast(u16x2, tv[u].y));
-        mx[2] = __builtin_elementwise_max(mx[2], __builtin_bit_cast(u16x2, tv[u].z));
-        mx[3] = __builtin_elementwise_max(mx[3], __builtin_bit_cast(u16x2, tv[u].w));
+        mx[0] = __builtin_elementwise_max(mx[0], __builtin_bit_cast(i16x2, tv[u].x));
+        mx[1] = __builtin_elementwise_max(mx[1], __builtin_bit_cast(i16x2, tv[u].y));
+        mx[2] = __builtin_elementwise_max(mx[2], __builtin_bit_cast(i16x2, tv[u].z));
+        mx[3] = __builtin_elementwise_max(mx[3], __builtin_bit_cast(i16x2, tv[u].w));
       }
     }
     {  // pooled tile t-1 out (tile -1: dropped)
@@ -672,43 +673,63 @@ __global__ __launch_bounds__(256, 2) void stem_pool_v3_kernel(const uint8_t* __r
       const int ooff = (t > 0 && pool_lane) ? ((((b * Po + ph0 + pr) * Po + pc0p + pc) * v2::COUT + c8 * 8) * 2) : OOB;
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4s, o), orr, ooff, 0, 0);
     }
-    // epilogue(t): ReLU -> bf16 stem tile t (the bias rode in as the MFMA's C); stem pixels
-    // outside the image -> 0.  On the fp32 bit patterns as integers (negative floats, -0 included,
-    // are negative integers): clamp(e, 0, lim) with lim = 0 for such a row block, INT_MAX else --
-    // one v_med3_i32 per value (a float med3 / max gets NaN-canonicalising maxes added by hipcc)
+    // epilogue(t): pre-activation -> bf16 stem tile t (the bias rode in as the MFMA's C).  The ReLU
+    // is the pool's: a max of bf16 bit patterns as SIGNED 16-bit integers starting from 0 orders
+    // the positive values correctly and sends every negative one (sign bit set) below the 0, so
+    // max(0, taps) = ReLU(max(taps)) = max(ReLU(taps)) -- no per-value op here.  Stem pixels outside
+    // the image (row / column -1, only in the first strip / first tile of a row) are forced to 0.
     const int sc0 = 2 * (half * (NT * v2::TPW) + t * v2::TPW) - 1;
-    const uint32_t zero = (sr0 < 0 ? m_r0 : 0u) | (sc0 < 0 ? m_c0 : 0u);
     bf16* tp = tile_buf(t) + (wm * 80 + fr) * v2::TSTR + wn * 32 + fq * 4;
+    const int wm_u = __builtin_amdgcn_readfirstlane(wm);  // wave-uniform: scalar branches below
+    if (sr0 < 0 || sc0 < 0) {  // block-uniform
+      const uint32_t zero = (sr0 < 0 ? m_r0 : 0u) | (sc0 < 0 ? m_c0 : 0u);
 #pragma unroll
-    for (int i = 0; i < 5; ++i) {
-      if ((m_pad >> i) & 1u) continue;
-      const int lim = ((zero >> i) & 1u) ? 0 : 0x7fffffff;
+      for (int i = 0; i < 5; ++i) {
+        if (i == 4 && wm_u == 1) continue;  // row block 9: past the tile (rows 135-143 of block 8 are
+                                            // written too; the pool never reads them)
+        const int keep = ((zero >> i) & 1u) ? 0 : -1;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        bf16x4 v;
+        for (int j = 0; j < 2; ++j) {
+          bf16x4 v;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float e = acc[i][j][r];
-          const int ei = __builtin_bit_cast(int, e);
-          v[r] = (bf16)__builtin_bit_cast(float, min(max(ei, 0), lim));
+          for (int r = 0; r < 4; ++r) {
+            const float e = acc[i][j][r];
+            v[r] = (bf16)__builtin_bit_cast(float, __builtin_bit_cast(int, e) & keep);
+          }
+          *reinterpret_cast<uint2*>(tp + i * 16 * v2::TSTR + j * 16) = __builtin_bit_cast(uint2, v);
         }
-        *reinterpret_cast<uint2*>(tp + i * 16 * v2::TSTR + j * 16) = __builtin_bit_cast(uint2, v);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        if (i == 4 && wm_u == 1) continue;  // row block 9: past the tile (rows 135-143 of block 8 are
+                                            // written too; the pool never reads them)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          bf16x4 v;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float e = acc[i][j][r];
+            v[r] = (bf16)e;
+          }
+          *reinterpret_cast<uint2*>(tp + i * 16 * v2::TSTR + j * 16) = __builtin_bit_cast(uint2, v);
+        }
       }
     }
     lds_barrier();
   }
   {  // the last tile's pool
     const bf16* tpl = tile_buf(NT - 1);
-    u16x2 mx[4] = {u16x2{0, 0}, u16x2{0, 0}, u16x2{0, 0}, u16x2{0, 0}};
+    i16x2 mx[4] = {i16x2{0, 0}, i16x2{0, 0}, i16x2{0, 0}, i16x2{0, 0}};
 #pragma unroll
     for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
       for (int dx = 0; dx < 3; ++dx) {
         const uint4 v = *reinterpret_cast<const uint4*>(tpl + ((2 * pr + dy) * v2::SC + 2 * pc + dx) * v2::TSTR + c8 * 8);
-        mx[0] = __builtin_elementwise_max(mx[0], __builtin_bit_cast(u16x2, v.x));
-        mx[1] = __builtin_elementwise_max(mx[1], __builtin_bit_cast(u16x2, v.y));
-        mx[2] = __builtin_elementwise_max(mx[2], __builtin_bit_cast(u16x2, v.z));
-        mx[3] = __builtin_elementwise_max(mx[3], __builtin_bit_cast(u16x2, v.w));
+        mx[0] = __builtin_elementwise_max(mx[0], __builtin_bit_cast(i16x2, v.x));
+        mx[1] = __builtin_elementwise_max(mx[1], __builtin_bit_cast(i16x2, v.y));
+        mx[2] = __builtin_elementwise_max(mx[2], __builtin_bit_cast(i16x2, v.z));
+        mx[3] = __builtin_elementwise_max(mx[3], __builtin_bit_cast(i16x2, v.w));
       }
     const int pc0 = half * (NT * v2::TPW) + (NT - 1) * v2::TPW;
     const uint4 o{__builtin_bit_cast(uint32_t, mx[0]), __builtin_bit_cast(uint32_t, mx[1]),
