@@ -554,7 +554,7 @@ __global__ __launch_bounds__(256, 2) void stem_pool_v3_kernel(const uint8_t* __r
     for (int r = 0; r < 4; ++r) bq[j][r] = bias[wn * 32 + j * 16 + fq * 4 + r];
   }
   int abase[5];
-  uint32_t m_pad = 0, m_r0 = 0, m_c0 = 0;
+  uint32_t m_r0 = 0, m_c0 = 0;  // per row block: stem row 0, stem column 0
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
     const int rb = wm * 5 + i;
@@ -562,7 +562,6 @@ __global__ __launch_bounds__(256, 2) void stem_pool_v3_kernel(const uint8_t* __r
     const int p = p0 < v2::SP ? p0 : v2::SP - 1;
     const int r = p / v2::SC, c = p - (p / v2::SC) * v2::SC;
     abase[i] = ((2 * r) * v2::PSTR + 4 + 2 * c + 2 * fq) * 8;
-    m_pad |= (uint32_t)(p0 >= v2::SP) << i;
     m_r0 |= (uint32_t)(r == 0) << i;
     m_c0 |= (uint32_t)(c == 0) << i;
   }
