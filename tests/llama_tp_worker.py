@@ -57,10 +57,15 @@ def serve(m, rank, world, cfg):
     try:
         if rank == 0:
             g = torch.Generator().manual_seed(11)
-            for i in range(6):
+            # SERVE_NREQ requests of SERVE_MAXNEW + (i % SERVE_SPREAD) new tokens each (the TP=8 case
+            # runs 12 of 10-16 tokens through the 4 slots: admissions keep arriving while others decode)
+            nreq, base, spread = (int(os.environ.get(k, d)) for k, d in
+                                  (("SERVE_NREQ", "6"), ("SERVE_MAXNEW", "6"), ("SERVE_SPREAD", "3")))
+            for i in range(nreq):
                 n = int(torch.randint(3, 30, (1,), generator=g))
                 reqs.append((torch.randint(3, cfg.vocab - 1, (n,), generator=g).tolist(),
-                             GenParams(max_new_tokens=6 + i % 3, top_k=[1, 8][i % 2], temperature=0.8, seed=i)))
+                             GenParams(max_new_tokens=base + i % spread, top_k=[1, 8][i % 2], temperature=0.8,
+                                       seed=i)))
             eng.start()
             futs = [eng.submit(ids, gp) for ids, gp in reqs]
             for f in futs:

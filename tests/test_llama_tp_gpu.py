@@ -134,7 +134,7 @@ def test_fused_tp_matches_tp1(tmp_path, world):
 SERVE_CASES = {
     # Llama-3-8B's TP = 8 head split with the one-shot IPC all-reduce: the device-resident serving
     # iterations (one captured graph per decode step incl. the X4 gather + pick)
-    8: (CASES[8][0], dict(CASES[8][1])),
+    8: (CASES[8][0], dict(CASES[8][1], SERVE_NREQ="12", SERVE_MAXNEW="10", SERVE_SPREAD="7")),
     # rank 1 stalls before its first decode iteration past the peers' one-shot wait bound: every
     # request in flight must FAIL (TPCommError), none may return tokens from partial sums
     "stall": (CASES["stall"][0], {k: v for k, v in CASES["stall"][1].items()}),
@@ -182,7 +182,9 @@ def test_tp_serving_continuous_device_path(tmp_path, case):
         assert all(isinstance(x, list) and x for x in results[4:]), results
         assert all(i["car"] == 0 and i["failures"] >= 1 for i in infos), infos
         return
-    assert all(isinstance(x, list) and 1 <= len(x) <= 8 for x in results), results
+    nreq = int(extra_env.get("SERVE_NREQ", "6"))
+    max_new = int(extra_env.get("SERVE_MAXNEW", "6")) + int(extra_env.get("SERVE_SPREAD", "3")) - 1
+    assert len(results) == nreq and all(isinstance(x, list) and 1 <= len(x) <= max_new for x in results), results
     # the served tokens: the same staggered greedy / seeded requests through a TP=1 ContinuousLlama
     # of the same weights must give the same token lists; a list may differ only from a step where
     # TP=1's own decision is within rounding of flipping (teacher-forced, as in the test above)
@@ -196,7 +198,9 @@ def test_tp_serving_continuous_device_path(tmp_path, case):
         t = next((j for j in range(min(len(got), len(want))) if got[j] != want[j]), min(len(got), len(want)))
         robust = _tp1_decision_robust(cfg_kw, ids, gpl, want, t)
         assert not robust, f"request {i}: TP=8 {got} vs TP=1 {want} diverge at a decisive step {t}"
-    assert same >= 3 and robust_steps >= 12, (same, robust_steps, results, ref)
+    # most token lists equal TP=1's outright, and enough decisive steps were compared to mean it
+    assert same >= max(3, nreq // 2) and robust_steps >= max(12, 3 * nreq), (same, robust_steps, results, ref)
+    print(f"TP=8 served tokens: {same} of {nreq} lists equal TP=1's, {robust_steps} decisive steps compared")
     for r, i in enumerate(infos):
         if r and i.get("follower"):  # per-iteration host cost of following rank 0 (X5 header)
             f = i["follower"]
