@@ -85,6 +85,7 @@ _SIGS = {
     "mls_d2h_push": [P, P, _c.c_longlong, I, P],
     "mls_stem_set_stamps": [P],
     "mls_stem_set_version": [I],
+    "mls_flash_set_version": [I],
     "mls_image_decode": [P, P, P, L, I, P, P],
     "mls_decode_pick": [P, P, I, I, I, P, P, P, P, P, P, P, I, P, P, P, P, P],
     "mls_ar_destroy": [P],

@@ -256,6 +256,200 @@ __global__ __launch_bounds__(64 * NW) void flash_fwd_kernel(const AttnArgs a) {
   }
 }
 
+// flash_fwd2_kernel<D>: the prefill kernel with the O accumulator transposed and the per-score VALU cut
+// (Llama prefill, D = 128: the v1 loop issued ~450 VALU + ~170 SALU per wave per 64-key tile against
+// 32 MFMAs -- 193 TFLOP/s at B = 8 x 512, profiles/r6_flash_llama_probe.txt).  Same tiling, loads and
+// LDS layouts as flash_fwd_kernel; per tile and wave:
+//   * O^T += V^T P^T: the PV MFMA with its operands swapped (the V fragment read by ds_read_tr16 is the
+//     A operand's layout as well), so the accumulator holds O[q = lane column][d rows] and the softmax
+//     rescale / final 1 / l are lane-local -- no cross-lane shuffles of alpha or 1 / l;
+//   * the row sum l stays a per-lane partial over the lane's own keys (combined once, at the end);
+//   * scores stay unscaled: the row max is taken raw, one FMA per score forms x * scale - m;
+//     -1e30 instead of -inf for the running max removes every "no key yet" select;
+//   * the key-range / causal mask runs only on the tiles that need it (wave-uniform branch), where
+//     16-key sub-tiles wholly above the diagonal also skip their MFMAs;
+//   * tile load offsets are computed once and advanced by one add per tile.
+template <int D, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 3) void flash_fwd2_kernel(const AttnArgs a) {
+  constexpr int NT = 64 * NW;
+  constexpr int BQ = 16 * NW, BKV = 64;
+  constexpr int CPR = D / 8;
+  constexpr int KK = D / 32;
+  constexpr int DT = D / 16;
+  constexpr int VST = D * 2 + 32;
+  constexpr int K_BYTES = BKV * D * 2;
+  constexpr int V_BYTES = BKV * VST;
+  __shared__ __attribute__((aligned(16))) char smem[K_BYTES + V_BYTES];
+  char* Ks = smem;
+  char* Vs = smem + K_BYTES;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, fr = lane & 15;
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int hk = h / (a.Hq / a.Hkv);
+  const int q0 = blockIdx.x * BQ;
+  const int qw = q0 + wid * 16;
+  MLS_CHECK(!a.kv_lens || a.kv_lens[b] <= a.S, 302);
+  const int L = a.kv_lens ? min(a.kv_lens[b], a.S) : a.S;
+  const long tok0 = (long)b * a.S, tokq = (long)b * a.q_rows;
+
+  const rsrc_t qr = make_rsrc(a.q, a.q_bytes);
+  const rsrc_t kr = make_rsrc(a.k, a.k_bytes);
+  const rsrc_t vr = make_rsrc(a.v, a.v_bytes);
+
+  bf16x8 qf[KK];  // Q^T fragments (B operand of S^T = K Q^T): Q[q = qw + fr][d = 32kk + 8g .. +7]
+  {
+    const int q = qw + fr;
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      const int off = q < a.q_rows ? (int)(((tokq + q) * a.q_stride + (long)h * D + 32 * kk + 8 * g) * 2) : OOB;
+      qf[kk] = __builtin_bit_cast(bf16x8, bload16(qr, off));
+    }
+  }
+
+  f32x4 acc_o[DT];  // acc_o[dt][j] = O[q = qw + fr][d = 16dt + 4g + j] (unnormalised)
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) acc_o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float c = a.scale_log2;
+  float m_run = -1e30f;  // running max of the scaled scores of query fr (log2 units)
+  float l_run = 0.f;     // this lane's partial of the row sum (its own keys only)
+
+  int kv_end = L;
+  if (a.causal) kv_end = min(kv_end, q0 + BQ);
+  const int ntiles = (kv_end + BKV - 1) / BKV;
+
+  constexpr int NI = (BKV * CPR) / NT;
+  static_assert(NI * NT == BKV * CPR, "tile chunks split evenly over the block");
+  int krow[NI], koff[NI], voff[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int idx = tid + NT * i;
+    const int row = idx / CPR, ch = idx % CPR;
+    krow[i] = row;
+    koff[i] = (int)(((tok0 + row) * a.k_stride + (long)hk * D + ch * 8) * 2);
+    voff[i] = (int)(((tok0 + row) * a.v_stride + (long)hk * D + ch * 8) * 2);
+  }
+  const int kstep = BKV * a.k_stride * 2, vstep = BKV * a.v_stride * 2;
+  uint4 kreg[NI], vreg[NI];
+  auto load_tile = [&](int kt) {
+    const int kv0 = kt * BKV;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const bool ok = kv0 + krow[i] < L;
+      kreg[i] = bload16(kr, ok ? koff[i] + kt * kstep : OOB);
+      vreg[i] = bload16(vr, ok ? voff[i] + kt * vstep : OOB);
+    }
+  };
+  if (ntiles > 0) load_tile(0);
+
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int kv0 = kt * BKV;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int idx = tid + NT * i;
+      const int row = idx / CPR, ch = idx % CPR;
+      *reinterpret_cast<uint4*>(Ks + row * (D * 2) + ((ch ^ (row & (CPR - 1))) * 16)) = kreg[i];
+      *reinterpret_cast<uint4*>(Vs + row * VST + ch * 16) = vreg[i];
+    }
+    __syncthreads();
+    if (kt + 1 < ntiles) load_tile(kt + 1);
+
+    // keys kv0 + 16t + 4g + j against query qw + fr; a mask only where the tile crosses the key
+    // range end or (causal) the wave's diagonal
+    const bool edge = kv0 + BKV > L || (a.causal && kv0 + BKV - 1 > qw);
+    f32x4 s[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      // a causal sub-tile wholly above the wave's diagonal: no MFMAs (masked to -inf below)
+      if (a.causal && kv0 + 16 * t > qw + 15) continue;
+      const int row = 16 * t + fr;
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        const int ch = 4 * kk + g;
+        const bf16x8 kf = __builtin_bit_cast(
+            bf16x8, *reinterpret_cast<const uint4*>(Ks + row * (D * 2) + ((ch ^ (row & (CPR - 1))) * 16)));
+        s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[kk], s[t], 0, 0, 0);
+      }
+    }
+    if (edge) {
+      const int qabs = qw + fr;
+      const int lim = a.causal ? min(L - 1, qabs) : L - 1;  // last visible key of this query
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (kv0 + 16 * t + 4 * g + j > lim) s[t][j] = -INFINITY;
+    }
+    float mt = fmaxf(fmaxf(fmaxf(s[0][0], s[0][1]), fmaxf(s[0][2], s[0][3])),
+                     fmaxf(fmaxf(s[1][0], s[1][1]), fmaxf(s[1][2], s[1][3])));
+    mt = fmaxf(mt, fmaxf(fmaxf(fmaxf(s[2][0], s[2][1]), fmaxf(s[2][2], s[2][3])),
+                         fmaxf(fmaxf(s[3][0], s[3][1]), fmaxf(s[3][2], s[3][3]))));
+    mt = fmaxf(mt, xor16_f(mt));
+    mt = fmaxf(mt, xor32_f(mt));
+    const float m_new = fmaxf(m_run, mt * c);  // -inf * c stays -inf; m_run >= -1e30
+    const float alpha = fast_exp2(m_run - m_new);
+    m_run = m_new;
+    float ls = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float p = fast_exp2(fmaf(s[t][j], c, -m_new));  // masked: exp2(-inf) = 0
+        s[t][j] = p;
+        ls += p;
+      }
+    l_run = fmaf(l_run, alpha, ls);
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) acc_o[dt] *= alpha;
+    // ---- O^T += V^T P^T: two 32-key k-steps, key order permuted identically in both operands ----
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      if (a.causal && kv0 + 32 * st > qw + 15) continue;  // both sub-tiles above the diagonal
+      bf16x8 pf;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pf[j] = (bf16)s[2 * st][j];
+        pf[4 + j] = (bf16)s[2 * st + 1][j];
+      }
+      const int qq = fr >> 2, pp = fr & 3;
+      const int row0 = 32 * st + 4 * g + qq;
+      const int row1 = row0 + 16;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const int colb = (16 * dt + 4 * pp) * 2;
+        const short4v r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS short4v*)(Vs + row0 * VST + colb));
+        const short4v r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS short4v*)(Vs + row1 * VST + colb));
+        typedef short short8v __attribute__((ext_vector_type(8)));
+        const short8v vv = {r0[0], r0[1], r0[2], r0[3], r1[0], r1[1], r1[2], r1[3]};
+        acc_o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pf, acc_o[dt], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- normalise (lane-local 1 / l of query fr) and store through LDS as 16-B row stores
+  float l = l_run + xor16_f(l_run);
+  l += xor32_f(l);
+  const float inv_l = l > 0.f ? 1.f / l : 0.f;
+  bf16* Os = reinterpret_cast<bf16*>(smem) + wid * 16 * D;  // the K tile's space: past the last barrier
+  static_assert(NW * 16 * D * 2 <= K_BYTES, "output tiles fit the K tile");
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+    bf16x4 o4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o4[j] = (bf16)(acc_o[dt][j] * inv_l);
+    *reinterpret_cast<bf16x4*>(Os + fr * D + 16 * dt + 4 * g) = o4;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int cc = lane; cc < 16 * CPR; cc += 64) {
+    const int r = cc / CPR, ch = cc % CPR;
+    const int q = qw + r;
+    if (q < a.q_rows) st16(a.o + (tokq + q) * a.o_stride + (long)h * D + ch * 8, ld16(Os + r * D + ch * 8));
+  }
+}
+
 // ------------------------------------------------------------------------------- decode
 struct DecodeArgs {
   const bf16* q;   // [B][q_stride], head h at h*D (rope mode: the fused QKV row, K at Hq*D, V at (Hq+Hkv)*D)
@@ -819,7 +1013,20 @@ __global__ __launch_bounds__(D) void decode_combine_kernel(const DecodeArgs a, i
 
 }  // namespace
 
+// D = 128 (Llama prefill): 2 = the transposed-O kernel (default), 1 = the v1 loop (A/B; MLS_FLASH_V)
+static int g_flash_ver = [] {
+  const char* e = getenv("MLS_FLASH_V");
+  return e ? atoi(e) : 2;
+}();
+
 extern "C" {
+
+int mls_flash_set_version(int v) {  // returns the previous version
+  if (v != 1 && v != 2) return MLS_BAD_ARG;
+  const int old = g_flash_ver;
+  g_flash_ver = v;
+  return old;
+}
 
 // q/k/v point at the first element of head 0 of token 0; strides are token-row strides.  q_rows:
 // query (and output) rows per sequence -- S for full attention; fewer = the first q_rows positions
@@ -871,6 +1078,8 @@ int mls_flash_attention_rows(const void* q, const void* k, const void* v, void* 
   dim3 grid((q_rows + 63) / 64, Hq, B);
   if (D == 64)
     hipLaunchKernelGGL(flash_fwd_kernel<64>, grid, dim3(256), 0, (hipStream_t)stream, a);
+  else if (D == 128 && g_flash_ver == 2)
+    hipLaunchKernelGGL(flash_fwd2_kernel<128>, grid, dim3(256), 0, (hipStream_t)stream, a);
   else if (D == 128)
     hipLaunchKernelGGL(flash_fwd_kernel<128>, grid, dim3(256), 0, (hipStream_t)stream, a);
   else

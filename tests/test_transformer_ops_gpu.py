@@ -191,6 +191,40 @@ def test_decode_attention_8k_context(ops, impl, chunk):
     assert not cnt.any()
 
 
+@pytest.mark.parametrize("cfg", [
+    # B, S, Hq, Hkv, causal, lens, spike row
+    (8, 512, 32, 8, True, None, None),          # Llama-3-8B TP = 1 prefill shape
+    (2, 200, 8, 2, True, [200, 77], 150),       # partial last tile, padded sequence, late spike
+    (3, 130, 4, 1, False, [130, 64, 1], 100),   # bidirectional, lens at a tile edge / one key
+    (1, 70, 4, 4, True, None, 3),               # early spike, then tiles that must not rescale it away
+])
+def test_flash_attention_v2_matches_v1_and_fp32(ops, cfg):
+    """The D = 128 transposed-O prefill kernel (csrc/attention.hip flash_fwd2_kernel: lane-local
+    rescale, per-lane row-sum partials, masks only on edge tiles, causal sub-tiles skipped) vs the
+    v1 kernel and the fp32 reference."""
+    B, S, Hq, Hkv, causal, lens, spike = cfg
+    D = 128
+    torch.manual_seed(8)
+    qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device=DEV)
+    if spike is not None:  # one key aligned with every query: the running max jumps at that tile
+        qkv[spike, Hq * D: (Hq + Hkv) * D] = qkv[:, :D].mean(0).repeat(Hkv) * 40
+    qkv = qkv.to(torch.bfloat16)
+    kv_lens = torch.tensor(lens, device=DEV, dtype=torch.int32) if lens else None
+    lib = ops.lib()
+    old = lib.mls_flash_set_version(1)
+    try:
+        v1 = ops.flash_attention(qkv, B, S, Hq, Hkv, D, kv_lens=kv_lens, causal=causal)
+        lib.mls_flash_set_version(2)
+        v2 = ops.flash_attention(qkv, B, S, Hq, Hkv, D, kv_lens=kv_lens, causal=causal)
+        torch.cuda.synchronize()
+    finally:
+        lib.mls_flash_set_version(old)
+    ref = R.attention(qkv, B, S, Hq, Hkv, D, kv_lens=kv_lens, causal=causal)
+    assert torch.isfinite(v2.float()).all()
+    assert rel(v2, ref) < 2e-2
+    assert rel(v2, v1) < 2e-2
+
+
 def test_flash_attention_8k_causal(ops):
     """Causal prefill of an 8192-token prompt with the TP = 8 rank's head split."""
     torch.manual_seed(7)
