@@ -269,6 +269,9 @@ __global__ __launch_bounds__(64 * NW) void flash_fwd_kernel(const AttnArgs a) {
 //   * the key-range / causal mask runs only on the tiles that need it (wave-uniform branch), where
 //     16-key sub-tiles wholly above the diagonal also skip their MFMAs;
 //   * tile load offsets are computed once and advanced by one add per tile.
+// One tile body with wave-uniform branches, 158 VGPRs: 3 waves per SIMD.  (Full and edge tiles as
+// two straight-line copies of the body took 196 VGPRs -- 2 waves per SIMD -- and measured 71-73 vs
+// 62 us at B = 8 x 512: profiles/r6_flash_v2_vs_v1.jsonl.)
 template <int D, int NW = 4>
 __global__ __launch_bounds__(64 * NW, 3) void flash_fwd2_kernel(const AttnArgs a) {
   constexpr int NT = 64 * NW;
@@ -340,29 +343,14 @@ __global__ __launch_bounds__(64 * NW, 3) void flash_fwd2_kernel(const AttnArgs a
       vreg[i] = bload16(vr, ok ? voff[i] + kt * vstep : OOB);
     }
   };
-  if (ntiles > 0) load_tile(0);
-
-  for (int kt = 0; kt < ntiles; ++kt) {
-    const int kv0 = kt * BKV;
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const int idx = tid + NT * i;
-      const int row = idx / CPR, ch = idx % CPR;
-      *reinterpret_cast<uint4*>(Ks + row * (D * 2) + ((ch ^ (row & (CPR - 1))) * 16)) = kreg[i];
-      *reinterpret_cast<uint4*>(Vs + row * VST + ch * 16) = vreg[i];
-    }
-    __syncthreads();
-    if (kt + 1 < ntiles) load_tile(kt + 1);
-
-    // keys kv0 + 16t + 4g + j against query qw + fr; a mask only where the tile crosses the key
-    // range end or (causal) the wave's diagonal
-    const bool edge = kv0 + BKV > L || (a.causal && kv0 + BKV - 1 > qw);
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  auto tile_body = [&](int kv0, bool EDGE) {
     f32x4 s[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
       // a causal sub-tile wholly above the wave's diagonal: no MFMAs (masked to -inf below)
-      if (a.causal && kv0 + 16 * t > qw + 15) continue;
+      if (EDGE && a.causal && kv0 + 16 * t > qw + 15) continue;
       const int row = 16 * t + fr;
 #pragma unroll
       for (int kk = 0; kk < KK; ++kk) {
@@ -372,7 +360,7 @@ __global__ __launch_bounds__(64 * NW, 3) void flash_fwd2_kernel(const AttnArgs a
         s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[kk], s[t], 0, 0, 0);
       }
     }
-    if (edge) {
+    if (EDGE) {
       const int qabs = qw + fr;
       const int lim = a.causal ? min(L - 1, qabs) : L - 1;  // last visible key of this query
 #pragma unroll
@@ -390,22 +378,27 @@ __global__ __launch_bounds__(64 * NW, 3) void flash_fwd2_kernel(const AttnArgs a
     const float m_new = fmaxf(m_run, mt * c);  // -inf * c stays -inf; m_run >= -1e30
     const float alpha = fast_exp2(m_run - m_new);
     m_run = m_new;
-    float ls = 0.f;
+    // x * scale - m as packed FMAs (v_pk_fma_f32), two scores per instruction
+    const f32x2 c2 = {c, c}, nm2 = {-m_new, -m_new};
+    f32x2 ls2 = {0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float p = fast_exp2(fmaf(s[t][j], c, -m_new));  // masked: exp2(-inf) = 0
-        s[t][j] = p;
-        ls += p;
+      for (int jj = 0; jj < 2; ++jj) {
+        f32x2 x = {s[t][2 * jj], s[t][2 * jj + 1]};
+        x = __builtin_elementwise_fma(x, c2, nm2);
+        const f32x2 p = {fast_exp2(x[0]), fast_exp2(x[1])};  // masked: exp2(-inf) = 0
+        s[t][2 * jj] = p[0];
+        s[t][2 * jj + 1] = p[1];
+        ls2 += p;
       }
-    l_run = fmaf(l_run, alpha, ls);
+    l_run = fmaf(l_run, alpha, ls2[0] + ls2[1]);
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) acc_o[dt] *= alpha;
     // ---- O^T += V^T P^T: two 32-key k-steps, key order permuted identically in both operands ----
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
-      if (a.causal && kv0 + 32 * st > qw + 15) continue;  // both sub-tiles above the diagonal
+      if (EDGE && a.causal && kv0 + 32 * st > qw + 15) continue;  // both sub-tiles above the diagonal
       bf16x8 pf;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -425,6 +418,24 @@ __global__ __launch_bounds__(64 * NW, 3) void flash_fwd2_kernel(const AttnArgs a
         acc_o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vv), pf, acc_o[dt], 0, 0, 0);
       }
     }
+  };
+  if (ntiles > 0) load_tile(0);
+
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int kv0 = kt * BKV;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int idx = tid + NT * i;
+      const int row = idx / CPR, ch = idx % CPR;
+      *reinterpret_cast<uint4*>(Ks + row * (D * 2) + ((ch ^ (row & (CPR - 1))) * 16)) = kreg[i];
+      *reinterpret_cast<uint4*>(Vs + row * VST + ch * 16) = vreg[i];
+    }
+    __syncthreads();
+    if (kt + 1 < ntiles) load_tile(kt + 1);
+
+    // keys kv0 + 16t + 4g + j against query qw + fr; the mask (and the causal sub-tile skip) only
+    // where the tile crosses the key range end or the wave's diagonal
+    tile_body(kv0, kv0 + BKV > L || (a.causal && kv0 + BKV - 1 > qw));
     __syncthreads();
   }
 
@@ -432,21 +443,23 @@ __global__ __launch_bounds__(64 * NW, 3) void flash_fwd2_kernel(const AttnArgs a
   float l = l_run + xor16_f(l_run);
   l += xor32_f(l);
   const float inv_l = l > 0.f ? 1.f / l : 0.f;
-  bf16* Os = reinterpret_cast<bf16*>(smem) + wid * 16 * D;  // the K tile's space: past the last barrier
-  static_assert(NW * 16 * D * 2 <= K_BYTES, "output tiles fit the K tile");
+  // rows padded by 16 B: the 16 query rows of one 8-B write land in different banks
+  constexpr int OST = D + 8;
+  bf16* Os = reinterpret_cast<bf16*>(smem) + wid * 16 * OST;  // K / V tile space: past the last barrier
+  static_assert(NW * 16 * OST * 2 <= K_BYTES + V_BYTES, "output tiles fit the K / V tiles");
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) {
     bf16x4 o4;
 #pragma unroll
     for (int j = 0; j < 4; ++j) o4[j] = (bf16)(acc_o[dt][j] * inv_l);
-    *reinterpret_cast<bf16x4*>(Os + fr * D + 16 * dt + 4 * g) = o4;
+    *reinterpret_cast<bf16x4*>(Os + fr * OST + 16 * dt + 4 * g) = o4;
   }
   __syncthreads();
 #pragma unroll
   for (int cc = lane; cc < 16 * CPR; cc += 64) {
     const int r = cc / CPR, ch = cc % CPR;
     const int q = qw + r;
-    if (q < a.q_rows) st16(a.o + (tokq + q) * a.o_stride + (long)h * D + ch * 8, ld16(Os + r * D + ch * 8));
+    if (q < a.q_rows) st16(a.o + (tokq + q) * a.o_stride + (long)h * D + ch * 8, ld16(Os + r * OST + ch * 8));
   }
 }
 
