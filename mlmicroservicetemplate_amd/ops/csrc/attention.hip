@@ -273,7 +273,7 @@ __global__ __launch_bounds__(64 * NW) void flash_fwd_kernel(const AttnArgs a) {
 // two straight-line copies of the body took 196 VGPRs -- 2 waves per SIMD -- and measured 71-73 vs
 // 62 us at B = 8 x 512: profiles/r6_flash_v2_vs_v1.jsonl.)
 template <int D, int NW = 4>
-__global__ __launch_bounds__(64 * NW, 3) void flash_fwd2_kernel(const AttnArgs a) {
+__global__ __launch_bounds__(64 * NW, NW == 8 ? 2 : 3) void flash_fwd2_kernel(const AttnArgs a) {
   constexpr int NT = 64 * NW;
   constexpr int BQ = 16 * NW, BKV = 64;
   constexpr int CPR = D / 8;
@@ -334,13 +334,13 @@ __global__ __launch_bounds__(64 * NW, 3) void flash_fwd2_kernel(const AttnArgs a
   }
   const int kstep = BKV * a.k_stride * 2, vstep = BKV * a.v_stride * 2;
   uint4 kreg[NI], vreg[NI];
-  auto load_tile = [&](int kt) {
+  auto load_into = [&](int kt, uint4 (&kd)[NI], uint4 (&vd)[NI]) {
     const int kv0 = kt * BKV;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const bool ok = kv0 + krow[i] < L;
-      kreg[i] = bload16(kr, ok ? koff[i] + kt * kstep : OOB);
-      vreg[i] = bload16(vr, ok ? voff[i] + kt * vstep : OOB);
+      kd[i] = bload16(kr, ok ? koff[i] + kt * kstep : OOB);
+      vd[i] = bload16(vr, ok ? voff[i] + kt * vstep : OOB);
     }
   };
   typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -419,7 +419,11 @@ __global__ __launch_bounds__(64 * NW, 3) void flash_fwd2_kernel(const AttnArgs a
       }
     }
   };
-  if (ntiles > 0) load_tile(0);
+  // 8-wave blocks (BERT, S <= 128: two tiles): tile 1's loads go out right behind tile 0's, as in v1
+  const bool pre = NW == 8 && a.pre;
+  uint4 kpre[NI], vpre[NI];
+  if (ntiles > 0) load_into(0, kreg, vreg);
+  if (pre && ntiles > 1) load_into(1, kpre, vpre);
 
   for (int kt = 0; kt < ntiles; ++kt) {
     const int kv0 = kt * BKV;
@@ -431,7 +435,17 @@ __global__ __launch_bounds__(64 * NW, 3) void flash_fwd2_kernel(const AttnArgs a
       *reinterpret_cast<uint4*>(Vs + row * VST + ch * 16) = vreg[i];
     }
     __syncthreads();
-    if (kt + 1 < ntiles) load_tile(kt + 1);
+    if (kt + 1 < ntiles) {
+      if (pre && kt == 0) {
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+          kreg[i] = kpre[i];
+          vreg[i] = vpre[i];
+        }
+      } else {
+        load_into(kt + 1, kreg, vreg);
+      }
+    }
 
     // keys kv0 + 16t + 4g + j against query qw + fr; the mask (and the causal sub-tile skip) only
     // where the tile crosses the key range end or the wave's diagonal
@@ -1085,7 +1099,10 @@ int mls_flash_attention_rows(const void* q, const void* k, const void* v, void* 
     return e ? atoi(e) : 8;
   }();
   if (D == 64 && q_rows > 64 && q_rows <= 128 && nw_env == 8) {
-    hipLaunchKernelGGL((flash_fwd_kernel<64, 8>), dim3(1, Hq, B), dim3(512), 0, (hipStream_t)stream, a);
+    if (g_flash_ver == 2)
+      hipLaunchKernelGGL((flash_fwd2_kernel<64, 8>), dim3(1, Hq, B), dim3(512), 0, (hipStream_t)stream, a);
+    else
+      hipLaunchKernelGGL((flash_fwd_kernel<64, 8>), dim3(1, Hq, B), dim3(512), 0, (hipStream_t)stream, a);
     return (int)hipGetLastError();
   }
   dim3 grid((q_rows + 63) / 64, Hq, B);

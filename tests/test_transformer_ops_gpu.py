@@ -192,18 +192,20 @@ def test_decode_attention_8k_context(ops, impl, chunk):
 
 
 @pytest.mark.parametrize("cfg", [
-    # B, S, Hq, Hkv, causal, lens, spike row
-    (8, 512, 32, 8, True, None, None),          # Llama-3-8B TP = 1 prefill shape
-    (2, 200, 8, 2, True, [200, 77], 150),       # partial last tile, padded sequence, late spike
-    (3, 130, 4, 1, False, [130, 64, 1], 100),   # bidirectional, lens at a tile edge / one key
-    (1, 70, 4, 4, True, None, 3),               # early spike, then tiles that must not rescale it away
+    # B, S, Hq, Hkv, D, causal, lens, spike row
+    (8, 512, 32, 8, 128, True, None, None),          # Llama-3-8B TP = 1 prefill shape
+    (2, 200, 8, 2, 128, True, [200, 77], 150),       # partial last tile, padded sequence, late spike
+    (3, 130, 4, 1, 128, False, [130, 64, 1], 100),   # bidirectional, lens at a tile edge / one key
+    (1, 70, 4, 4, 128, True, None, 3),               # early spike, then tiles that must not rescale it away
+    (32, 128, 12, 12, 64, False, None, None),        # BERT-base: one 8-wave block per (sequence, head)
+    (4, 128, 12, 12, 64, False, [1, 64, 65, 127], 100),  # 8-wave block: lens at the tile edges
+    (2, 100, 4, 2, 64, True, None, 50),              # 8-wave block, causal + GQA
 ])
 def test_flash_attention_v2_matches_v1_and_fp32(ops, cfg):
-    """The D = 128 transposed-O prefill kernel (csrc/attention.hip flash_fwd2_kernel: lane-local
-    rescale, per-lane row-sum partials, masks only on edge tiles, causal sub-tiles skipped) vs the
-    v1 kernel and the fp32 reference."""
-    B, S, Hq, Hkv, causal, lens, spike = cfg
-    D = 128
+    """The transposed-O prefill kernel (csrc/attention.hip flash_fwd2_kernel: lane-local rescale,
+    per-lane row-sum partials, masks only on edge tiles, causal sub-tiles skipped; D = 128 4-wave
+    and BERT's D = 64 8-wave blocks) vs the v1 kernel and the fp32 reference."""
+    B, S, Hq, Hkv, D, causal, lens, spike = cfg
     torch.manual_seed(8)
     qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device=DEV)
     if spike is not None:  # one key aligned with every query: the running max jumps at that tile
