@@ -222,6 +222,18 @@ def run_rank(args) -> int:
     events: list = []
 
 
+    # MLS_BENCH_WAIT_ANY=1: refill from whichever in-flight batch completes first (polling their
+    # done events) instead of the oldest -- how a server's batcher refills a freed slot
+    wait_any = os.environ.get("MLS_BENCH_WAIT_ANY", "0") == "1"
+
+    def oldest_or_first_done(pending):
+        if not wait_any:
+            return 0
+        while True:
+            for k, t in enumerate(pending):
+                if t.slot.ev_done.query():
+                    return k
+
     def run_steps(n, lat):
         pending = []
         nxt = engine.prepare(pool[0]) if prestage and n else None
@@ -235,7 +247,7 @@ def run_rank(args) -> int:
                 pending.append(engine.submit(pool[i % len(pool)]))
             host_s[0] += time.perf_counter() - t0
             if len(pending) >= args.inflight:
-                t = pending.pop(0)
+                t = pending.pop(oldest_or_first_done(pending))
                 t.wait()
                 lat.append(time.perf_counter() - t.t_arrive)
                 events.append((t.t_arrive, time.perf_counter(), getattr(t, "stamps", None),
