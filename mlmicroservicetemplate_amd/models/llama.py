@@ -459,6 +459,9 @@ class LlamaTP:
             self.packed: Dict[str, torch.Tensor] = {}
             self.pk_variant = int(os.environ.get("MLS_PACKED_VARIANT", "9"))
             self.pk_fold = os.environ.get("MLS_PACKED_FOLD", "1") == "1"
+            # prefill at TP = 1 with the residual add in the o / down GEMM epilogues too (the
+            # following RMSNorm then reads one stream and writes one: 64 instead of 128 B per element)
+            self.prefill_fold = os.environ.get("MLS_PREFILL_FOLD", "0") == "1"
             self.ar_fuse = os.environ.get("MLS_AR_FUSE", "1") == "1"  # GEMM-fused TP all-reduce (decode)
             self.ar_fused_calls = 0  # projections issued with the fused all-reduce (eager + captured)
             self.fuse_combine = os.environ.get("MLS_FUSE_COMBINE", "1") == "1"
@@ -661,7 +664,7 @@ class LlamaTP:
         # TP = 1: the residual add rides in the o / down epilogues (h = r + a Wo^T, r' = h + g Wd^T), so
         # the next pre-norm GEMM reads one activation stream instead of two (r + delta) and writes no
         # residual copy.  With TP > 1 the add has to wait for the all-reduce.
-        fold = self.tp == 1 and bool(packed) and self.pk_fold
+        fold = self.tp == 1 and ((bool(packed) and self.pk_fold) or (not decode and getattr(self, "prefill_fold", False)))
         # decode: the o-projection merges the split-KV partials in its prologue (one launch instead of
         # two) while every block's share of partials is small -- B x local q heads <= 32: one emulated
         # TP = 8 rank 1.166 -> 1.125 ms/token at batch 1, 1.294 -> 1.254 at 4; TP = 1 batch 1 level,
