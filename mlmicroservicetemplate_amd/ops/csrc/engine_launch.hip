@@ -7,6 +7,7 @@
 // time that delays every refill of a freed slot and the whole first wave of the bench's window.
 #include "common.h"
 
+#include <cstdlib>
 #include <time.h>
 
 typedef unsigned int u32x4v_e __attribute__((__vector_size__(16)));
@@ -50,7 +51,9 @@ __global__ __launch_bounds__(256) void h2d_pull_kernel(const void* src, void* ds
 // a device-to-device copy by all of the workgroups -- PCIe sets the host pull's ~90 us with 8 of
 // them, HBM wants more.  The cell is read with system-scope loads (no cache may hold the previous
 // launch's words) and made wave-uniform for the buffer descriptor.
-template <int U>
+// SA: cache-policy bits of the device-side stores (0 = default; 2 = nt: stream past the L2 the
+// co-running batches' convolutions work out of -- MLS_PULL_STORE_AUX, an A/B knob)
+template <int U, int SA = 0>
 __global__ __launch_bounds__(256) void h2d_pull_cell_kernel(const unsigned long long* src_cell, void* dst,
                                                             uint32_t bytes) {
   const unsigned long long a = __hip_atomic_load(src_cell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -72,9 +75,17 @@ __global__ __launch_bounds__(256) void h2d_pull_cell_kernel(const unsigned long 
       v[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(s, off + u * stride, 0, 2));  // nt
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v_e, v[u]), d, off + u * stride, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v_e, v[u]), d, off + u * stride, 0, SA);
     off += U * stride;
   }
+}
+
+static int pull_store_aux() {
+  static const int v = [] {
+    const char* e = getenv("MLS_PULL_STORE_AUX");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
 }
 
 extern "C" {
@@ -88,8 +99,16 @@ int mls_h2d_pull_cell(const void* src_cell, void* dst, long long bytes, int bloc
   if (!src_cell || !dst || bytes <= 0 || bytes % 16 || bytes >= (1LL << 30) || blocks <= 0 || blocks > 1024)
     return MLS_BAD_ARG;
   constexpr int U = 8;
-  hipLaunchKernelGGL(h2d_pull_cell_kernel<U>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
-                     (const unsigned long long*)src_cell, dst, (uint32_t)bytes);
+  const int sa = pull_store_aux();
+  if (sa == 2)
+    hipLaunchKernelGGL((h2d_pull_cell_kernel<U, 2>), dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                       (const unsigned long long*)src_cell, dst, (uint32_t)bytes);
+  else if (sa == 3)
+    hipLaunchKernelGGL((h2d_pull_cell_kernel<U, 3>), dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                       (const unsigned long long*)src_cell, dst, (uint32_t)bytes);
+  else
+    hipLaunchKernelGGL(h2d_pull_cell_kernel<U>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                       (const unsigned long long*)src_cell, dst, (uint32_t)bytes);
   return (int)hipGetLastError();
 }
 

@@ -87,10 +87,25 @@ def main():
     g0, g1 = build(False), build(True)  # (their eager warm-up allocates the per-stream head scratch)
     ga, gb = build_fwd(xs), build_fwd(xs2)
 
+    # SYNC=event (default): side stream + event waits; none: no waits (timing only); same: the pull
+    # on the slot's own stream after its graph (in-order, no cross-stream dependency)
+    SYNC = os.environ.get("SYNC", "event")
+
     def run_hidden(reps=60):
         def rnd(k):
             gs, nxt = (ga, xs2) if k % 2 == 0 else (gb, xs)
             for i, (g, s, sd) in enumerate(zip(gs, ss, sides)):
+                if SYNC == "none":  # timing only (races the buffers): no cross-stream wait at all
+                    with torch.cuda.stream(sd):
+                        ops.h2d_pull(hs[i], nxt[i], blocks=8)
+                    with torch.cuda.stream(s):
+                        g.replay()
+                    continue
+                if SYNC == "same":  # the pull as a separate launch on the slot's own stream (no cross-stream)
+                    with torch.cuda.stream(s):
+                        g.replay()
+                        ops.h2d_pull(hs[i], nxt[i], blocks=8)
+                    continue
                 ev = torch.cuda.Event()
                 with torch.cuda.stream(sd):
                     sd.wait_stream(s)  # the buffer it overwrites was read by the graph before last
