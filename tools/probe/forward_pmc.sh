@@ -1,6 +1,6 @@
 # Whole-forward PMC totals of the fused ResNet-50 (bs=32), one rocprofv3 pass per counter group.
 export TMPDIR=/tmp
-OUT=$GRAFT_REPO_ROOT/gpurun_out/fwd_pmc
+OUT=$GRAFT_REPO_ROOT/gpurun_out/${TAG:-fwd_pmc}
 mkdir -p $OUT
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" \
