@@ -49,6 +49,7 @@ from .gemm_ops import (  # noqa: F401
     pack_skinny_reference,
     silu_mul_interleaved,
     skinny_fp8,
+    mgemm,
     skinny_packed,
     skinny_packed_ar,
     split_counters,
@@ -56,6 +57,7 @@ from .gemm_ops import (  # noqa: F401
 from .dispatch import (  # noqa: F401
     BLAS_MIN_M,
     TILE_MIN_M,
+    mgemm_route,
     linear,
     linear_ln,
     ln_foldable,

@@ -81,6 +81,17 @@ def _compile(src: str, hdr_hash: str, obj_dir: str, verbose: bool, debug: bool =
     return obj
 
 
+def _check_no_missing_stubs(so: str) -> None:
+    """A kernel template whose host-side stub failed to instantiate links into a .so that only fails
+    at dlopen ("undefined symbol: ...__device_stub__..."): refuse to install such a library."""
+    nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
+    r = subprocess.run([nm, "-D", "--undefined-only", so], capture_output=True, text=True)
+    missing = [ln.split()[-1] for ln in r.stdout.splitlines() if "__device_stub__" in ln]
+    if missing:
+        os.remove(so)
+        raise RuntimeError(f"{os.path.basename(so)}: kernel stubs not instantiated: {missing[:4]}")
+
+
 def build(force: bool = False, verbose: bool = False, jobs: Optional[int] = None, debug: bool = False) -> str:
     os.makedirs(OUT_DIR, exist_ok=True)
     obj_dir = os.path.join(OUT_DIR, "obj_debug" if debug else "obj")
@@ -103,6 +114,7 @@ def build(force: bool = False, verbose: bool = False, jobs: Optional[int] = None
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr[-8000:]}")
+    _check_no_missing_stubs(out + ".tmp")
     os.replace(out + ".tmp", out)
     with open(stamp_file, "w") as f:
         f.write(stamp)

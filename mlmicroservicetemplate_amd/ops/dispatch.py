@@ -7,7 +7,7 @@ from typing import Optional
 import torch
 
 from ._core import ACT_GELU, ACT_NONE, ACT_SILU_MUL, _act
-from .gemm_ops import _bias_bf16, gemm, gemm_tile, gemm_tile_ln, silu_mul_interleaved
+from .gemm_ops import _bias_bf16, gemm, gemm_tile, gemm_tile_ln, mgemm, silu_mul_interleaved
 from .tables import small_m_plan_for, tile_cfg_for, tile_route_for
 
 
@@ -26,6 +26,20 @@ BLAS_MIN_M = TILE_MIN_M  # kept for callers that split "large" from "small" toke
 
 _GEMM_IMPL = os.environ.get("MLS_GEMM_IMPL", "auto")  # auto: the table routes; native; blas
 
+# MLS_MGEMM=1: 17..256-row projections with K >= 4096 (Llama-3-8B decode at 17-256 slots, short
+# prefills) go to the weight-streaming medium-M kernel (csrc/mgemm.hip), where N keeps its activation
+# re-reads in check.  Off by default: in the model it measured slower than the table routes --
+# decode 64 / 128 / 256 rows 5.38 / 6.53 / 8.88 vs 4.97-5.06 / 6.17-6.19 / 8.62 ms per step,
+# 256-slot serving 16.5k vs 16.8-16.9k tok/s (profiles/r6_mgemm_llama_e2e_ab.jsonl).
+_MGEMM = os.environ.get("MLS_MGEMM", "0") == "1"
+
+
+def mgemm_route(M: int, N: int, K: int) -> bool:
+    """Whether :func:`linear` sends an ``[M, K] x [N, K]^T`` projection to :func:`mgemm`."""
+    if not _MGEMM or not 16 < M <= 256 or N % 64 or K % 256 or K < 4096:
+        return False
+    return N <= 4096 or (N <= 8192 and M <= 128)
+
 
 def linear(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, act=ACT_NONE,
            residual: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
@@ -40,6 +54,11 @@ def linear(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     N = w.shape[0]
     if impl == "blas" or (impl == "auto" and _GEMM_IMPL == "blas"):
         return _linear_blas(a, w, bias, code, residual)
+    if (impl in ("auto", "native") and mgemm_route(M, N, K) and a.device.type == "cuda" and a.stride(1) == 1
+            and w.is_contiguous() and (residual is None or residual.is_contiguous())
+            and code in (ACT_NONE, ACT_SILU_MUL) and not (code == ACT_SILU_MUL and residual is not None)):
+        return mgemm(a, w, bias, act=code, residual=residual,
+                     workspace=workspace if workspace is not None and workspace.dtype == torch.float32 else None)
     if impl == "tile" or (impl in ("auto", "native") and M >= TILE_MIN_M and K % 64 == 0 and N % 16 == 0
                           and a.device.type == "cuda" and a.is_contiguous() and w.is_contiguous()):
         kind, cfg, sk = tile_route_for(M, N, K) if impl in ("auto", "native") else ("tile",) + tile_cfg_for(M, N, K)

@@ -271,6 +271,42 @@ def pack_skinny_reference(w: torch.Tensor) -> torch.Tensor:
     return w.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).reshape(-1).contiguous()
 
 
+def mgemm(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, act=ACT_NONE,
+          residual: Optional[torch.Tensor] = None, splitk: int = 0,
+          workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Medium-M weight-streaming GEMM (csrc/mgemm.hip): ``act(a @ w.T + bias) (+ residual)`` for
+    17..256-row decode batches -- weights straight to registers, activations through an LDS ring.
+    a ``[M, K]`` (row stride may exceed K), w ``[N, K]``; N % 64 == 0, K % 256 == 0; ``act="silu_mul"``
+    as :func:`gemm`.  ``splitk`` <= 0: the launcher's pick (K slices within one block per CU)."""
+    dev = a.device
+    _need(w, "w", torch.bfloat16, dev)
+    if a.dtype != torch.bfloat16 or a.device != dev or a.dim() != 2 or a.stride(1) != 1:
+        raise ValueError("a: bf16 [M, K] with unit column stride")
+    M, K = a.shape
+    N = w.shape[0]
+    if w.shape[1] != K or not 0 < M <= 256 or N % 64 or K % 256:
+        raise ValueError(f"mgemm: M {M} (1..256), N {N} (% 64), K {K} (% 256)")
+    code = _act(act)
+    if bias is not None:
+        _need(bias, "bias", torch.float32, dev)
+    n_out = N // 2 if code == ACT_SILU_MUL else N
+    if residual is not None:
+        _need(residual, "residual", torch.bfloat16, dev)
+        if code == ACT_SILU_MUL or tuple(residual.shape) != (M, N):
+            raise ValueError("residual: [M, N], not with silu_mul")
+    out = torch.empty(M, n_out, device=dev, dtype=torch.bfloat16)
+    if splitk <= 0:
+        splitk = int(lib().mls_mgemm_auto_split(N, K, 0))
+    need = splitk * M * N if splitk > 1 else 0
+    if need and (workspace is None or workspace.numel() * workspace.element_size() < need * 4):
+        workspace = torch.empty(need, device=dev, dtype=torch.float32)
+    wsp, wsb = _workspace_args(workspace) if need else (None, 0)
+    rc = lib().mls_mgemm(a.data_ptr(), w.data_ptr(), _ptr(bias), _ptr(residual), out.data_ptr(), wsp, wsb,
+                         M, N, K, a.stride(0), code, splitk, stream_ptr(dev))
+    check(rc, "mls_mgemm")
+    return out
+
+
 def skinny_packed(x: torch.Tensor, wp: torch.Tensor, N: int, *, delta: Optional[torch.Tensor] = None,
                   resid_out: Optional[torch.Tensor] = None, norm: bool = False, act=ACT_NONE,
                   bias: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
