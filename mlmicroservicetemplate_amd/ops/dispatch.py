@@ -26,19 +26,26 @@ BLAS_MIN_M = TILE_MIN_M  # kept for callers that split "large" from "small" toke
 
 _GEMM_IMPL = os.environ.get("MLS_GEMM_IMPL", "auto")  # auto: the table routes; native; blas
 
-# MLS_MGEMM=1: 17..256-row projections with K >= 4096 (Llama-3-8B decode at 17-256 slots, short
-# prefills) go to the weight-streaming medium-M kernel (csrc/mgemm.hip), where N keeps its activation
-# re-reads in check.  Off by default: in the model it measured slower than the table routes --
-# decode 64 / 128 / 256 rows 5.38 / 6.53 / 8.88 vs 4.97-5.06 / 6.17-6.19 / 8.62 ms per step,
-# 256-slot serving 16.5k vs 16.8-16.9k tok/s (profiles/r6_mgemm_llama_e2e_ab.jsonl).
-_MGEMM = os.environ.get("MLS_MGEMM", "0") == "1"
+# MLS_MGEMM=1: 17..128-row projections with N <= 4096 and K in [4096, 8192) -- Llama-3-8B's o_proj
+# in decode at 17-128 slots -- go to the weight-streaming medium-M kernel (csrc/mgemm.hip);
+# MLS_MGEMM=all also sends down_proj / qkv shapes.  Off by default.  Alone, with the weights L2-cold
+# as in a decode step and the model's workspace (tools/probe/mgemm_probe.py,
+# profiles/r6_mgemm_probe_vs_routes.jsonl), us, mgemm vs the table route: o_proj 16.0 / 18.6 vs
+# 24.4 / 20.2 at 64 / 128 rows, level at 256; down_proj slower (39.6 / 49.7 / 69.2 vs 34.7 / 41.9 /
+# 70.2); qkv level.  Inside the decode step it loses: o_proj routed, decode 32 / 64 / 128 rows
+# 4.42-4.45 / 5.01-5.03 / 6.34-6.37 vs 4.36-4.37 / 4.98-4.99 / 6.26-6.27 ms per step
+# (profiles/r6_mgemm_o_route_llama_e2e_ab.jsonl); o + down + qkv routed, 64 / 128 / 256 rows 5.38 /
+# 6.53 / 8.88 vs 4.97-5.06 / 6.17-6.19 / 8.62 (profiles/r6_mgemm_llama_e2e_ab.jsonl).
+_MGEMM = os.environ.get("MLS_MGEMM", "0")
 
 
 def mgemm_route(M: int, N: int, K: int) -> bool:
     """Whether :func:`linear` sends an ``[M, K] x [N, K]^T`` projection to :func:`mgemm`."""
-    if not _MGEMM or not 16 < M <= 256 or N % 64 or K % 256 or K < 4096:
+    if _MGEMM == "0" or not 16 < M <= 256 or N % 64 or K % 256 or K < 4096:
         return False
-    return N <= 4096 or (N <= 8192 and M <= 128)
+    if _MGEMM == "all":
+        return N <= 4096 or (N <= 8192 and M <= 128)
+    return M <= 128 and N <= 4096 and K < 8192
 
 
 def linear(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, act=ACT_NONE,

@@ -10,11 +10,11 @@ tail -2 $OUT/tests.log
 : > $OUT/llama.jsonl
 for i in ${ROUNDS_SEQ:-1 2}; do
   for v in 0 1; do
-    MLS_MGEMM=$v timeout -k 10 400 python3 tools/bench_models.py llama --batches 64 128 256 --prompt 128 2>> $OUT/err \
+    MLS_MGEMM=$v timeout -k 10 400 python3 tools/bench_models.py llama --batches ${BATCHES:-64 128 256} --prompt 128 2>> $OUT/err \
       | python3 -c "import sys,json
 for l in sys.stdin:
     d=json.loads(l); d['mgemm']=$v; print(json.dumps(d))" >> $OUT/llama.jsonl || exit 1
-    MLS_MGEMM=$v timeout -k 10 400 python3 tools/bench_models.py llama-serve --batches 256 --requests 1024 --prompt 128 --new 64 2>> $OUT/err \
+    MLS_MGEMM=$v timeout -k 10 400 python3 tools/bench_models.py llama-serve --batches ${SERVE:-256} --requests $((4 * ${SERVE:-256})) --prompt 128 --new 64 2>> $OUT/err \
       | python3 -c "import sys,json
 for l in sys.stdin:
     d=json.loads(l); d['mgemm']=$v; print(json.dumps(d))" >> $OUT/llama.jsonl || exit 1
