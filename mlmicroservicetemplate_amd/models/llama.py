@@ -701,8 +701,26 @@ class LlamaTP:
                 return ops.skinny_packed(x, packed[name], p[name].shape[0], residual=residual, variant=self.pk_variant)
             return ops.linear(x, p[name], residual=residual, workspace=ws)
 
+        # TP = 1 above 24 tokens (no packed / fused-norm GEMMs): o_proj and down_proj leave their split-K
+        # slabs to one kernel that adds them to the residual stream and normalises it for the next
+        # projection (ops.linear_add_rmsnorm) -- one launch instead of reduce + RMSNorm, bit-identical.
+        # A projection it cannot take (no split on that shape) runs the plain pair.
+        fuse_rn = self.tp == 1 and not packed and not fuse and not fold and getattr(self, "fuse_add_norm", True)
+        xn_pending = [None]  # RMSNorm(r) computed by the previous projection's fused reduce
+
+        def proj_add_norm(x, name):
+            """r += x @ W_name^T in place, and RMSNorm(r) staged for the next pre_norm; False: not taken."""
+            xn = ops.linear_add_rmsnorm(x, p[name], r, self.ones, eps, ws) if fuse_rn else None
+            xn_pending[0] = xn
+            if xn is not None:
+                self.add_norm_fused = getattr(self, "add_norm_fused", 0) + 1
+            return xn is not None
+
         def pre_norm(x, name, d, act=ops.ACT_NONE):
             w = p[name]
+            if xn_pending[0] is not None:
+                xn, xn_pending[0] = xn_pending[0], None
+                return ops.linear(xn, w, act=act, workspace=ws), x
             if use_fp8(name, x.shape[1]):
                 q, sc = fp8[name]
                 r_new = None if d is None else torch.empty_like(x)
@@ -766,6 +784,12 @@ class LlamaTP:
                 h = linear(a, f"l{i}.o", residual=r)
                 gu, _ = pre_norm(h, f"l{i}.gate_up", None, act=ops.ACT_SILU_MUL)
                 r = linear(gu, f"l{i}.down", residual=h)
+                continue
+            if delta is None and proj_add_norm(a, f"l{i}.o"):
+                gu, r = pre_norm(r, f"l{i}.gate_up", None, act=ops.ACT_SILU_MUL)
+                if i + 1 < cfg.layers and proj_add_norm(gu, f"l{i}.down"):
+                    continue  # delta stays None: the down output is in r, its RMSNorm staged for qkv
+                delta = row_parallel(gu, f"l{i}.down")
                 continue
             o = row_parallel(a, f"l{i}.o")
             gu, r = pre_norm(r, f"l{i}.gate_up", o, act=ops.ACT_SILU_MUL)

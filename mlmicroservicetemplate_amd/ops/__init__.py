@@ -58,6 +58,7 @@ from .dispatch import (  # noqa: F401
     BLAS_MIN_M,
     TILE_MIN_M,
     mgemm_route,
+    linear_add_rmsnorm,
     linear,
     linear_ln,
     ln_foldable,

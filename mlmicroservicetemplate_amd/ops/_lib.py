@@ -95,6 +95,7 @@ _SIGS = {
     "mls_flash_attention_rows": [P, P, P, P, I, I, I, I, I, I, I, I, I, I, P, I, F, P],
     "mls_skinny_gemm": [P, P, P, P, P, P, SZ, I, I, I, I, I, P],
     "mls_mgemm": [P, P, P, P, P, P, SZ, I, I, I, I, I, I, P], "mls_mgemm_auto_split": [I, I, I],
+    "mls_gemm_slabs": [P, P, P, SZ, I, I, I, I, I, P, P], "mls_splitk_add_rmsnorm": [P, SZ, I, I, I, P, P, P, F, P],
     "mls_skinny_gemm_norm": [P, P, P, P, P, P, P, P, SZ, I, I, I, I, I, I, F, P],
     "mls_skinny_pack": [P, P, I, I, P],
     "mls_skinny_packed": [P, P, P, P, P, P, P, I, I, I, I, I, F, I, P],

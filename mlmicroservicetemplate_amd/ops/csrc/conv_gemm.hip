@@ -959,7 +959,12 @@ int* splitk_counters(hipStream_t st, long ntiles) {
   return p;
 }
 
-int launch_conv(ConvArgs a, int mode, int cfg, int splitk, size_t ws_bytes, hipStream_t st) {
+// defer_split != null: leave the split-K fp32 slabs [split][M][N] in `ws` for the caller to reduce
+// (mls_splitk_add_rmsnorm: the reduce fused with the next residual add + RMSNorm) -- no in-launch or
+// separate reduce, no bf16 output; *defer_split = the split used.  MLS_UNSUPPORTED (nothing launched)
+// when the shape would not split.
+int launch_conv(ConvArgs a, int mode, int cfg, int splitk, size_t ws_bytes, hipStream_t st,
+                int* defer_split = nullptr) {
   if (a.act == ACT_SILU_MUL && a.N % 16 != 0) return MLS_BAD_ARG;
   if (a.N % 8 != 0 || a.M <= 0 || a.N <= 0 || a.K <= 0 || a.K % 8 != 0) return MLS_BAD_ARG;
   {
@@ -968,6 +973,7 @@ int launch_conv(ConvArgs a, int mode, int cfg, int splitk, size_t ws_bytes, hipS
     a.o_bytes = (uint32_t)ob;
   }
   if (cfg >= 20 && cfg <= 22 && mode == MODE_DUAL) cfg = 0;  // persistent kernel: no dual mode
+  if (defer_split && cfg >= 20 && cfg <= 22) cfg = 0;           // no split-K there
   if (cfg >= 20 && cfg <= 22) {
     if (a.act != ACT_SILU_MUL && (splitk <= 1)) {
       a.splitk = 1;
@@ -1012,7 +1018,10 @@ int launch_conv(ConvArgs a, int mode, int cfg, int splitk, size_t ws_bytes, hipS
   const long ntiles = otiles * splitk;
   if (ntiles > 0x7fffffffL) return MLS_BAD_ARG;
   a.cnt = nullptr;
-  if (splitk > 1 && (size_t)splitk * a.M * a.N * sizeof(float) < 0x7FFFFFF0ull) {
+  if (defer_split) {
+    if (splitk <= 1 || a.act != ACT_NONE || a.res || a.scale || a.bias) return MLS_UNSUPPORTED;
+    *defer_split = splitk;
+  } else if (splitk > 1 && (size_t)splitk * a.M * a.N * sizeof(float) < 0x7FFFFFF0ull) {
     a.cnt = splitk_counters(st, otiles);
     a.ws_bytes = (uint32_t)((size_t)splitk * a.M * a.N * sizeof(float));
   }
@@ -1025,7 +1034,7 @@ int launch_conv(ConvArgs a, int mode, int cfg, int splitk, size_t ws_bytes, hipS
     case MODE_DUAL: launch_mode<MODE_DUAL>(cfg, grid, st, a); break;
     default: return MLS_UNSUPPORTED;
   }
-  if (splitk > 1 && a.cnt == nullptr) {
+  if (splitk > 1 && a.cnt == nullptr && !defer_split) {
     const long total = (long)a.M * (a.N / 8);
     int blocks = (int)((total + 255) / 256);
     if (blocks > 4096) blocks = 4096;
@@ -1183,6 +1192,28 @@ int mls_gemm(const void* A, const void* W, const float* scale, const float* bias
   a.x_bytes = (uint32_t)xb;
   a.w_bytes = (uint32_t)wb;
   return launch_conv(a, MODE_1X1, cfg, splitk, ws_bytes, (hipStream_t)stream);
+}
+
+// out-less GEMM: A [M][K] . W[N][K]^T as split-K fp32 slabs [split][M][N] in ws, reduced by the
+// caller (mls_splitk_add_rmsnorm).  *split_used = the split; MLS_UNSUPPORTED when it would be 1.
+int mls_gemm_slabs(const void* A, const void* W, void* ws, size_t ws_bytes, int M, int N, int K, int cfg, int splitk,
+                   int* split_used, void* stream) {
+  if (!split_used || !ws) return MLS_BAD_ARG;
+  ConvArgs a{};
+  a.x = (const bf16*)A;
+  a.w = (const bf16*)W;
+  a.ws = (float*)ws;
+  a.B = M; a.H = 1; a.W = 1; a.Cin = K; a.Ho = 1; a.Wo = 1; a.N = N; a.KH = 1; a.KW = 1; a.stride = 1; a.pad = 0;
+  a.M = M;
+  a.K = K;
+  a.act = ACT_NONE;
+  a.ldo = N;
+  a.ldr = N;
+  const size_t xb = (size_t)M * K * 2, wb = (size_t)N * K * 2;
+  if (xb >= 0x7FFFFFFFull || wb >= 0x7FFFFFFFull) return MLS_UNSUPPORTED;
+  a.x_bytes = (uint32_t)xb;
+  a.w_bytes = (uint32_t)wb;
+  return launch_conv(a, MODE_1X1, cfg, splitk, ws_bytes, (hipStream_t)stream, split_used);
 }
 
 // the tile config / split-K the heuristic would pick (for the autotuner and tests)

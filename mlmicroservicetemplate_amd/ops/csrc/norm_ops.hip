@@ -180,6 +180,77 @@ __global__ __launch_bounds__(256) void layernorm_rowblock_kernel(const bf16* __r
   }
 }
 
+// A projection's split-K reduce fused with the residual add + RMSNorm that follows it (Llama-3-8B
+// above 24 tokens per step: o_proj -> the gate_up pre-norm, down_proj -> the next qkv pre-norm).  One
+// block per row; the same arithmetic as conv_gemm.hip's reduce (fp32 slabs summed in slice order,
+// rounded to bf16) followed by layernorm_rowblock_kernel (+ residual, rounded and written back,
+// RMS statistics of the rounded row, x * rstd * gamma): one launch instead of two.  Slices past
+// `split` read zero through the buffer range check, so all slab loads are in flight together.
+template <int CPT, int MAXS>
+__global__ __launch_bounds__(256) void splitk_add_rmsnorm_kernel(const float* __restrict__ ws, uint32_t ws_bytes,
+                                                                 int split, int M, bf16* __restrict__ res,
+                                                                 const bf16* __restrict__ gamma, bf16* __restrict__ out,
+                                                                 int D, float eps) {
+  __shared__ float red[16];
+  const long row = blockIdx.x;
+  const int t = threadIdx.x;
+  const int nch = D >> 3;
+  const rsrc_t wr = make_rsrc(ws, ws_bytes);
+  uint4 rraw[CPT], graw[CPT];
+  float4 x[MAXS][CPT][2];
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    const int off = min(t + 256 * c, nch - 1) * 8;
+    rraw[c] = ld16(res + row * D + off);
+    graw[c] = ld16(gamma + off);
+#pragma unroll
+    for (int s2 = 0; s2 < MAXS; ++s2) {
+      const int b = s2 < split ? (int)((((size_t)s2 * M + row) * D + off) * 4) : OOB;
+      x[s2][c][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(wr, b, 0, 0));
+      x[s2][c][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(wr, b == OOB ? OOB : b + 16, 0, 0));
+    }
+  }
+  float v[CPT][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    const int ch = t + 256 * c;
+    const bool live = ch < nch;
+    float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s2 = 0; s2 < MAXS; ++s2) {
+      o[0] += x[s2][c][0].x; o[1] += x[s2][c][0].y; o[2] += x[s2][c][0].z; o[3] += x[s2][c][0].w;
+      o[4] += x[s2][c][1].x; o[5] += x[s2][c][1].y; o[6] += x[s2][c][1].z; o[7] += x[s2][c][1].w;
+    }
+    unpack8(pack8(o), v[c]);  // the projection's bf16 output
+    float r[8];
+    unpack8(rraw[c], r);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[c][e] += r[e];
+    const uint4 p = pack8(v[c]);
+    if (live) st16(res + row * D + ch * 8, p);
+    unpack8(p, v[c]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      v[c][e] = live ? v[c][e] : 0.f;
+      ss += v[c][e] * v[c][e];
+    }
+  }
+  ss = block_sum(ss, red + 8);
+  const float rstd = rsqrtf(ss * (1.f / (float)D) + eps);
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    const int ch = t + 256 * c;
+    if (ch < nch) {
+      float g[8], o[8];
+      unpack8(graw[c], g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (v[c][e] - 0.f) * rstd * g[e] + 0.f;
+      st16(out + row * D + ch * 8, pack8(o));
+    }
+  }
+}
+
 // BERT embeddings: out[t] = LN(word[id] + pos[t % S] + type[tt]) ; one wave per token
 template <int CPL>
 // ids / type_ids: token t of sequence t / S at (t / S) * id_stride + t % S -- contiguous [B][S] with
@@ -543,6 +614,29 @@ int mls_kv_append(const void* qkv, int row_stride, int k_col, int v_col, const i
   hipLaunchKernelGGL(kv_append_kernel, dim3(grid_for(work, 256)), dim3(256), 0, (hipStream_t)stream,
                      (const bf16*)qkv, row_stride, k_col, v_col, slots, (bf16*)k_cache, (bf16*)v_cache, tokens, Hkv,
                      D, hm_rows);
+  return (int)hipGetLastError();
+}
+
+
+// ws: split-K fp32 slabs [split][M][D] (conv_gemm.hip mls_gemm_slabs), split 1..8; res [M][D] bf16 is
+// updated in place (res += the reduced projection, rounded to bf16); out [M][D] = RMSNorm(res) * gamma.
+int mls_splitk_add_rmsnorm(const float* ws, size_t ws_bytes, int split, int M, int D, void* res, const void* gamma,
+                           void* out, float eps, void* stream) {
+  if (!ws || !res || !gamma || !out || M <= 0 || D <= 0 || D % 8 || D > 256 * 8 * 2 || split < 1 || split > 8 ||
+      ws_bytes < (size_t)split * M * D * 4 || (size_t)split * M * D * 4 >= 0x7FFFFFF0ull)
+    return MLS_BAD_ARG;
+  const uint32_t wb = (uint32_t)((size_t)split * M * D * 4);
+  hipStream_t st = (hipStream_t)stream;
+#define SRN_LAUNCH(C, S)                                                                                       \
+  hipLaunchKernelGGL((splitk_add_rmsnorm_kernel<C, S>), dim3((unsigned)M), dim3(256), 0, st, ws, wb, split, M, \
+                     (bf16*)res, (const bf16*)gamma, (bf16*)out, D, eps)
+  const bool one = D / 8 <= 256;
+  if (split <= 4) {
+    if (one) SRN_LAUNCH(1, 4); else SRN_LAUNCH(2, 4);
+  } else {
+    if (one) SRN_LAUNCH(1, 8); else SRN_LAUNCH(2, 8);
+  }
+#undef SRN_LAUNCH
   return (int)hipGetLastError();
 }
 

@@ -80,6 +80,50 @@ def linear(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     return gemm(a, w, bias, act=code, residual=residual, workspace=workspace)
 
 
+# Llama above 24 tokens per step: a split-K projection whose output only feeds "residual += y;
+# x = RMSNorm(residual)" (o_proj, down_proj) leaves its fp32 slabs to one kernel that reduces them,
+# adds the residual and normalises (ops mls_gemm_slabs + mls_splitk_add_rmsnorm): one launch instead
+# of the reduce + RMSNorm pair.  MLS_FUSE_ADD_NORM=0 turns it off.
+_FUSE_ADD_NORM = os.environ.get("MLS_FUSE_ADD_NORM", "1") != "0"
+
+
+def linear_add_rmsnorm(a: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, gamma: torch.Tensor, eps: float,
+                       workspace: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    """``residual += a @ w.T`` (in place, rounded to bf16 as :func:`linear` + the residual add would) and
+    returns ``RMSNorm(residual) * gamma`` -- bit-identical to :func:`linear` followed by
+    ``rmsnorm(y, gamma, residual=residual, residual_out=residual)``, in two launches instead of three.
+    Returns None (nothing launched) where the shape is not on a split-K conv_gemm route (24 < M <
+    TILE_MIN_M, split > 1, 2048 <= N <= 4096: narrower rows normalise on the wave-per-row kernel,
+    whose sum order differs) or the workspace is too small: the caller runs the plain pair."""
+    M, K = a.shape
+    N = w.shape[0]
+    if (not _FUSE_ADD_NORM or _GEMM_IMPL == "blas" or not 24 < M < TILE_MIN_M or N % 8 or K % 8
+            or not 2048 <= N <= 4096  # the widths the row-block RMSNorm takes: the same arithmetic
+            or workspace is None or workspace.dtype != torch.float32 or not a.is_contiguous()
+            or not w.is_contiguous() or not residual.is_contiguous() or tuple(residual.shape) != (M, N)
+            or residual.dtype != torch.bfloat16 or gamma.numel() != N):
+        return None
+    import ctypes
+
+    from ._lib import check, lib, stream_ptr
+
+    plan = small_m_plan_for(M, N, K)
+    cfg, sk = (plan[0], plan[1]) if plan is not None and plan[0] > 0 else (0, 0)
+    split = ctypes.c_int(0)
+    wsb = workspace.numel() * 4
+    dev = a.device
+    rc = lib().mls_gemm_slabs(a.data_ptr(), w.data_ptr(), workspace.data_ptr(), wsb, M, N, K, cfg, sk,
+                              ctypes.byref(split), stream_ptr(dev))
+    if rc == 1002:  # MLS_UNSUPPORTED: this shape would not split -- nothing was launched
+        return None
+    check(rc, "mls_gemm_slabs")
+    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    rc = lib().mls_splitk_add_rmsnorm(workspace.data_ptr(), wsb, split.value, M, N, residual.data_ptr(),
+                                      gamma.data_ptr(), out.data_ptr(), float(eps), stream_ptr(dev))
+    check(rc, "mls_splitk_add_rmsnorm")
+    return out
+
+
 def ln_foldable(M: int, N: int, K: int) -> bool:
     """Whether :func:`linear_ln` runs this shape where :func:`linear` would use the tile kernel too
     (large M; K and N multiples of the 128-column statistics blocks) -- callers keep an explicit
