@@ -973,7 +973,7 @@ int launch_conv(ConvArgs a, int mode, int cfg, int splitk, size_t ws_bytes, hipS
     a.o_bytes = (uint32_t)ob;
   }
   if (cfg >= 20 && cfg <= 22 && mode == MODE_DUAL) cfg = 0;  // persistent kernel: no dual mode
-  if (defer_split && cfg >= 20 && cfg <= 22) cfg = 0;           // no split-K there
+  if (defer_split && cfg >= 20 && cfg <= 22) return MLS_UNSUPPORTED;  // persistent: never splits
   if (cfg >= 20 && cfg <= 22) {
     if (a.act != ACT_SILU_MUL && (splitk <= 1)) {
       a.splitk = 1;
