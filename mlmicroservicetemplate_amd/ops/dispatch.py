@@ -85,6 +85,8 @@ def linear(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
 # adds the residual and normalises (ops mls_gemm_slabs + mls_splitk_add_rmsnorm): one launch instead
 # of the reduce + RMSNorm pair.  MLS_FUSE_ADD_NORM=0 turns it off.
 _FUSE_ADD_NORM = os.environ.get("MLS_FUSE_ADD_NORM", "1") != "0"
+# the largest row count it takes (the tile route's threshold minus one by default; A/B knob)
+_ADD_NORM_MAX_M = int(os.environ.get("MLS_ADD_NORM_MAX_M", str(TILE_MIN_M - 1)))
 
 
 def linear_add_rmsnorm(a: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, gamma: torch.Tensor, eps: float,
@@ -97,7 +99,7 @@ def linear_add_rmsnorm(a: torch.Tensor, w: torch.Tensor, residual: torch.Tensor,
     whose sum order differs) or the workspace is too small: the caller runs the plain pair."""
     M, K = a.shape
     N = w.shape[0]
-    if (not _FUSE_ADD_NORM or _GEMM_IMPL == "blas" or not 24 < M < TILE_MIN_M or N % 8 or K % 8
+    if (not _FUSE_ADD_NORM or _GEMM_IMPL == "blas" or not 24 < M <= _ADD_NORM_MAX_M or N % 8 or K % 8
             or not 2048 <= N <= 4096  # the widths the row-block RMSNorm takes: the same arithmetic
             or workspace is None or workspace.dtype != torch.float32 or not a.is_contiguous()
             or not w.is_contiguous() or not residual.is_contiguous() or tuple(residual.shape) != (M, N)
