@@ -1,12 +1,14 @@
 """Projection dispatch policy (``linear``): which GEMM kernel a transformer projection runs on."""
 from __future__ import annotations
 
+import ctypes
 import os
 from typing import Optional
 
 import torch
 
 from ._core import ACT_GELU, ACT_NONE, ACT_SILU_MUL, _act
+from ._lib import check, lib, stream_ptr
 from .gemm_ops import _bias_bf16, gemm, gemm_tile, gemm_tile_ln, mgemm, silu_mul_interleaved
 from .tables import small_m_plan_for, tile_cfg_for, tile_route_for
 
@@ -85,6 +87,7 @@ def linear(a: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
 # adds the residual and normalises (ops mls_gemm_slabs + mls_splitk_add_rmsnorm): one launch instead
 # of the reduce + RMSNorm pair.  MLS_FUSE_ADD_NORM=0 turns it off.
 _FUSE_ADD_NORM = os.environ.get("MLS_FUSE_ADD_NORM", "1") != "0"
+_MLS_UNSUPPORTED = 1002  # csrc/common.h MlsStatus
 # the largest row count it takes (the tile route's threshold minus one by default; A/B knob)
 _ADD_NORM_MAX_M = int(os.environ.get("MLS_ADD_NORM_MAX_M", str(TILE_MIN_M - 1)))
 
@@ -105,10 +108,6 @@ def linear_add_rmsnorm(a: torch.Tensor, w: torch.Tensor, residual: torch.Tensor,
             or not w.is_contiguous() or not residual.is_contiguous() or tuple(residual.shape) != (M, N)
             or residual.dtype != torch.bfloat16 or gamma.numel() != N):
         return None
-    import ctypes
-
-    from ._lib import check, lib, stream_ptr
-
     plan = small_m_plan_for(M, N, K)
     cfg, sk = (plan[0], plan[1]) if plan is not None and plan[0] > 0 else (0, 0)
     split = ctypes.c_int(0)
@@ -116,7 +115,7 @@ def linear_add_rmsnorm(a: torch.Tensor, w: torch.Tensor, residual: torch.Tensor,
     dev = a.device
     rc = lib().mls_gemm_slabs(a.data_ptr(), w.data_ptr(), workspace.data_ptr(), wsb, M, N, K, cfg, sk,
                               ctypes.byref(split), stream_ptr(dev))
-    if rc == 1002:  # MLS_UNSUPPORTED: this shape would not split -- nothing was launched
+    if rc == _MLS_UNSUPPORTED:  # this shape would not split -- nothing was launched
         return None
     check(rc, "mls_gemm_slabs")
     out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
