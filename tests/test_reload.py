@@ -177,11 +177,16 @@ def test_reload_two_ranks_broadcasts_to_every_rank(frontend):
         want = expected_classes(9, a)
         body, h = upload(a)
         ranks = set()
-        for _ in range(60):  # fresh connections land on both ranks; every rank serves the new weights
+        # fresh connections land on both ranks; every rank serves the new weights.  SO_REUSEPORT spreads
+        # new connections by hash, and under a loaded CPU (parallel test workers) a rank can miss a
+        # burst of them, so the loop paces itself instead of relying on 60 back-to-back tries
+        for i in range(400):
             ranks.add(requests.get(url + "/info", timeout=5).json()["rank"])
             assert requests.post(url + "/predict", data=body, headers=h, timeout=5).json()["result"]["classes"] == want
             if len(ranks) == 2:
                 break
+            if i >= 40:
+                time.sleep(0.05)
         assert ranks == {0, 1}
     finally:
         os.killpg(proc.pid, signal.SIGTERM)
